@@ -1,0 +1,188 @@
+/*
+ * orbgpu.h -- C ABI of the MI355X (gfx950) ORB extract + match hot path.
+ *
+ * This is the drop-in boundary for yxqc/ORBSLAM2_with_quadrics's per-frame feature path.  Every entry
+ * point names the reference interface it replaces.  Plain pointers and sizes only; no OpenCV or torch
+ * types.  All functions return an int status (ORBGPU_OK == 0) unless documented otherwise.
+ *
+ * Threading: one orbgpu_ctx == one ORBextractor instance (its own HIP stream, device buffers and
+ * pinned staging).  A context is not re-entrant (as ORB_SLAM2::ORBextractor is not: mvImagePyramid is
+ * mutable state); distinct contexts may be used concurrently from different host threads
+ * (src/Frame.cc:78-81 runs the left/right extractors on two std::threads).
+ */
+#ifndef ORBGPU_H
+#define ORBGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBGPU_OK 0
+#define ORBGPU_ERR_ARG (-1)         /* bad argument (NULL, wrong size, out of range) */
+#define ORBGPU_ERR_HIP (-2)         /* HIP runtime error (no device, launch failure, OOM) */
+#define ORBGPU_ERR_CAPACITY (-3)    /* caller capacity too small; *n holds the required count */
+#define ORBGPU_ERR_UNSUPPORTED (-4) /* geometry the reference itself cannot handle (e.g. a pyramid
+                                       level narrower than one 30-px FAST cell) */
+#define ORBGPU_ERR_INTERNAL (-5)    /* a device-side capacity guard tripped (reported, never silent) */
+
+/* Same 28-byte layout as cv::KeyPoint {Point2f pt; float size, angle, response; int octave,
+ * class_id;} so a std::vector<cv::KeyPoint> can be filled in place. */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbgpu_keypoint;
+
+typedef struct orbgpu_ctx orbgpu_ctx;
+
+/* ---- ORBextractor -------------------------------------------------------------------------- */
+
+/* Replaces ORBextractor::ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST,
+ * int minThFAST) -- include/ORBextractor.h:51-52, src/ORBextractor.cc:410-470.  `device` is the HIP
+ * device ordinal.  Returns NULL on failure. */
+orbgpu_ctx* orbgpu_create(int device, int nfeatures, float scaleFactor, int nlevels, int iniThFAST,
+                          int minThFAST);
+/* Replaces ORBextractor::~ORBextractor (include/ORBextractor.h:54). */
+void orbgpu_destroy(orbgpu_ctx* ctx);
+
+/* Inline getters of include/ORBextractor.h:63-83.  Vector getters write nlevels floats. */
+int orbgpu_get_levels(const orbgpu_ctx* ctx);
+float orbgpu_get_scale_factor(const orbgpu_ctx* ctx);
+int orbgpu_get_scale_factors(const orbgpu_ctx* ctx, float* out);
+int orbgpu_get_inverse_scale_factors(const orbgpu_ctx* ctx, float* out);
+int orbgpu_get_scale_sigma_squares(const orbgpu_ctx* ctx, float* out);
+int orbgpu_get_inverse_scale_sigma_squares(const orbgpu_ctx* ctx, float* out);
+/* mnFeaturesPerLevel (src/ORBextractor.cc:435-446); nlevels ints. */
+int orbgpu_get_features_per_level(const orbgpu_ctx* ctx, int* out);
+
+/* Replaces void ORBextractor::operator()(InputArray image, InputArray mask, vector<KeyPoint>& kps,
+ * OutputArray descriptors) -- include/ORBextractor.h:59-61, src/ORBextractor.cc:1043-1105.
+ * img: host u8 grey image, `step` bytes per row.  Keypoints (level-0 coordinates, levels 0..n-1
+ * concatenated) go to kps[0..*n), descriptors to desc (row-major *n x 32 bytes).  The mask is ignored
+ * by the reference and therefore absent here.  cols==0 || rows==0 mirrors `_image.empty()`: returns OK
+ * with *n = -1 and the outputs untouched.  If cap < required, returns ORBGPU_ERR_CAPACITY with *n set.
+ * A capacity of orbgpu_max_keypoints(ctx) is always sufficient. */
+int orbgpu_extract(orbgpu_ctx* ctx, const uint8_t* img, int cols, int rows, size_t step,
+                   orbgpu_keypoint* kps, uint8_t* desc, int cap, int* n);
+int orbgpu_max_keypoints(const orbgpu_ctx* ctx);
+
+/* Backs the public member std::vector<cv::Mat> mvImagePyramid (include/ORBextractor.h:85), read by
+ * Frame::ComputeStereoMatches (src/Frame.cc:473,563,575,580): lazy download of level `level` of the
+ * LAST frame processed (frame 0 of the last batch).  dst==NULL only queries *cols/*rows. */
+int orbgpu_get_level(orbgpu_ctx* ctx, int level, uint8_t* dst, size_t dst_step, int* cols, int* rows);
+
+/* ---- batched, device-resident extraction (MI355X-native extension; same per-frame result) --- */
+
+/* Extract B frames that already live in HBM: frame b starts at d_imgs + b*frame_stride, rows are
+ * `pitch` bytes apart.  Enqueued on the context stream; returns without synchronising.  Results stay
+ * on the device (orbgpu_batch_outputs) until orbgpu_batch_download. */
+int orbgpu_extract_batch_device(orbgpu_ctx* ctx, const uint8_t* d_imgs, int B, int cols, int rows,
+                                size_t pitch, size_t frame_stride);
+/* Device pointers of the last batch: kps[b*frame_cap + i], desc[(b*frame_cap + i)*32],
+ * counts[b] (final keypoint count of frame b).  Valid until the next batch call. */
+int orbgpu_batch_outputs(orbgpu_ctx* ctx, orbgpu_keypoint** d_kps, uint8_t** d_desc, int** d_counts,
+                         int* frame_cap);
+/* Synchronise and copy frame b of the last batch to the host. */
+int orbgpu_batch_download(orbgpu_ctx* ctx, int b, orbgpu_keypoint* kps, uint8_t* desc, int cap,
+                          int* n);
+
+/* ---- Frame grid (src/Frame.cc:230-245, 327-392) ----------------------------------------------- */
+
+/* Grid geometry of ComputeImageBounds + grid scales (src/Frame.cc:207-223, 436-464) for an
+ * undistorted image: mnMinX=0, mnMaxX=cols, mnMinY=0, mnMaxY=rows, inv = 64/W, 48/H. */
+typedef struct {
+    float minX, minY, maxX, maxY, invW, invH;
+} orbgpu_grid_geom;
+int orbgpu_grid_geom_for_image(int cols, int rows, orbgpu_grid_geom* g);
+
+/* ---- ORBmatcher ------------------------------------------------------------------------------- */
+
+/* Replaces int ORBmatcher::DescriptorDistance(const Mat&, const Mat&) -- src/ORBmatcher.cc:1647-1663
+ * (host-side, 32-byte rows). */
+int orbgpu_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* A host snapshot of the Frame fields the matchers read: mvKeysUn, mDescriptors, mvuRight and the
+ * grid geometry (static members of Frame in the reference). */
+typedef struct {
+    int n;
+    const orbgpu_keypoint* kps;
+    const uint8_t* desc;   /* n x 32 */
+    const float* uright;   /* n floats, or NULL (monocular: all -1) */
+    orbgpu_grid_geom grid;
+    const float* scale_factors; /* mvScaleFactors, nlevels */
+    int nlevels;
+} orbgpu_frame_view;
+
+/* Replaces int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, vector<Point2f>&
+ * vbPrevMatched, vector<int>& vnMatches12, int windowSize) with ORBmatcher(nnratio, checkOri) --
+ * src/ORBmatcher.cc:405-520, include/ORBmatcher.h:69.  prev_xy: 2*F1.n floats (in/out),
+ * matches12: F1.n ints (out).  *nmatches receives the return value of the reference. */
+int orbgpu_search_for_initialization(orbgpu_ctx* ctx, const orbgpu_frame_view* F1,
+                                     const orbgpu_frame_view* F2, float nnratio, int checkOri,
+                                     float* prev_xy, int* matches12, int windowSize, int* nmatches);
+
+/* Device-resident batch form: frame `ref` of ctx_ref's last batch is F1 for every frame b of ctx's last
+ * batch (F2 = frame b), as Tracking::MonocularInitialization matches each new frame against the
+ * initial frame (src/Tracking.cc:563-635).  d_prev_xy: B x ref_cap x 2 floats (in/out, device),
+ * d_matches12: B x ref_cap ints (device), d_nmatches: B ints (device).  Enqueued on ctx's stream. */
+int orbgpu_search_for_initialization_batch(orbgpu_ctx* ctx_ref, int ref, orbgpu_ctx* ctx,
+                                           orbgpu_grid_geom grid, float nnratio, int checkOri,
+                                           int windowSize, float* d_prev_xy, int* d_matches12,
+                                           int* d_nmatches);
+
+/* Map points as seen by SearchByProjection (MapPoint fields, include/MapPoint.h:91-99, snapshot
+ * gathered under the reference's per-point mutexes). */
+typedef struct {
+    int m;
+    const uint8_t* track_in_view; /* mbTrackInView */
+    const uint8_t* is_bad;        /* isBad() */
+    const int32_t* level;         /* mnTrackScaleLevel */
+    const float* view_cos;        /* mTrackViewCos */
+    const float* proj_x;          /* mTrackProjX */
+    const float* proj_y;          /* mTrackProjY */
+    const float* proj_xr;         /* mTrackProjXR */
+    const int32_t* n_obs;         /* Observations() */
+    const uint8_t* desc;          /* GetDescriptor(), m x 32 */
+} orbgpu_mappoints_view;
+
+/* Replaces int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints,
+ * const float th) with ORBmatcher(nnratio) -- src/ORBmatcher.cc:45-137, include/ORBmatcher.h:48.
+ * owner (F.n ints, in/out) = F.mvpMapPoints as map-point indices (-1 == NULL); owner_obs (F.n ints,
+ * in/out) = mvpMapPoints[i]->Observations()>0 for the current owner. */
+int orbgpu_search_by_projection(orbgpu_ctx* ctx, const orbgpu_frame_view* F,
+                                const orbgpu_mappoints_view* mp, float nnratio, float th,
+                                int32_t* owner, int32_t* owner_obs, int* nmatches);
+
+/* ---- stream / timing helpers ------------------------------------------------------------------ */
+
+/* The context's hipStream_t (as void*), e.g. for torch.cuda.ExternalStream. */
+void* orbgpu_stream(orbgpu_ctx* ctx);
+int orbgpu_synchronize(orbgpu_ctx* ctx);
+/* Per-stage HIP-event timing of the batch pipeline (off by default).  When on, every stage of
+ * orbgpu_extract_batch_device / *_batch is bracketed by events on the context stream;
+ * orbgpu_stage_times writes up to cap (name, milliseconds) pairs of the last batch and returns the
+ * number of stages. */
+int orbgpu_set_stage_timing(orbgpu_ctx* ctx, int on);
+int orbgpu_stage_times(orbgpu_ctx* ctx, const char** names, float* ms, int cap);
+/* Human-readable message for the last error on this context (static storage, never NULL). */
+const char* orbgpu_last_error(const orbgpu_ctx* ctx);
+
+/* Introspection of the last batch (parity tests): FAST candidates of (frame b, level) as packed u64
+ * {x-16:16, y-16:16, response:8} in arbitrary order, and the octree output of (b, level) in list order
+ * as u32 {x:16, y:16} (level pixels) + u8 response.  Return the count (or < 0 on error). */
+int orbgpu_debug_candidates(orbgpu_ctx* ctx, int b, int level, uint64_t* out, int cap);
+int orbgpu_debug_octree(orbgpu_ctx* ctx, int b, int level, uint32_t* xy, uint8_t* resp, int cap);
+
+/* Device memory helpers for callers without a HIP runtime of their own (tests, bench). */
+void* orbgpu_device_alloc(orbgpu_ctx* ctx, size_t bytes);
+int orbgpu_device_free(orbgpu_ctx* ctx, void* p);
+int orbgpu_memcpy_h2d(orbgpu_ctx* ctx, void* dst, const void* src, size_t bytes);
+int orbgpu_memcpy_d2h(orbgpu_ctx* ctx, void* dst, const void* src, size_t bytes);
+int orbgpu_memset_d(orbgpu_ctx* ctx, void* dst, int value, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

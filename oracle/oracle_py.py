@@ -1,0 +1,235 @@
+"""ctypes binding of the CPU oracle (oracle/build/liborb_oracle.so) -- TEST INFRASTRUCTURE ONLY.
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg; the product
+(orbslam2_with_quadrics_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liborb_oracle.so")
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KP_DTYPE.itemsize == 28
+
+
+def build() -> str:
+    subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        vp, i32, f32, u8p = C.c_void_p, C.c_int, C.c_float, C.c_void_p
+        L.oo_create.restype = vp
+        L.oo_create.argtypes = [i32, f32, i32, i32, i32]
+        L.oo_destroy.argtypes = [vp]
+        L.oo_extract.restype = i32
+        L.oo_extract.argtypes = [vp, u8p, i32, i32, i32, vp, vp, i32]
+        L.oo_scale_tables.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.oo_level_size.argtypes = [vp, i32, C.POINTER(i32), C.POINTER(i32)]
+        L.oo_level_image.restype = C.POINTER(C.c_uint8)
+        L.oo_level_image.argtypes = [vp, i32]
+        L.oo_level_candidates.restype = i32
+        L.oo_level_candidates.argtypes = [vp, i32, vp, vp, i32]
+        L.oo_resize_linear.argtypes = [vp, i32, i32, vp, i32, i32]
+        L.oo_gaussian7.argtypes = [vp, i32, i32, vp]
+        L.oo_fast_score.restype = i32
+        L.oo_fast_score.argtypes = [vp, i32, i32, i32]
+        L.oo_fastatan2.restype = f32
+        L.oo_fastatan2.argtypes = [f32, f32]
+        L.oo_sincos.argtypes = [f32, C.POINTER(f32), C.POINTER(f32)]
+        L.oo_descriptor_distance.restype = i32
+        L.oo_descriptor_distance.argtypes = [vp, vp]
+        L.oo_grid_params.argtypes = [i32, i32] + [C.POINTER(f32)] * 6
+        L.oo_grid_build.argtypes = [vp]
+        L.oo_features_in_area.restype = i32
+        L.oo_features_in_area.argtypes = [vp, f32, f32, f32, i32, i32, vp]
+        L.oo_search_for_initialization.restype = i32
+        L.oo_search_for_initialization.argtypes = [vp, vp, f32, i32, vp, vp, i32]
+        L.oo_search_by_projection.restype = i32
+        L.oo_search_by_projection.argtypes = [vp, vp, f32, f32, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class OracleExtractor:
+    """Mirror of ORB_SLAM2::ORBextractor backed by the C oracle."""
+
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7):
+        self._L = lib()
+        self.nfeatures, self.nlevels = nfeatures, nlevels
+        self._h = self._L.oo_create(nfeatures, scale_factor, nlevels, ini_th, min_th)
+        if not self._h:
+            raise ValueError("bad extractor parameters")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.oo_destroy(self._h)
+            self._h = None
+
+    def tables(self):
+        n = self.nlevels
+        sf, isf, s2, is2 = (np.zeros(n, np.float32) for _ in range(4))
+        fpl = np.zeros(n, np.int32)
+        umax = np.zeros(16, np.int32)
+        self._L.oo_scale_tables(self._h, _p(sf), _p(isf), _p(s2), _p(is2), _p(fpl), _p(umax))
+        return dict(scale=sf, inv_scale=isf, sigma2=s2, inv_sigma2=is2, features_per_level=fpl,
+                    umax=umax)
+
+    def __call__(self, img: np.ndarray):
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        cap = self.nfeatures + 64 * self.nlevels + 64
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = self._L.oo_extract(self._h, _p(img), img.shape[1], img.shape[0], img.strides[0],
+                               _p(kps), _p(desc), cap)
+        if n < 0:
+            raise RuntimeError("oracle capacity exceeded")
+        return kps[:n].copy(), desc[:n].copy()
+
+    def level(self, level: int) -> np.ndarray:
+        w, h = C.c_int(), C.c_int()
+        self._L.oo_level_size(self._h, level, C.byref(w), C.byref(h))
+        ptr = self._L.oo_level_image(self._h, level)
+        return np.ctypeslib.as_array(ptr, shape=(h.value, w.value)).copy()
+
+    def candidates(self, level: int):
+        n = self._L.oo_level_candidates(self._h, level, None, None, 0)
+        xy = np.zeros((max(n, 1), 2), np.float32)
+        resp = np.zeros(max(n, 1), np.float32)
+        self._L.oo_level_candidates(self._h, level, _p(xy), _p(resp), n)
+        return xy[:n], resp[:n]
+
+
+# ------------------------------------------------------------------------------------------------
+# Frame / matcher mirrors
+# ------------------------------------------------------------------------------------------------
+class _OOFrame(C.Structure):
+    _fields_ = [("n", C.c_int), ("kps", C.c_void_p), ("desc", C.c_void_p), ("uright", C.c_void_p),
+                ("minX", C.c_float), ("minY", C.c_float), ("maxX", C.c_float), ("maxY", C.c_float),
+                ("gridInvW", C.c_float), ("gridInvH", C.c_float), ("scale_factors", C.c_void_p),
+                ("nlevels", C.c_int), ("cell_start", C.c_void_p), ("cell_items", C.c_void_p)]
+
+
+class OracleFrame:
+    """Snapshot of the Frame fields the matchers read (mvKeysUn, mDescriptors, mvuRight, grid)."""
+
+    def __init__(self, kps, desc, cols, rows, scale_factors, uright=None):
+        L = lib()
+        self.kps = np.ascontiguousarray(kps)
+        self.desc = np.ascontiguousarray(desc, dtype=np.uint8)
+        self.scale_factors = np.ascontiguousarray(scale_factors, dtype=np.float32)
+        self.uright = None if uright is None else np.ascontiguousarray(uright, np.float32)
+        self.cell_start = np.zeros(64 * 48 + 1, np.int32)
+        self.cell_items = np.zeros(max(len(self.kps), 1), np.int32)
+        vals = [C.c_float() for _ in range(6)]
+        L.oo_grid_params(cols, rows, *[C.byref(v) for v in vals])
+        self.bounds = [v.value for v in vals]
+        s = _OOFrame()
+        s.n = len(self.kps)
+        s.kps = _p(self.kps).value
+        s.desc = _p(self.desc).value
+        s.uright = None if self.uright is None else _p(self.uright).value
+        s.minX, s.minY, s.maxX, s.maxY, s.gridInvW, s.gridInvH = self.bounds
+        s.scale_factors = _p(self.scale_factors).value
+        s.nlevels = len(self.scale_factors)
+        s.cell_start = _p(self.cell_start).value
+        s.cell_items = _p(self.cell_items).value
+        self._s = s
+        L.oo_grid_build(C.byref(s))
+
+    def features_in_area(self, x, y, r, min_level=-1, max_level=-1):
+        out = np.zeros(max(len(self.kps), 1), np.int32)
+        n = lib().oo_features_in_area(C.byref(self._s), x, y, r, min_level, max_level, _p(out))
+        return out[:n].copy()
+
+
+def search_for_initialization(f1: OracleFrame, f2: OracleFrame, prev_xy, nnratio=0.9,
+                              check_ori=True, window=100):
+    prev = np.ascontiguousarray(prev_xy, np.float32).copy()
+    m12 = np.zeros(max(len(f1.kps), 1), np.int32)
+    n = lib().oo_search_for_initialization(C.byref(f1._s), C.byref(f2._s), nnratio, int(check_ori),
+                                           _p(prev), _p(m12), window)
+    return n, m12[:len(f1.kps)].copy(), prev
+
+
+class _OOMapPoints(C.Structure):
+    _fields_ = [("m", C.c_int), ("track_in_view", C.c_void_p), ("is_bad", C.c_void_p),
+                ("level", C.c_void_p), ("view_cos", C.c_void_p), ("proj_x", C.c_void_p),
+                ("proj_y", C.c_void_p), ("proj_xr", C.c_void_p), ("n_obs", C.c_void_p),
+                ("desc", C.c_void_p)]
+
+
+def search_by_projection(f: OracleFrame, mp: dict, nnratio=0.8, th=3.0, owner=None, owner_obs=None):
+    n = len(f.kps)
+    owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+    owner_obs = (np.zeros(n, np.int32) if owner_obs is None
+                 else np.ascontiguousarray(owner_obs, np.int32).copy())
+    arrs = dict(track_in_view=np.ascontiguousarray(mp["track_in_view"], np.uint8),
+                is_bad=np.ascontiguousarray(mp["is_bad"], np.uint8),
+                level=np.ascontiguousarray(mp["level"], np.int32),
+                view_cos=np.ascontiguousarray(mp["view_cos"], np.float32),
+                proj_x=np.ascontiguousarray(mp["proj_x"], np.float32),
+                proj_y=np.ascontiguousarray(mp["proj_y"], np.float32),
+                proj_xr=np.ascontiguousarray(mp["proj_xr"], np.float32),
+                n_obs=np.ascontiguousarray(mp["n_obs"], np.int32),
+                desc=np.ascontiguousarray(mp["desc"], np.uint8))
+    s = _OOMapPoints()
+    s.m = len(arrs["level"])
+    for k, v in arrs.items():
+        setattr(s, k, _p(v).value)
+    nm = lib().oo_search_by_projection(C.byref(f._s), C.byref(s), nnratio, th, _p(owner), _p(owner_obs))
+    return nm, owner, owner_obs
+
+
+def descriptor_distance(a, b) -> int:
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().oo_descriptor_distance(_p(a), _p(b))
+
+
+def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().oo_resize_linear(_p(src), src.shape[1], src.shape[0], _p(dst), dw, dh)
+    return dst
+
+
+def gaussian7(src: np.ndarray) -> np.ndarray:
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros_like(src)
+    lib().oo_gaussian7(_p(src), src.shape[1], src.shape[0], _p(dst))
+    return dst
+
+
+def fast_score(img: np.ndarray, x: int, y: int) -> int:
+    img = np.ascontiguousarray(img, np.uint8)
+    return lib().oo_fast_score(_p(img), img.strides[0], x, y)
+
+
+def fastatan2(y: float, x: float) -> float:
+    return lib().oo_fastatan2(y, x)
+
+
+def sincos(a: float):
+    s, c = C.c_float(), C.c_float()
+    lib().oo_sincos(a, C.byref(s), C.byref(c))
+    return s.value, c.value

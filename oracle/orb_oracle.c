@@ -1,0 +1,933 @@
+/*
+ * oracle/orb_oracle.c -- TEST INFRASTRUCTURE ONLY (see orb_oracle.h for the parity status).
+ *
+ * Plain-C restatement of the reference's per-frame ORB hot path.  Every function cites the reference
+ * file:line it follows.  Build: see oracle/Makefile (gcc -O2 -ffp-contract=off; FMAs explicit).
+ */
+#include "orb_oracle.h"
+#include "oo_math.h"
+
+#include <assert.h>
+#include <limits.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define OO_PATCH_SIZE 31
+#define OO_HALF_PATCH 15
+#define OO_EDGE 19
+#define OO_MAXLEVELS 32
+#define OO_GRID_COLS 64
+#define OO_GRID_ROWS 48
+
+#include "orb_pattern.inc" /* static const signed char oo_orb_pattern[256*4] (x0,y0,x1,y1 per pair) */
+
+/* ------------------------------------------------------------------------------------------------ */
+/* small growable arrays                                                                              */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct { float x, y, resp; } oo_cand;  /* the fields of cv::KeyPoint the octree reads */
+typedef struct { oo_cand* v; int n, cap; } oo_candvec;
+
+static void cv_push(oo_candvec* a, oo_cand c)
+{
+    if (a->n == a->cap) {
+        a->cap = a->cap ? a->cap * 2 : 16;
+        a->v = (oo_cand*)realloc(a->v, sizeof(oo_cand) * (size_t)a->cap);
+    }
+    a->v[a->n++] = c;
+}
+
+struct oo_extractor {
+    int nfeatures, nlevels, iniTh, minTh;
+    double scaleFactor;                       /* double member, src/ORBextractor.h:98 */
+    float sf[OO_MAXLEVELS], isf[OO_MAXLEVELS], sig2[OO_MAXLEVELS], isig2[OO_MAXLEVELS];
+    int nfeat[OO_MAXLEVELS];
+    int umax[OO_HALF_PATCH + 1];
+    /* last call */
+    int lw[OO_MAXLEVELS], lh[OO_MAXLEVELS];
+    uint8_t* lev[OO_MAXLEVELS];
+    oo_candvec cand[OO_MAXLEVELS];
+};
+
+/* ORBextractor::ORBextractor, src/ORBextractor.cc:410-470 */
+oo_extractor* oo_create(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+{
+    if (nlevels < 1 || nlevels > OO_MAXLEVELS) return NULL;
+    oo_extractor* e = (oo_extractor*)calloc(1, sizeof(oo_extractor));
+    e->nfeatures = nfeatures;
+    e->scaleFactor = (double)scaleFactor;
+    e->nlevels = nlevels;
+    e->iniTh = iniThFAST;
+    e->minTh = minThFAST;
+    e->sf[0] = 1.0f;
+    e->sig2[0] = 1.0f;
+    for (int i = 1; i < nlevels; i++) {
+        e->sf[i] = (float)((double)e->sf[i - 1] * e->scaleFactor); /* float*double -> double -> float */
+        e->sig2[i] = e->sf[i] * e->sf[i];
+    }
+    for (int i = 0; i < nlevels; i++) {
+        e->isf[i] = 1.0f / e->sf[i];
+        e->isig2[i] = 1.0f / e->sig2[i];
+    }
+    const float factor = (float)(1.0f / e->scaleFactor);
+    float nd = (float)nfeatures * (1.0f - factor) /
+               (1.0f - (float)pow((double)factor, (double)nlevels));
+    int sum = 0;
+    for (int l = 0; l < nlevels - 1; l++) {
+        e->nfeat[l] = oo_cvround(nd);
+        sum += e->nfeat[l];
+        nd *= factor;
+    }
+    e->nfeat[nlevels - 1] = nfeatures - sum > 0 ? nfeatures - sum : 0;
+
+    /* umax, src/ORBextractor.cc:454-469 */
+    int v, v0;
+    const int vmax = oo_cvfloor(OO_HALF_PATCH * sqrtf(2.f) / 2 + 1);
+    const int vmin = oo_cvceil(OO_HALF_PATCH * sqrtf(2.f) / 2);
+    const double hp2 = OO_HALF_PATCH * OO_HALF_PATCH;
+    for (v = 0; v <= vmax; ++v) e->umax[v] = oo_cvround_d(sqrt(hp2 - v * v));
+    for (v = OO_HALF_PATCH, v0 = 0; v >= vmin; --v) {
+        while (e->umax[v0] == e->umax[v0 + 1]) ++v0;
+        e->umax[v] = v0;
+        ++v0;
+    }
+    return e;
+}
+
+void oo_destroy(oo_extractor* e)
+{
+    if (!e) return;
+    for (int l = 0; l < OO_MAXLEVELS; l++) {
+        free(e->lev[l]);
+        free(e->cand[l].v);
+    }
+    free(e);
+}
+
+int oo_nlevels(const oo_extractor* e) { return e->nlevels; }
+
+void oo_scale_tables(const oo_extractor* e, float* scale, float* inv_scale, float* sigma2,
+                     float* inv_sigma2, int* fpl, int* umax16)
+{
+    for (int l = 0; l < e->nlevels; l++) {
+        if (scale) scale[l] = e->sf[l];
+        if (inv_scale) inv_scale[l] = e->isf[l];
+        if (sigma2) sigma2[l] = e->sig2[l];
+        if (inv_sigma2) inv_sigma2[l] = e->isig2[l];
+        if (fpl) fpl[l] = e->nfeat[l];
+    }
+    if (umax16) memcpy(umax16, e->umax, sizeof(int) * 16);
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* cv::resize INTER_LINEAR, CV_8UC1 (external; call site src/ORBextractor.cc:1120).  Generic           */
+/* fixed-point path, scalar vertical form.                                            */
+/* ------------------------------------------------------------------------------------------------ */
+void oo_resize_linear(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh)
+{
+    const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+    const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+    int* xofs = (int*)malloc(sizeof(int) * (size_t)dw);
+    short* alpha = (short*)malloc(sizeof(short) * 2 * (size_t)dw);
+    int xmax = dw;
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = oo_cvfloor(fx);
+        fx -= (float)sx;
+        if (sx < 0) { fx = 0.f; sx = 0; }
+        if (sx + 1 >= sw) {
+            if (dx < xmax) xmax = dx;
+            if (sx >= sw - 1) { fx = 0.f; sx = sw - 1; }
+        }
+        xofs[dx] = sx;
+        alpha[2 * dx] = (short)oo_cvround((1.f - fx) * 2048);
+        alpha[2 * dx + 1] = (short)oo_cvround(fx * 2048);
+    }
+    int* rows = (int*)malloc(sizeof(int) * 2 * (size_t)dw);
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = oo_cvfloor(fy);
+        fy -= (float)sy;
+        const int b0 = (short)oo_cvround((1.f - fy) * 2048), b1 = (short)oo_cvround(fy * 2048);
+        for (int k = 0; k < 2; k++) {
+            int y = sy + k;
+            y = y >= 0 ? (y < sh ? y : sh - 1) : 0;
+            const uint8_t* S = src + (size_t)y * sw;
+            int* D = rows + (size_t)k * dw;
+            for (int dx = 0; dx < dw; dx++) {
+                const int x = xofs[dx];
+                D[dx] = dx < xmax ? S[x] * alpha[2 * dx] + S[x + 1] * alpha[2 * dx + 1] : S[x] * 2048;
+            }
+        }
+        uint8_t* o = dst + (size_t)dy * dw;
+        for (int dx = 0; dx < dw; dx++) {
+            int val = (b0 * rows[dx] + b1 * rows[dw + dx] + (1 << 21)) >> 22;
+            o[dx] = (uint8_t)(val < 0 ? 0 : val > 255 ? 255 : val);
+        }
+    }
+    free(rows);
+    free(xofs);
+    free(alpha);
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* cv::GaussianBlur 7x7 sigma 2 BORDER_REFLECT_101 on CV_8U (src/ORBextractor.cc:1086)              */
+/* ------------------------------------------------------------------------------------------------ */
+static const int oo_gk[7] = {18, 34, 49, 55, 49, 34, 18}; /* cvRound(256*k), DESIGN.md §3.2 */
+
+static inline int oo_reflect101(int i, int n)
+{
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        if (i >= n) i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+void oo_gaussian7(const uint8_t* src, int w, int h, uint8_t* dst)
+{
+    int* tmp = (int*)malloc(sizeof(int) * (size_t)w * (size_t)h);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int s = 0;
+            for (int k = -3; k <= 3; k++) s += oo_gk[k + 3] * src[(size_t)y * w + oo_reflect101(x + k, w)];
+            tmp[(size_t)y * w + x] = s;
+        }
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int s = 0;
+            for (int k = -3; k <= 3; k++) s += oo_gk[k + 3] * tmp[(size_t)oo_reflect101(y + k, h) * w + x];
+            int v = (s + (1 << 15)) >> 16;
+            dst[(size_t)y * w + x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+        }
+    free(tmp);
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* cv::FAST(img, kps, threshold, nonmax=true), TYPE_9_16 (external; src/ORBextractor.cc:809,814)      */
+/* ------------------------------------------------------------------------------------------------ */
+static const int oo_circle[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},  {3, -1},
+                                     {2, -2}, {1, -3},  {0, -3},  {-1, -3}, {-2, -2}, {-3, -1},
+                                     {-3, 0}, {-3, 1},  {-2, 2},  {-1, 3}};
+
+static void oo_make_offsets(int* pixel, int stride)
+{
+    int k;
+    for (k = 0; k < 16; k++) pixel[k] = oo_circle[k][0] + oo_circle[k][1] * stride;
+    for (; k < 25; k++) pixel[k] = pixel[k - 16];
+}
+
+static inline int oo_imin(int a, int b) { return a < b ? a : b; }
+static inline int oo_imax(int a, int b) { return a > b ? a : b; }
+
+/* cornerScore<16> */
+static int oo_corner_score(const uint8_t* ptr, const int* pixel, int threshold)
+{
+    int d[25], k, v = ptr[0];
+    for (k = 0; k < 25; k++) d[k] = v - ptr[pixel[k]];
+    int a0 = threshold;
+    for (k = 0; k < 16; k += 2) {
+        int a = oo_imin(d[k + 1], d[k + 2]);
+        a = oo_imin(a, d[k + 3]);
+        if (a <= a0) continue;
+        a = oo_imin(a, d[k + 4]);
+        a = oo_imin(a, d[k + 5]);
+        a = oo_imin(a, d[k + 6]);
+        a = oo_imin(a, d[k + 7]);
+        a = oo_imin(a, d[k + 8]);
+        a0 = oo_imax(a0, oo_imin(a, d[k]));
+        a0 = oo_imax(a0, oo_imin(a, d[k + 9]));
+    }
+    int b0 = -a0;
+    for (k = 0; k < 16; k += 2) {
+        int b = oo_imax(d[k + 1], d[k + 2]);
+        b = oo_imax(b, d[k + 3]);
+        b = oo_imax(b, d[k + 4]);
+        b = oo_imax(b, d[k + 5]);
+        if (b >= b0) continue;
+        b = oo_imax(b, d[k + 6]);
+        b = oo_imax(b, d[k + 7]);
+        b = oo_imax(b, d[k + 8]);
+        b0 = oo_imin(b0, oo_imax(b, d[k]));
+        b0 = oo_imin(b0, oo_imax(b, d[k + 9]));
+    }
+    return -b0 - 1;
+}
+
+/* the 9-of-16 contiguous segment test */
+static int oo_is_corner(const uint8_t* ptr, const int* pixel, int t)
+{
+    const int v = ptr[0];
+    int count = 0;
+    for (int k = 0; k < 25; k++) {
+        if (ptr[pixel[k]] < v - t) { if (++count > 8) return 1; }
+        else count = 0;
+    }
+    count = 0;
+    for (int k = 0; k < 25; k++) {
+        if (ptr[pixel[k]] > v + t) { if (++count > 8) return 1; }
+        else count = 0;
+    }
+    return 0;
+}
+
+int oo_fast_score(const uint8_t* img, int stride, int x, int y)
+{
+    int pixel[25];
+    oo_make_offsets(pixel, stride);
+    const uint8_t* p = img + (size_t)y * stride + x;
+    if (!oo_is_corner(p, pixel, 0)) return -1;
+    return oo_corner_score(p, pixel, 0);
+}
+
+/* FAST on the ROI [x0,x1) x [y0,y1) of an image with the given stride; appends keypoints in ROI
+ * coordinates, raster order, exactly as FAST_t<16> with nonmax_suppression emits them. */
+static void oo_fast_roi(const uint8_t* img, int stride, int x0, int y0, int x1, int y1, int threshold,
+                        oo_candvec* out)
+{
+    const int cols = x1 - x0, rows = y1 - y0;
+    if (threshold < 0) threshold = 0;
+    if (threshold > 255) threshold = 255;
+    if (rows < 7 || cols < 7) return;  /* no interior (the reference's loops are then empty) */
+    int pixel[25];
+    oo_make_offsets(pixel, stride);
+    uint8_t* buf = (uint8_t*)calloc((size_t)rows * cols, 1); /* score map, 0 = not a corner */
+    for (int i = 3; i < rows - 3; i++)
+        for (int j = 3; j < cols - 3; j++) {
+            const uint8_t* p = img + (size_t)(y0 + i) * stride + (x0 + j);
+            if (oo_is_corner(p, pixel, threshold))
+                buf[(size_t)i * cols + j] = (uint8_t)oo_corner_score(p, pixel, threshold);
+        }
+    for (int i = 3; i < rows - 3; i++)
+        for (int j = 3; j < cols - 3; j++) {
+            const int s = buf[(size_t)i * cols + j];
+            if (!s) continue; /* not a corner (a score-0 corner can never pass the strict test) */
+            const uint8_t* pr = buf + (size_t)(i - 1) * cols;
+            const uint8_t* cr = buf + (size_t)i * cols;
+            const uint8_t* nr = buf + (size_t)(i + 1) * cols;
+            if (s > pr[j - 1] && s > pr[j] && s > pr[j + 1] && s > cr[j - 1] && s > cr[j + 1] &&
+                s > nr[j - 1] && s > nr[j] && s > nr[j + 1]) {
+                oo_cand c = {(float)j, (float)i, (float)s};
+                cv_push(out, c);
+            }
+        }
+    free(buf);
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Octree: ExtractorNode::DivideNode + ORBextractor::DistributeOctTree,                               */
+/* src/ORBextractor.cc:481-537, 539-763.  std::list replaced by an index-linked list over a bump pool  */
+/* so that the (size, pointer) sort of :684 orders ties by creation order.            */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct {
+    int ulx, uly, urx, ury, blx, bly, brx, bry;
+    oo_candvec keys;
+    int noMore;
+    int prev, next; /* list links, -1 = none */
+} oo_node;
+
+typedef struct {
+    oo_node* v;
+    int n, cap;
+    int head, tail, size;
+} oo_nodelist;
+
+static int nl_new(oo_nodelist* L)
+{
+    if (L->n == L->cap) {
+        L->cap = L->cap ? L->cap * 2 : 64;
+        L->v = (oo_node*)realloc(L->v, sizeof(oo_node) * (size_t)L->cap);
+    }
+    memset(&L->v[L->n], 0, sizeof(oo_node));
+    L->v[L->n].prev = L->v[L->n].next = -1;
+    return L->n++;
+}
+static void nl_push_front(oo_nodelist* L, int id)
+{
+    L->v[id].prev = -1;
+    L->v[id].next = L->head;
+    if (L->head >= 0) L->v[L->head].prev = id; else L->tail = id;
+    L->head = id;
+    L->size++;
+}
+static void nl_push_back(oo_nodelist* L, int id)
+{
+    L->v[id].next = -1;
+    L->v[id].prev = L->tail;
+    if (L->tail >= 0) L->v[L->tail].next = id; else L->head = id;
+    L->tail = id;
+    L->size++;
+}
+static int nl_erase(oo_nodelist* L, int id) /* returns next */
+{
+    oo_node* n = &L->v[id];
+    const int nx = n->next;
+    if (n->prev >= 0) L->v[n->prev].next = n->next; else L->head = n->next;
+    if (n->next >= 0) L->v[n->next].prev = n->prev; else L->tail = n->prev;
+    L->size--;
+    free(n->keys.v);
+    n->keys.v = NULL;
+    return nx;
+}
+
+/* children are created (pool ids) in n1..n4 order, as the four locals of the reference */
+static void oo_divide(oo_nodelist* L, int pid, int ch[4])
+{
+    for (int k = 0; k < 4; k++) ch[k] = nl_new(L);
+    oo_node* p = &L->v[pid];
+    oo_node *n1 = &L->v[ch[0]], *n2 = &L->v[ch[1]], *n3 = &L->v[ch[2]], *n4 = &L->v[ch[3]];
+    const int halfX = (int)ceilf((float)(p->urx - p->ulx) / 2);
+    const int halfY = (int)ceilf((float)(p->bry - p->uly) / 2);
+    n1->ulx = p->ulx; n1->uly = p->uly;
+    n1->urx = p->ulx + halfX; n1->ury = p->uly;
+    n1->blx = p->ulx; n1->bly = p->uly + halfY;
+    n1->brx = p->ulx + halfX; n1->bry = p->uly + halfY;
+    n2->ulx = n1->urx; n2->uly = n1->ury;
+    n2->urx = p->urx; n2->ury = p->ury;
+    n2->blx = n1->brx; n2->bly = n1->bry;
+    n2->brx = p->urx; n2->bry = p->uly + halfY;
+    n3->ulx = n1->blx; n3->uly = n1->bly;
+    n3->urx = n1->brx; n3->ury = n1->bry;
+    n3->blx = p->blx; n3->bly = p->bly;
+    n3->brx = n1->brx; n3->bry = p->bly;
+    n4->ulx = n3->urx; n4->uly = n3->ury;
+    n4->urx = n2->brx; n4->ury = n2->bry;
+    n4->blx = n3->brx; n4->bly = n3->bry;
+    n4->brx = p->brx; n4->bry = p->bry;
+    for (int i = 0; i < p->keys.n; i++) {
+        const oo_cand kp = p->keys.v[i];
+        oo_node* dst;
+        if (kp.x < n1->urx) dst = kp.y < n1->bry ? n1 : n3;
+        else dst = kp.y < n1->bry ? n2 : n4;
+        cv_push(&dst->keys, kp);
+    }
+    for (int k = 0; k < 4; k++)
+        if (L->v[ch[k]].keys.n == 1) L->v[ch[k]].noMore = 1;
+}
+
+typedef struct { int size, id; } oo_sizeptr;
+static int oo_sizeptr_cmp(const void* a, const void* b)
+{
+    const oo_sizeptr *x = (const oo_sizeptr*)a, *y = (const oo_sizeptr*)b;
+    if (x->size != y->size) return x->size < y->size ? -1 : 1;
+    return x->id < y->id ? -1 : (x->id > y->id);
+}
+
+static int oo_distribute(const oo_candvec* in, int minX, int maxX, int minY, int maxY, int N,
+                         oo_cand* out)
+{
+    const int nIni = (int)roundf((float)(maxX - minX) / (maxY - minY));
+    const float hX = (float)(maxX - minX) / nIni;
+    oo_nodelist L;
+    memset(&L, 0, sizeof(L));
+    L.head = L.tail = -1;
+    int* ini = (int*)malloc(sizeof(int) * (size_t)(nIni > 0 ? nIni : 1));
+    for (int i = 0; i < nIni; i++) {
+        const int id = nl_new(&L);
+        oo_node* ni = &L.v[id];
+        ni->ulx = (int)(hX * (float)i); ni->uly = 0;
+        ni->urx = (int)(hX * (float)(i + 1)); ni->ury = 0;
+        ni->blx = ni->ulx; ni->bly = maxY - minY;
+        ni->brx = ni->urx; ni->bry = maxY - minY;
+        nl_push_back(&L, id);
+        ini[i] = id;
+    }
+    for (int i = 0; i < in->n; i++) {
+        const size_t r = (size_t)(in->v[i].x / hX);
+        cv_push(&L.v[ini[r]].keys, in->v[i]);
+    }
+    for (int it = L.head; it >= 0;) {
+        if (L.v[it].keys.n == 1) { L.v[it].noMore = 1; it = L.v[it].next; }
+        else if (L.v[it].keys.n == 0) it = nl_erase(&L, it);
+        else it = L.v[it].next;
+    }
+    free(ini);
+
+    int bFinish = 0;
+    oo_sizeptr* vsp = NULL;
+    int nsp = 0, capsp = 0;
+#define PUSH_SP(sz, idv)                                                                  \
+    do {                                                                                  \
+        if (nsp == capsp) { capsp = capsp ? 2 * capsp : 64;                               \
+            vsp = (oo_sizeptr*)realloc(vsp, sizeof(oo_sizeptr) * (size_t)capsp); }        \
+        vsp[nsp].size = (sz); vsp[nsp].id = (idv); nsp++;                                 \
+    } while (0)
+
+    while (!bFinish) {
+        int prevSize = L.size;
+        int nToExpand = 0;
+        nsp = 0;
+        for (int it = L.head; it >= 0;) {
+            if (L.v[it].noMore) { it = L.v[it].next; continue; }
+            int ch[4];
+            oo_divide(&L, it, ch);
+            for (int k = 0; k < 4; k++) {
+                const int c = ch[k];
+                if (L.v[c].keys.n > 0) {
+                    nl_push_front(&L, c);
+                    if (L.v[c].keys.n > 1) { nToExpand++; PUSH_SP(L.v[c].keys.n, c); }
+                }
+            }
+            it = nl_erase(&L, it);
+        }
+        if (L.size >= N || L.size == prevSize) {
+            bFinish = 1;
+        } else if (L.size + nToExpand * 3 > N) {
+            while (!bFinish) {
+                prevSize = L.size;
+                oo_sizeptr* prev = (oo_sizeptr*)malloc(sizeof(oo_sizeptr) * (size_t)(nsp ? nsp : 1));
+                const int nprev = nsp;
+                memcpy(prev, vsp, sizeof(oo_sizeptr) * (size_t)nsp);
+                nsp = 0;
+                qsort(prev, (size_t)nprev, sizeof(oo_sizeptr), oo_sizeptr_cmp);
+                for (int j = nprev - 1; j >= 0; j--) {
+                    int ch[4];
+                    oo_divide(&L, prev[j].id, ch);
+                    for (int k = 0; k < 4; k++) {
+                        const int c = ch[k];
+                        if (L.v[c].keys.n > 0) {
+                            nl_push_front(&L, c);
+                            if (L.v[c].keys.n > 1) PUSH_SP(L.v[c].keys.n, c);
+                        }
+                    }
+                    nl_erase(&L, prev[j].id);
+                    if (L.size >= N) break;
+                }
+                free(prev);
+                if (L.size >= N || L.size == prevSize) bFinish = 1;
+            }
+        }
+    }
+#undef PUSH_SP
+    free(vsp);
+
+    int nout = 0;
+    for (int it = L.head; it >= 0; it = L.v[it].next) {
+        const oo_candvec* k = &L.v[it].keys;
+        int best = 0;
+        float maxr = k->v[0].resp;
+        for (int i = 1; i < k->n; i++)
+            if (k->v[i].resp > maxr) { best = i; maxr = k->v[i].resp; }
+        out[nout++] = k->v[best];
+    }
+    for (int i = 0; i < L.n; i++) free(L.v[i].keys.v);
+    free(L.v);
+    return nout;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* IC_Angle (src/ORBextractor.cc:77-104) and computeOrbDescriptor (:108-147)                         */
+/* ------------------------------------------------------------------------------------------------ */
+static float oo_ic_angle(const uint8_t* img, int stride, float px, float py, const int* umax)
+{
+    int m01 = 0, m10 = 0;
+    const uint8_t* center = img + (size_t)oo_cvround(py) * stride + oo_cvround(px);
+    for (int u = -OO_HALF_PATCH; u <= OO_HALF_PATCH; ++u) m10 += u * center[u];
+    for (int v = 1; v <= OO_HALF_PATCH; ++v) {
+        int v_sum = 0;
+        const int d = umax[v];
+        for (int u = -d; u <= d; ++u) {
+            const int vp = center[u + v * stride], vm = center[u - v * stride];
+            v_sum += vp - vm;
+            m10 += u * (vp + vm);
+        }
+        m01 += v * v_sum;
+    }
+    return oo_fast_atan2((float)m01, (float)m10);
+}
+
+static void oo_orb_descriptor(float kx, float ky, float angle_deg, const uint8_t* img, int stride,
+                              uint8_t* desc)
+{
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float angle = angle_deg * factorPI;
+    float a, b;
+    oo_sincosf(angle, &b, &a);
+    const uint8_t* center = img + (size_t)oo_cvround(ky) * stride + oo_cvround(kx);
+    const signed char* pat = oo_orb_pattern;
+    for (int i = 0; i < 32; ++i) {
+        int val = 0;
+        for (int k = 0; k < 8; k++, pat += 4) {
+            int t[2];
+            for (int q = 0; q < 2; q++) {
+                const float x = (float)pat[2 * q], y = (float)pat[2 * q + 1];
+                /* GCC -O3 -march=native contraction of the GET_VALUE expressions */
+                const int row = oo_cvround(fmaf(x, b, y * a));
+                const int col = oo_cvround(fmaf(x, a, -(y * b)));
+                t[q] = center[row * stride + col];
+            }
+            val |= (t[0] < t[1]) << k;
+        }
+        desc[i] = (uint8_t)val;
+    }
+}
+
+float oo_fastatan2(float y, float x) { return oo_fast_atan2(y, x); }
+void oo_sincos(float ang, float* s, float* c) { oo_sincosf(ang, s, c); }
+
+/* ------------------------------------------------------------------------------------------------ */
+/* ORBextractor::operator() (src/ORBextractor.cc:1043-1105) with ComputePyramid (:1107-1132) and      */
+/* ComputeKeyPointsOctTree (:765-853).                                                                */
+/* ------------------------------------------------------------------------------------------------ */
+int oo_extract(oo_extractor* e, const uint8_t* img, int cols, int rows, int step, oo_keypoint* kps,
+               uint8_t* desc, int cap)
+{
+    if (!img || cols <= 0 || rows <= 0) return 0; /* _image.empty(): outputs untouched */
+    const int nl = e->nlevels;
+    /* ComputePyramid */
+    for (int l = 0; l < nl; l++) {
+        const int w = oo_cvround((float)cols * e->isf[l]);
+        const int h = oo_cvround((float)rows * e->isf[l]);
+        free(e->lev[l]);
+        e->lev[l] = (uint8_t*)malloc((size_t)w * (size_t)h);
+        e->lw[l] = w;
+        e->lh[l] = h;
+        if (l == 0) {
+            for (int y = 0; y < h; y++) memcpy(e->lev[0] + (size_t)y * w, img + (size_t)y * step, (size_t)w);
+        } else {
+            oo_resize_linear(e->lev[l - 1], e->lw[l - 1], e->lh[l - 1], e->lev[l], w, h);
+        }
+    }
+    /* ComputeKeyPointsOctTree */
+    oo_keypoint* all[OO_MAXLEVELS];
+    int nall[OO_MAXLEVELS];
+    const float W = 30;
+    for (int l = 0; l < nl; l++) {
+        const uint8_t* im = e->lev[l];
+        const int lw = e->lw[l], lh = e->lh[l];
+        const int minBX = OO_EDGE - 3, minBY = minBX;
+        const int maxBX = lw - OO_EDGE + 3, maxBY = lh - OO_EDGE + 3;
+        oo_candvec* cand = &e->cand[l];
+        cand->n = 0;
+        const float width = (float)(maxBX - minBX), height = (float)(maxBY - minBY);
+        const int nCols = (int)(width / W), nRows = (int)(height / W);
+        const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+        oo_candvec cell = {0, 0, 0};
+        for (int i = 0; i < nRows; i++) {
+            const float iniY = (float)(minBY + i * hCell);
+            float maxY = iniY + hCell + 6;
+            if (iniY >= maxBY - 3) continue;
+            if (maxY > maxBY) maxY = (float)maxBY;
+            for (int j = 0; j < nCols; j++) {
+                const float iniX = (float)(minBX + j * wCell);
+                float maxX = iniX + wCell + 6;
+                if (iniX >= maxBX - 6) continue;
+                if (maxX > maxBX) maxX = (float)maxBX;
+                cell.n = 0;
+                oo_fast_roi(im, lw, (int)iniX, (int)iniY, (int)maxX, (int)maxY, e->iniTh, &cell);
+                if (cell.n == 0) oo_fast_roi(im, lw, (int)iniX, (int)iniY, (int)maxX, (int)maxY, e->minTh, &cell);
+                for (int k = 0; k < cell.n; k++) {
+                    oo_cand c = cell.v[k];
+                    c.x += (float)(j * wCell);
+                    c.y += (float)(i * hCell);
+                    cv_push(cand, c);
+                }
+            }
+        }
+        free(cell.v);
+        oo_cand* dist = (oo_cand*)malloc(sizeof(oo_cand) * (size_t)(cand->n + 1));
+        const int nd = oo_distribute(cand, minBX, maxBX, minBY, maxBY, e->nfeat[l], dist);
+        const int scaledPatchSize = (int)(OO_PATCH_SIZE * e->sf[l]);
+        all[l] = (oo_keypoint*)malloc(sizeof(oo_keypoint) * (size_t)(nd + 1));
+        nall[l] = nd;
+        for (int i = 0; i < nd; i++) {
+            oo_keypoint* k = &all[l][i];
+            k->x = dist[i].x + (float)minBX;
+            k->y = dist[i].y + (float)minBY;
+            k->size = (float)scaledPatchSize;
+            k->angle = -1.f;
+            k->response = dist[i].resp;
+            k->octave = l;
+            k->class_id = -1;
+        }
+        free(dist);
+    }
+    for (int l = 0; l < nl; l++)
+        for (int i = 0; i < nall[l]; i++)
+            all[l][i].angle = oo_ic_angle(e->lev[l], e->lw[l], all[l][i].x, all[l][i].y, e->umax);
+
+    int total = 0;
+    for (int l = 0; l < nl; l++) total += nall[l];
+    if (total > cap) {
+        for (int l = 0; l < nl; l++) free(all[l]);
+        return -1;
+    }
+    int off = 0;
+    for (int l = 0; l < nl; l++) {
+        if (nall[l] == 0) { free(all[l]); continue; }
+        uint8_t* blurred = (uint8_t*)malloc((size_t)e->lw[l] * (size_t)e->lh[l]);
+        oo_gaussian7(e->lev[l], e->lw[l], e->lh[l], blurred);
+        for (int i = 0; i < nall[l]; i++)
+            oo_orb_descriptor(all[l][i].x, all[l][i].y, all[l][i].angle, blurred, e->lw[l],
+                              desc + (size_t)(off + i) * 32);
+        free(blurred);
+        if (l != 0) {
+            const float s = e->sf[l];
+            for (int i = 0; i < nall[l]; i++) { all[l][i].x *= s; all[l][i].y *= s; }
+        }
+        memcpy(kps + off, all[l], sizeof(oo_keypoint) * (size_t)nall[l]);
+        off += nall[l];
+        free(all[l]);
+    }
+    return total;
+}
+
+int oo_level_size(const oo_extractor* e, int level, int* cols, int* rows)
+{
+    if (level < 0 || level >= e->nlevels) return -1;
+    *cols = e->lw[level];
+    *rows = e->lh[level];
+    return 0;
+}
+const uint8_t* oo_level_image(const oo_extractor* e, int level) { return e->lev[level]; }
+int oo_level_candidates(const oo_extractor* e, int level, float* xy, float* resp, int cap)
+{
+    const oo_candvec* c = &e->cand[level];
+    for (int i = 0; i < c->n && i < cap; i++) {
+        xy[2 * i] = c->v[i].x;
+        xy[2 * i + 1] = c->v[i].y;
+        resp[i] = c->v[i].resp;
+    }
+    return c->n;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1647-1663)                                      */
+/* ------------------------------------------------------------------------------------------------ */
+int oo_descriptor_distance(const uint8_t* a, const uint8_t* b)
+{
+    int dist = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t x, y;
+        memcpy(&x, a + 4 * i, 4);
+        memcpy(&y, b + 4 * i, 4);
+        uint32_t v = x ^ y;
+        v = v - ((v >> 1) & 0x55555555);
+        v = (v & 0x33333333) + ((v >> 2) & 0x33333333);
+        dist += (int)((((v + (v >> 4)) & 0xF0F0F0F) * 0x1010101) >> 24);
+    }
+    return dist;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Frame grid: ComputeImageBounds (no distortion, src/Frame.cc:457-463), grid scales (:212-213),     */
+/* AssignFeaturesToGrid (:230-245), PosInGrid (:382-392), GetFeaturesInArea (:327-380)               */
+/* ------------------------------------------------------------------------------------------------ */
+void oo_grid_params(int cols, int rows, float* minX, float* minY, float* maxX, float* maxY,
+                    float* invW, float* invH)
+{
+    *minX = 0.0f;
+    *maxX = (float)cols;
+    *minY = 0.0f;
+    *maxY = (float)rows;
+    *invW = (float)OO_GRID_COLS / (*maxX - *minX);
+    *invH = (float)OO_GRID_ROWS / (*maxY - *minY);
+}
+
+static int oo_pos_in_grid(const oo_frame* f, const oo_keypoint* kp, int* px, int* py)
+{
+    *px = (int)roundf((kp->x - f->minX) * f->gridInvW);
+    *py = (int)roundf((kp->y - f->minY) * f->gridInvH);
+    if (*px < 0 || *px >= OO_GRID_COLS || *py < 0 || *py >= OO_GRID_ROWS) return 0;
+    return 1;
+}
+
+void oo_grid_build(oo_frame* f)
+{
+    const int nc = OO_GRID_COLS * OO_GRID_ROWS;
+    int* cnt = (int*)calloc((size_t)nc + 1, sizeof(int));
+    for (int i = 0; i < f->n; i++) {
+        int px, py;
+        if (oo_pos_in_grid(f, &f->kps[i], &px, &py)) cnt[px * OO_GRID_ROWS + py]++;
+    }
+    f->cell_start[0] = 0;
+    for (int c = 0; c < nc; c++) f->cell_start[c + 1] = f->cell_start[c] + cnt[c];
+    memset(cnt, 0, sizeof(int) * (size_t)nc);
+    for (int i = 0; i < f->n; i++) {
+        int px, py;
+        if (oo_pos_in_grid(f, &f->kps[i], &px, &py)) {
+            const int c = px * OO_GRID_ROWS + py;
+            f->cell_items[f->cell_start[c] + cnt[c]++] = i;
+        }
+    }
+    free(cnt);
+}
+
+int oo_features_in_area(const oo_frame* f, float x, float y, float r, int minLevel, int maxLevel,
+                        int* out)
+{
+    int n = 0;
+    const int nMinCellX = oo_imax(0, (int)floorf((x - f->minX - r) * f->gridInvW));
+    if (nMinCellX >= OO_GRID_COLS) return 0;
+    const int nMaxCellX = oo_imin(OO_GRID_COLS - 1, (int)ceilf((x - f->minX + r) * f->gridInvW));
+    if (nMaxCellX < 0) return 0;
+    const int nMinCellY = oo_imax(0, (int)floorf((y - f->minY - r) * f->gridInvH));
+    if (nMinCellY >= OO_GRID_ROWS) return 0;
+    const int nMaxCellY = oo_imin(OO_GRID_ROWS - 1, (int)ceilf((y - f->minY + r) * f->gridInvH));
+    if (nMaxCellY < 0) return 0;
+    const int bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+            const int c = ix * OO_GRID_ROWS + iy;
+            for (int j = f->cell_start[c]; j < f->cell_start[c + 1]; j++) {
+                const int idx = f->cell_items[j];
+                const oo_keypoint* kp = &f->kps[idx];
+                if (bCheckLevels) {
+                    if (kp->octave < minLevel) continue;
+                    if (maxLevel >= 0 && kp->octave > maxLevel) continue;
+                }
+                const float distx = kp->x - x, disty = kp->y - y;
+                if (fabsf(distx) < r && fabsf(disty) < r) out[n++] = idx;
+            }
+        }
+    return n;
+}
+
+/* ORBmatcher::ComputeThreeMaxima (src/ORBmatcher.cc:1601-1642) */
+static void oo_three_maxima(const int* histo_len, int L, int* ind1, int* ind2, int* ind3)
+{
+    int max1 = 0, max2 = 0, max3 = 0;
+    for (int i = 0; i < L; i++) {
+        const int s = histo_len[i];
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            *ind3 = *ind2; *ind2 = *ind1; *ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            *ind3 = *ind2; *ind2 = i;
+        } else if (s > max3) {
+            max3 = s;
+            *ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) { *ind2 = -1; *ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { *ind3 = -1; }
+}
+
+#define OO_TH_HIGH 100
+#define OO_TH_LOW 50
+#define OO_HISTO 30
+
+/* ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:405-520) */
+int oo_search_for_initialization(const oo_frame* F1, const oo_frame* F2, float nnratio, int checkOri,
+                                 float* prev_xy, int* matches12, int windowSize)
+{
+    int nmatches = 0;
+    for (int i = 0; i < F1->n; i++) matches12[i] = -1;
+    int* hist = (int*)malloc(sizeof(int) * OO_HISTO * (size_t)(F1->n + 1));
+    int hlen[OO_HISTO] = {0};
+    const float factor = 1.0f / OO_HISTO;
+    int* vMatchedDistance = (int*)malloc(sizeof(int) * (size_t)(F2->n + 1));
+    int* vnMatches21 = (int*)malloc(sizeof(int) * (size_t)(F2->n + 1));
+    int* idx = (int*)malloc(sizeof(int) * (size_t)(F2->n + 1));
+    for (int i = 0; i < F2->n; i++) { vMatchedDistance[i] = INT_MAX; vnMatches21[i] = -1; }
+
+    for (int i1 = 0; i1 < F1->n; i1++) {
+        const oo_keypoint kp1 = F1->kps[i1];
+        const int level1 = kp1.octave;
+        if (level1 > 0) continue;
+        const int nc = oo_features_in_area(F2, prev_xy[2 * i1], prev_xy[2 * i1 + 1], (float)windowSize,
+                                           level1, level1, idx);
+        if (nc == 0) continue;
+        const uint8_t* d1 = F1->desc + (size_t)i1 * 32;
+        int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+        for (int c = 0; c < nc; c++) {
+            const int i2 = idx[c];
+            const int dist = oo_descriptor_distance(d1, F2->desc + (size_t)i2 * 32);
+            if (vMatchedDistance[i2] <= dist) continue;
+            if (dist < bestDist) { bestDist2 = bestDist; bestDist = dist; bestIdx2 = i2; }
+            else if (dist < bestDist2) bestDist2 = dist;
+        }
+        if (bestDist <= OO_TH_LOW) {
+            if (bestDist < (float)bestDist2 * nnratio) {
+                if (vnMatches21[bestIdx2] >= 0) {
+                    matches12[vnMatches21[bestIdx2]] = -1;
+                    nmatches--;
+                }
+                matches12[i1] = bestIdx2;
+                vnMatches21[bestIdx2] = i1;
+                vMatchedDistance[bestIdx2] = bestDist;
+                nmatches++;
+                if (checkOri) {
+                    float rot = F1->kps[i1].angle - F2->kps[bestIdx2].angle;
+                    if (rot < 0.0) rot += 360.0f;
+                    int bin = (int)roundf(rot * factor);
+                    if (bin == OO_HISTO) bin = 0;
+                    assert(bin >= 0 && bin < OO_HISTO);
+                    hist[bin * (F1->n + 1) + hlen[bin]++] = i1;
+                }
+            }
+        }
+    }
+    if (checkOri) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        oo_three_maxima(hlen, OO_HISTO, &ind1, &ind2, &ind3);
+        for (int i = 0; i < OO_HISTO; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int j = 0; j < hlen[i]; j++) {
+                const int idx1 = hist[i * (F1->n + 1) + j];
+                if (matches12[idx1] >= 0) { matches12[idx1] = -1; nmatches--; }
+            }
+        }
+    }
+    for (int i1 = 0; i1 < F1->n; i1++)
+        if (matches12[i1] >= 0) {
+            prev_xy[2 * i1] = F2->kps[matches12[i1]].x;
+            prev_xy[2 * i1 + 1] = F2->kps[matches12[i1]].y;
+        }
+    free(hist);
+    free(vMatchedDistance);
+    free(vnMatches21);
+    free(idx);
+    return nmatches;
+}
+
+/* ORBmatcher::RadiusByViewingCos (src/ORBmatcher.cc:131-137) */
+static float oo_radius_by_viewing_cos(float viewCos) { return viewCos > 0.998 ? 2.5f : 4.0f; }
+
+/* ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th) (src/ORBmatcher.cc:45-129) */
+int oo_search_by_projection(const oo_frame* F, const oo_mappoints* mp, float nnratio, float th,
+                            int* owner, int* owner_obs)
+{
+    int nmatches = 0;
+    const int bFactor = th != 1.0;
+    int* idx = (int*)malloc(sizeof(int) * (size_t)(F->n + 1));
+    for (int m = 0; m < mp->m; m++) {
+        if (!mp->track_in_view[m]) continue;
+        if (mp->is_bad[m]) continue;
+        const int nPredictedLevel = mp->level[m];
+        float r = oo_radius_by_viewing_cos(mp->view_cos[m]);
+        if (bFactor) r *= th;
+        const int nc = oo_features_in_area(F, mp->proj_x[m], mp->proj_y[m],
+                                           r * F->scale_factors[nPredictedLevel], nPredictedLevel - 1,
+                                           nPredictedLevel, idx);
+        if (nc == 0) continue;
+        const uint8_t* MPdescriptor = mp->desc + (size_t)m * 32;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (int c = 0; c < nc; c++) {
+            const int i = idx[c];
+            if (owner[i] >= 0 && owner_obs[i]) continue;
+            if (F->uright && F->uright[i] > 0) {
+                const float er = fabsf(mp->proj_xr[m] - F->uright[i]);
+                if (er > r * F->scale_factors[nPredictedLevel]) continue;
+            }
+            const int dist = oo_descriptor_distance(MPdescriptor, F->desc + (size_t)i * 32);
+            if (dist < bestDist) {
+                bestDist2 = bestDist; bestDist = dist;
+                bestLevel2 = bestLevel; bestLevel = F->kps[i].octave;
+                bestIdx = i;
+            } else if (dist < bestDist2) {
+                bestLevel2 = F->kps[i].octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= OO_TH_HIGH) {
+            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+            owner[bestIdx] = m;
+            owner_obs[bestIdx] = mp->n_obs[m] > 0;
+            nmatches++;
+        }
+    }
+    free(idx);
+    return nmatches;
+}

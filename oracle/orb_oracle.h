@@ -1,0 +1,112 @@
+/*
+ * oracle/orb_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, single-threaded restatement of the reference's ORB extraction + matching hot path
+ * (yxqc/ORBSLAM2_with_quadrics src/ORBextractor.cc, src/ORBmatcher.cc, src/Frame.cc).  It is the
+ * checker for the HIP product (orbslam2_with_quadrics_amd/csrc) and the CPU baseline ("port") in
+ * bench.py.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ *
+ * PARITY STATUS: parity with the reference *binary* is UNPINNED -- the reference needs OpenCV 3.x,
+ * Eigen3 and Pangolin, none of which exist in this image, and the reference ships no tests or golden
+ * vectors.  Individual pieces are pinned: glibc sincosf (exhaustive, tools/verify_sincosf.c), GCC's FMA
+ * contraction of the rBRIEF rotation (tools/probe_contraction.sh), the FAST score against its
+ * definition (tests/test_oracle_pins.py), the ORB sampling pattern against the reference source text.
+ * The OpenCV primitives follow the semantics written down in DESIGN.md §3 (scalar resize, 257-sum
+ * Gaussian kernel, scalar fastAtan2).
+ */
+#ifndef ORB_ORACLE_H
+#define ORB_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same 28-byte layout as cv::KeyPoint {Point2f pt; float size, angle, response; int octave, class_id;} */
+typedef struct {
+    float x, y, size, angle, response;
+    int octave, class_id;
+} oo_keypoint;
+
+typedef struct oo_extractor oo_extractor;
+
+oo_extractor* oo_create(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST);
+void oo_destroy(oo_extractor* e);
+int oo_nlevels(const oo_extractor* e);
+void oo_scale_tables(const oo_extractor* e, float* scale, float* inv_scale, float* sigma2,
+                     float* inv_sigma2, int* features_per_level, int* umax16);
+
+/* ORBextractor::operator() (src/ORBextractor.cc:1043-1105).  Writes at most cap keypoints / rows.
+ * Returns the number of keypoints, or -1 if cap is too small (nothing is written in that case). */
+int oo_extract(oo_extractor* e, const uint8_t* img, int cols, int rows, int step, oo_keypoint* kps,
+               uint8_t* desc, int cap);
+
+/* Debug/introspection of the last oo_extract call. */
+int oo_level_size(const oo_extractor* e, int level, int* cols, int* rows);
+const uint8_t* oo_level_image(const oo_extractor* e, int level);       /* unpadded, stride = cols */
+/* FAST candidates of a level in the reference's vToDistributeKeys order (x, y relative to minBorder,
+ * response).  Returns the count; writes at most cap. */
+int oo_level_candidates(const oo_extractor* e, int level, float* xy, float* resp, int cap);
+
+/* Single-primitive entry points (used by tests to pin pieces). */
+void oo_resize_linear(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh);
+void oo_gaussian7(const uint8_t* src, int w, int h, uint8_t* dst);
+int oo_fast_score(const uint8_t* img, int stride, int x, int y);      /* M-1 or -1 (see DESIGN) */
+float oo_fastatan2(float y, float x);
+void oo_sincos(float ang, float* s, float* c);
+int oo_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* ---------------------------------------------------------------------------------------------
+ * Frame grid (src/Frame.cc:230-245, 327-392) and matchers (src/ORBmatcher.cc).
+ * A "frame view" is a plain SoA snapshot of what the reference reads from Frame.
+ * --------------------------------------------------------------------------------------------- */
+typedef struct {
+    int n;                      /* N keypoints */
+    const oo_keypoint* kps;     /* mvKeysUn */
+    const uint8_t* desc;        /* mDescriptors, n x 32 */
+    const float* uright;        /* mvuRight (may be NULL => all -1) */
+    float minX, minY, maxX, maxY;         /* mnMinX.. (static in reference) */
+    float gridInvW, gridInvH;             /* mfGridElementWidthInv/HeightInv */
+    const float* scale_factors;           /* mvScaleFactors */
+    int nlevels;
+    /* grid CSR (64 x 48 cells, cell index = ix*48+iy), filled by oo_grid_build */
+    int* cell_start;            /* 64*48+1 */
+    int* cell_items;            /* n */
+} oo_frame;
+
+void oo_grid_params(int cols, int rows, float* minX, float* minY, float* maxX, float* maxY,
+                    float* invW, float* invH);
+void oo_grid_build(oo_frame* f);
+/* Frame::GetFeaturesInArea; returns count written to out (cap >= n is always enough). */
+int oo_features_in_area(const oo_frame* f, float x, float y, float r, int minLevel, int maxLevel,
+                        int* out);
+
+/* ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:405-520).  prev_xy: 2*n1 floats (in/out),
+ * matches12: n1 ints (out).  Returns nmatches. */
+int oo_search_for_initialization(const oo_frame* f1, const oo_frame* f2, float nnratio,
+                                 int checkOri, float* prev_xy, int* matches12, int windowSize);
+
+/* ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th) (src/ORBmatcher.cc:45-129).
+ * Map points as SoA.  owner (n ints, in/out): map point index owning each keypoint, or -1;
+ * owner_obs (n ints, in/out): Observations()>0 flag of the current owner.  Returns nmatches. */
+typedef struct {
+    int m;
+    const uint8_t* track_in_view;  /* mbTrackInView */
+    const uint8_t* is_bad;         /* isBad() */
+    const int* level;              /* mnTrackScaleLevel */
+    const float* view_cos;         /* mTrackViewCos */
+    const float* proj_x;           /* mTrackProjX */
+    const float* proj_y;           /* mTrackProjY */
+    const float* proj_xr;          /* mTrackProjXR */
+    const int* n_obs;              /* Observations() */
+    const uint8_t* desc;           /* GetDescriptor(), m x 32 */
+} oo_mappoints;
+
+int oo_search_by_projection(const oo_frame* f, const oo_mappoints* mp, float nnratio, float th,
+                            int* owner, int* owner_obs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,120 @@
+"""ctypes loader of the in-tree gfx950 library (liborbgpu.so) -- the C ABI of include/orbgpu.h.
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU is visible, calls fail
+loudly (RuntimeError).  torch is imported first when available so that torch and this library share
+one HIP runtime in the process (both link libamdhip64.so.7).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liborbgpu.so")
+
+# Every symbol include/orbgpu.h declares (checked by tests/test_lib_abi.py).
+EXPORTS = [
+    "orbgpu_create", "orbgpu_destroy", "orbgpu_get_levels", "orbgpu_get_scale_factor",
+    "orbgpu_get_scale_factors", "orbgpu_get_inverse_scale_factors", "orbgpu_get_scale_sigma_squares",
+    "orbgpu_get_inverse_scale_sigma_squares", "orbgpu_get_features_per_level", "orbgpu_extract",
+    "orbgpu_max_keypoints", "orbgpu_get_level", "orbgpu_extract_batch_device", "orbgpu_batch_outputs",
+    "orbgpu_batch_download", "orbgpu_grid_geom_for_image", "orbgpu_descriptor_distance",
+    "orbgpu_search_for_initialization", "orbgpu_search_for_initialization_batch",
+    "orbgpu_search_by_projection", "orbgpu_stream", "orbgpu_synchronize", "orbgpu_set_stage_timing",
+    "orbgpu_stage_times", "orbgpu_last_error", "orbgpu_debug_candidates", "orbgpu_debug_octree",
+    "orbgpu_device_alloc", "orbgpu_device_free", "orbgpu_memcpy_h2d", "orbgpu_memcpy_d2h",
+    "orbgpu_memset_d",
+]
+
+OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
+
+
+class KeyPointC(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
+
+
+class GridGeom(C.Structure):
+    _fields_ = [("minX", C.c_float), ("minY", C.c_float), ("maxX", C.c_float), ("maxY", C.c_float),
+                ("invW", C.c_float), ("invH", C.c_float)]
+
+
+class FrameView(C.Structure):
+    _fields_ = [("n", C.c_int), ("kps", C.c_void_p), ("desc", C.c_void_p), ("uright", C.c_void_p),
+                ("grid", GridGeom), ("scale_factors", C.c_void_p), ("nlevels", C.c_int)]
+
+
+class MapPointsView(C.Structure):
+    _fields_ = [("m", C.c_int), ("track_in_view", C.c_void_p), ("is_bad", C.c_void_p),
+                ("level", C.c_void_p), ("view_cos", C.c_void_p), ("proj_x", C.c_void_p),
+                ("proj_y", C.c_void_p), ("proj_xr", C.c_void_p), ("n_obs", C.c_void_p),
+                ("desc", C.c_void_p)]
+
+
+_lib = None
+
+
+def _declare(L):
+    vp, i32, f32, sz = C.c_void_p, C.c_int, C.c_float, C.c_size_t
+    L.orbgpu_create.restype = vp
+    L.orbgpu_create.argtypes = [i32, i32, f32, i32, i32, i32]
+    L.orbgpu_destroy.argtypes = [vp]
+    L.orbgpu_get_levels.argtypes = [vp]
+    L.orbgpu_get_scale_factor.restype = f32
+    L.orbgpu_get_scale_factor.argtypes = [vp]
+    for n in ("orbgpu_get_scale_factors", "orbgpu_get_inverse_scale_factors",
+              "orbgpu_get_scale_sigma_squares", "orbgpu_get_inverse_scale_sigma_squares",
+              "orbgpu_get_features_per_level"):
+        getattr(L, n).argtypes = [vp, vp]
+    L.orbgpu_extract.argtypes = [vp, vp, i32, i32, sz, vp, vp, i32, C.POINTER(i32)]
+    L.orbgpu_max_keypoints.argtypes = [vp]
+    L.orbgpu_get_level.argtypes = [vp, i32, vp, sz, C.POINTER(i32), C.POINTER(i32)]
+    L.orbgpu_extract_batch_device.argtypes = [vp, vp, i32, i32, i32, sz, sz]
+    L.orbgpu_batch_outputs.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(i32)]
+    L.orbgpu_batch_download.argtypes = [vp, i32, vp, vp, i32, C.POINTER(i32)]
+    L.orbgpu_grid_geom_for_image.argtypes = [i32, i32, C.POINTER(GridGeom)]
+    L.orbgpu_descriptor_distance.argtypes = [vp, vp]
+    L.orbgpu_search_for_initialization.argtypes = [vp, C.POINTER(FrameView), C.POINTER(FrameView), f32,
+                                                   i32, vp, vp, i32, C.POINTER(i32)]
+    L.orbgpu_search_for_initialization_batch.argtypes = [vp, i32, vp, GridGeom, f32, i32, i32, vp, vp, vp]
+    L.orbgpu_search_by_projection.argtypes = [vp, C.POINTER(FrameView), C.POINTER(MapPointsView), f32,
+                                              f32, vp, vp, C.POINTER(i32)]
+    L.orbgpu_stream.restype = vp
+    L.orbgpu_stream.argtypes = [vp]
+    L.orbgpu_synchronize.argtypes = [vp]
+    L.orbgpu_set_stage_timing.argtypes = [vp, i32]
+    L.orbgpu_stage_times.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(f32), i32]
+    L.orbgpu_last_error.restype = C.c_char_p
+    L.orbgpu_last_error.argtypes = [vp]
+    L.orbgpu_debug_candidates.argtypes = [vp, i32, i32, vp, i32]
+    L.orbgpu_debug_octree.argtypes = [vp, i32, i32, vp, vp, i32]
+    L.orbgpu_device_alloc.restype = vp
+    L.orbgpu_device_alloc.argtypes = [vp, sz]
+    L.orbgpu_device_free.argtypes = [vp, vp]
+    L.orbgpu_memcpy_h2d.argtypes = [vp, vp, vp, sz]
+    L.orbgpu_memcpy_d2h.argtypes = [vp, vp, vp, sz]
+    L.orbgpu_memset_d.argtypes = [vp, vp, i32, sz]
+
+
+def lib(load_torch_first: bool = True):
+    """Load liborbgpu.so (raises RuntimeError when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"HIP library missing: {LIB_PATH} (run __graft_entry__.build() or "
+                               "python -m orbslam2_with_quadrics_amd.build_ext)")
+        if load_torch_first:
+            try:
+                import torch  # noqa: F401  (one HIP runtime per process)
+            except Exception:
+                pass
+        L = C.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def check(ctx, rc: int, what: str):
+    if rc != OK:
+        msg = lib().orbgpu_last_error(ctx) if ctx else b""
+        raise RuntimeError(f"{what} failed with status {rc}: {msg.decode(errors='replace')}")

@@ -1,0 +1,65 @@
+"""Build the gfx950 HIP library in-tree: orbslam2_with_quadrics_amd/liborbgpu.so.
+
+hipcc cross-compiles for gfx950 without a GPU.  -ffp-contract=off keeps every float/double rounding
+step of the reference explicit (the fused multiply-adds the reference build performs are written as
+fmaf/fma in the source).  The .so is git-ignored but travels to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "liborbgpu.so")
+SOURCES = ["orb_extract.hip", "orb_match.hip", "orbgpu_capi.cpp"]
+HEADERS = ["orbgpu_internal.h", "orbgpu_launch.h", "orb_math_dev.h", "orb_pattern.inc",
+           os.path.join("..", "..", "include", "orbgpu.h")]
+ARCH = os.environ.get("ORBGPU_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
+         "-Wall", "-Wno-unused-result", "-Wno-comment"]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm is required to build the HIP library)")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    for f in SOURCES + HEADERS + [os.path.basename(__file__)]:
+        p = os.path.join(CSRC, f) if f != os.path.basename(__file__) else os.path.abspath(__file__)
+        if os.path.exists(p) and os.path.getmtime(p) > t:
+            return True
+    return False
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    objs = []
+    cc = hipcc()
+    tmp = os.path.join(HERE, "build")
+    os.makedirs(tmp, exist_ok=True)
+    for src in SOURCES:
+        obj = os.path.join(tmp, src + ".o")
+        cmd = [cc, f"--offload-arch={ARCH}", *FLAGS, "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        objs.append(obj)
+    out_tmp = LIB + ".tmp"
+    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out_tmp, *objs]
+    subprocess.check_call(cmd)
+    os.replace(out_tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

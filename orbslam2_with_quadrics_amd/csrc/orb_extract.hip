@@ -1,0 +1,830 @@
+// orb_extract.hip -- gfx950 kernels of ORBextractor::operator() (src/ORBextractor.cc:1043-1105).
+//
+//   k1 og_resize_kernel    : one chained pyramid level (cv::resize INTER_LINEAR 8U, scalar form)
+//   k2 og_fast_cells_kernel: one 64-lane wave per FAST cell: ROI -> LDS, FAST-9 score, cell-local
+//                            3x3 NMS, the reference's 20 -> 7 threshold fallback, ballot/mbcnt
+//                            compaction into the (frame, level) candidate slots
+//   k3 og_octree_kernel    : one 1024-thread workgroup per (frame, level): the DistributeOctTree list
+//                            simulation as data-parallel rounds (LDS node table, block scans)
+//   k4 og_describe_kernel  : one wave per keypoint: 43x43 raw patch -> LDS, IC angle, fused 7x7
+//                            Gaussian to a 37x37 patch, rBRIEF 256 tests, ballot-packed 32 B
+//   k5 og_grid_kernel      : Frame::AssignFeaturesToGrid, CSR grid per frame
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "orb_math_dev.h"
+#include "orbgpu_internal.h"
+#include "orbgpu_launch.h"
+
+typedef unsigned long long u64;
+
+#include "orb_pattern.inc"  // static const signed char oo_orb_pattern[1024]
+__constant__ signed char og_pattern[1024];
+static bool g_pattern_uploaded_dev[64] = {false};
+
+// ------------------------------------------------------------------------------------------------
+// k1: pyramid level l from level l-1 (src/ORBextractor.cc:1120)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void og_resize_kernel(const uint8_t* __restrict__ src, long long src_pitch,
+                                                        long long src_fstride, uint8_t* __restrict__ dst,
+                                                        long long dst_pitch, long long dst_fstride, int dw,
+                                                        int dh, const int4* __restrict__ xtab,
+                                                        const int4* __restrict__ ytab, int xmax)
+{
+    const int f = blockIdx.z;
+    const int dy = blockIdx.y;
+    const int dx0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (dy >= dh || dx0 >= dw) return;
+    const int4 yt = ytab[dy];  // {row0 (clipped), row1 (clipped), beta0, beta1}
+    const uint8_t* S0 = src + (long long)f * src_fstride + (long long)yt.x * src_pitch;
+    const uint8_t* S1 = src + (long long)f * src_fstride + (long long)yt.y * src_pitch;
+    uint8_t* D = dst + (long long)f * dst_fstride + (long long)dy * dst_pitch;
+    uint32_t packed = 0;
+    const int n = min(4, dw - dx0);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (k < n) {
+            const int dx = dx0 + k;
+            const int4 xt = xtab[dx];  // {sx, alpha0, alpha1, -}
+            int d0, d1;
+            if (dx < xmax) {
+                d0 = S0[xt.x] * xt.y + S0[xt.x + 1] * xt.z;
+                d1 = S1[xt.x] * xt.y + S1[xt.x + 1] * xt.z;
+            } else {
+                d0 = S0[xt.x] * 2048;
+                d1 = S1[xt.x] * 2048;
+            }
+            int v = (yt.z * d0 + yt.w * d1 + (1 << 21)) >> 22;
+            v = v < 0 ? 0 : (v > 255 ? 255 : v);
+            packed |= (uint32_t)v << (8 * k);
+        }
+    }
+    if (n == 4 && ((((uintptr_t)(D + dx0)) & 3) == 0)) {
+        *(uint32_t*)(D + dx0) = packed;
+    } else {
+        for (int k = 0; k < n; k++) D[dx0 + k] = (uint8_t)(packed >> (8 * k));
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k2: FAST cells (src/ORBextractor.cc:789-829 + cv::FAST TYPE_9_16 with nonmax suppression)
+// ------------------------------------------------------------------------------------------------
+// M(p) = max over the 16 contiguous 9-arcs and both polarities of min |I(p) - I(arc)|; the pixel is a
+// FAST corner at threshold t iff M > t and then cornerScore<16> == M - 1.
+__device__ __forceinline__ int og_fast_M(const uint8_t* p, int st)
+{
+    const int v = p[0];
+    int d[16];
+    d[0] = v - p[3 * st];
+    d[1] = v - p[1 + 3 * st];
+    d[2] = v - p[2 + 2 * st];
+    d[3] = v - p[3 + 1 * st];
+    d[4] = v - p[3];
+    d[5] = v - p[3 - 1 * st];
+    d[6] = v - p[2 - 2 * st];
+    d[7] = v - p[1 - 3 * st];
+    d[8] = v - p[-3 * st];
+    d[9] = v - p[-1 - 3 * st];
+    d[10] = v - p[-2 - 2 * st];
+    d[11] = v - p[-3 - 1 * st];
+    d[12] = v - p[-3];
+    d[13] = v - p[-3 + 1 * st];
+    d[14] = v - p[-2 + 2 * st];
+    d[15] = v - p[-1 + 3 * st];
+    int mn2[16], mx2[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn2[k] = min(d[k], d[(k + 1) & 15]);
+        mx2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+    int mn4[16], mx4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+    }
+    int apos = -1024, bneg = 1024;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int mn8 = min(mn4[k], mn4[(k + 4) & 15]);
+        const int mx8 = max(mx4[k], mx4[(k + 4) & 15]);
+        apos = max(apos, min(mn8, d[(k + 8) & 15]));
+        bneg = min(bneg, max(mx8, d[(k + 8) & 15]));
+    }
+    const int M = max(apos, -bneg);
+    return M > 0 ? M : 0;
+}
+
+#define OG_ROI_MAX (OG_MAX_CELL_W + 6)
+
+__device__ __forceinline__ bool og_nms_keep(const uint8_t* Ms, int dw, int dh, int i, int j, int t)
+{
+    const int m = Ms[i * dw + j];
+    if (m <= t) return false;
+    const int s = m - 1;
+#pragma unroll
+    for (int di = -1; di <= 1; di++)
+#pragma unroll
+        for (int dj = -1; dj <= 1; dj++) {
+            if (di == 0 && dj == 0) continue;
+            const int ii = i + di, jj = j + dj;
+            int nb = 0;
+            if (ii >= 0 && ii < dh && jj >= 0 && jj < dw) {
+                const int mn = Ms[ii * dw + jj];
+                nb = mn > t ? mn - 1 : 0;
+            }
+            if (!(s > nb)) return false;
+        }
+    return true;
+}
+
+__global__ __launch_bounds__(64) void og_fast_cells_kernel(OgPlan P, const OgCell* __restrict__ cells,
+                                                           const uint8_t* __restrict__ img0, long long pitch0,
+                                                           long long fstride0, const uint8_t* __restrict__ pyr,
+                                                           u64* __restrict__ cand, int* __restrict__ cand_count,
+                                                           int* __restrict__ status)
+{
+    __shared__ uint8_t roi[OG_ROI_MAX * OG_ROI_MAX];
+    __shared__ uint8_t Ms[OG_MAX_CELL_W * OG_MAX_CELL_W];
+    const int f = blockIdx.y;
+    const OgCell cd = cells[blockIdx.x];
+    const int l = cd.level;
+    const OgLevel& L = P.lv[l];
+    const int lane = threadIdx.x;
+    const uint8_t* img;
+    long long pitch;
+    if (l == 0) {
+        img = img0 + (long long)f * fstride0;
+        pitch = pitch0;
+    } else {
+        img = pyr + (long long)f * P.pyr_per_frame + L.pyr_off;
+        pitch = L.pitch;
+    }
+    const int rw = cd.x1 - cd.x0, rh = cd.y1 - cd.y0;
+    const int dw = rw - 6, dh = rh - 6;
+    if (dw <= 0 || dh <= 0) return;
+    for (int r = 0; r < rh; r++) {
+        const uint8_t* srow = img + (long long)(cd.y0 + r) * pitch + cd.x0;
+        for (int c = lane; c < rw; c += 64) roi[r * rw + c] = srow[c];
+    }
+    __syncthreads();
+    const int npx = dw * dh;
+    for (int idx = lane; idx < npx; idx += 64) {
+        const int i = idx / dw, j = idx - (idx / dw) * dw;
+        Ms[idx] = (uint8_t)og_fast_M(&roi[(i + 3) * rw + (j + 3)], rw);
+    }
+    __syncthreads();
+    int t = min(max(P.iniTh, 0), 255);
+    int cnt = 0;
+    for (int idx = lane; idx - lane < npx; idx += 64) {
+        bool keep = false;
+        if (idx < npx) {
+            const int i = idx / dw, j = idx - (idx / dw) * dw;
+            keep = og_nms_keep(Ms, dw, dh, i, j, t);
+        }
+        cnt += __popcll(__ballot(keep));
+    }
+    if (cnt == 0) {
+        t = min(max(P.minTh, 0), 255);
+        for (int idx = lane; idx - lane < npx; idx += 64) {
+            bool keep = false;
+            if (idx < npx) {
+                const int i = idx / dw, j = idx - (idx / dw) * dw;
+                keep = og_nms_keep(Ms, dw, dh, i, j, t);
+            }
+            cnt += __popcll(__ballot(keep));
+        }
+    }
+    if (cnt == 0) return;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(&cand_count[f * P.nlevels + l], cnt);
+    base = __shfl(base, 0);
+    if (base + cnt > L.cand_cap) {  // cannot happen (cap is the exact NMS bound); reported if it does
+        if (lane == 0) atomicOr(status, 1);
+        return;
+    }
+    u64* out = cand + (long long)f * P.cand_per_frame + L.cand_off + base;
+    int run = 0;
+    // ROI origin relative to minBorder: x_rel = (x0 - minB) + j + 3
+    const int ox = cd.x0 - L.minB + 3, oy = cd.y0 - L.minB + 3;
+    for (int idx = lane; idx - lane < npx; idx += 64) {
+        bool keep = false;
+        int i = 0, j = 0;
+        if (idx < npx) {
+            i = idx / dw;
+            j = idx - i * dw;
+            keep = og_nms_keep(Ms, dw, dh, i, j, t);
+        }
+        const u64 mask = __ballot(keep);
+        if (keep) {
+            const int pos = run + __popcll(mask & ((1ull << lane) - 1ull));
+            out[pos] = og_pack_cand(ox + j, oy + i, Ms[idx] - 1);
+        }
+        run += __popcll(mask);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k3: octree (src/ORBextractor.cc:481-537, 539-763), one workgroup per (frame, level)
+// ------------------------------------------------------------------------------------------------
+struct OctNode {
+    short x0, y0, x1, y1;
+    int cnt;
+    int cid;  // creation order == allocation order of the reference's list nodes
+};
+
+#define OCT_NT 1024
+
+// exclusive block scan of one int per thread; returns the exclusive prefix, *total = sum
+__device__ __forceinline__ int og_block_excl_scan(int v, int* wsum, int* total)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        const int nw = blockDim.x >> 6;
+        int s = lane < nw ? wsum[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(s, o);
+            if (lane >= o) s += y;
+        }
+        if (lane < nw) wsum[lane] = s;  // inclusive per-wave totals
+    }
+    __syncthreads();
+    const int before = w ? wsum[w - 1] : 0;
+    *total = wsum[(blockDim.x >> 6) - 1];
+    __syncthreads();
+    return before + x - v;
+}
+
+__device__ __forceinline__ int og_quadrant(int x, int y, const OctNode& n)
+{
+    const int halfX = (n.x1 - n.x0 + 1) >> 1;  // ceil((float)(UR.x-UL.x)/2), exact for ints
+    const int halfY = (n.y1 - n.y0 + 1) >> 1;
+    const int mx = n.x0 + halfX, my = n.y0 + halfY;
+    return x < mx ? (y < my ? 0 : 2) : (y < my ? 1 : 3);
+}
+
+__device__ __forceinline__ OctNode og_child(const OctNode& p, int q)
+{
+    const int halfX = (p.x1 - p.x0 + 1) >> 1, halfY = (p.y1 - p.y0 + 1) >> 1;
+    const int mx = p.x0 + halfX, my = p.y0 + halfY;
+    OctNode c;
+    c.x0 = (short)((q & 1) ? mx : p.x0);
+    c.x1 = (short)((q & 1) ? p.x1 : mx);
+    c.y0 = (short)((q & 2) ? my : p.y0);
+    c.y1 = (short)((q & 2) ? p.y1 : my);
+    c.cnt = 0;
+    c.cid = 0;
+    return c;
+}
+
+// candidate order key: (cell row, cell col, row in cell, col in cell) == vToDistributeKeys order
+__device__ __forceinline__ unsigned og_cand_order(int x, int y, const OgLevel& L)
+{
+    const int ci = (y - 3) / L.hCell, cj = (x - 3) / L.wCell;
+    const int ly = y - 3 - ci * L.hCell, lx = x - 3 - cj * L.wCell;
+    return (unsigned)(((ci * L.nCols + cj) * L.hCell + ly) * L.wCell + lx);
+}
+
+__global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* __restrict__ cand,
+                                                           const int* __restrict__ cand_count,
+                                                           uint16_t* __restrict__ node_of,
+                                                           uint32_t* __restrict__ oct_xy,
+                                                           uint8_t* __restrict__ oct_resp,
+                                                           int* __restrict__ oct_count, int* __restrict__ status)
+{
+    __shared__ OctNode nodes[2][OG_OCT_MAXL];
+    __shared__ uint8_t fresh[2][OG_OCT_MAXL];
+    __shared__ int splitRank[OG_OCT_MAXL];
+    __shared__ int splitNode[OG_OCT_MAXL];
+    __shared__ int newPos[OG_OCT_MAXL];
+    __shared__ int aux[OG_OCT_MAXL];
+    __shared__ __attribute__((aligned(16))) int childCnt[4 * OG_OCT_MAXL];
+    __shared__ int childPos[4 * OG_OCT_MAXL];
+    __shared__ int wsum[32];
+    __shared__ int sv[16];
+
+    const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    const OgLevel& L = P.lv[l];
+    const int C = min(cand_count[f * P.nlevels + l], L.cand_cap);
+    const u64* K = cand + (long long)f * P.cand_per_frame + L.cand_off;
+    uint16_t* NO = node_of + (long long)f * P.cand_per_frame + L.cand_off;
+    const int N = L.N;
+    const int nIni = L.nIni;
+    const int H = L.maxBY - L.minB;
+
+    // ---- roots (src/ORBextractor.cc:552-585)
+    for (int r = tid; r < nIni; r += OCT_NT) childCnt[r] = 0;
+    __syncthreads();
+    for (int k = tid; k < C; k += OCT_NT) {
+        const int x = (int)(K[k] & 0xffff);
+        int r = (int)((float)x / L.hX);
+        r = min(r, nIni - 1);
+        NO[k] = (uint16_t)r;
+        atomicAdd(&childCnt[r], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int Ln = 0;
+        for (int r = 0; r < nIni; r++) {
+            if (childCnt[r] > 0) {
+                OctNode n;
+                n.x0 = (short)(int)(L.hX * (float)r);
+                n.x1 = (short)(int)(L.hX * (float)(r + 1));
+                n.y0 = 0;
+                n.y1 = (short)H;
+                n.cnt = childCnt[r];
+                n.cid = r;
+                nodes[0][Ln] = n;
+                fresh[0][Ln] = 0;
+                childPos[r] = Ln++;
+            } else {
+                childPos[r] = -1;
+            }
+        }
+        sv[0] = Ln;      // list length
+        sv[1] = 0;       // mode: 0 normal, 1 final
+        sv[2] = nIni;    // next creation id
+        sv[3] = 0;       // done
+        sv[4] = 0;       // current buffer
+    }
+    __syncthreads();
+    for (int k = tid; k < C; k += OCT_NT) NO[k] = (uint16_t)childPos[NO[k]];
+    __syncthreads();
+
+    for (int round = 0; round < 4096; round++) {
+        const int Ln = sv[0], mode = sv[1], cur = sv[4];
+        if (sv[3]) break;
+        OctNode* cn = nodes[cur];
+        uint8_t* cf = fresh[cur];
+        OctNode* nn = nodes[cur ^ 1];
+        uint8_t* nf = fresh[cur ^ 1];
+        __syncthreads();
+        // ---- choose the split set and its order
+        const int i = tid;
+        int S;
+        bool flag = false;
+        if (mode == 0) {
+            flag = i < Ln && cn[i].cnt > 1;
+            const int rank = og_block_excl_scan(flag ? 1 : 0, wsum, &S);
+            if (i < Ln) splitRank[i] = flag ? rank : -1;
+            if (flag) splitNode[rank] = i;
+        } else {
+            // vSizeAndPointerToNode of the previous round, sorted ascending by (size, ptr) and walked
+            // from the back (src/ORBextractor.cc:684-685): order = descending (cnt, creation id)
+            flag = i < Ln && cf[i] && cn[i].cnt > 1;
+            const int c = og_block_excl_scan(flag ? 1 : 0, wsum, &S);
+            if (flag) aux[c] = i;
+            __syncthreads();
+            if (i < Ln) splitRank[i] = -1;
+            if (flag) {
+                const int mc = cn[i].cnt, mid = cn[i].cid;
+                int rank = 0;
+                for (int q = 0; q < S; q++) {
+                    const OctNode& o = cn[aux[q]];
+                    rank += (o.cnt > mc) || (o.cnt == mc && o.cid > mid);
+                }
+                splitRank[i] = rank;
+                splitNode[rank] = i;
+            }
+        }
+        if (S == 0) {  // nothing to split: size == prevSize -> bFinish
+            if (tid == 0) sv[3] = 1;
+            __syncthreads();
+            break;
+        }
+        for (int q = tid; q < 4 * S; q += OCT_NT) childCnt[q] = 0;
+        __syncthreads();
+        // ---- count keys per child (DivideNode, :511-526)
+        for (int k = tid; k < C; k += OCT_NT) {
+            const int n = NO[k];
+            const int r = splitRank[n];
+            if (r >= 0) {
+                const u64 kv = K[k];
+                const int q = og_quadrant((int)(kv & 0xffff), (int)((kv >> 16) & 0xffff), cn[n]);
+                atomicAdd(&childCnt[4 * r + q], 1);
+            }
+        }
+        __syncthreads();
+        // ---- per split: non-empty children, break point of the final phase (:730-731)
+        int nc = 0, nexp = 0;
+        if (i < S) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int c = childCnt[4 * i + q];
+                nc += c > 0;
+                nexp += c > 1;
+            }
+        }
+        int totNc;
+        const int exNc = og_block_excl_scan(nc, wsum, &totNc);
+        int A = S;
+        if (mode == 1) {
+            // grow after splitting 0..i = sum_{r<=i} (nc_r - 1) = exNc + nc - (i+1)
+            const bool reach = i < S && (Ln + exNc + nc - (i + 1) >= N);
+            if (tid == 0) sv[5] = S;
+            __syncthreads();
+            if (reach) atomicMin(&sv[5], i + 1);
+            __syncthreads();
+            A = sv[5];
+        }
+        // total children of the applied splits
+        if (i == A - 1) sv[6] = exNc + nc;
+        __syncthreads();
+        const int T = sv[6];
+        // ---- place children: groups in reverse split order, each n4,n3,n2,n1 (push_front, :621-660)
+        if (i < A) {
+            const OctNode par = cn[splitNode[i]];
+            const int groupStart = T - (exNc + nc);
+            const int cidBase = sv[2] + exNc;
+            int before = 0;  // non-empty children among q' < q (creation order n1..n4)
+            for (int q = 0; q < 4; q++) {
+                const int c = childCnt[4 * i + q];
+                if (c > 0) {
+                    const int after = nc - before - 1;  // non-empty among q' > q
+                    const int pos = groupStart + after;
+                    OctNode ch = og_child(par, q);
+                    ch.cnt = c;
+                    ch.cid = cidBase + before;
+                    childPos[4 * i + q] = pos;
+                    if (pos < OG_OCT_MAXL) {
+                        nn[pos] = ch;
+                        nf[pos] = 1;
+                    }
+                    before++;
+                } else {
+                    childPos[4 * i + q] = -1;
+                }
+            }
+        }
+        // ---- kept nodes follow, in their old order
+        const bool kept = i < Ln && (splitRank[i] < 0 || splitRank[i] >= A);
+        int keptTot;
+        const int kr = og_block_excl_scan(kept ? 1 : 0, wsum, &keptTot);
+        if (kept) {
+            const int pos = T + kr;
+            newPos[i] = pos;
+            if (pos < OG_OCT_MAXL) {
+                nn[pos] = cn[i];
+                nf[pos] = 0;
+            }
+        }
+        int expTot;
+        (void)og_block_excl_scan(i < A ? nexp : 0, wsum, &expTot);
+        const int Lnew = T + keptTot;
+        if (Lnew > OG_OCT_MAXL) {
+            if (tid == 0) {
+                atomicOr(status, 2);
+                sv[3] = 1;
+                sv[0] = 0;
+            }
+            __syncthreads();
+            break;
+        }
+        __syncthreads();
+        // ---- remap keys to their new list positions
+        for (int k = tid; k < C; k += OCT_NT) {
+            const int n = NO[k];
+            const int r = splitRank[n];
+            if (r >= 0 && r < A) {
+                const u64 kv = K[k];
+                const int q = og_quadrant((int)(kv & 0xffff), (int)((kv >> 16) & 0xffff), cn[n]);
+                NO[k] = (uint16_t)childPos[4 * r + q];
+            } else {
+                NO[k] = (uint16_t)newPos[n];
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const int prevSize = Ln;
+            sv[0] = Lnew;
+            sv[2] += T;
+            sv[4] = cur ^ 1;
+            if (mode == 0) {
+                if (Lnew >= N || Lnew == prevSize) sv[3] = 1;
+                else if (Lnew + expTot * 3 > N) sv[1] = 1;
+            } else {
+                if (Lnew >= N || Lnew == prevSize) sv[3] = 1;
+            }
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    // ---- retain the best keypoint per node (:744-760): max response, first in vKeys order on ties
+    const int Ln = sv[0];
+    u64* best = (u64*)childCnt;  // 2*MAXL u64 of room
+    for (int n = tid; n < Ln; n += OCT_NT) best[n] = 0;
+    __syncthreads();
+    for (int k = tid; k < C; k += OCT_NT) {
+        const u64 kv = K[k];
+        const int x = (int)(kv & 0xffff), y = (int)((kv >> 16) & 0xffff), resp = (int)((kv >> 32) & 0xff);
+        const unsigned ord = og_cand_order(x, y, L);
+        atomicMax(&best[NO[k]], ((u64)resp << 32) | (u64)(0xffffffffu - ord));
+    }
+    __syncthreads();
+    const int nout = min(Ln, L.kcap);
+    for (int n = tid; n < nout; n += OCT_NT) {
+        const u64 b = best[n];
+        const unsigned ord = 0xffffffffu - (unsigned)(b & 0xffffffffu);
+        const int lx = ord % L.wCell;
+        unsigned t2 = ord / L.wCell;
+        const int ly = t2 % L.hCell;
+        t2 /= L.hCell;
+        const int cj = t2 % L.nCols, ci = t2 / L.nCols;
+        const int x = cj * L.wCell + 3 + lx + L.minB, y = ci * L.hCell + 3 + ly + L.minB;
+        const long long o = (long long)f * P.kcap_total + L.koff + n;
+        oct_xy[o] = (uint32_t)x | ((uint32_t)y << 16);
+        oct_resp[o] = (uint8_t)(b >> 32);
+    }
+    if (tid == 0) {
+        oct_count[f * P.nlevels + l] = nout;
+        if (Ln > L.kcap) atomicOr(status, 4);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k4: orientation + blur + rBRIEF + assembly (src/ORBextractor.cc:77-147, 851-852, 1076-1104)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int og_reflect101(int i, int n)
+{
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        if (i >= n) i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+#define DK_WAVES 4
+#define RAW_W 43
+#define RAW_S 44
+#define BL_W 37
+
+__global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, const uint8_t* __restrict__ img0,
+                                                                    long long pitch0, long long fstride0,
+                                                                    const uint8_t* __restrict__ pyr,
+                                                                    const uint32_t* __restrict__ oct_xy,
+                                                                    const uint8_t* __restrict__ oct_resp,
+                                                                    const int* __restrict__ oct_count,
+                                                                    orbgpu_kp_dev* __restrict__ kps,
+                                                                    uint8_t* __restrict__ desc,
+                                                                    int* __restrict__ counts)
+{
+    __shared__ uint8_t raw[DK_WAVES][RAW_W * RAW_S];
+    __shared__ uint16_t hb[DK_WAVES][RAW_W * BL_W];
+    __shared__ uint8_t bl[DK_WAVES][BL_W * BL_W + 3];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.y;
+    const int g = blockIdx.x * DK_WAVES + w;
+    // which level does keypoint g belong to (levels concatenated 0..L-1, :1076-1104)
+    int l = -1, li = 0, total = 0;
+    for (int q = 0; q < P.nlevels; q++) {
+        const int c = oct_count[f * P.nlevels + q];
+        if (l < 0 && g < total + c) {
+            l = q;
+            li = g - total;
+        }
+        total += c;
+    }
+    if (g == 0 && lane == 0) counts[f] = total;
+    const bool active = l >= 0;
+    uint8_t* R = raw[w];
+    uint16_t* Hb = hb[w];
+    uint8_t* Bl = bl[w];
+    int cx = 0, cy = 0, resp = 0, lw = 1, lh = 1;
+    if (active) {
+        const OgLevel& L = P.lv[l];
+        const long long o = (long long)f * P.kcap_total + L.koff + li;
+        const uint32_t xy = oct_xy[o];
+        cx = (int)(xy & 0xffff);
+        cy = (int)(xy >> 16);
+        resp = oct_resp[o];
+        lw = L.w;
+        lh = L.h;
+        const uint8_t* img;
+        long long pitch;
+        if (l == 0) {
+            img = img0 + (long long)f * fstride0;
+            pitch = pitch0;
+        } else {
+            img = pyr + (long long)f * P.pyr_per_frame + L.pyr_off;
+            pitch = L.pitch;
+        }
+        for (int idx = lane; idx < RAW_W * RAW_W; idx += 64) {
+            const int r = idx / RAW_W, c = idx - (idx / RAW_W) * RAW_W;
+            const int yy = og_reflect101(cy - 21 + r, lh), xx = og_reflect101(cx - 21 + c, lw);
+            R[r * RAW_S + c] = img[(long long)yy * pitch + xx];
+        }
+    }
+    __syncthreads();
+    // ---- IC_Angle on the unblurred level (:77-104); integer moments are order-independent
+    int m01 = 0, m10 = 0;
+    if (active) {
+        const uint8_t* ctr = R + 21 * RAW_S + 21;
+        if (lane < 31) m10 += (lane - 15) * ctr[lane - 15];
+        for (int v = 1; v <= OG_HALF_PATCH; v++) {
+            const int d = P.umax[v];
+            const int u = lane - d;
+            if (u <= d) {
+                const int vp = ctr[u + v * RAW_S], vm = ctr[u - v * RAW_S];
+                m01 += v * (vp - vm);
+                m10 += u * (vp + vm);
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            m01 += __shfl_xor(m01, o);
+            m10 += __shfl_xor(m10, o);
+        }
+    }
+    const float angle = og_fast_atan2((float)m01, (float)m10);
+    // ---- 7x7 Gaussian (sigma 2, BORDER_REFLECT_101) of the 37x37 window the tests can reach
+    const int gk[7] = {18, 34, 49, 55, 49, 34, 18};
+    if (active) {
+        for (int idx = lane; idx < RAW_W * BL_W; idx += 64) {
+            const int r = idx / BL_W, c = idx - (idx / BL_W) * BL_W;
+            const uint8_t* s = R + r * RAW_S + c;
+            int acc = 0;
+#pragma unroll
+            for (int t = 0; t < 7; t++) acc += gk[t] * s[t];
+            Hb[idx] = (uint16_t)acc;
+        }
+    }
+    __syncthreads();
+    if (active) {
+        for (int idx = lane; idx < BL_W * BL_W; idx += 64) {
+            const int r = idx / BL_W, c = idx - (idx / BL_W) * BL_W;
+            int acc = 0;
+#pragma unroll
+            for (int t = 0; t < 7; t++) acc += gk[t] * (int)Hb[(r + t) * BL_W + c];
+            int v = (acc + (1 << 15)) >> 16;
+            Bl[idx] = (uint8_t)(v > 255 ? 255 : v);
+        }
+    }
+    __syncthreads();
+    if (!active) return;
+    // ---- rBRIEF (:108-147)
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    float a, b;
+    og_sincosf(angle * factorPI, &b, &a);
+    const uint8_t* ctr = Bl + 18 * BL_W + 18;
+    u64 words[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int p = lane + 64 * t;
+        const signed char* pt = og_pattern + 4 * p;
+        int val[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const float x = (float)pt[2 * q], y = (float)pt[2 * q + 1];
+            const int row = og_cvround(__builtin_fmaf(x, b, y * a));
+            const int col = og_cvround(__builtin_fmaf(x, a, -(y * b)));
+            val[q] = ctr[row * BL_W + col];
+        }
+        words[t] = __ballot(val[0] < val[1]);
+    }
+    const long long o = (long long)f * P.frame_cap + g;
+    if (lane < 4) {
+        u64 v = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+        ((u64*)(desc + o * 32))[lane] = v;
+    }
+    if (lane == 0) {
+        const OgLevel& L = P.lv[l];
+        orbgpu_kp_dev k;
+        float x = (float)cx, y = (float)cy;
+        if (l != 0) {
+            x = x * L.scale;
+            y = y * L.scale;
+        }
+        k.x = x;
+        k.y = y;
+        k.size = (float)L.patch_size;
+        k.angle = angle;
+        k.response = (float)resp;
+        k.octave = l;
+        k.class_id = -1;
+        kps[o] = k;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k5: Frame::AssignFeaturesToGrid (src/Frame.cc:230-245, PosInGrid :382-392)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void og_grid_kernel(const orbgpu_kp_dev* __restrict__ kps,
+                                                      const int* __restrict__ counts, int frame_cap,
+                                                      OgGridGeom G, int* __restrict__ cell_start,
+                                                      int* __restrict__ cell_items)
+{
+    __shared__ int cnt[OG_GRID_CELLS + 1];
+    __shared__ int wsum[32];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int n = counts[f];
+    const orbgpu_kp_dev* K = kps + (long long)f * frame_cap;
+    int* CS = cell_start + (long long)f * (OG_GRID_CELLS + 1);
+    int* CI = cell_items + (long long)f * frame_cap;
+    for (int c = tid; c < OG_GRID_CELLS; c += 256) cnt[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+        const int px = (int)roundf((K[i].x - G.minX) * G.invW);
+        const int py = (int)roundf((K[i].y - G.minY) * G.invH);
+        if (px >= 0 && px < OG_GRID_COLS && py >= 0 && py < OG_GRID_ROWS) atomicAdd(&cnt[px * OG_GRID_ROWS + py], 1);
+    }
+    __syncthreads();
+    // exclusive scan over 3072 cells, 12 per thread
+    const int per = OG_GRID_CELLS / 256;
+    int local[OG_GRID_CELLS / 256];
+    int s = 0;
+    for (int q = 0; q < per; q++) {
+        local[q] = s;
+        s += cnt[tid * per + q];
+    }
+    int tot;
+    const int ex = og_block_excl_scan(s, wsum, &tot);
+    for (int q = 0; q < per; q++) CS[tid * per + q] = ex + local[q];
+    if (tid == 0) CS[OG_GRID_CELLS] = tot;
+    __syncthreads();
+    for (int q = 0; q < per; q++) cnt[tid * per + q] = ex + local[q];  // cursors
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+        const int px = (int)roundf((K[i].x - G.minX) * G.invW);
+        const int py = (int)roundf((K[i].y - G.minY) * G.invH);
+        if (px >= 0 && px < OG_GRID_COLS && py >= 0 && py < OG_GRID_ROWS) {
+            const int pos = atomicAdd(&cnt[px * OG_GRID_ROWS + py], 1);
+            CI[pos] = i;
+        }
+    }
+    __syncthreads();
+    __threadfence_block();
+    // restore ascending index order inside each cell (push_back order of the reference)
+    for (int c = tid; c < OG_GRID_CELLS; c += 256) {
+        const int b = CS[c], e = CS[c + 1];
+        for (int p = b + 1; p < e; p++) {
+            const int v = CI[p];
+            int q = p - 1;
+            while (q >= b && CI[q] > v) {
+                CI[q + 1] = CI[q];
+                q--;
+            }
+            CI[q + 1] = v;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------------
+hipError_t og_upload_pattern(int device)
+{
+    if (device >= 0 && device < 64 && g_pattern_uploaded_dev[device]) return hipSuccess;
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(og_pattern), oo_orb_pattern, sizeof(oo_orb_pattern), 0,
+                                     hipMemcpyHostToDevice);
+    if (e == hipSuccess && device >= 0 && device < 64) g_pattern_uploaded_dev[device] = true;
+    return e;
+}
+
+void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,
+                      long long dst_pitch, long long dst_fstride, int dw, int dh, const int4* xtab, const int4* ytab,
+                      int xmax, int B)
+{
+    dim3 block(64);
+    dim3 grid((dw + 4 * 64 - 1) / (4 * 64), dh, B);
+    hipLaunchKernelGGL(og_resize_kernel, grid, block, 0, s, src, src_pitch, src_fstride, dst, dst_pitch, dst_fstride,
+                       dw, dh, xtab, ytab, xmax);
+}
+
+void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,
+                    long long fstride0, const uint8_t* pyr, u64* cand, int* cand_count, int* status, int B)
+{
+    hipLaunchKernelGGL(og_fast_cells_kernel, dim3(P.total_cells, B), dim3(64), 0, s, P, cells, img0, pitch0, fstride0,
+                       pyr, cand, cand_count, status);
+}
+
+void og_launch_octree(hipStream_t s, const OgPlan& P, const u64* cand, const int* cand_count, uint16_t* node_of,
+                      uint32_t* oct_xy, uint8_t* oct_resp, int* oct_count, int* status, int B)
+{
+    hipLaunchKernelGGL(og_octree_kernel, dim3(P.nlevels, B), dim3(OCT_NT), 0, s, P, cand, cand_count, node_of, oct_xy,
+                       oct_resp, oct_count, status);
+}
+
+void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, long long pitch0, long long fstride0,
+                        const uint8_t* pyr, const uint32_t* oct_xy, const uint8_t* oct_resp, const int* oct_count,
+                        orbgpu_kp_dev* kps, uint8_t* desc, int* counts, int B)
+{
+    const int blocks = (P.frame_cap + DK_WAVES - 1) / DK_WAVES;
+    hipLaunchKernelGGL(og_describe_kernel, dim3(blocks, B), dim3(64 * DK_WAVES), 0, s, P, img0, pitch0, fstride0, pyr,
+                       oct_xy, oct_resp, oct_count, kps, desc, counts);
+}
+
+void og_launch_grid(hipStream_t s, const orbgpu_kp_dev* kps, const int* counts, int frame_cap, OgGridGeom G,
+                    int* cell_start, int* cell_items, int B)
+{
+    hipLaunchKernelGGL(og_grid_kernel, dim3(B), dim3(256), 0, s, kps, counts, frame_cap, G, cell_start, cell_items);
+}

@@ -1,0 +1,425 @@
+// orb_match.hip -- gfx950 kernels of the per-frame Hamming matchers.
+//
+//   og_search_init_kernel : ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:405-520), one
+//       64-lane wave per (F1, F2) pair.  Queries run in the reference's order (the vMatchedDistance /
+//       vnMatches21 state couples them, :444, :463-470); the candidates of one query are scored in
+//       parallel (XOR + popcount over 8 u32) and reduced to (best, second) with a lexicographic
+//       (distance, candidate position) wave min -- exactly the reference's strict-< update order.
+//   og_proj_count/fill/resolve : ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th)
+//       (src/ORBmatcher.cc:45-137).  Candidate lists + distances are built in parallel (one thread per
+//       map point); the order-dependent claim resolution (:87-89, :123) is a single ordered pass over
+//       the precomputed lists.
+#include <hip/hip_runtime.h>
+#include <limits.h>
+#include <stdint.h>
+
+#include "orb_math_dev.h"
+#include "orbgpu_internal.h"
+#include "orbgpu_launch.h"
+
+typedef unsigned long long u64;
+
+#define TH_HIGH 100
+#define TH_LOW 50
+#define HISTO_LENGTH 30
+
+struct OgCellRange {
+    int x0, x1, y0, y1;  // inclusive; empty if x0 > x1
+};
+
+// Frame::GetFeaturesInArea cell window (src/Frame.cc:332-346)
+__device__ __forceinline__ OgCellRange og_cell_range(const OgGridGeom& G, float x, float y, float r)
+{
+    OgCellRange c;
+    c.x0 = max(0, (int)floorf((x - G.minX - r) * G.invW));
+    c.x1 = min(OG_GRID_COLS - 1, (int)ceilf((x - G.minX + r) * G.invW));
+    c.y0 = max(0, (int)floorf((y - G.minY - r) * G.invH));
+    c.y1 = min(OG_GRID_ROWS - 1, (int)ceilf((y - G.minY + r) * G.invH));
+    if (c.x0 >= OG_GRID_COLS || c.x1 < 0 || c.y0 >= OG_GRID_ROWS || c.y1 < 0) c.x0 = 1, c.x1 = 0;
+    return c;
+}
+
+__device__ __forceinline__ void og_load_desc(const uint8_t* p, uint4& a, uint4& b)
+{
+    const uint4* q = (const uint4*)p;
+    a = q[0];
+    b = q[1];
+}
+
+__device__ __forceinline__ u64 og_wave_min_u64(u64 v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const u64 w = __shfl_xor(v, o);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int og_wave_sum(int v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// SearchForInitialization
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void og_search_init_kernel(OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G,
+                                                            float nnratio, int checkOri, int windowSize,
+                                                            float* __restrict__ prev_xy, int prev_stride,
+                                                            int* __restrict__ matches12, int match_stride,
+                                                            int* __restrict__ nmatches)
+{
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const int n1 = F1.counts[ref];
+    const int n2 = F2.counts[b];
+    int* vMD = smem;                  // vMatchedDistance [cap2]
+    int* v21 = vMD + F2.frame_cap;    // vnMatches21      [cap2]
+    int* m12 = v21 + F2.frame_cap;    // vnMatches12      [cap1]
+    int* binOf = m12 + F1.frame_cap;  // rot-hist bin the match was pushed to, -1 = none [cap1]
+    __shared__ int hist[HISTO_LENGTH];
+    for (int i = lane; i < n2; i += 64) {
+        vMD[i] = INT_MAX;
+        v21[i] = -1;
+    }
+    for (int i = lane; i < n1; i += 64) {
+        m12[i] = -1;
+        binOf[i] = -1;
+    }
+    if (lane < HISTO_LENGTH) hist[lane] = 0;
+    __syncthreads();
+    const orbgpu_kp_dev* K1 = F1.kps + (long long)ref * F1.frame_cap;
+    const uint8_t* D1 = F1.desc + (long long)ref * F1.frame_cap * 32;
+    const orbgpu_kp_dev* K2 = F2.kps + (long long)b * F2.frame_cap;
+    const uint8_t* D2 = F2.desc + (long long)b * F2.frame_cap * 32;
+    const int* CS = F2.cell_start + (long long)b * (OG_GRID_CELLS + 1);
+    const int* CI = F2.cell_items + (long long)b * F2.frame_cap;
+    float* PV = prev_xy + (long long)b * prev_stride;
+    const float r = (float)windowSize;
+    const float factor = 1.0f / HISTO_LENGTH;
+    int nm = 0;
+    for (int i1 = 0; i1 < n1; i1++) {
+        const int level1 = K1[i1].octave;
+        if (level1 > 0) continue;
+        const float x = PV[2 * i1], y = PV[2 * i1 + 1];
+        const OgCellRange cr = og_cell_range(G, x, y, r);
+        if (cr.x0 > cr.x1) continue;
+        uint4 da, db;
+        og_load_desc(D1 + (long long)i1 * 32, da, db);
+        const int ncy = cr.y1 - cr.y0 + 1;
+        const int ncells = (cr.x1 - cr.x0 + 1) * ncy;
+        u64 best1 = ~0ull, best2 = ~0ull;  // lane-local two smallest (dist<<32 | pos)
+        int bestI2 = -1;
+        int posBase = 0;
+        for (int c0 = 0; c0 < ncells; c0 += 64) {
+            const int c = c0 + lane;
+            int cell = 0, cnt = 0;
+            if (c < ncells) {
+                cell = (cr.x0 + c / ncy) * OG_GRID_ROWS + (cr.y0 + c % ncy);
+                cnt = CS[cell + 1] - CS[cell];
+            }
+            // wave exclusive scan of cnt
+            int incl = cnt;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o);
+                if (lane >= o) incl += t;
+            }
+            const int T = __shfl(incl, 63);
+            for (int e = lane; e - lane < T; e += 64) {
+                // owning lane of flat candidate e: the first lane whose inclusive sum exceeds e.
+                // Every lane runs the shuffles (inactive-lane reads of ds_bpermute are undefined).
+                const int ee = min(e, T - 1);
+                int lo = 0;  // binary lifting: number of lanes with incl <= ee (uniform 6 steps)
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1) {
+                    const int v = __shfl(incl, lo + step - 1);
+                    if (v <= ee) lo += step;
+                }
+                const int ownerIncl = __shfl(incl, lo), ownerCnt = __shfl(cnt, lo), ownerCell = __shfl(cell, lo);
+                bool valid = false;
+                int dist = 0, i2 = -1;
+                if (e < T) {
+                    const int k = e - (ownerIncl - ownerCnt);
+                    i2 = CI[CS[ownerCell] + k];
+                    const orbgpu_kp_dev kp2 = K2[i2];
+                    // level filter: minLevel == maxLevel == level1 == 0 (src/Frame.cc:361-368)
+                    if (kp2.octave >= level1 && kp2.octave <= level1) {
+                        const float distx = kp2.x - x, disty = kp2.y - y;
+                        if (fabsf(distx) < r && fabsf(disty) < r) {
+                            uint4 ea, eb;
+                            og_load_desc(D2 + (long long)i2 * 32, ea, eb);
+                            dist = og_hamming(da, db, ea, eb);
+                            valid = !(vMD[i2] <= dist);  // src/ORBmatcher.cc:444
+                        }
+                    }
+                }
+                if (valid) {
+                    const u64 key = ((u64)(unsigned)dist << 32) | (unsigned)(posBase + e);
+                    if (key < best1) {
+                        best2 = best1;
+                        best1 = key;
+                        bestI2 = i2;
+                    } else if (key < best2) {
+                        best2 = key;
+                    }
+                }
+            }
+            posBase += T;
+        }
+        const u64 gbest = og_wave_min_u64(best1);
+        if (gbest == ~0ull) continue;
+        const u64 mine2 = (best1 == gbest) ? best2 : best1;
+        const u64 gsecond = og_wave_min_u64(mine2);
+        const u64 owner = __ballot(best1 == gbest);
+        const int ol = __ffsll((long long)owner) - 1;
+        const int bestIdx2 = __shfl(bestI2, ol);
+        const int bestDist = (int)(gbest >> 32);
+        const int bestDist2 = gsecond == ~0ull ? INT_MAX : (int)(gsecond >> 32);
+        if (bestDist <= TH_LOW && bestDist < (float)bestDist2 * nnratio) {
+            if (lane == 0) {
+                const int prev = v21[bestIdx2];
+                if (prev >= 0) {
+                    m12[prev] = -1;
+                    nm--;
+                }
+                m12[i1] = bestIdx2;
+                v21[bestIdx2] = i1;
+                vMD[bestIdx2] = bestDist;
+                nm++;
+                if (checkOri) {
+                    float rot = K1[i1].angle - K2[bestIdx2].angle;
+                    if (rot < 0.0) rot += 360.0f;
+                    int bin = (int)roundf(rot * factor);
+                    if (bin == HISTO_LENGTH) bin = 0;
+                    binOf[i1] = bin;
+                    hist[bin]++;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    nm = __shfl(nm, 0);
+    if (checkOri) {
+        // ComputeThreeMaxima (src/ORBmatcher.cc:1601-1642)
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        int max1 = 0, max2 = 0, max3 = 0;
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            const int s = hist[i];
+            if (s > max1) {
+                max3 = max2; max2 = max1; max1 = s;
+                ind3 = ind2; ind2 = ind1; ind1 = i;
+            } else if (s > max2) {
+                max3 = max2; max2 = s;
+                ind3 = ind2; ind2 = i;
+            } else if (s > max3) {
+                max3 = s;
+                ind3 = i;
+            }
+        }
+        if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+        else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+        int dropped = 0;
+        for (int i = lane; i < n1; i += 64) {
+            const int bin = binOf[i];
+            if (bin >= 0 && bin != ind1 && bin != ind2 && bin != ind3 && m12[i] >= 0) {
+                m12[i] = -1;
+                dropped++;
+            }
+        }
+        nm -= og_wave_sum(dropped);
+    }
+    __syncthreads();
+    int* M = matches12 + (long long)b * match_stride;
+    for (int i = lane; i < n1; i += 64) {
+        const int j = m12[i];
+        M[i] = j;
+        if (j >= 0) {
+            PV[2 * i] = K2[j].x;
+            PV[2 * i + 1] = K2[j].y;
+        }
+    }
+    if (lane == 0) nmatches[b] = nm;
+}
+
+void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G, float nnratio,
+                           int checkOri, int windowSize, float* prev_xy, int prev_stride, int* matches12,
+                           int match_stride, int* nmatches, int B)
+{
+    const size_t shm = sizeof(int) * (2 * (size_t)F2.frame_cap + 2 * (size_t)F1.frame_cap);
+    hipLaunchKernelGGL(og_search_init_kernel, dim3(B), dim3(64), shm, s, F1, ref, F2, G, nnratio, checkOri,
+                       windowSize, prev_xy, prev_stride, matches12, match_stride, nmatches);
+}
+
+// ------------------------------------------------------------------------------------------------
+// SearchByProjection(Frame&, const vector<MapPoint*>&, th)
+// ------------------------------------------------------------------------------------------------
+struct OgProjCand {
+    int idx;
+    short dist;
+    short octave;
+};
+
+// Enumerate (or count) the candidates of map point m in GetFeaturesInArea order, applying the static
+// filters (levels, window, stereo check); claims are dynamic and applied in the ordered pass.
+template <bool FILL>
+__device__ int og_proj_enum(const OgFrameDev& F, const OgGridGeom& G, const float* sf, const OgMapPointsDev& mp,
+                            int m, float th, OgProjCand* out)
+{
+    if (!mp.track_in_view[m] || mp.is_bad[m]) return 0;
+    const int lvl = mp.level[m];
+    float r = mp.view_cos[m] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos, :131-137
+    if (th != 1.0) r *= th;
+    const float R = r * sf[lvl];
+    const float x = mp.proj_x[m], y = mp.proj_y[m];
+    const OgCellRange cr = og_cell_range(G, x, y, R);
+    if (cr.x0 > cr.x1) return 0;
+    const int minLevel = lvl - 1, maxLevel = lvl;
+    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    uint4 da, db;
+    if (FILL) og_load_desc(mp.desc + (long long)m * 32, da, db);
+    int n = 0;
+    for (int ix = cr.x0; ix <= cr.x1; ix++)
+        for (int iy = cr.y0; iy <= cr.y1; iy++) {
+            const int cell = ix * OG_GRID_ROWS + iy;
+            for (int j = F.cell_start[cell]; j < F.cell_start[cell + 1]; j++) {
+                const int idx = F.cell_items[j];
+                const orbgpu_kp_dev kp = F.kps[idx];
+                if (bCheckLevels) {
+                    if (kp.octave < minLevel) continue;
+                    if (maxLevel >= 0 && kp.octave > maxLevel) continue;
+                }
+                const float distx = kp.x - x, disty = kp.y - y;
+                if (!(fabsf(distx) < R && fabsf(disty) < R)) continue;
+                if (F.uright && F.uright[idx] > 0) {
+                    const float er = fabsf(mp.proj_xr[m] - F.uright[idx]);
+                    if (er > r * sf[lvl]) continue;
+                }
+                if (FILL) {
+                    uint4 ea, eb;
+                    og_load_desc(F.desc + (long long)idx * 32, ea, eb);
+                    OgProjCand c;
+                    c.idx = idx;
+                    c.dist = (short)og_hamming(da, db, ea, eb);
+                    c.octave = (short)kp.octave;
+                    out[n] = c;
+                }
+                n++;
+            }
+        }
+    return n;
+}
+
+__global__ __launch_bounds__(256) void og_proj_count_kernel(OgFrameDev F, OgGridGeom G, const float* sf,
+                                                            OgMapPointsDev mp, float th, int* cnt)
+{
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= mp.m) return;
+    cnt[m] = og_proj_enum<false>(F, G, sf, mp, m, th, nullptr);
+}
+
+__global__ __launch_bounds__(1024) void og_scan_kernel(const int* cnt, int n, int* off)
+{
+    // single-workgroup exclusive scan (n is the map-point count, a few thousand)
+    __shared__ int wsum[16];
+    __shared__ int carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < n; base += 1024) {
+        const int i = base + threadIdx.x;
+        const int v = i < n ? cnt[i] : 0;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        int x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int s = 0;
+            for (int q = 0; q < 16; q++) {
+                const int t = wsum[q];
+                wsum[q] = s;
+                s += t;
+            }
+        }
+        __syncthreads();
+        if (i < n) off[i] = carry + wsum[w] + x - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += wsum[15] + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) off[n] = carry;
+}
+
+__global__ __launch_bounds__(256) void og_proj_fill_kernel(OgFrameDev F, OgGridGeom G, const float* sf,
+                                                           OgMapPointsDev mp, float th, const int* off,
+                                                           OgProjCand* cands)
+{
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= mp.m) return;
+    og_proj_enum<true>(F, G, sf, mp, m, th, cands + off[m]);
+}
+
+// ordered claim resolution: a single lane replays the reference loop over the precomputed lists
+__global__ __launch_bounds__(64) void og_proj_resolve_kernel(OgMapPointsDev mp, const int* off,
+                                                             const OgProjCand* cands, float nnratio, int n,
+                                                             int* owner, int* owner_obs, int* nmatches)
+{
+    if (threadIdx.x != 0) return;
+    int nm = 0;
+    for (int m = 0; m < mp.m; m++) {
+        const int b = off[m], e = off[m + 1];
+        if (b == e) continue;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (int c = b; c < e; c++) {
+            const OgProjCand cc = cands[c];
+            if (owner[cc.idx] >= 0 && owner_obs[cc.idx]) continue;  // :87-89
+            const int dist = cc.dist;
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestLevel2 = bestLevel;
+                bestLevel = cc.octave;
+                bestIdx = cc.idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = cc.octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= TH_HIGH) {
+            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+            owner[bestIdx] = m;
+            owner_obs[bestIdx] = mp.n_obs[m] > 0;
+            nm++;
+        }
+    }
+    *nmatches = nm;
+}
+
+void og_launch_proj_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, float th,
+                          int* cnt, int* off)
+{
+    const int blocks = (mp.m + 255) / 256;
+    if (blocks > 0) hipLaunchKernelGGL(og_proj_count_kernel, dim3(blocks), dim3(256), 0, s, F, G, sf, mp, th, cnt);
+    hipLaunchKernelGGL(og_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, mp.m, off);
+}
+
+void og_launch_proj_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp,
+                            float nnratio, float th, const int* off, OgProjCand* cands, int* owner, int* owner_obs,
+                            int* nmatches)
+{
+    const int blocks = (mp.m + 255) / 256;
+    if (blocks > 0)
+        hipLaunchKernelGGL(og_proj_fill_kernel, dim3(blocks), dim3(256), 0, s, F, G, sf, mp, th, off, cands);
+    hipLaunchKernelGGL(og_proj_resolve_kernel, dim3(1), dim3(64), 0, s, mp, off, cands, nnratio, 0, owner, owner_obs,
+                       nmatches);
+}
+
+size_t og_proj_cand_size() { return sizeof(OgProjCand); }

@@ -1,0 +1,85 @@
+// orb_math_dev.h -- bit-exact device restatements of the scalar float/double steps of the reference
+// path.  The library is compiled with -ffp-contract=off: every fused multiply-add below is written
+// out (fmaf / fma) exactly where the reference build performs one, and nowhere else.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// cvRound(float): cvtss2si under the default MXCSR = round-half-even (v_rndne_f32).
+__device__ __forceinline__ int og_cvround(float v) { return (int)__builtin_rintf(v); }
+
+// cv::fastAtan2 (OpenCV 3.x scalar, no FMA), called at src/ORBextractor.cc:103.
+__device__ __forceinline__ float og_fast_atan2(float y, float x)
+{
+    const float k = (float)(180.0 / 3.14159265358979323846);
+    const float p1 = 0.9997878412794807f * k;
+    const float p3 = -0.3258083974640975f * k;
+    const float p5 = 0.1555786518463281f * k;
+    const float p7 = -0.04432655554792128f * k;
+    const float eps = (float)2.2204460492503131e-16;
+    float ax = fabsf(x), ay = fabsf(y), a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + eps);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + eps);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// glibc 2.35 x86_64 sincosf (FMA ifunc variant) for |y| < 120; the reference's
+// `(float)cos(angle), (float)sin(angle)` (src/ORBextractor.cc:113) is one sincosf call under
+// GCC -O3 -march=native.  Same double-precision operation sequence as the host libm machine code.
+__constant__ const double og_sincosf_tab[2][14] = {
+    {1.0, -1.0, -1.0, 1.0, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 0x1.0p+0,
+     -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7,
+     -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16},
+    {1.0, -1.0, -1.0, 1.0, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -0x1.0p+0,
+     0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7,
+     0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16},
+};
+
+__device__ __forceinline__ void og_sincosf(float y, float* sinp, float* cosp)
+{
+    const uint32_t t = (__float_as_uint(y) >> 20) & 0x7ff;
+    const double* T;
+    double xs, x2;
+    int n = 0;
+    if (t < 0x3f4) {
+        if (t < 0x398) { *sinp = y; *cosp = 1.0f; return; }
+        T = og_sincosf_tab[0];
+        xs = (double)y;
+        x2 = __dmul_rn(xs, xs);
+    } else {
+        const double x = (double)y;
+        const double* T0 = og_sincosf_tab[0];
+        n = (((int32_t)__dmul_rn(x, T0[4])) + 0x800000) >> 24;
+        const double r = __fma_rn(-(double)n, T0[5], x);
+        T = og_sincosf_tab[(n & 2) ? 1 : 0];
+        xs = __dmul_rn(r, T0[n & 3]);
+        x2 = __dmul_rn(r, r);
+    }
+    const double x3 = __dmul_rn(x2, xs), x4 = __dmul_rn(x2, x2);
+    const double x5 = __dmul_rn(x2, x3), x6 = __dmul_rn(x2, x4);
+    const double s1v = __fma_rn(x2, T[12], T[10]);
+    const double c2v = __fma_rn(x2, T[13], T[11]);
+    const double c1v = __fma_rn(x2, T[7], T[6]);
+    const double s = __fma_rn(x3, T[8], xs);
+    const double c = __fma_rn(x4, T[9], c1v);
+    const float so = (float)__fma_rn(s1v, x5, s);
+    const float co = (float)__fma_rn(c2v, x6, c);
+    if (n & 1) { *sinp = co; *cosp = so; }
+    else       { *sinp = so; *cosp = co; }
+}
+
+// ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1647-1663): popcount of the XOR of 8 u32 words.
+__device__ __forceinline__ int og_hamming(const uint4 a0, const uint4 a1, const uint4 b0, const uint4 b1)
+{
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}

@@ -1,0 +1,859 @@
+// orbgpu_capi.cpp -- host runtime of the gfx950 ORB path: plan construction (the reference's scalar
+// setup math, reproduced exactly), device buffer management, the per-batch launch sequence and the
+// extern "C" boundary declared in include/orbgpu.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/orbgpu.h"
+#include "orbgpu_internal.h"
+#include "orbgpu_launch.h"
+
+static_assert(sizeof(orbgpu_keypoint) == 28, "cv::KeyPoint layout");
+static_assert(sizeof(orbgpu_kp_dev) == 28, "cv::KeyPoint layout");
+
+namespace {
+
+inline int cv_round(float v) { return (int)std::lrintf(v); }
+inline int cv_round_d(double v) { return (int)std::lrint(v); }
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;  // elements
+};
+
+struct StageTimer {
+    bool on = false;
+    std::vector<hipEvent_t> ev;
+    std::vector<const char*> names;
+    int used = 0;
+    std::vector<float> last_ms;
+    std::vector<const char*> last_names;
+};
+
+}  // namespace
+
+struct orbgpu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    // ORBextractor parameters and scale tables (src/ORBextractor.cc:410-470)
+    int nfeatures = 0, nlevels = 0, iniTh = 0, minTh = 0;
+    double scaleFactor = 0;  // `double scaleFactor` member, include/ORBextractor.h:98
+    std::vector<float> sf, isf, sig2, isig2;
+    std::vector<int> nfeat;
+    int umax[16] = {0};
+    // plan for the current geometry
+    int W = 0, H = 0;
+    bool planned = false;
+    OgPlan plan{};
+    std::vector<OgCell> cells_h;
+    std::vector<int4> xtab_h, ytab_h;
+    DevBuf<OgCell> cells;
+    DevBuf<int4> tabs;
+    // batch buffers
+    int Bcap = 0;
+    DevBuf<uint8_t> pyr;
+    DevBuf<unsigned long long> cand;
+    DevBuf<int> cand_count;
+    DevBuf<uint16_t> node_of;
+    DevBuf<uint32_t> oct_xy;
+    DevBuf<uint8_t> oct_resp;
+    DevBuf<int> oct_count;
+    DevBuf<orbgpu_kp_dev> kps;
+    DevBuf<uint8_t> desc;
+    DevBuf<int> counts;
+    DevBuf<int> cell_start, cell_items;
+    DevBuf<int> status;
+    // last batch
+    const uint8_t* last_img = nullptr;
+    long long last_pitch = 0, last_fstride = 0;
+    int last_B = 0;
+    OgGridGeom grid_geom{};
+    // single-frame host path
+    DevBuf<uint8_t> in_img;
+    // matcher scratch
+    DevBuf<uint8_t> mscratch;
+    StageTimer timer;
+    std::string err;
+};
+
+static thread_local std::string g_create_err;
+
+#define HIP_TRY(ctx, expr)                                                                          \
+    do {                                                                                            \
+        hipError_t _e = (expr);                                                                     \
+        if (_e != hipSuccess) {                                                                     \
+            if (ctx) (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(_e);                \
+            return ORBGPU_ERR_HIP;                                                                  \
+        }                                                                                           \
+    } while (0)
+
+template <class T>
+static hipError_t ensure(DevBuf<T>& b, size_t n)
+{
+    if (b.n >= n && b.p) return hipSuccess;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+    hipError_t e = hipMalloc((void**)&b.p, std::max<size_t>(n, 1) * sizeof(T));
+    if (e == hipSuccess) b.n = n;
+    return e;
+}
+
+template <class T>
+static void release(DevBuf<T>& b)
+{
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// plan: geometry of one image size (all quantities the reference derives per call)
+// ------------------------------------------------------------------------------------------------
+static int build_plan(orbgpu_ctx* c, int W, int H)
+{
+    if (c->planned && c->W == W && c->H == H) return ORBGPU_OK;
+    OgPlan P{};
+    P.nlevels = c->nlevels;
+    P.iniTh = c->iniTh;
+    P.minTh = c->minTh;
+    std::memcpy(P.umax, c->umax, sizeof(P.umax));
+    std::vector<OgCell> cells;
+    std::vector<int4> tabs;
+    long long pyr_off = 0, cand_off = 0;
+    int koff = 0;
+    int pw = W, ph = H;
+    for (int l = 0; l < c->nlevels; l++) {
+        OgLevel& L = P.lv[l];
+        // ComputePyramid level size (src/ORBextractor.cc:1111-1112)
+        L.w = cv_round((float)W * c->isf[l]);
+        L.h = cv_round((float)H * c->isf[l]);
+        L.pitch = (L.w + 63) & ~63;
+        if (l >= 1) {
+            L.pyr_off = pyr_off;
+            pyr_off += ((long long)L.pitch * L.h + 255) & ~255LL;
+        }
+        // FAST cell grid (src/ORBextractor.cc:773-787)
+        L.minB = OG_EDGE - 3;
+        L.maxBX = L.w - OG_EDGE + 3;
+        L.maxBY = L.h - OG_EDGE + 3;
+        const float width = (float)(L.maxBX - L.minB), height = (float)(L.maxBY - L.minB);
+        const float Wc = 30;
+        L.nCols = (int)(width / Wc);
+        L.nRows = (int)(height / Wc);
+        if (L.nCols < 1 || L.nRows < 1 || L.w < 2 * OG_EDGE + 8 || L.h < 2 * OG_EDGE + 8) {
+            c->err = "pyramid level " + std::to_string(l) + " (" + std::to_string(L.w) + "x" + std::to_string(L.h) +
+                     ") is smaller than one FAST cell: the reference divides by zero here";
+            return ORBGPU_ERR_UNSUPPORTED;
+        }
+        L.wCell = (int)std::ceil(width / L.nCols);
+        L.hCell = (int)std::ceil(height / L.nRows);
+        if (L.wCell > OG_MAX_CELL_W || L.hCell > OG_MAX_CELL_W) {
+            c->err = "cell larger than the LDS tile";
+            return ORBGPU_ERR_UNSUPPORTED;
+        }
+        L.cell_base = (int)cells.size();
+        long long cap = 0;
+        for (int i = 0; i < L.nRows; i++) {
+            const float iniY = (float)(L.minB + i * L.hCell);
+            float maxY = iniY + L.hCell + 6;
+            if (iniY >= L.maxBY - 3) continue;
+            if (maxY > L.maxBY) maxY = (float)L.maxBY;
+            for (int j = 0; j < L.nCols; j++) {
+                const float iniX = (float)(L.minB + j * L.wCell);
+                float maxX = iniX + L.wCell + 6;
+                if (iniX >= L.maxBX - 6) continue;
+                if (maxX > L.maxBX) maxX = (float)L.maxBX;
+                OgCell cd;
+                cd.level = (short)l;
+                cd.i = (short)i;
+                cd.j = (short)j;
+                cd.pad = 0;
+                cd.x0 = (short)(int)iniX;
+                cd.y0 = (short)(int)iniY;
+                cd.x1 = (short)(int)maxX;
+                cd.y1 = (short)(int)maxY;
+                const int dw = cd.x1 - cd.x0 - 6, dh = cd.y1 - cd.y0 - 6;
+                if (dw <= 0 || dh <= 0) continue;
+                cells.push_back(cd);
+                cap += (long long)((dw + 1) / 2) * ((dh + 1) / 2);  // NMS keeps an independent set
+            }
+        }
+        L.ncells = (int)cells.size() - L.cell_base;
+        L.cand_off = cand_off;
+        L.cand_cap = (int)std::max<long long>(cap, 1);
+        cand_off += (L.cand_cap + 31) & ~31;
+        // octree (src/ORBextractor.cc:543-545)
+        L.N = c->nfeat[l];
+        L.nIni = (int)std::round((float)(L.maxBX - L.minB) / (L.maxBY - L.minB));
+        if (L.nIni < 1) {
+            c->err = "image aspect ratio gives zero initial octree nodes (the reference divides by zero)";
+            return ORBGPU_ERR_UNSUPPORTED;
+        }
+        L.hX = (float)(L.maxBX - L.minB) / L.nIni;
+        L.kcap = std::max(L.N + 3, 4 * L.nIni);
+        if (L.kcap > OG_OCT_MAXL - 8) {
+            c->err = "features per level exceed the LDS octree capacity";
+            return ORBGPU_ERR_UNSUPPORTED;
+        }
+        L.koff = koff;
+        koff += L.kcap;
+        L.scale = c->sf[l];
+        L.patch_size = (int)(OG_PATCH * c->sf[l]);
+        // resize tables: cv::resize INTER_LINEAR fixed point (generic path, scalar vertical form)
+        if (l >= 1) {
+            const int sw = pw, sh = ph, dw = L.w, dh = L.h;
+            const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+            const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+            L.xtab_off = (int)tabs.size();
+            L.xmax = dw;
+            for (int dx = 0; dx < dw; dx++) {
+                float fx = (float)((dx + 0.5) * scale_x - 0.5);
+                int sx = (int)std::floor(fx);
+                fx -= (float)sx;
+                if (sx < 0) {
+                    fx = 0.f;
+                    sx = 0;
+                }
+                if (sx + 1 >= sw) {
+                    if (dx < L.xmax) L.xmax = dx;
+                    if (sx >= sw - 1) {
+                        fx = 0.f;
+                        sx = sw - 1;
+                    }
+                }
+                tabs.push_back(make_int4(sx, (short)cv_round((1.f - fx) * 2048), (short)cv_round(fx * 2048), 0));
+            }
+            L.ytab_off = (int)tabs.size();
+            for (int dy = 0; dy < dh; dy++) {
+                float fy = (float)((dy + 0.5) * scale_y - 0.5);
+                int sy = (int)std::floor(fy);
+                fy -= (float)sy;
+                auto clip = [sh](int y) { return y >= 0 ? (y < sh ? y : sh - 1) : 0; };
+                tabs.push_back(make_int4(clip(sy), clip(sy + 1), (short)cv_round((1.f - fy) * 2048),
+                                         (short)cv_round(fy * 2048)));
+            }
+        }
+        pw = L.w;
+        ph = L.h;
+    }
+    P.total_cells = (int)cells.size();
+    P.kcap_total = koff;
+    P.frame_cap = koff;
+    P.cand_per_frame = cand_off;
+    P.pyr_per_frame = std::max<long long>(pyr_off, 256);
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, ensure(c->cells, cells.size()));
+    HIP_TRY(c, ensure(c->tabs, tabs.size()));
+    HIP_TRY(c, hipMemcpyAsync(c->cells.p, cells.data(), cells.size() * sizeof(OgCell), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->tabs.p, tabs.data(), tabs.size() * sizeof(int4), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->plan = P;
+    c->cells_h.swap(cells);
+    c->W = W;
+    c->H = H;
+    c->planned = true;
+    c->Bcap = 0;  // batch buffers must be re-sized for the new plan
+    orbgpu_grid_geom g;
+    orbgpu_grid_geom_for_image(W, H, &g);
+    c->grid_geom = OgGridGeom{g.minX, g.minY, g.maxX, g.maxY, g.invW, g.invH};
+    return ORBGPU_OK;
+}
+
+static int ensure_batch(orbgpu_ctx* c, int B)
+{
+    if (c->Bcap >= B) return ORBGPU_OK;
+    const OgPlan& P = c->plan;
+    const size_t Bn = (size_t)B;
+    HIP_TRY(c, ensure(c->pyr, Bn * (size_t)P.pyr_per_frame));
+    HIP_TRY(c, ensure(c->cand, Bn * (size_t)P.cand_per_frame));
+    HIP_TRY(c, ensure(c->cand_count, Bn * (size_t)P.nlevels));
+    HIP_TRY(c, ensure(c->node_of, Bn * (size_t)P.cand_per_frame));
+    HIP_TRY(c, ensure(c->oct_xy, Bn * (size_t)P.kcap_total));
+    HIP_TRY(c, ensure(c->oct_resp, Bn * (size_t)P.kcap_total));
+    HIP_TRY(c, ensure(c->oct_count, Bn * (size_t)P.nlevels));
+    HIP_TRY(c, ensure(c->kps, Bn * (size_t)P.frame_cap));
+    HIP_TRY(c, ensure(c->desc, Bn * (size_t)P.frame_cap * 32));
+    HIP_TRY(c, ensure(c->counts, Bn));
+    HIP_TRY(c, ensure(c->cell_start, Bn * (OG_GRID_CELLS + 1)));
+    HIP_TRY(c, ensure(c->cell_items, Bn * (size_t)P.frame_cap));
+    HIP_TRY(c, ensure(c->status, 4));
+    c->Bcap = B;
+    return ORBGPU_OK;
+}
+
+// ---- stage timing ---------------------------------------------------------------------------------
+static void timer_begin(orbgpu_ctx* c)
+{
+    c->timer.used = 0;
+    c->timer.names.clear();
+}
+static void timer_mark(orbgpu_ctx* c, const char* name)
+{
+    StageTimer& t = c->timer;
+    if (!t.on) return;
+    if ((int)t.ev.size() <= t.used) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        t.ev.push_back(e);
+    }
+    hipEventRecord(t.ev[t.used++], c->stream);
+    t.names.push_back(name);
+}
+
+static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitch, long long fstride)
+{
+    const OgPlan& P = c->plan;
+    hipStream_t s = c->stream;
+    timer_begin(c);
+    timer_mark(c, "start");
+    HIP_TRY(c, hipMemsetAsync(c->cand_count.p, 0, sizeof(int) * (size_t)B * P.nlevels, s));
+    HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(int) * 4, s));
+    // k1: chained pyramid, src/ORBextractor.cc:1107-1132
+    for (int l = 1; l < P.nlevels; l++) {
+        const OgLevel& L = P.lv[l];
+        const OgLevel& Lp = P.lv[l - 1];
+        const uint8_t* src = l == 1 ? d_imgs : c->pyr.p + Lp.pyr_off;
+        const long long sp = l == 1 ? pitch : Lp.pitch;
+        const long long sfs = l == 1 ? fstride : P.pyr_per_frame;
+        og_launch_resize(s, src, sp, sfs, c->pyr.p + L.pyr_off, L.pitch, P.pyr_per_frame, L.w, L.h,
+                         c->tabs.p + L.xtab_off, c->tabs.p + L.ytab_off, L.xmax, B);
+    }
+    timer_mark(c, "pyramid");
+    og_launch_fast(s, P, c->cells.p, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p, c->status.p, B);
+    timer_mark(c, "fast");
+    og_launch_octree(s, P, c->cand.p, c->cand_count.p, c->node_of.p, c->oct_xy.p, c->oct_resp.p, c->oct_count.p,
+                     c->status.p, B);
+    timer_mark(c, "octree");
+    og_launch_describe(s, P, d_imgs, pitch, fstride, c->pyr.p, c->oct_xy.p, c->oct_resp.p, c->oct_count.p, c->kps.p,
+                       c->desc.p, c->counts.p, B);
+    timer_mark(c, "describe");
+    og_launch_grid(s, c->kps.p, c->counts.p, P.frame_cap, c->grid_geom, c->cell_start.p, c->cell_items.p, B);
+    timer_mark(c, "grid");
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipEventRecord(c->done, s));
+    c->last_img = d_imgs;
+    c->last_pitch = pitch;
+    c->last_fstride = fstride;
+    c->last_B = B;
+    return ORBGPU_OK;
+}
+
+static int collect_timer(orbgpu_ctx* c)
+{
+    StageTimer& t = c->timer;
+    if (!t.on || t.used < 2) return 0;
+    if (hipEventSynchronize(t.ev[t.used - 1]) != hipSuccess) return 0;
+    t.last_ms.clear();
+    t.last_names.clear();
+    for (int i = 1; i < t.used; i++) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, t.ev[i - 1], t.ev[i]);
+        t.last_ms.push_back(ms);
+        t.last_names.push_back(t.names[i]);
+    }
+    return (int)t.last_ms.size();
+}
+
+static int check_status(orbgpu_ctx* c)
+{
+    int st[4] = {0};
+    HIP_TRY(c, hipMemcpyAsync(st, c->status.p, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (st[0]) {
+        c->err = "device capacity guard tripped (status " + std::to_string(st[0]) + ")";
+        return ORBGPU_ERR_INTERNAL;
+    }
+    return ORBGPU_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// extern "C"
+// ------------------------------------------------------------------------------------------------
+extern "C" {
+
+orbgpu_ctx* orbgpu_create(int device, int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+{
+    if (nlevels < 1 || nlevels > OG_MAXLEVELS || nfeatures < 0 || !(scaleFactor > 1.0f)) return nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return nullptr;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    orbgpu_ctx* c = new orbgpu_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess || og_upload_pattern(device) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    c->nfeatures = nfeatures;
+    c->nlevels = nlevels;
+    c->iniTh = iniThFAST;
+    c->minTh = minThFAST;
+    c->scaleFactor = (double)scaleFactor;
+    // src/ORBextractor.cc:415-446
+    c->sf.assign(nlevels, 0.f);
+    c->sig2.assign(nlevels, 0.f);
+    c->isf.assign(nlevels, 0.f);
+    c->isig2.assign(nlevels, 0.f);
+    c->nfeat.assign(nlevels, 0);
+    c->sf[0] = 1.0f;
+    c->sig2[0] = 1.0f;
+    for (int i = 1; i < nlevels; i++) {
+        c->sf[i] = (float)((double)c->sf[i - 1] * c->scaleFactor);
+        c->sig2[i] = c->sf[i] * c->sf[i];
+    }
+    for (int i = 0; i < nlevels; i++) {
+        c->isf[i] = 1.0f / c->sf[i];
+        c->isig2[i] = 1.0f / c->sig2[i];
+    }
+    const float factor = (float)(1.0f / c->scaleFactor);
+    float nd = (float)nfeatures * (1.0f - factor) / (1.0f - (float)std::pow((double)factor, (double)nlevels));
+    int sum = 0;
+    for (int l = 0; l < nlevels - 1; l++) {
+        c->nfeat[l] = cv_round(nd);
+        sum += c->nfeat[l];
+        nd *= factor;
+    }
+    c->nfeat[nlevels - 1] = std::max(nfeatures - sum, 0);
+    // umax, src/ORBextractor.cc:454-469
+    int v, v0;
+    const int vmax = (int)std::floor(OG_HALF_PATCH * std::sqrt(2.f) / 2 + 1);
+    const int vmin = (int)std::ceil(OG_HALF_PATCH * std::sqrt(2.f) / 2);
+    const double hp2 = OG_HALF_PATCH * OG_HALF_PATCH;
+    for (v = 0; v <= vmax; ++v) c->umax[v] = cv_round_d(std::sqrt(hp2 - v * v));
+    for (v = OG_HALF_PATCH, v0 = 0; v >= vmin; --v) {
+        while (c->umax[v0] == c->umax[v0 + 1]) ++v0;
+        c->umax[v] = v0;
+        ++v0;
+    }
+    return c;
+}
+
+void orbgpu_destroy(orbgpu_ctx* c)
+{
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    release(c->cells);
+    release(c->tabs);
+    release(c->pyr);
+    release(c->cand);
+    release(c->cand_count);
+    release(c->node_of);
+    release(c->oct_xy);
+    release(c->oct_resp);
+    release(c->oct_count);
+    release(c->kps);
+    release(c->desc);
+    release(c->counts);
+    release(c->cell_start);
+    release(c->cell_items);
+    release(c->status);
+    release(c->in_img);
+    release(c->mscratch);
+    for (hipEvent_t e : c->timer.ev) hipEventDestroy(e);
+    if (c->done) hipEventDestroy(c->done);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int orbgpu_get_levels(const orbgpu_ctx* c) { return c ? c->nlevels : ORBGPU_ERR_ARG; }
+float orbgpu_get_scale_factor(const orbgpu_ctx* c) { return c ? (float)c->scaleFactor : 0.f; }
+
+static int copy_vec(const orbgpu_ctx* c, const std::vector<float>& v, float* out)
+{
+    if (!c || !out) return ORBGPU_ERR_ARG;
+    std::memcpy(out, v.data(), v.size() * sizeof(float));
+    return ORBGPU_OK;
+}
+int orbgpu_get_scale_factors(const orbgpu_ctx* c, float* out) { return c ? copy_vec(c, c->sf, out) : ORBGPU_ERR_ARG; }
+int orbgpu_get_inverse_scale_factors(const orbgpu_ctx* c, float* out) { return c ? copy_vec(c, c->isf, out) : ORBGPU_ERR_ARG; }
+int orbgpu_get_scale_sigma_squares(const orbgpu_ctx* c, float* out) { return c ? copy_vec(c, c->sig2, out) : ORBGPU_ERR_ARG; }
+int orbgpu_get_inverse_scale_sigma_squares(const orbgpu_ctx* c, float* out)
+{
+    return c ? copy_vec(c, c->isig2, out) : ORBGPU_ERR_ARG;
+}
+int orbgpu_get_features_per_level(const orbgpu_ctx* c, int* out)
+{
+    if (!c || !out) return ORBGPU_ERR_ARG;
+    std::memcpy(out, c->nfeat.data(), c->nfeat.size() * sizeof(int));
+    return ORBGPU_OK;
+}
+
+int orbgpu_max_keypoints(const orbgpu_ctx* c)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    if (c->planned) return c->plan.frame_cap;
+    int s = 0;  // before the first frame: kcap = max(N+3, 4*nIni) with nIni <= 16 assumed
+    for (int l = 0; l < c->nlevels; l++) s += std::max(c->nfeat[l] + 3, 64);
+    return s;
+}
+
+int orbgpu_extract_batch_device(orbgpu_ctx* c, const uint8_t* d_imgs, int B, int cols, int rows, size_t pitch,
+                                size_t frame_stride)
+{
+    if (!c || !d_imgs || B < 1 || cols <= 0 || rows <= 0 || pitch < (size_t)cols) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    int r = build_plan(c, cols, rows);
+    if (r) return r;
+    r = ensure_batch(c, B);
+    if (r) return r;
+    return run_batch(c, d_imgs, B, (long long)pitch, (long long)frame_stride);
+}
+
+int orbgpu_batch_outputs(orbgpu_ctx* c, orbgpu_keypoint** d_kps, uint8_t** d_desc, int** d_counts, int* frame_cap)
+{
+    if (!c || !c->planned || !c->last_B) return ORBGPU_ERR_ARG;
+    if (d_kps) *d_kps = (orbgpu_keypoint*)c->kps.p;
+    if (d_desc) *d_desc = c->desc.p;
+    if (d_counts) *d_counts = c->counts.p;
+    if (frame_cap) *frame_cap = c->plan.frame_cap;
+    return ORBGPU_OK;
+}
+
+int orbgpu_batch_download(orbgpu_ctx* c, int b, orbgpu_keypoint* kps, uint8_t* desc, int cap, int* n)
+{
+    if (!c || !n || b < 0 || b >= c->last_B) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    int r = check_status(c);
+    collect_timer(c);
+    if (r) return r;
+    int cnt = 0;
+    HIP_TRY(c, hipMemcpy(&cnt, c->counts.p + b, sizeof(int), hipMemcpyDeviceToHost));
+    *n = cnt;
+    if (cnt > cap) return ORBGPU_ERR_CAPACITY;
+    const size_t o = (size_t)b * c->plan.frame_cap;
+    if (cnt > 0) {
+        if (kps) HIP_TRY(c, hipMemcpy(kps, c->kps.p + o, (size_t)cnt * sizeof(orbgpu_kp_dev), hipMemcpyDeviceToHost));
+        if (desc) HIP_TRY(c, hipMemcpy(desc, c->desc.p + o * 32, (size_t)cnt * 32, hipMemcpyDeviceToHost));
+    }
+    return ORBGPU_OK;
+}
+
+int orbgpu_extract(orbgpu_ctx* c, const uint8_t* img, int cols, int rows, size_t step, orbgpu_keypoint* kps,
+                   uint8_t* desc, int cap, int* n)
+{
+    if (!c || !n) return ORBGPU_ERR_ARG;
+    if (!img || cols <= 0 || rows <= 0) {  // _image.empty(): return without touching the outputs
+        *n = -1;
+        return ORBGPU_OK;
+    }
+    if (step < (size_t)cols) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t pitch = ((size_t)cols + 63) & ~(size_t)63;
+    HIP_TRY(c, ensure(c->in_img, pitch * (size_t)rows));
+    HIP_TRY(c, hipMemcpy2DAsync(c->in_img.p, pitch, img, step, (size_t)cols, (size_t)rows, hipMemcpyHostToDevice,
+                                c->stream));
+    int r = orbgpu_extract_batch_device(c, c->in_img.p, 1, cols, rows, pitch, pitch * (size_t)rows);
+    if (r) return r;
+    return orbgpu_batch_download(c, 0, kps, desc, cap, n);
+}
+
+int orbgpu_get_level(orbgpu_ctx* c, int level, uint8_t* dst, size_t dst_step, int* cols, int* rows)
+{
+    if (!c || level < 0 || level >= c->nlevels || !c->planned || !c->last_B) return ORBGPU_ERR_ARG;
+    const OgLevel& L = c->plan.lv[level];
+    if (cols) *cols = L.w;
+    if (rows) *rows = L.h;
+    if (!dst) return ORBGPU_OK;
+    if (dst_step < (size_t)L.w) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const uint8_t* src = level == 0 ? c->last_img : c->pyr.p + L.pyr_off;
+    const size_t sp = level == 0 ? (size_t)c->last_pitch : (size_t)L.pitch;
+    HIP_TRY(c, hipMemcpy2DAsync(dst, dst_step, src, sp, (size_t)L.w, (size_t)L.h, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return ORBGPU_OK;
+}
+
+int orbgpu_grid_geom_for_image(int cols, int rows, orbgpu_grid_geom* g)
+{
+    if (!g || cols <= 0 || rows <= 0) return ORBGPU_ERR_ARG;
+    g->minX = 0.0f;
+    g->maxX = (float)cols;
+    g->minY = 0.0f;
+    g->maxY = (float)rows;
+    g->invW = (float)OG_GRID_COLS / (g->maxX - g->minX);
+    g->invH = (float)OG_GRID_ROWS / (g->maxY - g->minY);
+    return ORBGPU_OK;
+}
+
+int orbgpu_descriptor_distance(const uint8_t* a, const uint8_t* b)
+{
+    int dist = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t x, y;
+        std::memcpy(&x, a + 4 * i, 4);
+        std::memcpy(&y, b + 4 * i, 4);
+        dist += __builtin_popcount(x ^ y);
+    }
+    return dist;
+}
+
+// ---- matchers -----------------------------------------------------------------------------------
+static uint8_t* scratch_carve(uint8_t*& cur, size_t bytes)
+{
+    uint8_t* p = cur;
+    cur += (bytes + 255) & ~(size_t)255;
+    return p;
+}
+
+int orbgpu_search_for_initialization(orbgpu_ctx* c, const orbgpu_frame_view* F1, const orbgpu_frame_view* F2,
+                                     float nnratio, int checkOri, float* prev_xy, int* matches12, int windowSize,
+                                     int* nmatches)
+{
+    if (!c || !F1 || !F2 || !prev_xy || !matches12 || !nmatches || F1->n < 0 || F2->n < 0) return ORBGPU_ERR_ARG;
+    if ((F1->n && (!F1->kps || !F1->desc)) || (F2->n && (!F2->kps || !F2->desc))) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const int cap1 = std::max(F1->n, 1), cap2 = std::max(F2->n, 1);
+    const size_t need = 8 * 256 + (size_t)cap1 * (28 + 32 + 8 + 4) + (size_t)cap2 * (28 + 32 + 4) +
+                        (OG_GRID_CELLS + 1) * 4 + 16;
+    HIP_TRY(c, ensure(c->mscratch, need));
+    uint8_t* cur = c->mscratch.p;
+    orbgpu_kp_dev* k1 = (orbgpu_kp_dev*)scratch_carve(cur, (size_t)cap1 * 28);
+    uint8_t* d1 = scratch_carve(cur, (size_t)cap1 * 32);
+    orbgpu_kp_dev* k2 = (orbgpu_kp_dev*)scratch_carve(cur, (size_t)cap2 * 28);
+    uint8_t* d2 = scratch_carve(cur, (size_t)cap2 * 32);
+    int* cnts = (int*)scratch_carve(cur, 16);
+    int* cs = (int*)scratch_carve(cur, (OG_GRID_CELLS + 1) * 4);
+    int* ci = (int*)scratch_carve(cur, (size_t)cap2 * 4);
+    float* pv = (float*)scratch_carve(cur, (size_t)cap1 * 8);
+    int* m12 = (int*)scratch_carve(cur, (size_t)cap1 * 4);
+    int* nm = (int*)scratch_carve(cur, 16);
+    hipStream_t s = c->stream;
+    int hc[2] = {F1->n, F2->n};
+    if (F1->n) {
+        HIP_TRY(c, hipMemcpyAsync(k1, F1->kps, (size_t)F1->n * 28, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(d1, F1->desc, (size_t)F1->n * 32, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(pv, prev_xy, (size_t)F1->n * 8, hipMemcpyHostToDevice, s));
+    }
+    if (F2->n) {
+        HIP_TRY(c, hipMemcpyAsync(k2, F2->kps, (size_t)F2->n * 28, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(d2, F2->desc, (size_t)F2->n * 32, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(c, hipMemcpyAsync(cnts, hc, sizeof(hc), hipMemcpyHostToDevice, s));
+    const OgGridGeom G{F2->grid.minX, F2->grid.minY, F2->grid.maxX, F2->grid.maxY, F2->grid.invW, F2->grid.invH};
+    og_launch_grid(s, k2, cnts + 1, cap2, G, cs, ci, 1);
+    OgFrameDev f1{k1, d1, cnts, nullptr, nullptr, nullptr, cap1};
+    OgFrameDev f2{k2, d2, cnts + 1, cs, ci, nullptr, cap2};
+    og_launch_search_init(s, f1, 0, f2, G, nnratio, checkOri, windowSize, pv, 2 * cap1, m12, cap1, nm, 1);
+    HIP_TRY(c, hipGetLastError());
+    int hnm = 0;
+    HIP_TRY(c, hipMemcpyAsync(&hnm, nm, sizeof(int), hipMemcpyDeviceToHost, s));
+    if (F1->n) {
+        HIP_TRY(c, hipMemcpyAsync(matches12, m12, (size_t)F1->n * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipMemcpyAsync(prev_xy, pv, (size_t)F1->n * 8, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(c, hipStreamSynchronize(s));
+    *nmatches = hnm;
+    return ORBGPU_OK;
+}
+
+int orbgpu_search_for_initialization_batch(orbgpu_ctx* cref, int ref, orbgpu_ctx* c, orbgpu_grid_geom grid,
+                                           float nnratio, int checkOri, int windowSize, float* d_prev_xy,
+                                           int* d_matches12, int* d_nmatches)
+{
+    if (!cref || !c || !cref->last_B || !c->last_B || ref < 0 || ref >= cref->last_B) return ORBGPU_ERR_ARG;
+    if (!d_prev_xy || !d_matches12 || !d_nmatches) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    if (cref != c) HIP_TRY(c, hipStreamWaitEvent(s, cref->done, 0));
+    const OgGridGeom G{grid.minX, grid.minY, grid.maxX, grid.maxY, grid.invW, grid.invH};
+    if (std::memcmp(&G, &c->grid_geom, sizeof(G)) != 0) {
+        c->grid_geom = G;
+        og_launch_grid(s, c->kps.p, c->counts.p, c->plan.frame_cap, G, c->cell_start.p, c->cell_items.p, c->last_B);
+    }
+    OgFrameDev f1{cref->kps.p, cref->desc.p, cref->counts.p, nullptr, nullptr, nullptr, cref->plan.frame_cap};
+    OgFrameDev f2{c->kps.p, c->desc.p, c->counts.p, c->cell_start.p, c->cell_items.p, nullptr, c->plan.frame_cap};
+    timer_mark(c, "match_init");
+    og_launch_search_init(s, f1, ref, f2, G, nnratio, checkOri, windowSize, d_prev_xy, 2 * cref->plan.frame_cap,
+                          d_matches12, cref->plan.frame_cap, d_nmatches, c->last_B);
+    timer_mark(c, "search_init");
+    HIP_TRY(c, hipGetLastError());
+    return ORBGPU_OK;
+}
+
+int orbgpu_search_by_projection(orbgpu_ctx* c, const orbgpu_frame_view* F, const orbgpu_mappoints_view* mp,
+                                float nnratio, float th, int32_t* owner, int32_t* owner_obs, int* nmatches)
+{
+    if (!c || !F || !mp || !owner || !owner_obs || !nmatches || F->n < 0 || mp->m < 0) return ORBGPU_ERR_ARG;
+    if (!F->scale_factors || F->nlevels < 1) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const int n = std::max(F->n, 1), m = std::max(mp->m, 1);
+    // generous bound for the candidate lists: every map point may see every keypoint of its levels;
+    // the count pass gives the exact total, so size the list region after it
+    const size_t fixed = 16 * 256 + (size_t)n * (28 + 32 + 4 + 4 + 4 + 4) + (OG_GRID_CELLS + 1) * 4 +
+                         (size_t)m * (1 + 1 + 4 + 4 + 4 + 4 + 4 + 4 + 32 + 4 + 4 + 4) + 64 + F->nlevels * 4;
+    HIP_TRY(c, ensure(c->mscratch, fixed));
+    uint8_t* cur = c->mscratch.p;
+    orbgpu_kp_dev* k = (orbgpu_kp_dev*)scratch_carve(cur, (size_t)n * 28);
+    uint8_t* d = scratch_carve(cur, (size_t)n * 32);
+    float* ur = (float*)scratch_carve(cur, (size_t)n * 4);
+    int* own = (int*)scratch_carve(cur, (size_t)n * 4);
+    int* obs = (int*)scratch_carve(cur, (size_t)n * 4);
+    int* cnts = (int*)scratch_carve(cur, 16);
+    int* cs = (int*)scratch_carve(cur, (OG_GRID_CELLS + 1) * 4);
+    int* ci = (int*)scratch_carve(cur, (size_t)n * 4);
+    float* sfd = (float*)scratch_carve(cur, (size_t)F->nlevels * 4);
+    uint8_t* tiv = scratch_carve(cur, (size_t)m);
+    uint8_t* bad = scratch_carve(cur, (size_t)m);
+    int* lvl = (int*)scratch_carve(cur, (size_t)m * 4);
+    float* vc = (float*)scratch_carve(cur, (size_t)m * 4);
+    float* px = (float*)scratch_carve(cur, (size_t)m * 4);
+    float* py = (float*)scratch_carve(cur, (size_t)m * 4);
+    float* pxr = (float*)scratch_carve(cur, (size_t)m * 4);
+    int* nobs = (int*)scratch_carve(cur, (size_t)m * 4);
+    uint8_t* md = scratch_carve(cur, (size_t)m * 32);
+    int* cnt = (int*)scratch_carve(cur, (size_t)m * 4);
+    int* off = (int*)scratch_carve(cur, (size_t)(m + 1) * 4);
+    int* nm = (int*)scratch_carve(cur, 16);
+    hipStream_t s = c->stream;
+    if (F->n) {
+        HIP_TRY(c, hipMemcpyAsync(k, F->kps, (size_t)F->n * 28, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(d, F->desc, (size_t)F->n * 32, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(own, owner, (size_t)F->n * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(obs, owner_obs, (size_t)F->n * 4, hipMemcpyHostToDevice, s));
+        if (F->uright) HIP_TRY(c, hipMemcpyAsync(ur, F->uright, (size_t)F->n * 4, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(c, hipMemcpyAsync(sfd, F->scale_factors, (size_t)F->nlevels * 4, hipMemcpyHostToDevice, s));
+    if (mp->m) {
+        HIP_TRY(c, hipMemcpyAsync(tiv, mp->track_in_view, (size_t)mp->m, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(bad, mp->is_bad, (size_t)mp->m, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(lvl, mp->level, (size_t)mp->m * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(vc, mp->view_cos, (size_t)mp->m * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(px, mp->proj_x, (size_t)mp->m * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(py, mp->proj_y, (size_t)mp->m * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(pxr, mp->proj_xr, (size_t)mp->m * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(nobs, mp->n_obs, (size_t)mp->m * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(md, mp->desc, (size_t)mp->m * 32, hipMemcpyHostToDevice, s));
+    }
+    int hc = F->n;
+    HIP_TRY(c, hipMemcpyAsync(cnts, &hc, sizeof(int), hipMemcpyHostToDevice, s));
+    const OgGridGeom G{F->grid.minX, F->grid.minY, F->grid.maxX, F->grid.maxY, F->grid.invW, F->grid.invH};
+    og_launch_grid(s, k, cnts, n, G, cs, ci, 1);
+    OgFrameDev fd{k, d, cnts, cs, ci, F->uright ? ur : nullptr, n};
+    OgMapPointsDev mpd{mp->m, tiv, bad, lvl, vc, px, py, pxr, nobs, md};
+    // exact candidate-list size from a count pass, then the list buffer
+    og_launch_proj_count(s, fd, G, sfd, mpd, th, cnt, off);
+    int total = 0;
+    HIP_TRY(c, hipMemcpyAsync(&total, off + mp->m, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    DevBuf<uint8_t> lists;
+    HIP_TRY(c, ensure(lists, (size_t)std::max(total, 1) * og_proj_cand_size()));
+    og_launch_proj_resolve(s, fd, G, sfd, mpd, nnratio, th, off, (OgProjCand*)lists.p, own, obs, nm);
+    HIP_TRY(c, hipGetLastError());
+    int hnm = 0;
+    HIP_TRY(c, hipMemcpyAsync(&hnm, nm, sizeof(int), hipMemcpyDeviceToHost, s));
+    if (F->n) {
+        HIP_TRY(c, hipMemcpyAsync(owner, own, (size_t)F->n * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipMemcpyAsync(owner_obs, obs, (size_t)F->n * 4, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(c, hipStreamSynchronize(s));
+    release(lists);
+    *nmatches = hnm;
+    return ORBGPU_OK;
+}
+
+int orbgpu_debug_candidates(orbgpu_ctx* c, int b, int level, uint64_t* out, int cap)
+{
+    if (!c || !c->last_B || b < 0 || b >= c->last_B || level < 0 || level >= c->nlevels) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const OgLevel& L = c->plan.lv[level];
+    int n = 0;
+    HIP_TRY(c, hipMemcpy(&n, c->cand_count.p + (size_t)b * c->nlevels + level, sizeof(int), hipMemcpyDeviceToHost));
+    n = std::min(n, L.cand_cap);
+    if (out && cap > 0)
+        HIP_TRY(c, hipMemcpy(out, c->cand.p + (size_t)b * c->plan.cand_per_frame + L.cand_off,
+                             (size_t)std::min(n, cap) * 8, hipMemcpyDeviceToHost));
+    return n;
+}
+
+int orbgpu_debug_octree(orbgpu_ctx* c, int b, int level, uint32_t* xy, uint8_t* resp, int cap)
+{
+    if (!c || !c->last_B || b < 0 || b >= c->last_B || level < 0 || level >= c->nlevels) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const OgLevel& L = c->plan.lv[level];
+    int n = 0;
+    HIP_TRY(c, hipMemcpy(&n, c->oct_count.p + (size_t)b * c->nlevels + level, sizeof(int), hipMemcpyDeviceToHost));
+    const size_t o = (size_t)b * c->plan.kcap_total + L.koff;
+    const int m = std::min(n, cap);
+    if (xy && m > 0) HIP_TRY(c, hipMemcpy(xy, c->oct_xy.p + o, (size_t)m * 4, hipMemcpyDeviceToHost));
+    if (resp && m > 0) HIP_TRY(c, hipMemcpy(resp, c->oct_resp.p + o, (size_t)m, hipMemcpyDeviceToHost));
+    return n;
+}
+
+void* orbgpu_stream(orbgpu_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int orbgpu_synchronize(orbgpu_ctx* c)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return check_status(c);
+}
+
+int orbgpu_set_stage_timing(orbgpu_ctx* c, int on)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    c->timer.on = on != 0;
+    return ORBGPU_OK;
+}
+
+int orbgpu_stage_times(orbgpu_ctx* c, const char** names, float* ms, int cap)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    const int n = collect_timer(c) ? (int)c->timer.last_ms.size() : (int)c->timer.last_ms.size();
+    for (int i = 0; i < n && i < cap; i++) {
+        if (names) names[i] = c->timer.last_names[i];
+        if (ms) ms[i] = c->timer.last_ms[i];
+    }
+    return n;
+}
+
+const char* orbgpu_last_error(const orbgpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void* orbgpu_device_alloc(orbgpu_ctx* c, size_t bytes)
+{
+    if (!c) return nullptr;
+    void* p = nullptr;
+    if (hipSetDevice(c->device) != hipSuccess || hipMalloc(&p, std::max<size_t>(bytes, 1)) != hipSuccess) return nullptr;
+    return p;
+}
+int orbgpu_device_free(orbgpu_ctx* c, void* p)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipFree(p));
+    return ORBGPU_OK;
+}
+int orbgpu_memcpy_h2d(orbgpu_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return ORBGPU_OK;
+}
+int orbgpu_memcpy_d2h(orbgpu_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return ORBGPU_OK;
+}
+int orbgpu_memset_d(orbgpu_ctx* c, void* dst, int value, size_t bytes)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipMemsetAsync(dst, value, bytes, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return ORBGPU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,69 @@
+// orbgpu_internal.h -- shared host/device definitions of the gfx950 ORB pipeline.
+//
+// Layout in HBM (per context, B frames per batch):
+//   pyramid   : levels 1..L-1 of every frame, each row padded to a 64-byte pitch (level 0 is read
+//               in place from the caller's frame buffer -- the reference pads it by 19 px, a region
+//               the hot path never reads, src/ORBextractor.cc:1113-1128).
+//   cand      : per (frame, level) FAST candidate slots, one u64 {x_rel:16, y_rel:16, response:8};
+//               slot capacity = the exact NMS bound of that level (no overflow possible).
+//   node_of   : per candidate u16 node index (octree scratch).
+//   octree out: per (frame, level) up to kcap u32 {x:16, y:16} + u8 response, list order.
+//   kps/desc  : per frame `frame_cap` orbgpu_keypoint (28 B AoS, cv::KeyPoint layout) + 32-B rows.
+#pragma once
+#include <stdint.h>
+
+#define OG_MAXLEVELS 16
+#define OG_EDGE 19
+#define OG_PATCH 31
+#define OG_HALF_PATCH 15
+#define OG_GRID_COLS 64
+#define OG_GRID_ROWS 48
+#define OG_GRID_CELLS (OG_GRID_COLS * OG_GRID_ROWS)
+#define OG_OCT_MAXL 1024   // max octree list length handled in LDS (N_l + 3 + slack)
+#define OG_MAX_CELL_W 64   // wCell <= 59 for any width (nCols = floor(w/30))
+
+struct OgLevel {
+    int w, h;              // level size
+    int pitch;             // bytes per row in the pyramid buffer (levels >= 1)
+    long long pyr_off;     // byte offset of the level inside one frame's pyramid block (levels >= 1)
+    // FAST cell grid, src/ORBextractor.cc:773-787
+    int minB, maxBX, maxBY;
+    int nCols, nRows, wCell, hCell;
+    int cell_base, ncells; // into the flat cell table
+    // octree, src/ORBextractor.cc:539-563
+    int N;                 // mnFeaturesPerLevel
+    int nIni;
+    float hX;
+    int kcap;              // octree output capacity of the level
+    int koff;              // offset of the level's octree slots inside a frame
+    long long cand_off;    // offset (entries) of the level's candidate slots inside a frame
+    int cand_cap;
+    // resize tables (levels >= 1), src/ORBextractor.cc:1120 -> cv::resize INTER_LINEAR
+    int xtab_off, ytab_off, xmax;
+    float scale;           // mvScaleFactor[l]
+    int patch_size;        // (int)(PATCH_SIZE * mvScaleFactor[l])
+};
+
+struct OgCell {            // one FAST cell ROI, src/ORBextractor.cc:789-829
+    short level, i, j, pad;
+    short x0, y0, x1, y1;  // ROI [x0,x1) x [y0,y1) in level pixels
+};
+
+struct OgPlan {
+    int nlevels;
+    int iniTh, minTh;
+    int total_cells;
+    int kcap_total;        // sum of kcap (octree slots per frame)
+    int frame_cap;         // final keypoints per frame (== kcap_total)
+    long long cand_per_frame;
+    long long pyr_per_frame;   // bytes
+    int umax[16];
+    OgLevel lv[OG_MAXLEVELS];
+};
+
+// packed FAST candidate
+__host__ __device__ inline unsigned long long og_pack_cand(int x, int y, int resp)
+{
+    return (unsigned long long)(unsigned)(x & 0xffff) | ((unsigned long long)(unsigned)(y & 0xffff) << 16) |
+           ((unsigned long long)(unsigned)(resp & 0xff) << 32);
+}

@@ -1,0 +1,67 @@
+// orbgpu_launch.h -- host-side launchers of the gfx950 kernels (implemented in the .hip files).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "orbgpu_internal.h"
+
+struct orbgpu_kp_dev {  // == orbgpu_keypoint == cv::KeyPoint (28 B)
+    float x, y, size, angle, response;
+    int octave, class_id;
+};
+
+struct OgGridGeom {
+    float minX, minY, maxX, maxY, invW, invH;
+};
+
+hipError_t og_upload_pattern(int device);
+
+void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,
+                      long long dst_pitch, long long dst_fstride, int dw, int dh, const int4* xtab, const int4* ytab,
+                      int xmax, int B);
+void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,
+                    long long fstride0, const uint8_t* pyr, unsigned long long* cand, int* cand_count, int* status,
+                    int B);
+void og_launch_octree(hipStream_t s, const OgPlan& P, const unsigned long long* cand, const int* cand_count,
+                      uint16_t* node_of, uint32_t* oct_xy, uint8_t* oct_resp, int* oct_count, int* status, int B);
+void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, long long pitch0, long long fstride0,
+                        const uint8_t* pyr, const uint32_t* oct_xy, const uint8_t* oct_resp, const int* oct_count,
+                        orbgpu_kp_dev* kps, uint8_t* desc, int* counts, int B);
+void og_launch_grid(hipStream_t s, const orbgpu_kp_dev* kps, const int* counts, int frame_cap, OgGridGeom G,
+                    int* cell_start, int* cell_items, int B);
+
+// matchers (orb_match.hip)
+struct OgFrameDev {        // device view of one or many frames (batch stride frame_cap)
+    const orbgpu_kp_dev* kps;
+    const uint8_t* desc;
+    const int* counts;     // per frame
+    const int* cell_start; // per frame OG_GRID_CELLS+1
+    const int* cell_items; // per frame frame_cap
+    const float* uright;   // per frame frame_cap, or nullptr
+    int frame_cap;
+};
+
+void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G, float nnratio,
+                           int checkOri, int windowSize, float* prev_xy, int prev_stride, int* matches12,
+                           int match_stride, int* nmatches, int B);
+
+struct OgMapPointsDev {
+    int m;
+    const uint8_t* track_in_view;
+    const uint8_t* is_bad;
+    const int* level;
+    const float* view_cos;
+    const float* proj_x;
+    const float* proj_y;
+    const float* proj_xr;
+    const int* n_obs;
+    const uint8_t* desc;
+};
+
+struct OgProjCand;
+size_t og_proj_cand_size();
+void og_launch_proj_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, float th,
+                          int* cnt, int* off);
+void og_launch_proj_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp,
+                            float nnratio, float th, const int* off, OgProjCand* cands, int* owner, int* owner_obs,
+                            int* nmatches);

@@ -1,0 +1,110 @@
+"""Python mirror of ORB_SLAM2::ORBmatcher (include/ORBmatcher.h:37-102) and of the Frame fields the
+per-frame matchers read (src/Frame.cc), over the gfx950 C ABI."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .extractor import KP_DTYPE, ORBextractor
+
+FRAME_GRID_COLS, FRAME_GRID_ROWS = 64, 48  # include/Frame.h:39-40
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class Frame:
+    """The subset of ORB_SLAM2::Frame the hot path produces and the matchers consume: mvKeysUn (no
+    distortion -> == mvKeys), mDescriptors, mvuRight, mvScaleFactors and the image bounds/grid scales."""
+
+    def __init__(self, keypoints, descriptors, cols: int, rows: int, scale_factors, uright=None):
+        self.mvKeysUn = np.ascontiguousarray(keypoints, dtype=KP_DTYPE)
+        self.mvKeys = self.mvKeysUn
+        self.mDescriptors = np.ascontiguousarray(descriptors, dtype=np.uint8)
+        self.mvScaleFactors = np.ascontiguousarray(scale_factors, dtype=np.float32)
+        self.N = len(self.mvKeysUn)
+        self.mvuRight = None if uright is None else np.ascontiguousarray(uright, np.float32)
+        g = _lib.GridGeom()
+        _lib.check(None, _lib.lib().orbgpu_grid_geom_for_image(cols, rows, C.byref(g)), "grid_geom")
+        self.grid = g
+
+    @classmethod
+    def from_image(cls, extractor: ORBextractor, image: np.ndarray):
+        k, d = extractor(image)
+        return cls(k, d, image.shape[1], image.shape[0], extractor.GetScaleFactors())
+
+    def view(self) -> _lib.FrameView:
+        v = _lib.FrameView()
+        v.n = self.N
+        v.kps = _p(self.mvKeysUn).value if self.N else None
+        v.desc = _p(self.mDescriptors).value if self.N else None
+        v.uright = None if self.mvuRight is None else _p(self.mvuRight).value
+        v.grid = self.grid
+        v.scale_factors = _p(self.mvScaleFactors).value
+        v.nlevels = len(self.mvScaleFactors)
+        return v
+
+
+class ORBmatcher:
+    TH_LOW, TH_HIGH, HISTO_LENGTH = 50, 100, 30  # src/ORBmatcher.cc:37-39
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, context: ORBextractor | None = None,
+                 device: int = 0):
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+        # HIP stream + scratch come from an extractor context (any will do)
+        self._own = context is None
+        self._ex = context if context is not None else ORBextractor(1000, 1.2, 8, 20, 7, device=device)
+
+    @staticmethod
+    def DescriptorDistance(a, b) -> int:
+        a = np.ascontiguousarray(a, np.uint8)
+        b = np.ascontiguousarray(b, np.uint8)
+        return _lib.lib().orbgpu_descriptor_distance(_p(a), _p(b))
+
+    def SearchForInitialization(self, F1: Frame, F2: Frame, vbPrevMatched: np.ndarray, windowSize: int = 10):
+        """Returns (nmatches, vnMatches12); vbPrevMatched (N1 x 2 float32) is updated in place."""
+        assert vbPrevMatched.dtype == np.float32 and vbPrevMatched.flags.c_contiguous
+        assert vbPrevMatched.shape == (F1.N, 2)
+        m12 = np.full(max(F1.N, 1), -1, np.int32)
+        nm = C.c_int(0)
+        v1, v2 = F1.view(), F2.view()
+        ctx = self._ex.ctx
+        rc = _lib.lib().orbgpu_search_for_initialization(ctx, C.byref(v1), C.byref(v2), self.mfNNratio,
+                                                         int(self.mbCheckOrientation), _p(vbPrevMatched),
+                                                         _p(m12), windowSize, C.byref(nm))
+        _lib.check(ctx, rc, "orbgpu_search_for_initialization")
+        return nm.value, m12[:F1.N].copy()
+
+    def SearchByProjection(self, F: Frame, mappoints: dict, th: float = 3.0, owner=None, owner_obs=None):
+        """mappoints: dict of SoA arrays (track_in_view, is_bad, level, view_cos, proj_x, proj_y,
+        proj_xr, n_obs, desc).  owner/owner_obs mirror F.mvpMapPoints.  Returns (nmatches, owner,
+        owner_obs)."""
+        n = F.N
+        owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+        owner_obs = (np.zeros(n, np.int32) if owner_obs is None
+                     else np.ascontiguousarray(owner_obs, np.int32).copy())
+        arrs = dict(track_in_view=np.ascontiguousarray(mappoints["track_in_view"], np.uint8),
+                    is_bad=np.ascontiguousarray(mappoints["is_bad"], np.uint8),
+                    level=np.ascontiguousarray(mappoints["level"], np.int32),
+                    view_cos=np.ascontiguousarray(mappoints["view_cos"], np.float32),
+                    proj_x=np.ascontiguousarray(mappoints["proj_x"], np.float32),
+                    proj_y=np.ascontiguousarray(mappoints["proj_y"], np.float32),
+                    proj_xr=np.ascontiguousarray(mappoints["proj_xr"], np.float32),
+                    n_obs=np.ascontiguousarray(mappoints["n_obs"], np.int32),
+                    desc=np.ascontiguousarray(mappoints["desc"], np.uint8))
+        mv = _lib.MapPointsView()
+        mv.m = len(arrs["level"])
+        for k, v in arrs.items():
+            setattr(mv, k, _p(v).value if v.size else None)
+        fv = F.view()
+        nm = C.c_int(0)
+        ctx = self._ex.ctx
+        rc = _lib.lib().orbgpu_search_by_projection(ctx, C.byref(fv), C.byref(mv), self.mfNNratio, th,
+                                                    _p(owner) if n else None, _p(owner_obs) if n else None,
+                                                    C.byref(nm))
+        _lib.check(ctx, rc, "orbgpu_search_by_projection")
+        return nm.value, owner, owner_obs
