@@ -132,6 +132,10 @@ int orbgpu_search_for_initialization_batch(orbgpu_ctx* ctx_ref, int ref, orbgpu_
                                            int windowSize, float* d_prev_xy, int* d_matches12,
                                            int* d_nmatches);
 
+/* vbPrevMatched[i] = F1.mvKeysUn[i].pt for every frame of ctx's last batch (src/Tracking.cc:573-575),
+ * device-side, into d_prev_xy laid out as in orbgpu_search_for_initialization_batch. */
+int orbgpu_prev_matched_from_frame(orbgpu_ctx* ctx_ref, int ref, orbgpu_ctx* ctx, float* d_prev_xy);
+
 /* Map points as seen by SearchByProjection (MapPoint fields, include/MapPoint.h:91-99, snapshot
  * gathered under the reference's per-point mutexes). */
 typedef struct {
@@ -181,6 +185,10 @@ int orbgpu_device_free(orbgpu_ctx* ctx, void* p);
 int orbgpu_memcpy_h2d(orbgpu_ctx* ctx, void* dst, const void* src, size_t bytes);
 int orbgpu_memcpy_d2h(orbgpu_ctx* ctx, void* dst, const void* src, size_t bytes);
 int orbgpu_memset_d(orbgpu_ctx* ctx, void* dst, int value, size_t bytes);
+/* Asynchronous device-to-device copy on the context stream. */
+int orbgpu_memcpy_d2d_async(orbgpu_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* Total FAST candidates of the last batch (all frames, all levels); synchronises.  < 0 on error. */
+long long orbgpu_batch_candidate_total(orbgpu_ctx* ctx);
 
 #ifdef __cplusplus
 }

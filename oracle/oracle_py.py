@@ -45,6 +45,8 @@ def lib():
         L.oo_level_image.argtypes = [vp, i32]
         L.oo_level_candidates.restype = i32
         L.oo_level_candidates.argtypes = [vp, i32, vp, vp, i32]
+        L.oo_distribute_octree.restype = i32
+        L.oo_distribute_octree.argtypes = [vp, vp, i32, i32, i32, i32, i32, i32, vp, vp]
         L.oo_resize_linear.argtypes = [vp, i32, i32, vp, i32, i32]
         L.oo_gaussian7.argtypes = [vp, i32, i32, vp]
         L.oo_fast_score.restype = i32
@@ -198,6 +200,16 @@ def search_by_projection(f: OracleFrame, mp: dict, nnratio=0.8, th=3.0, owner=No
         setattr(s, k, _p(v).value)
     nm = lib().oo_search_by_projection(C.byref(f._s), C.byref(s), nnratio, th, _p(owner), _p(owner_obs))
     return nm, owner, owner_obs
+
+
+def distribute_octree(xy, resp, minX, maxX, minY, maxY, N):
+    xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+    resp = np.ascontiguousarray(resp, np.float32)
+    cap = max(len(resp), N + 3, 64) + 64
+    oxy = np.zeros((cap, 2), np.float32)
+    orr = np.zeros(cap, np.float32)
+    m = lib().oo_distribute_octree(_p(xy), _p(resp), len(resp), minX, maxX, minY, maxY, N, _p(oxy), _p(orr))
+    return oxy[:m].copy(), orr[:m].copy()
 
 
 def descriptor_distance(a, b) -> int:

@@ -672,6 +672,26 @@ int oo_extract(oo_extractor* e, const uint8_t* img, int cols, int rows, int step
     return total;
 }
 
+int oo_distribute_octree(const float* xy, const float* resp, int n, int minX, int maxX, int minY, int maxY,
+                         int N, float* out_xy, float* out_resp)
+{
+    oo_candvec in = {0, 0, 0};
+    for (int i = 0; i < n; i++) {
+        oo_cand c = {xy[2 * i], xy[2 * i + 1], resp[i]};
+        cv_push(&in, c);
+    }
+    oo_cand* out = (oo_cand*)malloc(sizeof(oo_cand) * (size_t)(n + 1));
+    const int m = oo_distribute(&in, minX, maxX, minY, maxY, N, out);
+    for (int i = 0; i < m; i++) {
+        out_xy[2 * i] = out[i].x;
+        out_xy[2 * i + 1] = out[i].y;
+        out_resp[i] = out[i].resp;
+    }
+    free(out);
+    free(in.v);
+    return m;
+}
+
 int oo_level_size(const oo_extractor* e, int level, int* cols, int* rows)
 {
     if (level < 0 || level >= e->nlevels) return -1;

@@ -49,6 +49,11 @@ const uint8_t* oo_level_image(const oo_extractor* e, int level);       /* unpadd
  * response).  Returns the count; writes at most cap. */
 int oo_level_candidates(const oo_extractor* e, int level, float* xy, float* resp, int cap);
 
+/* DistributeOctTree on an explicit candidate list (x,y relative to minBorder, in vToDistributeKeys
+ * order).  out_xy/out_resp need room for max(N+3, 4*nIni, n) entries.  Returns the output count. */
+int oo_distribute_octree(const float* xy, const float* resp, int n, int minX, int maxX, int minY, int maxY,
+                         int N, float* out_xy, float* out_resp);
+
 /* Single-primitive entry points (used by tests to pin pieces). */
 void oo_resize_linear(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh);
 void oo_gaussian7(const uint8_t* src, int w, int h, uint8_t* dst);

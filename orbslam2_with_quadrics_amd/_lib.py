@@ -23,7 +23,8 @@ EXPORTS = [
     "orbgpu_search_by_projection", "orbgpu_stream", "orbgpu_synchronize", "orbgpu_set_stage_timing",
     "orbgpu_stage_times", "orbgpu_last_error", "orbgpu_debug_candidates", "orbgpu_debug_octree",
     "orbgpu_device_alloc", "orbgpu_device_free", "orbgpu_memcpy_h2d", "orbgpu_memcpy_d2h",
-    "orbgpu_memset_d",
+    "orbgpu_memset_d", "orbgpu_prev_matched_from_frame", "orbgpu_memcpy_d2d_async",
+    "orbgpu_batch_candidate_total",
 ]
 
 OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
@@ -94,6 +95,10 @@ def _declare(L):
     L.orbgpu_memcpy_h2d.argtypes = [vp, vp, vp, sz]
     L.orbgpu_memcpy_d2h.argtypes = [vp, vp, vp, sz]
     L.orbgpu_memset_d.argtypes = [vp, vp, i32, sz]
+    L.orbgpu_prev_matched_from_frame.argtypes = [vp, i32, vp, vp]
+    L.orbgpu_memcpy_d2d_async.argtypes = [vp, vp, vp, sz]
+    L.orbgpu_batch_candidate_total.restype = C.c_longlong
+    L.orbgpu_batch_candidate_total.argtypes = [vp]
 
 
 def lib(load_torch_first: bool = True):

@@ -255,6 +255,26 @@ void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2,
                        windowSize, prev_xy, prev_stride, matches12, match_stride, nmatches);
 }
 
+// Tracking::MonocularInitialization (src/Tracking.cc:573-575): vbPrevMatched[i] = F1.mvKeysUn[i].pt,
+// replicated for every frame of a batch.
+__global__ __launch_bounds__(256) void og_prev_from_frame_kernel(OgFrameDev F1, int ref, float* prev_xy,
+                                                                 int prev_stride)
+{
+    const int b = blockIdx.y;
+    const int n1 = F1.counts[ref];
+    const orbgpu_kp_dev* K1 = F1.kps + (long long)ref * F1.frame_cap;
+    float* PV = prev_xy + (long long)b * prev_stride;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n1; i += gridDim.x * blockDim.x) {
+        PV[2 * i] = K1[i].x;
+        PV[2 * i + 1] = K1[i].y;
+    }
+}
+
+void og_launch_prev_from_frame(hipStream_t s, OgFrameDev F1, int ref, float* prev_xy, int prev_stride, int B)
+{
+    hipLaunchKernelGGL(og_prev_from_frame_kernel, dim3(4, B), dim3(256), 0, s, F1, ref, prev_xy, prev_stride);
+}
+
 // ------------------------------------------------------------------------------------------------
 // SearchByProjection(Frame&, const vector<MapPoint*>&, th)
 // ------------------------------------------------------------------------------------------------

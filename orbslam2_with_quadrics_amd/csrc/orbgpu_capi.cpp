@@ -681,6 +681,17 @@ int orbgpu_search_for_initialization_batch(orbgpu_ctx* cref, int ref, orbgpu_ctx
     return ORBGPU_OK;
 }
 
+int orbgpu_prev_matched_from_frame(orbgpu_ctx* cref, int ref, orbgpu_ctx* c, float* d_prev_xy)
+{
+    if (!cref || !c || !cref->last_B || !c->last_B || ref < 0 || ref >= cref->last_B || !d_prev_xy) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (cref != c) HIP_TRY(c, hipStreamWaitEvent(c->stream, cref->done, 0));
+    OgFrameDev f1{cref->kps.p, cref->desc.p, cref->counts.p, nullptr, nullptr, nullptr, cref->plan.frame_cap};
+    og_launch_prev_from_frame(c->stream, f1, ref, d_prev_xy, 2 * cref->plan.frame_cap, c->last_B);
+    HIP_TRY(c, hipGetLastError());
+    return ORBGPU_OK;
+}
+
 int orbgpu_search_by_projection(orbgpu_ctx* c, const orbgpu_frame_view* F, const orbgpu_mappoints_view* mp,
                                 float nnratio, float th, int32_t* owner, int32_t* owner_obs, int* nmatches)
 {
@@ -848,6 +859,25 @@ int orbgpu_memcpy_d2h(orbgpu_ctx* c, void* dst, const void* src, size_t bytes)
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return ORBGPU_OK;
 }
+int orbgpu_memcpy_d2d_async(orbgpu_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    return ORBGPU_OK;
+}
+
+long long orbgpu_batch_candidate_total(orbgpu_ctx* c)
+{
+    if (!c || !c->last_B) return ORBGPU_ERR_ARG;
+    if (hipSetDevice(c->device) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) return ORBGPU_ERR_HIP;
+    std::vector<int> cc((size_t)c->last_B * c->nlevels);
+    if (hipMemcpy(cc.data(), c->cand_count.p, cc.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+        return ORBGPU_ERR_HIP;
+    long long t = 0;
+    for (int v : cc) t += v;
+    return t;
+}
+
 int orbgpu_memset_d(orbgpu_ctx* c, void* dst, int value, size_t bytes)
 {
     if (!c) return ORBGPU_ERR_ARG;

@@ -45,6 +45,8 @@ void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2,
                            int checkOri, int windowSize, float* prev_xy, int prev_stride, int* matches12,
                            int match_stride, int* nmatches, int B);
 
+void og_launch_prev_from_frame(hipStream_t s, OgFrameDev F1, int ref, float* prev_xy, int prev_stride, int B);
+
 struct OgMapPointsDev {
     int m;
     const uint8_t* track_in_view;

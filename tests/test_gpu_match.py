@@ -1,0 +1,174 @@
+"""GPU parity tests of the matchers: SearchForInitialization and SearchByProjection (through the C
+ABI) against the CPU oracle -- match indices, counts and updated state must be identical."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from orbslam2_with_quadrics_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _pair(gpu, oracle, pid, rows, cols, nf, shift=(7, 3)):
+    f1, f2 = synthetic.frame_pair(pid, rows, cols, shift)
+    ex = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
+    k1, d1 = ex(f1)
+    k2, d2 = ex(f2)
+    return ex, k1, d1, k2, d2
+
+
+@pytest.mark.parametrize("pid,rows,cols,nf", [(21, 1080, 1920, 2000), (22, 480, 640, 1000)])
+def test_search_for_initialization_golden(gpu, oracle, pid, rows, cols, nf):
+    ex, k1, d1, k2, d2 = _pair(gpu, oracle, pid, rows, cols, nf)
+    sf = ex.GetScaleFactors()
+    F1, F2 = gpu.Frame(k1, d1, cols, rows, sf), gpu.Frame(k2, d2, cols, rows, sf)
+    prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+    m = gpu.ORBmatcher(0.9, True, context=ex)
+    n, m12 = m.SearchForInitialization(F1, F2, prev, 100)
+    g = {c["pair_id"]: c for c in json.load(open(os.path.join(ROOT, "tests/golden/match_golden.json")))["cases"]}
+    assert n == g[pid]["nmatches"]
+    assert hashlib.sha256(m12.astype(np.int32).tobytes()).hexdigest() == g[pid]["matches_sha256"]
+    assert hashlib.sha256(prev.tobytes()).hexdigest() == g[pid]["prev_sha256"]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_search_for_initialization_vs_oracle_variants(gpu, oracle, seed):
+    rng = np.random.default_rng(seed)
+    shift = (int(rng.integers(-20, 20)), int(rng.integers(-20, 20)))
+    ex, k1, d1, k2, d2 = _pair(gpu, oracle, 50 + seed, 480, 640, 1000, shift)
+    sf = ex.GetScaleFactors()
+    # duplicate some F2 descriptors to force equal distances and steals
+    d2 = d2.copy()
+    d2[5:40:3] = d2[4:39:3]
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    win = int(rng.choice([10, 50, 100, 200]))
+    ratio = float(rng.choice([0.6, 0.9]))
+    ori = bool(seed % 2)
+    G1, G2 = gpu.Frame(k1, d1, 640, 480, sf), gpu.Frame(k2, d2, 640, 480, sf)
+    pg = np.ascontiguousarray(prev.copy())
+    n, m12 = gpu.ORBmatcher(ratio, ori, context=ex).SearchForInitialization(G1, G2, pg, win)
+    O1, O2 = oracle.OracleFrame(k1, d1, 640, 480, sf), oracle.OracleFrame(k2, d2, 640, 480, sf)
+    no, mo, po = oracle.search_for_initialization(O1, O2, prev, ratio, ori, win)
+    assert n == no
+    assert np.array_equal(m12, mo)
+    assert np.array_equal(pg, po)
+
+
+def _mappoints(rng, k, d, M, levels_ok=True):
+    src = rng.integers(0, len(k), M)
+    desc = d[src].copy()
+    flips = rng.random((M, 256)) < 0.05
+    desc ^= np.packbits(flips, axis=1)
+    return dict(track_in_view=np.ones(M, np.uint8), is_bad=np.zeros(M, np.uint8),
+                level=k["octave"][src].astype(np.int32),
+                view_cos=rng.uniform(0.9, 1.0, M).astype(np.float32),
+                proj_x=(k["x"][src] + rng.normal(0, 1, M)).astype(np.float32),
+                proj_y=(k["y"][src] + rng.normal(0, 1, M)).astype(np.float32),
+                proj_xr=np.full(M, -1, np.float32), n_obs=np.full(M, 2, np.int32), desc=desc)
+
+
+@pytest.mark.parametrize("th", [1.0, 3.0, 5.0])
+def test_search_by_projection_vs_oracle(gpu, oracle, th):
+    rng = np.random.default_rng(int(th * 10))
+    img = synthetic.frame(60, 1080, 1920)
+    ex = gpu.ORBextractor(4000, 1.2, 8, 20, 7)
+    k, d = ex(img)
+    mp = _mappoints(rng, k, d, 5000)
+    mp["n_obs"][::7] = 0  # some points without observations: they do not block later points
+    mp["track_in_view"][::11] = 0
+    mp["is_bad"][::13] = 1
+    sf = ex.GetScaleFactors()
+    F = gpu.Frame(k, d, 1920, 1080, sf)
+    n, own, obs = gpu.ORBmatcher(0.8, context=ex).SearchByProjection(F, mp, th)
+    no, owo, obo = oracle.search_by_projection(oracle.OracleFrame(k, d, 1920, 1080, sf), mp, 0.8, th)
+    assert n == no
+    assert np.array_equal(own, owo)
+    assert np.array_equal(obs, obo)
+
+
+def test_search_by_projection_stereo_and_preclaimed(gpu, oracle):
+    rng = np.random.default_rng(3)
+    img = synthetic.frame(61, 376, 1241)
+    ex = gpu.ORBextractor(2000, 1.2, 8, 20, 7)
+    k, d = ex(img)
+    mp = _mappoints(rng, k, d, 1500)
+    mp["proj_xr"] = (mp["proj_x"] - 30 + rng.normal(0, 2, len(mp["proj_x"]))).astype(np.float32)
+    uright = np.where(rng.random(len(k)) < 0.5, k["x"] - 30, -1).astype(np.float32)
+    owner0 = np.where(rng.random(len(k)) < 0.2, 7777, -1).astype(np.int32)
+    obs0 = ((owner0 >= 0) & (rng.random(len(k)) < 0.5)).astype(np.int32)
+    sf = ex.GetScaleFactors()
+    F = gpu.Frame(k, d, 1241, 376, sf, uright=uright)
+    n, own, obs = gpu.ORBmatcher(0.8, context=ex).SearchByProjection(F, mp, 3.0, owner0, obs0)
+    no, owo, obo = oracle.search_by_projection(oracle.OracleFrame(k, d, 1241, 376, sf, uright=uright), mp, 0.8, 3.0,
+                                               owner0, obs0)
+    assert n == no
+    assert np.array_equal(own, owo)
+    assert np.array_equal(obs, obo)
+
+
+def test_descriptor_distance(gpu, oracle):
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        a = rng.integers(0, 256, 32, dtype=np.uint8)
+        b = rng.integers(0, 256, 32, dtype=np.uint8)
+        assert gpu.ORBmatcher.DescriptorDistance(a, b) == oracle.descriptor_distance(a, b)
+
+
+def test_batch_search_for_initialization(gpu, oracle):
+    """Device-resident batch: frame 0 of a reference context is F1 for every frame of a batch."""
+    import ctypes as C
+
+    from orbslam2_with_quadrics_amd import _lib
+
+    rows, cols, B = 480, 640, 5
+    scene = synthetic.make_scene(synthetic.SEED_BASE + 77, rows, cols)
+    f1 = synthetic.render(scene, rows, cols, 0, 0, noise_seed=1)
+    frames = np.stack([synthetic.render(scene, rows, cols, 3 * b, 2 * b, noise_seed=10 + b) for b in range(B)])
+    exr = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    exb = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    d1 = exr.device_alloc(f1.nbytes)
+    db = exb.device_alloc(frames.nbytes)
+    exr.h2d(d1, f1)
+    exb.h2d(db, frames)
+    exr.extract_batch_device(d1, 1, cols, rows, cols, f1.nbytes)
+    exb.extract_batch_device(db, B, cols, rows, cols, rows * cols)
+    k1, de1 = exr.batch_download(0)
+    _, _, _, cap = exr.batch_outputs()
+    prev = np.zeros((B, cap, 2), np.float32)
+    prev[:, :len(k1), 0] = k1["x"]
+    prev[:, :len(k1), 1] = k1["y"]
+    d_prev = exb.device_alloc(prev.nbytes)
+    d_m = exb.device_alloc(B * cap * 4)
+    d_n = exb.device_alloc(B * 4)
+    exb.h2d(d_prev, prev)
+    g = _lib.GridGeom()
+    _lib.lib().orbgpu_grid_geom_for_image(cols, rows, C.byref(g))
+    rc = _lib.lib().orbgpu_search_for_initialization_batch(exr.ctx, 0, exb.ctx, g, 0.9, 1, 100,
+                                                           C.c_void_p(d_prev), C.c_void_p(d_m), C.c_void_p(d_n))
+    _lib.check(exb.ctx, rc, "batch")
+    exb.synchronize()
+    m_all = np.zeros((B, cap), np.int32)
+    n_all = np.zeros(B, np.int32)
+    p_all = np.zeros_like(prev)
+    exb.d2h(m_all, d_m)
+    exb.d2h(n_all, d_n)
+    exb.d2h(p_all, d_prev)
+    oe = oracle.OracleExtractor(1000)
+    ko1, do1 = oe(f1)
+    sf = exr.GetScaleFactors()
+    O1 = oracle.OracleFrame(ko1, do1, cols, rows, sf)
+    for b in range(B):
+        k2, dd2 = oe(frames[b])
+        O2 = oracle.OracleFrame(k2, dd2, cols, rows, sf)
+        no, mo, po = oracle.search_for_initialization(O1, O2, np.stack([ko1["x"], ko1["y"]], 1), 0.9, True, 100)
+        assert n_all[b] == no
+        assert np.array_equal(m_all[b, :len(ko1)], mo)
+        assert np.array_equal(p_all[b, :len(ko1)], po)
+    for p in (d1, db):
+        exr.device_free(p)
+    for p in (d_prev, d_m, d_n):
+        exb.device_free(p)

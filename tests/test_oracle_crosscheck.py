@@ -1,0 +1,139 @@
+"""CPU tests: the C oracle against independent pure-Python restatements (tests/refpy.py) on small
+adversarial inputs -- octree ties, FAST-cell fallbacks, matcher steals/claims/equal distances."""
+import numpy as np
+import pytest
+
+import refpy
+
+
+def _rand_cands(rng, n, W, H, resp_levels=4, dup_resp=True):
+    # distinct integer positions, responses drawn from a tiny set to force ties
+    pos = set()
+    while len(pos) < n:
+        pos.add((int(rng.integers(3, W - 3)), int(rng.integers(3, H - 3))))
+    pos = sorted(pos, key=lambda p: (rng.random(),))
+    resp = rng.integers(7, 7 + resp_levels, size=n) if dup_resp else rng.integers(7, 250, size=n)
+    return [(float(x), float(y), float(r)) for (x, y), r in zip(pos, resp)]
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_octree_matches_python_list_semantics(oracle, seed):
+    rng = np.random.default_rng(seed)
+    W = int(rng.integers(60, 700))
+    H = int(rng.integers(40, 400))
+    n = int(rng.integers(1, 600))
+    N = int(rng.integers(1, 260))
+    keys = _rand_cands(rng, min(n, (W - 6) * (H - 6) // 2), W, H, dup_resp=seed % 2 == 0)
+    minX, minY = 16, 16
+    maxX, maxY = minX + W, minY + H
+    if round(W / H) < 1:
+        pytest.skip("nIni == 0 divides by zero in the reference")
+    want = refpy.distribute_octree(keys, minX, maxX, minY, maxY, N)
+    xy = np.array([[k[0], k[1]] for k in keys], np.float32)
+    resp = np.array([k[2] for k in keys], np.float32)
+    gxy, gr = oracle.distribute_octree(xy, resp, minX, maxX, minY, maxY, N)
+    got = [(float(a), float(b), float(c)) for (a, b), c in zip(gxy, gr)]
+    assert got == [(float(np.float32(a)), float(np.float32(b)), float(np.float32(c))) for a, b, c in want]
+
+
+def test_octree_clustered_keys_degenerate_splits(oracle):
+    """Keys packed into a few tight clusters: many splits produce a single child."""
+    rng = np.random.default_rng(99)
+    keys = []
+    seen = set()
+    for cx, cy in [(100, 50), (101, 52), (400, 300), (401, 300), (402, 301)]:
+        for _ in range(30):
+            p = (cx + int(rng.integers(-3, 4)), cy + int(rng.integers(-3, 4)))
+            if p not in seen:
+                seen.add(p)
+                keys.append((float(p[0]), float(p[1]), float(rng.integers(7, 9))))
+    for N in (3, 10, 40, 200):
+        want = refpy.distribute_octree(keys, 16, 16 + 640, 16, 16 + 400, N)
+        xy = np.array([[k[0], k[1]] for k in keys], np.float32)
+        resp = np.array([k[2] for k in keys], np.float32)
+        gxy, gr = oracle.distribute_octree(xy, resp, 16, 16 + 640, 16, 16 + 400, N)
+        assert [(float(a), float(b), float(c)) for (a, b), c in zip(gxy, gr)] == \
+               [(float(a), float(b), float(c)) for a, b, c in want]
+
+
+def _small_frame(oracle, rng, n, cols=320, rows=240, levels=3):
+    from orbslam2_with_quadrics_amd.extractor import KP_DTYPE
+
+    k = np.zeros(n, KP_DTYPE)
+    k["x"] = rng.uniform(0, cols, n).astype(np.float32)
+    k["y"] = rng.uniform(0, rows, n).astype(np.float32)
+    k["octave"] = rng.integers(0, levels, n)
+    k["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+    k["size"] = 31
+    k["class_id"] = -1
+    # a handful of descriptor prototypes so that distances tie and ratio tests bite
+    protos = rng.integers(0, 256, size=(6, 32), dtype=np.uint8)
+    d = protos[rng.integers(0, 6, n)].copy()
+    flips = rng.random((n, 256)) < 0.04
+    d ^= np.packbits(flips, axis=1)
+    return k, d
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_search_for_initialization_matches_python(oracle, seed):
+    rng = np.random.default_rng(100 + seed)
+    cols, rows = 320, 240
+    sf = np.array([1.0, 1.2, 1.44], np.float32)
+    k1, d1 = _small_frame(oracle, rng, 150, cols, rows)
+    k2, d2 = _small_frame(oracle, rng, 170, cols, rows)
+    d2[:60] = d1[:60]  # shared descriptors -> competing claims (steals)
+    k2["x"][:60] = np.clip(k1["x"][:60] + rng.normal(0, 3, 60), 0, cols - 1)
+    k2["y"][:60] = np.clip(k1["y"][:60] + rng.normal(0, 3, 60), 0, rows - 1)
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    win = int(rng.choice([10, 40, 100]))
+    F1, F2 = oracle.OracleFrame(k1, d1, cols, rows, sf), oracle.OracleFrame(k2, d2, cols, rows, sf)
+    n, m12, p2 = oracle.search_for_initialization(F1, F2, prev, 0.9, True, win)
+    P1, P2 = refpy.PyFrame(k1, d1, cols, rows, sf), refpy.PyFrame(k2, d2, cols, rows, sf)
+    n_r, m12_r, p2_r = refpy.search_for_initialization(P1, P2, prev, 0.9, True, win)
+    assert n == n_r
+    assert np.array_equal(m12, m12_r)
+    assert np.array_equal(p2, p2_r)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_search_by_projection_matches_python(oracle, seed):
+    rng = np.random.default_rng(200 + seed)
+    cols, rows = 320, 240
+    sf = np.array([1.0, 1.2, 1.44], np.float32)
+    k, d = _small_frame(oracle, rng, 220, cols, rows)
+    M = 180
+    src = rng.integers(0, len(k), M)
+    mp = dict(track_in_view=(rng.random(M) < 0.9).astype(np.uint8),
+              is_bad=(rng.random(M) < 0.05).astype(np.uint8),
+              level=k["octave"][src].astype(np.int32),
+              view_cos=rng.choice([0.9985, 0.999, 0.95], M).astype(np.float32),
+              proj_x=(k["x"][src] + rng.normal(0, 1.5, M)).astype(np.float32),
+              proj_y=(k["y"][src] + rng.normal(0, 1.5, M)).astype(np.float32),
+              proj_xr=(k["x"][src] - 20).astype(np.float32),
+              n_obs=rng.integers(0, 3, M).astype(np.int32),
+              desc=d[src].copy())
+    uright = np.where(rng.random(len(k)) < 0.3, k["x"] - 20 + rng.normal(0, 2, len(k)), -1).astype(np.float32)
+    owner0 = np.where(rng.random(len(k)) < 0.1, 999, -1).astype(np.int32)
+    obs0 = (owner0 >= 0).astype(np.int32) * (rng.random(len(k)) < 0.5)
+    th = float(rng.choice([1.0, 3.0, 5.0]))
+    F = oracle.OracleFrame(k, d, cols, rows, sf, uright=uright)
+    n, own, obs = oracle.search_by_projection(F, mp, 0.8, th, owner0, obs0)
+    P = refpy.PyFrame(k, d, cols, rows, sf, uright=uright)
+    n_r, own_r, obs_r = refpy.search_by_projection(P, mp, 0.8, th, owner0, obs0)
+    assert n == n_r
+    assert np.array_equal(own, own_r)
+    assert np.array_equal(obs, obs_r)
+
+
+def test_features_in_area_matches_python(oracle):
+    rng = np.random.default_rng(7)
+    cols, rows = 640, 480
+    sf = np.array([1.0, 1.2, 1.44], np.float32)
+    k, d = _small_frame(oracle, rng, 400, cols, rows)
+    F = oracle.OracleFrame(k, d, cols, rows, sf)
+    P = refpy.PyFrame(k, d, cols, rows, sf)
+    for _ in range(300):
+        x, y = float(rng.uniform(-50, cols + 50)), float(rng.uniform(-50, rows + 50))
+        r = float(rng.choice([2.5, 10, 37.3, 100]))
+        lo, hi = int(rng.integers(-1, 3)), int(rng.integers(-1, 3))
+        assert F.features_in_area(x, y, r, lo, hi).tolist() == P.features_in_area(x, y, r, lo, hi)

@@ -1,0 +1,153 @@
+"""CPU tests: pin the oracle's pieces against everything that can be checked without the reference
+binary (which needs OpenCV/Eigen/Pangolin and cannot be built here -- DESIGN.md §4)."""
+import hashlib
+import json
+import math
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import refpy
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def test_scale_tables_match_survey(oracle):
+    """src/ORBextractor.cc:410-470 -- per-level budgets quoted in SURVEY.md §8 and umax."""
+    t = oracle.OracleExtractor(1000).tables()
+    assert t["features_per_level"].tolist() == [217, 181, 151, 126, 105, 87, 73, 60]
+    t2 = oracle.OracleExtractor(2000).tables()
+    assert t2["features_per_level"].tolist() == [434, 362, 302, 251, 209, 175, 145, 122]
+    t4 = oracle.OracleExtractor(4000).tables()
+    assert t4["features_per_level"][0] == 869
+    assert t["umax"].tolist() == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+    # float(float*double) chain of src/ORBextractor.cc:421 (double member scaleFactor)
+    sf = [np.float32(1.0)]
+    for _ in range(7):
+        sf.append(np.float32(np.float64(sf[-1]) * np.float64(np.float32(1.2))))
+    assert np.array_equal(t["scale"], np.array(sf, np.float32))
+
+
+def test_gaussian_kernel_table():
+    """cvRound(256 * getGaussianKernel(7, 2)) -> the 257-sum integer kernel the oracle/GPU use."""
+    x = np.arange(7) - 3.0
+    t = np.exp(-0.125 * x * x)
+    k = (t / t.sum()).astype(np.float32)
+    ik = [int(np.rint(np.float64(v) * 256)) for v in k]
+    assert ik == [18, 34, 49, 55, 49, 34, 18]
+
+
+def test_fast_score_matches_definition(oracle):
+    """cornerScore<16> == largest threshold for which the segment test still passes."""
+    rng = np.random.default_rng(1)
+    checked = corners = 0
+    for trial in range(1500):
+        patch = rng.integers(0, 256, size=(7, 7)).astype(np.uint8)
+        if trial % 3 == 0:  # force arcs so that corners are common
+            s = rng.integers(0, 16)
+            ln = rng.integers(8, 13)
+            val = rng.integers(0, 256)
+            for k in range(ln):
+                dx, dy = refpy.CIRCLE[(s + k) % 16]
+                patch[3 + dy, 3 + dx] = val
+        img = np.zeros((13, 13), np.uint8)
+        img[3:10, 3:10] = patch
+        got = oracle.fast_score(img, 6, 6)
+        want = refpy.fast_score_definition(patch)
+        assert got == want, (patch, got, want)
+        checked += 1
+        corners += want >= 0
+    assert corners > 300
+
+
+def test_sincosf_restatement_exhaustive_sample(tmp_path):
+    """oracle glibc-sincosf restatement vs this host's libm (every 61st float in [0, 8))."""
+    exe = tmp_path / "verify_sincosf"
+    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-fopenmp",
+                           os.path.join(ROOT, "tools", "verify_sincosf.c"), "-o", str(exe), "-lm"])
+    out = subprocess.check_output([str(exe), "61"]).decode()
+    assert out.strip().endswith("mismatches 0"), out
+
+
+def test_sincos_golden_vectors(oracle):
+    """Golden (angle -> sin, cos) pairs produced by libm sincosf (tests/golden/make_golden.py)."""
+    g = json.load(open(os.path.join(GOLDEN, "sincosf.json")))
+    for a, s, c in g["vectors"]:
+        gs, gc = oracle.sincos(np.float32(a))
+        assert np.float32(gs) == np.float32(s) and np.float32(gc) == np.float32(c)
+
+
+def test_fastatan2_accuracy_and_quadrants(oracle):
+    assert oracle.fastatan2(0.0, 0.0) == 0.0
+    assert oracle.fastatan2(1.0, 0.0) == 90.0
+    assert oracle.fastatan2(0.0, -1.0) == 180.0
+    assert oracle.fastatan2(-1.0, 0.0) == 270.0
+    rng = np.random.default_rng(5)
+    for _ in range(2000):
+        y, x = (float(v) for v in rng.integers(-200000, 200000, 2))
+        a = oracle.fastatan2(y, x)
+        ref = math.degrees(math.atan2(y, x)) % 360.0
+        d = abs(a - ref)
+        assert min(d, 360 - d) < 0.02
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/src/ORBextractor.cc"), reason="reference absent")
+def test_pattern_matches_reference_source():
+    """The committed rBRIEF pattern equals bit_pattern_31_ (src/ORBextractor.cc:150-408)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_orb_pattern
+
+    ref = gen_orb_pattern.parse()
+    for inc in ("oracle/orb_pattern.inc", "orbslam2_with_quadrics_amd/csrc/orb_pattern.inc"):
+        txt = open(os.path.join(ROOT, inc)).read()
+        body = txt[txt.index("{") + 1: txt.index("};")]
+        vals = [int(v) for v in re.findall(r"-?\d+", body)]
+        assert vals == ref, inc
+
+
+def test_pattern_copies_identical():
+    a = open(os.path.join(ROOT, "oracle/orb_pattern.inc")).read()
+    b = open(os.path.join(ROOT, "orbslam2_with_quadrics_amd/csrc/orb_pattern.inc")).read()
+    assert a == b
+
+
+def _have_fma():
+    try:
+        return " fma " in open("/proc/cpuinfo").read().replace("\n", " ")
+    except OSError:
+        return False
+
+
+@pytest.mark.skipif(not _have_fma(), reason="host CPU has no FMA: the reference build would not contract")
+def test_descriptor_rotation_contraction_probe(tmp_path):
+    """GCC -O3 -march=native fuses the rBRIEF sample rotation (src/ORBextractor.cc:118-120) as
+    fma(x,b,y*a) / fma(x,a,-(y*b)); the oracle and the GPU write exactly those forms."""
+    src = tmp_path / "probe.cc"
+    src.write_text(open(os.path.join(ROOT, "tools", "probe_contraction.cc")).read())
+    exe = tmp_path / "probe"
+    subprocess.check_call(["g++", "-O3", "-march=native", "-std=c++11", str(src), "-o", str(exe)])
+    out = subprocess.check_output([str(exe)]).decode()
+    assert "fused-first-product mismatches 0" in out, out
+
+
+def test_oracle_golden_extraction(oracle):
+    """Regression pin of the oracle on committed golden fixtures (hash of keypoints + descriptors)."""
+    from orbslam2_with_quadrics_amd import synthetic
+
+    g = json.load(open(os.path.join(GOLDEN, "extract_golden.json")))
+    for case in g["cases"]:
+        img = synthetic.frame(case["frame_id"], case["rows"], case["cols"])
+        assert hashlib.sha256(img.tobytes()).hexdigest() == case["image_sha256"]
+        k, d = oracle.OracleExtractor(case["nfeatures"])(img)
+        assert len(k) == case["n"]
+        assert hashlib.sha256(k.tobytes()).hexdigest() == case["kps_sha256"]
+        assert hashlib.sha256(d.tobytes()).hexdigest() == case["desc_sha256"]
+        head = np.array(case["head"], np.float64)
+        assert np.array_equal(np.stack([k["x"], k["y"], k["angle"], k["response"]], 1)[:len(head)]
+                              .astype(np.float64), head)
