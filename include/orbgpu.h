@@ -70,7 +70,7 @@ int orbgpu_max_keypoints(const orbgpu_ctx* ctx);
 
 /* Backs the public member std::vector<cv::Mat> mvImagePyramid (include/ORBextractor.h:85), read by
  * Frame::ComputeStereoMatches (src/Frame.cc:473,563,575,580): lazy download of level `level` of the
- * LAST frame processed (frame 0 of the last batch).  dst==NULL only queries *cols/*rows. */
+ * LAST frame processed (frame 0 of the last batch).  dst==NULL only queries the level size. */
 int orbgpu_get_level(orbgpu_ctx* ctx, int level, uint8_t* dst, size_t dst_step, int* cols, int* rows);
 
 /* ---- batched, device-resident extraction (MI355X-native extension; same per-frame result) --- */
