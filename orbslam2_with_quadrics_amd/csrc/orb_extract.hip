@@ -116,10 +116,47 @@ __device__ __forceinline__ int og_fast_M(const uint8_t* p, int st)
 }
 
 #define OG_ROI_MAX (OG_MAX_CELL_W + 6)
+#define OG_RS 72  // LDS row stride of the ROI tile: circle offsets become compile-time immediates
 
-__device__ __forceinline__ bool og_nms_keep(const uint8_t* Ms, int dw, int dh, int i, int j, int t)
+// exact M of the pixel at p (ROI tile with stride OG_RS)
+__device__ __forceinline__ int og_fast_M_tile(const uint8_t* p) { return og_fast_M(p, OG_RS); }
+
+// OpenCV FAST_t quick rejection (src: cv::FAST, pairs {k, k+8}): a pixel can only be a corner at
+// threshold t if for every opposite pair one pixel is darker than v-t (resp. brighter than v+t).
+// Necessary condition => every pixel that fails it has M <= t.
+__device__ __forceinline__ bool og_fast_quick(const uint8_t* p, int t)
 {
-    const int m = Ms[i * dw + j];
+    const int v = p[0];
+    const int lo = v - t, hi = v + t;
+    int c[16];
+    c[0] = p[3 * OG_RS];
+    c[1] = p[1 + 3 * OG_RS];
+    c[2] = p[2 + 2 * OG_RS];
+    c[3] = p[3 + 1 * OG_RS];
+    c[4] = p[3];
+    c[5] = p[3 - 1 * OG_RS];
+    c[6] = p[2 - 2 * OG_RS];
+    c[7] = p[1 - 3 * OG_RS];
+    c[8] = p[-3 * OG_RS];
+    c[9] = p[-1 - 3 * OG_RS];
+    c[10] = p[-2 - 2 * OG_RS];
+    c[11] = p[-3 - 1 * OG_RS];
+    c[12] = p[-3];
+    c[13] = p[-3 + 1 * OG_RS];
+    c[14] = p[-2 + 2 * OG_RS];
+    c[15] = p[-1 + 3 * OG_RS];
+    bool dark = true, bright = true;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        dark &= (c[k] < lo) | (c[k + 8] < lo);
+        bright &= (c[k] > hi) | (c[k + 8] > hi);
+    }
+    return dark | bright;
+}
+
+__device__ __forceinline__ bool og_nms_keep(const uint8_t* Ms, int i, int j, int dw, int dh, int t)
+{
+    const int m = Ms[i * OG_MAX_CELL_W + j];
     if (m <= t) return false;
     const int s = m - 1;
 #pragma unroll
@@ -130,7 +167,7 @@ __device__ __forceinline__ bool og_nms_keep(const uint8_t* Ms, int dw, int dh, i
             const int ii = i + di, jj = j + dj;
             int nb = 0;
             if (ii >= 0 && ii < dh && jj >= 0 && jj < dw) {
-                const int mn = Ms[ii * dw + jj];
+                const int mn = Ms[ii * OG_MAX_CELL_W + jj];
                 nb = mn > t ? mn - 1 : 0;
             }
             if (!(s > nb)) return false;
@@ -144,8 +181,9 @@ __global__ __launch_bounds__(64) void og_fast_cells_kernel(OgPlan P, const OgCel
                                                            u64* __restrict__ cand, int* __restrict__ cand_count,
                                                            int* __restrict__ status)
 {
-    __shared__ uint8_t roi[OG_ROI_MAX * OG_ROI_MAX];
-    __shared__ uint8_t Ms[OG_MAX_CELL_W * OG_MAX_CELL_W];
+    __shared__ __attribute__((aligned(16))) uint8_t roi[OG_ROI_MAX * OG_RS + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t Ms[OG_MAX_CELL_W * OG_MAX_CELL_W];
+    __shared__ uint16_t lst[OG_MAX_CELL_W * OG_MAX_CELL_W];
     const int f = blockIdx.y;
     const OgCell cd = cells[blockIdx.x];
     const int l = cd.level;
@@ -163,34 +201,72 @@ __global__ __launch_bounds__(64) void og_fast_cells_kernel(OgPlan P, const OgCel
     const int rw = cd.x1 - cd.x0, rh = cd.y1 - cd.y0;
     const int dw = rw - 6, dh = rh - 6;
     if (dw <= 0 || dh <= 0) return;
-    for (int r = 0; r < rh; r++) {
-        const uint8_t* srow = img + (long long)(cd.y0 + r) * pitch + cd.x0;
-        for (int c = lane; c < rw; c += 64) roi[r * rw + c] = srow[c];
+    // ---- ROI -> LDS with aligned dword loads (row r of the ROI at roi + r*OG_RS + sh)
+    {
+        // each row: dwords covering [x0, x1) from the aligned address below x0
+        for (int r = lane >> 4; r < rh; r += 4) {
+            const uint8_t* src = img + (long long)(cd.y0 + r) * pitch + cd.x0;
+            const int mis = (int)((uintptr_t)src & 3);
+            const uint32_t* s4 = (const uint32_t*)(src - mis);
+            const int nd = (rw + mis + 3) >> 2;
+            for (int q = lane & 15; q < nd; q += 16) {
+                const uint32_t w = s4[q];
+                // bytes q*4 - mis .. q*4 - mis + 3 of the row
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const int c = q * 4 + b - mis;
+                    if (c >= 0 && c < rw) roi[r * OG_RS + c] = (uint8_t)(w >> (8 * b));
+                }
+            }
+        }
+    }
+    // zero the score map of the detection area
+    for (int idx = lane * 4; idx < dh * OG_MAX_CELL_W; idx += 256) *(uint32_t*)&Ms[idx] = 0u;
+    __syncthreads();
+    const int t1 = min(max(P.iniTh, 0), 255), t2 = min(max(P.minTh, 0), 255);
+    const int tq = min(t1, t2);
+    // ---- stage 1: quick test on every detection pixel, ballot-compacted survivor list
+    int nsurv = 0;
+    const bool two = dw <= 32;
+    const int rowsPer = two ? 2 : 1;
+    const int li = two ? (lane >> 5) : 0, lj = two ? (lane & 31) : lane;
+    for (int i0 = 0; i0 < dh; i0 += rowsPer) {
+        const int i = i0 + li, j = lj;
+        bool sv = false;
+        if (i < dh && j < dw) sv = og_fast_quick(&roi[(i + 3) * OG_RS + (j + 3)], tq);
+        const u64 mask = __ballot(sv);
+        if (sv) lst[nsurv + __popcll(mask & ((1ull << lane) - 1ull))] = (uint16_t)(i * OG_MAX_CELL_W + j);
+        nsurv += __popcll(mask);
     }
     __syncthreads();
-    const int npx = dw * dh;
-    for (int idx = lane; idx < npx; idx += 64) {
-        const int i = idx / dw, j = idx - (idx / dw) * dw;
-        Ms[idx] = (uint8_t)og_fast_M(&roi[(i + 3) * rw + (j + 3)], rw);
+    if (nsurv == 0) return;
+    // ---- stage 2: exact M for the survivors (full-wave utilisation)
+    for (int e = lane; e < nsurv; e += 64) {
+        const int pix = lst[e];
+        const int i = pix / OG_MAX_CELL_W, j = pix % OG_MAX_CELL_W;
+        Ms[pix] = (uint8_t)og_fast_M_tile(&roi[(i + 3) * OG_RS + (j + 3)]);
     }
     __syncthreads();
-    int t = min(max(P.iniTh, 0), 255);
+    // ---- stage 3: NMS at iniThFAST; if the cell is empty, at minThFAST (src/ORBextractor.cc:809-816)
+    int t = t1;
     int cnt = 0;
-    for (int idx = lane; idx - lane < npx; idx += 64) {
+    for (int e0 = 0; e0 < nsurv; e0 += 64) {
+        const int e = e0 + lane;
         bool keep = false;
-        if (idx < npx) {
-            const int i = idx / dw, j = idx - (idx / dw) * dw;
-            keep = og_nms_keep(Ms, dw, dh, i, j, t);
+        if (e < nsurv) {
+            const int pix = lst[e];
+            keep = og_nms_keep(Ms, pix / OG_MAX_CELL_W, pix % OG_MAX_CELL_W, dw, dh, t);
         }
         cnt += __popcll(__ballot(keep));
     }
     if (cnt == 0) {
-        t = min(max(P.minTh, 0), 255);
-        for (int idx = lane; idx - lane < npx; idx += 64) {
+        t = t2;
+        for (int e0 = 0; e0 < nsurv; e0 += 64) {
+            const int e = e0 + lane;
             bool keep = false;
-            if (idx < npx) {
-                const int i = idx / dw, j = idx - (idx / dw) * dw;
-                keep = og_nms_keep(Ms, dw, dh, i, j, t);
+            if (e < nsurv) {
+                const int pix = lst[e];
+                keep = og_nms_keep(Ms, pix / OG_MAX_CELL_W, pix % OG_MAX_CELL_W, dw, dh, t);
             }
             cnt += __popcll(__ballot(keep));
         }
@@ -204,21 +280,20 @@ __global__ __launch_bounds__(64) void og_fast_cells_kernel(OgPlan P, const OgCel
         return;
     }
     u64* out = cand + (long long)f * P.cand_per_frame + L.cand_off + base;
-    int run = 0;
-    // ROI origin relative to minBorder: x_rel = (x0 - minB) + j + 3
     const int ox = cd.x0 - L.minB + 3, oy = cd.y0 - L.minB + 3;
-    for (int idx = lane; idx - lane < npx; idx += 64) {
+    int run = 0;
+    for (int e0 = 0; e0 < nsurv; e0 += 64) {
+        const int e = e0 + lane;
         bool keep = false;
-        int i = 0, j = 0;
-        if (idx < npx) {
-            i = idx / dw;
-            j = idx - i * dw;
-            keep = og_nms_keep(Ms, dw, dh, i, j, t);
+        int pix = 0;
+        if (e < nsurv) {
+            pix = lst[e];
+            keep = og_nms_keep(Ms, pix / OG_MAX_CELL_W, pix % OG_MAX_CELL_W, dw, dh, t);
         }
         const u64 mask = __ballot(keep);
         if (keep) {
             const int pos = run + __popcll(mask & ((1ull << lane) - 1ull));
-            out[pos] = og_pack_cand(ox + j, oy + i, Ms[idx] - 1);
+            out[pos] = og_pack_cand(ox + pix % OG_MAX_CELL_W, oy + pix / OG_MAX_CELL_W, Ms[pix] - 1);
         }
         run += __popcll(mask);
     }
