@@ -175,20 +175,25 @@ __device__ __forceinline__ bool og_nms_keep(const uint8_t* Ms, int i, int j, int
     return true;
 }
 
-__global__ __launch_bounds__(64) void og_fast_cells_kernel(OgPlan P, const OgCell* __restrict__ cells,
-                                                           const uint8_t* __restrict__ img0, long long pitch0,
-                                                           long long fstride0, const uint8_t* __restrict__ pyr,
-                                                           u64* __restrict__ cand, int* __restrict__ cand_count,
-                                                           int* __restrict__ status)
+#define FAST_NT 256
+
+// One 256-thread workgroup (4 waves) per FAST cell: the cell's ROI, score map and survivor list live in
+// LDS shared by the four waves (full occupancy at ~17 KB per workgroup).
+__global__ __launch_bounds__(FAST_NT) void og_fast_cells_kernel(OgPlan P, const OgCell* __restrict__ cells,
+                                                                const uint8_t* __restrict__ img0, long long pitch0,
+                                                                long long fstride0, const uint8_t* __restrict__ pyr,
+                                                                u64* __restrict__ cand, int* __restrict__ cand_count,
+                                                                int* __restrict__ status)
 {
     __shared__ __attribute__((aligned(16))) uint8_t roi[OG_ROI_MAX * OG_RS + 16];
     __shared__ __attribute__((aligned(16))) uint8_t Ms[OG_MAX_CELL_W * OG_MAX_CELL_W];
     __shared__ uint16_t lst[OG_MAX_CELL_W * OG_MAX_CELL_W];
+    __shared__ int sh_n[4];  // 0: survivors, 1: keep count, 2: emission base, 3: emission cursor
     const int f = blockIdx.y;
     const OgCell cd = cells[blockIdx.x];
     const int l = cd.level;
     const OgLevel& L = P.lv[l];
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
     const uint8_t* img;
     long long pitch;
     if (l == 0) {
@@ -201,89 +206,91 @@ __global__ __launch_bounds__(64) void og_fast_cells_kernel(OgPlan P, const OgCel
     const int rw = cd.x1 - cd.x0, rh = cd.y1 - cd.y0;
     const int dw = rw - 6, dh = rh - 6;
     if (dw <= 0 || dh <= 0) return;
-    // ---- ROI -> LDS with aligned dword loads (row r of the ROI at roi + r*OG_RS + sh)
-    {
-        // each row: dwords covering [x0, x1) from the aligned address below x0
-        for (int r = lane >> 4; r < rh; r += 4) {
-            const uint8_t* src = img + (long long)(cd.y0 + r) * pitch + cd.x0;
-            const int mis = (int)((uintptr_t)src & 3);
-            const uint32_t* s4 = (const uint32_t*)(src - mis);
-            const int nd = (rw + mis + 3) >> 2;
-            for (int q = lane & 15; q < nd; q += 16) {
-                const uint32_t w = s4[q];
-                // bytes q*4 - mis .. q*4 - mis + 3 of the row
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const int c = q * 4 + b - mis;
-                    if (c >= 0 && c < rw) roi[r * OG_RS + c] = (uint8_t)(w >> (8 * b));
-                }
-            }
+    if (tid < 4) sh_n[tid] = 0;
+    // ---- ROI -> LDS.  Fast path: 4-byte aligned rows -> whole dwords land at roi + r*OG_RS + 4q and
+    // the ROI origin sits `mis` bytes into every LDS row.
+    const uint8_t* row0 = img + (long long)cd.y0 * pitch + cd.x0;
+    const int mis = (int)((uintptr_t)row0 & 3);
+    const bool aligned_rows = ((pitch & 3) == 0);
+    uint8_t* T = roi + (aligned_rows ? mis : 0);  // T[r*OG_RS + c] = ROI pixel (r, c)
+    if (aligned_rows) {
+        const int nd = (rw + mis + 3) >> 2;
+        for (int r = tid >> 4; r < rh; r += FAST_NT / 16) {
+            const uint32_t* s4 = (const uint32_t*)(row0 + (long long)r * pitch - mis);
+            for (int q = tid & 15; q < nd; q += 16) *(uint32_t*)&roi[r * OG_RS + 4 * q] = s4[q];
+        }
+    } else {
+        for (int r = tid >> 6; r < rh; r += FAST_NT / 64) {
+            const uint8_t* src = row0 + (long long)r * pitch;
+            for (int c = lane; c < rw; c += 64) roi[r * OG_RS + c] = src[c];
         }
     }
-    // zero the score map of the detection area
-    for (int idx = lane * 4; idx < dh * OG_MAX_CELL_W; idx += 256) *(uint32_t*)&Ms[idx] = 0u;
+    for (int idx = tid * 4; idx < dh * OG_MAX_CELL_W; idx += FAST_NT * 4) *(uint32_t*)&Ms[idx] = 0u;
     __syncthreads();
     const int t1 = min(max(P.iniTh, 0), 255), t2 = min(max(P.minTh, 0), 255);
     const int tq = min(t1, t2);
     // ---- stage 1: quick test on every detection pixel, ballot-compacted survivor list
-    int nsurv = 0;
-    const bool two = dw <= 32;
-    const int rowsPer = two ? 2 : 1;
-    const int li = two ? (lane >> 5) : 0, lj = two ? (lane & 31) : lane;
-    for (int i0 = 0; i0 < dh; i0 += rowsPer) {
-        const int i = i0 + li, j = lj;
-        bool sv = false;
-        if (i < dh && j < dw) sv = og_fast_quick(&roi[(i + 3) * OG_RS + (j + 3)], tq);
-        const u64 mask = __ballot(sv);
-        if (sv) lst[nsurv + __popcll(mask & ((1ull << lane) - 1ull))] = (uint16_t)(i * OG_MAX_CELL_W + j);
-        nsurv += __popcll(mask);
+    {
+        const bool two = dw <= 32;
+        const int rowsPer = two ? FAST_NT / 32 : FAST_NT / 64;
+        const int li = two ? (tid >> 5) : (tid >> 6), lj = two ? (tid & 31) : lane;
+        for (int i0 = 0; i0 < dh; i0 += rowsPer) {
+            const int i = i0 + li, j = lj;
+            bool sv = false;
+            if (i < dh && j < dw) sv = og_fast_quick(&T[(i + 3) * OG_RS + (j + 3)], tq);
+            const u64 mask = __ballot(sv);
+            if (mask) {
+                int base = 0;
+                if (lane == 0) base = atomicAdd(&sh_n[0], __popcll(mask));
+                base = __shfl(base, 0);
+                if (sv) lst[base + __popcll(mask & ((1ull << lane) - 1ull))] = (uint16_t)(i * OG_MAX_CELL_W + j);
+            }
+        }
     }
     __syncthreads();
+    const int nsurv = sh_n[0];
     if (nsurv == 0) return;
-    // ---- stage 2: exact M for the survivors (full-wave utilisation)
-    for (int e = lane; e < nsurv; e += 64) {
+    // ---- stage 2: exact M for the survivors only
+    for (int e = tid; e < nsurv; e += FAST_NT) {
         const int pix = lst[e];
         const int i = pix / OG_MAX_CELL_W, j = pix % OG_MAX_CELL_W;
-        Ms[pix] = (uint8_t)og_fast_M_tile(&roi[(i + 3) * OG_RS + (j + 3)]);
+        Ms[pix] = (uint8_t)og_fast_M_tile(&T[(i + 3) * OG_RS + (j + 3)]);
     }
     __syncthreads();
     // ---- stage 3: NMS at iniThFAST; if the cell is empty, at minThFAST (src/ORBextractor.cc:809-816)
-    int t = t1;
-    int cnt = 0;
-    for (int e0 = 0; e0 < nsurv; e0 += 64) {
-        const int e = e0 + lane;
-        bool keep = false;
-        if (e < nsurv) {
-            const int pix = lst[e];
-            keep = og_nms_keep(Ms, pix / OG_MAX_CELL_W, pix % OG_MAX_CELL_W, dw, dh, t);
-        }
-        cnt += __popcll(__ballot(keep));
-    }
-    if (cnt == 0) {
-        t = t2;
-        for (int e0 = 0; e0 < nsurv; e0 += 64) {
-            const int e = e0 + lane;
+    auto count_keep = [&](int tt) {
+        int c = 0;
+        for (int e = tid; e - tid < nsurv; e += FAST_NT) {
             bool keep = false;
             if (e < nsurv) {
                 const int pix = lst[e];
-                keep = og_nms_keep(Ms, pix / OG_MAX_CELL_W, pix % OG_MAX_CELL_W, dw, dh, t);
+                keep = og_nms_keep(Ms, pix / OG_MAX_CELL_W, pix % OG_MAX_CELL_W, dw, dh, tt);
             }
-            cnt += __popcll(__ballot(keep));
+            c += __popcll(__ballot(keep));
         }
+        if (lane == 0 && c) atomicAdd(&sh_n[1], c);
+        __syncthreads();
+        return sh_n[1];
+    };
+    int t = t1;
+    int cnt = count_keep(t);
+    if (cnt == 0) {
+        t = t2;
+        __syncthreads();  // every wave has read the zero count before it changes
+        cnt = count_keep(t);
     }
     if (cnt == 0) return;
-    int base = 0;
-    if (lane == 0) base = atomicAdd(&cand_count[f * P.nlevels + l], cnt);
-    base = __shfl(base, 0);
-    if (base + cnt > L.cand_cap) {  // cannot happen (cap is the exact NMS bound); reported if it does
-        if (lane == 0) atomicOr(status, 1);
-        return;
+    if (tid == 0) {
+        const int base = atomicAdd(&cand_count[f * P.nlevels + l], cnt);
+        sh_n[2] = base;
+        if (base + cnt > L.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
     }
+    __syncthreads();
+    const int base = sh_n[2];
+    if (base + cnt > L.cand_cap) return;
     u64* out = cand + (long long)f * P.cand_per_frame + L.cand_off + base;
     const int ox = cd.x0 - L.minB + 3, oy = cd.y0 - L.minB + 3;
-    int run = 0;
-    for (int e0 = 0; e0 < nsurv; e0 += 64) {
-        const int e = e0 + lane;
+    for (int e = tid; e - tid < nsurv; e += FAST_NT) {
         bool keep = false;
         int pix = 0;
         if (e < nsurv) {
@@ -291,11 +298,15 @@ __global__ __launch_bounds__(64) void og_fast_cells_kernel(OgPlan P, const OgCel
             keep = og_nms_keep(Ms, pix / OG_MAX_CELL_W, pix % OG_MAX_CELL_W, dw, dh, t);
         }
         const u64 mask = __ballot(keep);
-        if (keep) {
-            const int pos = run + __popcll(mask & ((1ull << lane) - 1ull));
-            out[pos] = og_pack_cand(ox + pix % OG_MAX_CELL_W, oy + pix / OG_MAX_CELL_W, Ms[pix] - 1);
+        if (mask) {
+            int wb = 0;
+            if (lane == 0) wb = atomicAdd(&sh_n[3], __popcll(mask));
+            wb = __shfl(wb, 0);
+            if (keep) {
+                const int pos = wb + __popcll(mask & ((1ull << lane) - 1ull));
+                out[pos] = og_pack_cand(ox + pix % OG_MAX_CELL_W, oy + pix / OG_MAX_CELL_W, Ms[pix] - 1);
+            }
         }
-        run += __popcll(mask);
     }
 }
 
@@ -878,7 +889,7 @@ void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, lo
 void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,
                     long long fstride0, const uint8_t* pyr, u64* cand, int* cand_count, int* status, int B)
 {
-    hipLaunchKernelGGL(og_fast_cells_kernel, dim3(P.total_cells, B), dim3(64), 0, s, P, cells, img0, pitch0, fstride0,
+    hipLaunchKernelGGL(og_fast_cells_kernel, dim3(P.total_cells, B), dim3(FAST_NT), 0, s, P, cells, img0, pitch0, fstride0,
                        pyr, cand, cand_count, status);
 }
 
