@@ -22,47 +22,107 @@ typedef unsigned long long u64;
 __constant__ signed char og_pattern[1024];
 static bool g_pattern_uploaded_dev[64] = {false};
 
+// XCD-aware bijective remap (cdna_hip_programming.md §5.5 T1): workgroups are dealt round-robin over
+// the 8 XCDs (separate L2s); give each XCD one contiguous chunk of the logical index space so that
+// neighbouring FAST cells / keypoints, which share cache lines, hit the same L2.  Speed only.
+__device__ __forceinline__ unsigned og_xcd_remap(unsigned orig, unsigned nwg)
+{
+    const unsigned q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
 // ------------------------------------------------------------------------------------------------
 // k1: pyramid level l from level l-1 (src/ORBextractor.cc:1120)
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void og_resize_kernel(const uint8_t* __restrict__ src, long long src_pitch,
-                                                        long long src_fstride, uint8_t* __restrict__ dst,
-                                                        long long dst_pitch, long long dst_fstride, int dw,
-                                                        int dh, const int4* __restrict__ xtab,
-                                                        const int4* __restrict__ ytab, int xmax)
+#define RZ_NT 256
+#define RZ_ROWS 8                      // output rows per workgroup
+#define RZ_COLS (RZ_NT * 4)            // output columns per workgroup (4 per thread)
+#define RZ_SROWS 16                    // >= source rows an 8-row tile can touch (scale <= ~1.6)
+#define RZ_SCOLS 1664                  // >= source bytes of a 1024-column tile at scale 1.6 + slack
+
+// One workgroup = 8 output rows x 1024 output columns of one frame.  The source rows/columns the tile
+// touches are staged in LDS with coalesced dword loads; each output pixel then costs 4 LDS byte reads.
+// The arithmetic is the scalar fixed-point form of cv::resize INTER_LINEAR.
+__global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restrict__ src, long long src_pitch,
+                                                          long long src_fstride, uint8_t* __restrict__ dst,
+                                                          long long dst_pitch, long long dst_fstride, int sw,
+                                                          int sh, int dw, int dh, const int4* __restrict__ xtab,
+                                                          const int4* __restrict__ ytab, int xmax,
+                                                          int* __restrict__ status)
 {
-    const int f = blockIdx.z;
-    const int dy = blockIdx.y;
-    const int dx0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
-    if (dy >= dh || dx0 >= dw) return;
-    const int4 yt = ytab[dy];  // {row0 (clipped), row1 (clipped), beta0, beta1}
-    const uint8_t* S0 = src + (long long)f * src_fstride + (long long)yt.x * src_pitch;
-    const uint8_t* S1 = src + (long long)f * src_fstride + (long long)yt.y * src_pitch;
-    uint8_t* D = dst + (long long)f * dst_fstride + (long long)dy * dst_pitch;
-    uint32_t packed = 0;
-    const int n = min(4, dw - dx0);
+    __shared__ __attribute__((aligned(16))) uint8_t S[RZ_SROWS * RZ_SCOLS];
+    const int f = blockIdx.z, tid = threadIdx.x;
+    const int dy0 = blockIdx.y * RZ_ROWS, dx0 = blockIdx.x * RZ_COLS;
+    const int ny = min(RZ_ROWS, dh - dy0), nx = min(RZ_COLS, dw - dx0);
+    const int sy0 = ytab[dy0].x, sy1 = ytab[dy0 + ny - 1].y;   // clipped rows, monotone in dy
+    const int sx0 = xtab[dx0].x;
+    const int sx1 = min(xtab[dx0 + nx - 1].x + 1, sw - 1);
+    const uint8_t* base = src + (long long)f * src_fstride;
+    const int nrows = sy1 - sy0 + 1;
+    const bool al = ((src_pitch & 3) == 0) && ((((uintptr_t)base) & 3) == 0);
+    const int cx0 = al ? (sx0 & ~3) : sx0;                      // LDS column 0 <-> source column cx0
+    const int ncols = sx1 - cx0 + 1;
+    if (nrows > RZ_SROWS || ncols > RZ_SCOLS) {                 // unreachable: scaleFactor <= 1.6 on the host
+        if (tid == 0) atomicOr(status, 8);
+        return;
+    }
+    if (al) {
+        const int nd = (ncols + 3) >> 2;
+        const int fd = min(nd, (sw - cx0) >> 2);                 // dwords lying wholly inside the row
+        for (int idx = tid; idx < nrows * nd; idx += RZ_NT) {
+            const int r = idx / nd, q = idx - (idx / nd) * nd;
+            const uint8_t* sp = base + (long long)(sy0 + r) * src_pitch + cx0 + 4 * q;
+            if (q < fd) {
+                *(uint32_t*)&S[r * RZ_SCOLS + 4 * q] = *(const uint32_t*)sp;
+            } else {
+                for (int b = 0; b < 4 && 4 * q + b < ncols; b++) S[r * RZ_SCOLS + 4 * q + b] = sp[b];
+            }
+        }
+    } else {
+        for (int idx = tid; idx < nrows * ncols; idx += RZ_NT) {
+            const int r = idx / ncols, c = idx - (idx / ncols) * ncols;
+            S[r * RZ_SCOLS + c] = base[(long long)(sy0 + r) * src_pitch + cx0 + c];
+        }
+    }
+    __syncthreads();
+    int sx[4], a0[4], a1[4];
+    const int dxt = dx0 + 4 * tid;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        if (k < n) {
-            const int dx = dx0 + k;
-            const int4 xt = xtab[dx];  // {sx, alpha0, alpha1, -}
-            int d0, d1;
-            if (dx < xmax) {
-                d0 = S0[xt.x] * xt.y + S0[xt.x + 1] * xt.z;
-                d1 = S1[xt.x] * xt.y + S1[xt.x + 1] * xt.z;
-            } else {
-                d0 = S0[xt.x] * 2048;
-                d1 = S1[xt.x] * 2048;
-            }
+        const int dx = min(dxt + k, dw - 1);
+        const int4 xt = xtab[dx];
+        sx[k] = xt.x - cx0;
+        if (dx < xmax) {
+            a0[k] = xt.y;
+            a1[k] = xt.z;
+        } else {                                                // right border: S[sx]*2048
+            a0[k] = 2048;
+            a1[k] = 0;
+        }
+    }
+    if (dxt >= dw) return;
+    const int n = min(4, dw - dxt);
+    uint8_t* D = dst + (long long)f * dst_fstride + dxt;
+    for (int r = 0; r < ny; r++) {
+        const int4 yt = ytab[dy0 + r];
+        const uint8_t* R0 = S + (yt.x - sy0) * RZ_SCOLS;
+        const uint8_t* R1 = S + (yt.y - sy0) * RZ_SCOLS;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            // (a1 == 0 at the right border, where sx+1 may be the column past the tile: reads 0-weighted)
+            const int d0 = R0[sx[k]] * a0[k] + (a1[k] ? R0[sx[k] + 1] * a1[k] : 0);
+            const int d1 = R1[sx[k]] * a0[k] + (a1[k] ? R1[sx[k] + 1] * a1[k] : 0);
             int v = (yt.z * d0 + yt.w * d1 + (1 << 21)) >> 22;
             v = v < 0 ? 0 : (v > 255 ? 255 : v);
             packed |= (uint32_t)v << (8 * k);
         }
-    }
-    if (n == 4 && ((((uintptr_t)(D + dx0)) & 3) == 0)) {
-        *(uint32_t*)(D + dx0) = packed;
-    } else {
-        for (int k = 0; k < n; k++) D[dx0 + k] = (uint8_t)(packed >> (8 * k));
+        uint8_t* Dr = D + (long long)(dy0 + r) * dst_pitch;
+        if (n == 4 && ((((uintptr_t)Dr) & 3) == 0)) {
+            *(uint32_t*)Dr = packed;
+        } else {
+            for (int k = 0; k < n; k++) Dr[k] = (uint8_t)(packed >> (8 * k));
+        }
     }
 }
 
@@ -179,7 +239,7 @@ __device__ __forceinline__ bool og_nms_keep(const uint8_t* Ms, int i, int j, int
 
 // One 256-thread workgroup (4 waves) per FAST cell: the cell's ROI, score map and survivor list live in
 // LDS shared by the four waves (full occupancy at ~17 KB per workgroup).
-__global__ __launch_bounds__(FAST_NT) void og_fast_cells_kernel(OgPlan P, const OgCell* __restrict__ cells,
+__global__ __launch_bounds__(FAST_NT, 8) void og_fast_cells_kernel(OgPlan P, const OgCell* __restrict__ cells,
                                                                 const uint8_t* __restrict__ img0, long long pitch0,
                                                                 long long fstride0, const uint8_t* __restrict__ pyr,
                                                                 u64* __restrict__ cand, int* __restrict__ cand_count,
@@ -189,8 +249,9 @@ __global__ __launch_bounds__(FAST_NT) void og_fast_cells_kernel(OgPlan P, const 
     __shared__ __attribute__((aligned(16))) uint8_t Ms[OG_MAX_CELL_W * OG_MAX_CELL_W];
     __shared__ uint16_t lst[OG_MAX_CELL_W * OG_MAX_CELL_W];
     __shared__ int sh_n[4];  // 0: survivors, 1: keep count, 2: emission base, 3: emission cursor
-    const int f = blockIdx.y;
-    const OgCell cd = cells[blockIdx.x];
+    const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+    const int f = (int)(lin / gridDim.x);
+    const OgCell cd = cells[lin % gridDim.x];
     const int l = cd.level;
     const OgLevel& L = P.lv[l];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -214,11 +275,23 @@ __global__ __launch_bounds__(FAST_NT) void og_fast_cells_kernel(OgPlan P, const 
     const bool aligned_rows = ((pitch & 3) == 0);
     uint8_t* T = roi + (aligned_rows ? mis : 0);  // T[r*OG_RS + c] = ROI pixel (r, c)
     if (aligned_rows) {
+        // all loads of a thread issued before any LDS store: one memory latency, not five
         const int nd = (rw + mis + 3) >> 2;
-        for (int r = tid >> 4; r < rh; r += FAST_NT / 16) {
-            const uint32_t* s4 = (const uint32_t*)(row0 + (long long)r * pitch - mis);
-            for (int q = tid & 15; q < nd; q += 16) *(uint32_t*)&roi[r * OG_RS + 4 * q] = s4[q];
-        }
+        uint32_t buf[5][2];
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+#pragma unroll
+            for (int qq = 0; qq < 2; qq++) {
+                const int r = (tid >> 4) + 16 * k, q = (tid & 15) + 16 * qq;
+                buf[k][qq] = (r < rh && q < nd) ? ((const uint32_t*)(row0 + (long long)r * pitch - mis))[q] : 0u;
+            }
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+#pragma unroll
+            for (int qq = 0; qq < 2; qq++) {
+                const int r = (tid >> 4) + 16 * k, q = (tid & 15) + 16 * qq;
+                if (r < rh && q < nd) *(uint32_t*)&roi[r * OG_RS + 4 * q] = buf[k][qq];
+            }
     } else {
         for (int r = tid >> 6; r < rh; r += FAST_NT / 64) {
             const uint8_t* src = row0 + (long long)r * pitch;
@@ -668,8 +741,9 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     __shared__ uint16_t hb[DK_WAVES][RAW_W * BL_W];
     __shared__ uint8_t bl[DK_WAVES][BL_W * BL_W + 3];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int f = blockIdx.y;
-    const int g = blockIdx.x * DK_WAVES + w;
+    const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+    const int f = (int)(lin / gridDim.x);
+    const int g = (int)(lin % gridDim.x) * DK_WAVES + w;
     // which level does keypoint g belong to (levels concatenated 0..L-1, :1076-1104)
     int l = -1, li = 0, total = 0;
     for (int q = 0; q < P.nlevels; q++) {
@@ -877,13 +951,12 @@ hipError_t og_upload_pattern(int device)
 }
 
 void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,
-                      long long dst_pitch, long long dst_fstride, int dw, int dh, const int4* xtab, const int4* ytab,
-                      int xmax, int B)
+                      long long dst_pitch, long long dst_fstride, int sw, int sh, int dw, int dh, const int4* xtab,
+                      const int4* ytab, int xmax, int* status, int B)
 {
-    dim3 block(64);
-    dim3 grid((dw + 4 * 64 - 1) / (4 * 64), dh, B);
-    hipLaunchKernelGGL(og_resize_kernel, grid, block, 0, s, src, src_pitch, src_fstride, dst, dst_pitch, dst_fstride,
-                       dw, dh, xtab, ytab, xmax);
+    dim3 grid((dw + RZ_COLS - 1) / RZ_COLS, (dh + RZ_ROWS - 1) / RZ_ROWS, B);
+    hipLaunchKernelGGL(og_resize_kernel, grid, dim3(RZ_NT), 0, s, src, src_pitch, src_fstride, dst, dst_pitch,
+                       dst_fstride, sw, sh, dw, dh, xtab, ytab, xmax, status);
 }
 
 void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,

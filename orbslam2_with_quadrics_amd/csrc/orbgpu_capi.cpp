@@ -325,8 +325,8 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
         const uint8_t* src = l == 1 ? d_imgs : c->pyr.p + Lp.pyr_off;
         const long long sp = l == 1 ? pitch : Lp.pitch;
         const long long sfs = l == 1 ? fstride : P.pyr_per_frame;
-        og_launch_resize(s, src, sp, sfs, c->pyr.p + L.pyr_off, L.pitch, P.pyr_per_frame, L.w, L.h,
-                         c->tabs.p + L.xtab_off, c->tabs.p + L.ytab_off, L.xmax, B);
+        og_launch_resize(s, src, sp, sfs, c->pyr.p + L.pyr_off, L.pitch, P.pyr_per_frame, Lp.w, Lp.h, L.w, L.h,
+                         c->tabs.p + L.xtab_off, c->tabs.p + L.ytab_off, L.xmax, c->status.p, B);
     }
     timer_mark(c, "pyramid");
     og_launch_fast(s, P, c->cells.p, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p, c->status.p, B);
@@ -383,7 +383,9 @@ extern "C" {
 
 orbgpu_ctx* orbgpu_create(int device, int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
 {
-    if (nlevels < 1 || nlevels > OG_MAXLEVELS || nfeatures < 0 || !(scaleFactor > 1.0f)) return nullptr;
+    // scaleFactor <= 1.6 keeps one 8x1024 resize tile's source inside the LDS staging buffer
+    if (nlevels < 1 || nlevels > OG_MAXLEVELS || nfeatures < 0 || !(scaleFactor > 1.0f) || scaleFactor > 1.6f)
+        return nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return nullptr;
     if (hipSetDevice(device) != hipSuccess) return nullptr;

@@ -17,8 +17,8 @@ struct OgGridGeom {
 hipError_t og_upload_pattern(int device);
 
 void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,
-                      long long dst_pitch, long long dst_fstride, int dw, int dh, const int4* xtab, const int4* ytab,
-                      int xmax, int B);
+                      long long dst_pitch, long long dst_fstride, int sw, int sh, int dw, int dh, const int4* xtab,
+                      const int4* ytab, int xmax, int* status, int B);
 void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,
                     long long fstride0, const uint8_t* pyr, unsigned long long* cand, int* cand_count, int* status,
                     int B);

@@ -22,14 +22,23 @@ STAGE = {"og_fast_cells_kernel": "fast", "og_octree_kernel": "octree", "og_descr
 
 def main():
     d = sys.argv[1]
-    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per-dispatch values]
+    # kernel -> grid size -> counter -> [per-dispatch values]; the largest grid of a kernel is the
+    # B-frame launch (the bench also extracts the 1-frame initial frame)
+    raw = defaultdict(lambda: defaultdict(lambda: defaultdict(list)))
     for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = short(r["Kernel_Name"])
-            gy = int(r.get("Grid_Size_Y", r.get("Grid_Size", "1").split(",")[0]) or 1) if "Grid_Size_Y" in r else 1
-            if k in ("og_fast_cells_kernel", "og_octree_kernel", "og_describe_kernel") and gy <= 1:
-                continue  # skip the 1-frame launches of the initial frame
-            vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            raw[k][int(float(r["Grid_Size"]))][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    vals = {}
+    for k, by_grid in raw.items():
+        if k.startswith("og_resize"):  # 7 levels per batch: keep all launches of the B-frame batch
+            merged = defaultdict(list)
+            for g, cs in by_grid.items():
+                for c, v in cs.items():
+                    merged[c].extend(v)
+            vals[k] = merged
+        else:
+            vals[k] = by_grid[max(by_grid)]
     out = {}
     for k, cs in vals.items():
         m = {c: sum(v) / len(v) for c, v in cs.items()}
