@@ -453,6 +453,8 @@ __device__ __forceinline__ unsigned og_cand_order(int x, int y, const OgLevel& L
     return (unsigned)(((ci * L.nCols + cj) * L.hCell + ly) * L.wCell + lx);
 }
 
+#define OCT_U 8  // candidates per thread per pass with all loads hoisted (latency batching)
+
 __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* __restrict__ cand,
                                                            const int* __restrict__ cand_count,
                                                            uint16_t* __restrict__ node_of,
@@ -466,8 +468,9 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
     __shared__ int splitNode[OG_OCT_MAXL];
     __shared__ int newPos[OG_OCT_MAXL];
     __shared__ int aux[OG_OCT_MAXL];
-    __shared__ __attribute__((aligned(16))) int childCnt[4 * OG_OCT_MAXL];
-    __shared__ int childPos[4 * OG_OCT_MAXL];
+    __shared__ __attribute__((aligned(16))) int childCnt[2][4 * OG_OCT_MAXL];  // indexed 4*node + quadrant
+    __shared__ uint16_t childPos[4 * OG_OCT_MAXL];
+    __shared__ u64 best[OG_OCT_MAXL];
     __shared__ int wsum[32];
     __shared__ int sv[16];
 
@@ -481,65 +484,103 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
     const int H = L.maxBY - L.minB;
 
     // ---- roots (src/ORBextractor.cc:552-585)
-    for (int r = tid; r < nIni; r += OCT_NT) childCnt[r] = 0;
+    for (int r = tid; r < nIni; r += OCT_NT) childCnt[1][r] = 0;
     __syncthreads();
-    for (int k = tid; k < C; k += OCT_NT) {
-        const int x = (int)(K[k] & 0xffff);
-        int r = (int)((float)x / L.hX);
-        r = min(r, nIni - 1);
-        NO[k] = (uint16_t)r;
-        atomicAdd(&childCnt[r], 1);
+    for (int base = tid; base < C; base += OCT_NT * OCT_U) {
+        u64 kv[OCT_U];
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++) {
+            const int k = base + u * OCT_NT;
+            kv[u] = k < C ? K[k] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++) {
+            const int k = base + u * OCT_NT;
+            if (k < C) {
+                int r = (int)((float)(int)(kv[u] & 0xffff) / L.hX);
+                r = min(r, nIni - 1);
+                NO[k] = (uint16_t)r;
+                atomicAdd(&childCnt[1][r], 1);
+            }
+        }
     }
     __syncthreads();
     if (tid == 0) {
         int Ln = 0;
         for (int r = 0; r < nIni; r++) {
-            if (childCnt[r] > 0) {
+            const int c = childCnt[1][r];
+            if (c > 0) {
                 OctNode n;
                 n.x0 = (short)(int)(L.hX * (float)r);
                 n.x1 = (short)(int)(L.hX * (float)(r + 1));
                 n.y0 = 0;
                 n.y1 = (short)H;
-                n.cnt = childCnt[r];
+                n.cnt = c;
                 n.cid = r;
                 nodes[0][Ln] = n;
                 fresh[0][Ln] = 0;
-                childPos[r] = Ln++;
+                aux[r] = Ln++;
             } else {
-                childPos[r] = -1;
+                aux[r] = -1;
             }
         }
         sv[0] = Ln;      // list length
-        sv[1] = 0;       // mode: 0 normal, 1 final
+        sv[1] = 0;       // mode of the coming round: 0 normal pass, 1 final phase
         sv[2] = nIni;    // next creation id
-        sv[3] = 0;       // done
-        sv[4] = 0;       // current buffer
+        sv[3] = Ln == 0; // done (an empty list can never grow)
+        sv[4] = 0;       // current node buffer
+        sv[7] = 0;       // current child-count buffer
+        sv[8] = 0;       // `best` filled by a key pass
     }
     __syncthreads();
-    for (int k = tid; k < C; k += OCT_NT) NO[k] = (uint16_t)childPos[NO[k]];
+    for (int q = tid; q < 4 * OG_OCT_MAXL; q += OCT_NT) childCnt[0][q] = 0;
+    __syncthreads();
+    // remap keys to root positions and count the children of the first pass's splits (cnt > 1)
+    for (int base = tid; base < C; base += OCT_NT * OCT_U) {
+        u64 kv[OCT_U];
+        int no[OCT_U];
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++) {
+            const int k = base + u * OCT_NT;
+            kv[u] = k < C ? K[k] : 0ull;
+            no[u] = k < C ? NO[k] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++) {
+            const int k = base + u * OCT_NT;
+            if (k < C) {
+                const int n = aux[no[u]];
+                NO[k] = (uint16_t)n;
+                const OctNode& nd = nodes[0][n];
+                if (nd.cnt > 1)
+                    atomicAdd(&childCnt[0][4 * n + og_quadrant((int)(kv[u] & 0xffff), (int)((kv[u] >> 16) & 0xffff), nd)], 1);
+            }
+        }
+    }
     __syncthreads();
 
     for (int round = 0; round < 4096; round++) {
-        const int Ln = sv[0], mode = sv[1], cur = sv[4];
         if (sv[3]) break;
+        const int Ln = sv[0], mode = sv[1], cur = sv[4], cc = sv[7];
         OctNode* cn = nodes[cur];
         uint8_t* cf = fresh[cur];
         OctNode* nn = nodes[cur ^ 1];
         uint8_t* nf = fresh[cur ^ 1];
+        const int* CC = childCnt[cc];
+        int* NCC = childCnt[cc ^ 1];
         __syncthreads();
-        // ---- choose the split set and its order
+        // ---- the split set of this round and its order
         const int i = tid;
         int S;
-        bool flag = false;
         if (mode == 0) {
-            flag = i < Ln && cn[i].cnt > 1;
+            const bool flag = i < Ln && cn[i].cnt > 1;
             const int rank = og_block_excl_scan(flag ? 1 : 0, wsum, &S);
             if (i < Ln) splitRank[i] = flag ? rank : -1;
             if (flag) splitNode[rank] = i;
         } else {
-            // vSizeAndPointerToNode of the previous round, sorted ascending by (size, ptr) and walked
-            // from the back (src/ORBextractor.cc:684-685): order = descending (cnt, creation id)
-            flag = i < Ln && cf[i] && cn[i].cnt > 1;
+            // vSizeAndPointerToNode of the previous round sorted ascending by (size, ptr) and walked from
+            // the back (src/ORBextractor.cc:684-685): order = descending (cnt, creation id)
+            const bool flag = i < Ln && cf[i] && cn[i].cnt > 1;
             const int c = og_block_excl_scan(flag ? 1 : 0, wsum, &S);
             if (flag) aux[c] = i;
             __syncthreads();
@@ -560,25 +601,14 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
             __syncthreads();
             break;
         }
-        for (int q = tid; q < 4 * S; q += OCT_NT) childCnt[q] = 0;
         __syncthreads();
-        // ---- count keys per child (DivideNode, :511-526)
-        for (int k = tid; k < C; k += OCT_NT) {
-            const int n = NO[k];
-            const int r = splitRank[n];
-            if (r >= 0) {
-                const u64 kv = K[k];
-                const int q = og_quadrant((int)(kv & 0xffff), (int)((kv >> 16) & 0xffff), cn[n]);
-                atomicAdd(&childCnt[4 * r + q], 1);
-            }
-        }
-        __syncthreads();
-        // ---- per split: non-empty children, break point of the final phase (:730-731)
-        int nc = 0, nexp = 0;
+        // ---- per split (in split order): non-empty children, the final phase's break point (:730-731)
+        int nc = 0, nexp = 0, sn = 0;
         if (i < S) {
+            sn = splitNode[i];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const int c = childCnt[4 * i + q];
+                const int c = CC[4 * sn + q];
                 nc += c > 0;
                 nexp += c > 1;
             }
@@ -587,7 +617,6 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
         const int exNc = og_block_excl_scan(nc, wsum, &totNc);
         int A = S;
         if (mode == 1) {
-            // grow after splitting 0..i = sum_{r<=i} (nc_r - 1) = exNc + nc - (i+1)
             const bool reach = i < S && (Ln + exNc + nc - (i + 1) >= N);
             if (tid == 0) sv[5] = S;
             __syncthreads();
@@ -595,32 +624,28 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
             __syncthreads();
             A = sv[5];
         }
-        // total children of the applied splits
         if (i == A - 1) sv[6] = exNc + nc;
         __syncthreads();
         const int T = sv[6];
-        // ---- place children: groups in reverse split order, each n4,n3,n2,n1 (push_front, :621-660)
+        // ---- children: groups in reverse split order, each n4,n3,n2,n1 (push_front, :621-660)
         if (i < A) {
-            const OctNode par = cn[splitNode[i]];
+            const OctNode par = cn[sn];
             const int groupStart = T - (exNc + nc);
             const int cidBase = sv[2] + exNc;
             int before = 0;  // non-empty children among q' < q (creation order n1..n4)
             for (int q = 0; q < 4; q++) {
-                const int c = childCnt[4 * i + q];
+                const int c = CC[4 * sn + q];
                 if (c > 0) {
-                    const int after = nc - before - 1;  // non-empty among q' > q
-                    const int pos = groupStart + after;
+                    const int pos = groupStart + (nc - before - 1);
                     OctNode ch = og_child(par, q);
                     ch.cnt = c;
                     ch.cid = cidBase + before;
-                    childPos[4 * i + q] = pos;
+                    childPos[4 * sn + q] = (uint16_t)pos;
                     if (pos < OG_OCT_MAXL) {
                         nn[pos] = ch;
                         nf[pos] = 1;
                     }
                     before++;
-                } else {
-                    childPos[4 * i + q] = -1;
                 }
             }
         }
@@ -648,47 +673,88 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
             __syncthreads();
             break;
         }
+        // ---- termination / next mode (src/ORBextractor.cc:669-677, 734-735), decided before the key pass
+        int done = 0, nextMode = mode;
+        if (mode == 0) {
+            if (Lnew >= N || Lnew == Ln) done = 1;
+            else if (Lnew + expTot * 3 > N) nextMode = 1;
+        } else {
+            if (Lnew >= N || Lnew == Ln) done = 1;
+        }
+        for (int q = tid; q < 4 * Lnew; q += OCT_NT) NCC[q] = 0;
+        if (done)
+            for (int q = tid; q < Lnew; q += OCT_NT) best[q] = 0ull;
         __syncthreads();
-        // ---- remap keys to their new list positions
-        for (int k = tid; k < C; k += OCT_NT) {
-            const int n = NO[k];
-            const int r = splitRank[n];
-            if (r >= 0 && r < A) {
-                const u64 kv = K[k];
-                const int q = og_quadrant((int)(kv & 0xffff), (int)((kv >> 16) & 0xffff), cn[n]);
-                NO[k] = (uint16_t)childPos[4 * r + q];
-            } else {
-                NO[k] = (uint16_t)newPos[n];
+        // ---- one pass over the keys: move to the new list position, and either count the children of
+        // the next round's split candidates or (last round) keep the best key per node (:744-760)
+        for (int base = tid; base < C; base += OCT_NT * OCT_U) {
+            u64 kv[OCT_U];
+            int no[OCT_U];
+#pragma unroll
+            for (int u = 0; u < OCT_U; u++) {
+                const int k = base + u * OCT_NT;
+                kv[u] = k < C ? K[k] : 0ull;
+                no[u] = k < C ? NO[k] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < OCT_U; u++) {
+                const int k = base + u * OCT_NT;
+                if (k < C) {
+                    const int n = no[u];
+                    const int x = (int)(kv[u] & 0xffff), y = (int)((kv[u] >> 16) & 0xffff);
+                    const int r = splitRank[n];
+                    int n2;
+                    if (r >= 0 && r < A) n2 = childPos[4 * n + og_quadrant(x, y, cn[n])];
+                    else n2 = newPos[n];
+                    NO[k] = (uint16_t)n2;
+                    if (done) {
+                        const int resp = (int)((kv[u] >> 32) & 0xff);
+                        atomicMax(&best[n2], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
+                    } else {
+                        const OctNode& nd = nn[n2];
+                        if (nd.cnt > 1 && (nextMode == 0 || nf[n2])) atomicAdd(&NCC[4 * n2 + og_quadrant(x, y, nd)], 1);
+                    }
+                }
             }
         }
         __syncthreads();
         if (tid == 0) {
-            const int prevSize = Ln;
             sv[0] = Lnew;
+            sv[1] = nextMode;
             sv[2] += T;
+            sv[3] = done;
             sv[4] = cur ^ 1;
-            if (mode == 0) {
-                if (Lnew >= N || Lnew == prevSize) sv[3] = 1;
-                else if (Lnew + expTot * 3 > N) sv[1] = 1;
-            } else {
-                if (Lnew >= N || Lnew == prevSize) sv[3] = 1;
-            }
+            sv[7] = cc ^ 1;
+            sv[8] = done;  // `best` is valid
         }
         __syncthreads();
     }
     __syncthreads();
-    // ---- retain the best keypoint per node (:744-760): max response, first in vKeys order on ties
     const int Ln = sv[0];
-    u64* best = (u64*)childCnt;  // 2*MAXL u64 of room
-    for (int n = tid; n < Ln; n += OCT_NT) best[n] = 0;
-    __syncthreads();
-    for (int k = tid; k < C; k += OCT_NT) {
-        const u64 kv = K[k];
-        const int x = (int)(kv & 0xffff), y = (int)((kv >> 16) & 0xffff), resp = (int)((kv >> 32) & 0xff);
-        const unsigned ord = og_cand_order(x, y, L);
-        atomicMax(&best[NO[k]], ((u64)resp << 32) | (u64)(0xffffffffu - ord));
+    if (!sv[8]) {  // finished without a final key pass (empty split set): one pass for the best key
+        for (int n = tid; n < Ln; n += OCT_NT) best[n] = 0ull;
+        __syncthreads();
+        for (int base = tid; base < C; base += OCT_NT * OCT_U) {
+            u64 kv[OCT_U];
+            int no[OCT_U];
+#pragma unroll
+            for (int u = 0; u < OCT_U; u++) {
+                const int k = base + u * OCT_NT;
+                kv[u] = k < C ? K[k] : 0ull;
+                no[u] = k < C ? NO[k] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < OCT_U; u++) {
+                const int k = base + u * OCT_NT;
+                if (k < C) {
+                    const int x = (int)(kv[u] & 0xffff), y = (int)((kv[u] >> 16) & 0xffff);
+                    const int resp = (int)((kv[u] >> 32) & 0xff);
+                    atomicMax(&best[no[u]], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
+                }
+            }
+        }
+        __syncthreads();
     }
-    __syncthreads();
     const int nout = min(Ln, L.kcap);
     for (int n = tid; n < nout; n += OCT_NT) {
         const u64 b = best[n];

@@ -64,13 +64,104 @@ __device__ __forceinline__ int og_wave_sum(int v)
 }
 
 // ------------------------------------------------------------------------------------------------
-// SearchForInitialization
+// SearchForInitialization, two phases:
+//  A. og_init_cand_kernel  -- one wave per (pair, F1 keypoint): Frame::GetFeaturesInArea on F2's grid
+//     (src/Frame.cc:327-380: cells ix-major, then iy, then cell order), level filter, window test,
+//     Hamming distance; the list {dist:16 | i2:16} is written in candidate order.  Fully parallel.
+//  B. og_init_resolve_kernel -- one wave per pair replays the reference's ordered loop
+//     (src/ORBmatcher.cc:418-487): only the state-dependent vMatchedDistance filter (:444), the
+//     best/second reduction and the steal/rot-hist bookkeeping remain sequential.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void og_search_init_kernel(OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G,
-                                                            float nnratio, int checkOri, int windowSize,
-                                                            float* __restrict__ prev_xy, int prev_stride,
-                                                            int* __restrict__ matches12, int match_stride,
-                                                            int* __restrict__ nmatches)
+__global__ __launch_bounds__(256) void og_init_cand_kernel(OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G,
+                                                           int windowSize, const float* __restrict__ prev_xy,
+                                                           int prev_stride, uint32_t* __restrict__ lists,
+                                                           int list_cap, int* __restrict__ list_n)
+{
+    const int b = blockIdx.y, lane = threadIdx.x & 63;
+    const int i1 = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int n1 = F1.counts[ref];
+    if (i1 >= F1.frame_cap) return;
+    int* NC = list_n + (long long)b * F1.frame_cap;
+    if (i1 >= n1) return;
+    const orbgpu_kp_dev* K1 = F1.kps + (long long)ref * F1.frame_cap;
+    const int level1 = K1[i1].octave;
+    if (level1 > 0) {
+        if (lane == 0) NC[i1] = 0;
+        return;
+    }
+    const float* PV = prev_xy + (long long)b * prev_stride;
+    const float x = PV[2 * i1], y = PV[2 * i1 + 1];
+    const float r = (float)windowSize;
+    const OgCellRange cr = og_cell_range(G, x, y, r);
+    if (cr.x0 > cr.x1) {
+        if (lane == 0) NC[i1] = 0;
+        return;
+    }
+    const uint8_t* D1 = F1.desc + (long long)ref * F1.frame_cap * 32;
+    const orbgpu_kp_dev* K2 = F2.kps + (long long)b * F2.frame_cap;
+    const uint8_t* D2 = F2.desc + (long long)b * F2.frame_cap * 32;
+    const int* CS = F2.cell_start + (long long)b * (OG_GRID_CELLS + 1);
+    const int* CI = F2.cell_items + (long long)b * F2.frame_cap;
+    uint32_t* LST = lists + ((long long)b * F1.frame_cap + i1) * list_cap;
+    uint4 da, db;
+    og_load_desc(D1 + (long long)i1 * 32, da, db);
+    const int ncy = cr.y1 - cr.y0 + 1;
+    const int ncells = (cr.x1 - cr.x0 + 1) * ncy;
+    int n = 0;
+    for (int c0 = 0; c0 < ncells; c0 += 64) {
+        const int c = c0 + lane;
+        int cell = 0, cnt = 0;
+        if (c < ncells) {
+            cell = (cr.x0 + c / ncy) * OG_GRID_ROWS + (cr.y0 + c % ncy);
+            cnt = CS[cell + 1] - CS[cell];
+        }
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o);
+            if (lane >= o) incl += t;
+        }
+        const int T = __shfl(incl, 63);
+        const int cellStart = c < ncells ? CS[cell] : 0;
+        for (int e = lane; e - lane < T; e += 64) {
+            const int ee = min(e, T - 1);
+            int lo = 0;  // binary lifting: number of lanes whose inclusive count is <= ee
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+                const int v = __shfl(incl, lo + step - 1);
+                if (v <= ee) lo += step;
+            }
+            const int ownerIncl = __shfl(incl, lo), ownerCnt = __shfl(cnt, lo), ownerStart = __shfl(cellStart, lo);
+            bool valid = false;
+            uint32_t entry = 0;
+            if (e < T) {
+                const int i2 = CI[ownerStart + e - (ownerIncl - ownerCnt)];
+                const orbgpu_kp_dev kp2 = K2[i2];
+                if (kp2.octave >= level1 && kp2.octave <= level1) {  // src/Frame.cc:361-368
+                    const float distx = kp2.x - x, disty = kp2.y - y;
+                    if (fabsf(distx) < r && fabsf(disty) < r) {
+                        uint4 ea, eb;
+                        og_load_desc(D2 + (long long)i2 * 32, ea, eb);
+                        entry = ((uint32_t)og_hamming(da, db, ea, eb) << 16) | (uint32_t)i2;
+                        valid = true;
+                    }
+                }
+            }
+            const u64 mask = __ballot(valid);
+            const int pos = n + __popcll(mask & ((1ull << lane) - 1ull));
+            if (valid && pos < list_cap) LST[pos] = entry;
+            n += __popcll(mask);
+        }
+    }
+    if (lane == 0) NC[i1] = min(n, list_cap) | (n > list_cap ? (int)0x80000000 : 0);
+}
+
+__global__ __launch_bounds__(64) void og_init_resolve_kernel(OgFrameDev F1, int ref, OgFrameDev F2, float nnratio,
+                                                             int checkOri, float* __restrict__ prev_xy,
+                                                             int prev_stride, const uint32_t* __restrict__ lists,
+                                                             int list_cap, const int* __restrict__ list_n,
+                                                             int* __restrict__ matches12, int match_stride,
+                                                             int* __restrict__ nmatches, int* __restrict__ status)
 {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int b = blockIdx.x, lane = threadIdx.x;
@@ -92,91 +183,50 @@ __global__ __launch_bounds__(64) void og_search_init_kernel(OgFrameDev F1, int r
     if (lane < HISTO_LENGTH) hist[lane] = 0;
     __syncthreads();
     const orbgpu_kp_dev* K1 = F1.kps + (long long)ref * F1.frame_cap;
-    const uint8_t* D1 = F1.desc + (long long)ref * F1.frame_cap * 32;
     const orbgpu_kp_dev* K2 = F2.kps + (long long)b * F2.frame_cap;
-    const uint8_t* D2 = F2.desc + (long long)b * F2.frame_cap * 32;
-    const int* CS = F2.cell_start + (long long)b * (OG_GRID_CELLS + 1);
-    const int* CI = F2.cell_items + (long long)b * F2.frame_cap;
+    const int* NC = list_n + (long long)b * F1.frame_cap;
+    const uint32_t* LB = lists + (long long)b * F1.frame_cap * list_cap;
     float* PV = prev_xy + (long long)b * prev_stride;
-    const float r = (float)windowSize;
     const float factor = 1.0f / HISTO_LENGTH;
     int nm = 0;
+    // software pipeline: the first chunk of query i1+1 is in flight while query i1 is resolved
+    int ncNext = n1 > 0 ? NC[0] : 0;
+    uint32_t entNext = (n1 > 0 && lane < (ncNext & 0x7fffffff)) ? LB[lane] : 0u;
     for (int i1 = 0; i1 < n1; i1++) {
-        const int level1 = K1[i1].octave;
-        if (level1 > 0) continue;
-        const float x = PV[2 * i1], y = PV[2 * i1 + 1];
-        const OgCellRange cr = og_cell_range(G, x, y, r);
-        if (cr.x0 > cr.x1) continue;
-        uint4 da, db;
-        og_load_desc(D1 + (long long)i1 * 32, da, db);
-        const int ncy = cr.y1 - cr.y0 + 1;
-        const int ncells = (cr.x1 - cr.x0 + 1) * ncy;
-        u64 best1 = ~0ull, best2 = ~0ull;  // lane-local two smallest (dist<<32 | pos)
-        int bestI2 = -1;
-        int posBase = 0;
-        for (int c0 = 0; c0 < ncells; c0 += 64) {
-            const int c = c0 + lane;
-            int cell = 0, cnt = 0;
-            if (c < ncells) {
-                cell = (cr.x0 + c / ncy) * OG_GRID_ROWS + (cr.y0 + c % ncy);
-                cnt = CS[cell + 1] - CS[cell];
-            }
-            // wave exclusive scan of cnt
-            int incl = cnt;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int t = __shfl_up(incl, o);
-                if (lane >= o) incl += t;
-            }
-            const int T = __shfl(incl, 63);
-            for (int e = lane; e - lane < T; e += 64) {
-                // owning lane of flat candidate e: the first lane whose inclusive sum exceeds e.
-                // Every lane runs the shuffles (inactive-lane reads of ds_bpermute are undefined).
-                const int ee = min(e, T - 1);
-                int lo = 0;  // binary lifting: number of lanes with incl <= ee (uniform 6 steps)
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1) {
-                    const int v = __shfl(incl, lo + step - 1);
-                    if (v <= ee) lo += step;
-                }
-                const int ownerIncl = __shfl(incl, lo), ownerCnt = __shfl(cnt, lo), ownerCell = __shfl(cell, lo);
-                bool valid = false;
-                int dist = 0, i2 = -1;
-                if (e < T) {
-                    const int k = e - (ownerIncl - ownerCnt);
-                    i2 = CI[CS[ownerCell] + k];
-                    const orbgpu_kp_dev kp2 = K2[i2];
-                    // level filter: minLevel == maxLevel == level1 == 0 (src/Frame.cc:361-368)
-                    if (kp2.octave >= level1 && kp2.octave <= level1) {
-                        const float distx = kp2.x - x, disty = kp2.y - y;
-                        if (fabsf(distx) < r && fabsf(disty) < r) {
-                            uint4 ea, eb;
-                            og_load_desc(D2 + (long long)i2 * 32, ea, eb);
-                            dist = og_hamming(da, db, ea, eb);
-                            valid = !(vMD[i2] <= dist);  // src/ORBmatcher.cc:444
-                        }
-                    }
-                }
-                if (valid) {
-                    const u64 key = ((u64)(unsigned)dist << 32) | (unsigned)(posBase + e);
+        const int ncRaw = ncNext;
+        const uint32_t ent0 = entNext;
+        if (i1 + 1 < n1) {
+            ncNext = NC[i1 + 1];
+            entNext = lane < (ncNext & 0x7fffffff) ? LB[(long long)(i1 + 1) * list_cap + lane] : 0u;
+        }
+        if (ncRaw < 0) {  // candidate list overflowed its slot: reported, never silent
+            if (lane == 0) atomicOr(status, 16);
+            continue;
+        }
+        const int nc = ncRaw;
+        if (nc == 0) continue;
+        u64 best1 = ~0ull, best2 = ~0ull;  // lane-local two smallest (dist, list position, i2)
+        for (int e0 = 0; e0 < nc; e0 += 64) {
+            const int e = e0 + lane;
+            if (e < nc) {
+                const uint32_t ent = e0 == 0 ? ent0 : LB[(long long)i1 * list_cap + e];
+                const int i2 = (int)(ent & 0xffff), dist = (int)(ent >> 16);
+                if (!(vMD[i2] <= dist)) {  // src/ORBmatcher.cc:444
+                    const u64 key = ((u64)dist << 32) | ((u64)e << 16) | (u64)i2;
                     if (key < best1) {
                         best2 = best1;
                         best1 = key;
-                        bestI2 = i2;
                     } else if (key < best2) {
                         best2 = key;
                     }
                 }
             }
-            posBase += T;
         }
         const u64 gbest = og_wave_min_u64(best1);
         if (gbest == ~0ull) continue;
         const u64 mine2 = (best1 == gbest) ? best2 : best1;
         const u64 gsecond = og_wave_min_u64(mine2);
-        const u64 owner = __ballot(best1 == gbest);
-        const int ol = __ffsll((long long)owner) - 1;
-        const int bestIdx2 = __shfl(bestI2, ol);
+        const int bestIdx2 = (int)(gbest & 0xffff);
         const int bestDist = (int)(gbest >> 32);
         const int bestDist2 = gsecond == ~0ull ? INT_MAX : (int)(gsecond >> 32);
         if (bestDist <= TH_LOW && bestDist < (float)bestDist2 * nnratio) {
@@ -238,7 +288,7 @@ __global__ __launch_bounds__(64) void og_search_init_kernel(OgFrameDev F1, int r
     for (int i = lane; i < n1; i += 64) {
         const int j = m12[i];
         M[i] = j;
-        if (j >= 0) {
+        if (j >= 0) {  // update vbPrevMatched (src/ORBmatcher.cc:515-517)
             PV[2 * i] = K2[j].x;
             PV[2 * i + 1] = K2[j].y;
         }
@@ -248,11 +298,14 @@ __global__ __launch_bounds__(64) void og_search_init_kernel(OgFrameDev F1, int r
 
 void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G, float nnratio,
                            int checkOri, int windowSize, float* prev_xy, int prev_stride, int* matches12,
-                           int match_stride, int* nmatches, int B)
+                           int match_stride, int* nmatches, uint32_t* lists, int list_cap, int* list_n, int* status,
+                           int B)
 {
+    hipLaunchKernelGGL(og_init_cand_kernel, dim3((F1.frame_cap + 3) / 4, B), dim3(256), 0, s, F1, ref, F2, G,
+                       windowSize, prev_xy, prev_stride, lists, list_cap, list_n);
     const size_t shm = sizeof(int) * (2 * (size_t)F2.frame_cap + 2 * (size_t)F1.frame_cap);
-    hipLaunchKernelGGL(og_search_init_kernel, dim3(B), dim3(64), shm, s, F1, ref, F2, G, nnratio, checkOri,
-                       windowSize, prev_xy, prev_stride, matches12, match_stride, nmatches);
+    hipLaunchKernelGGL(og_init_resolve_kernel, dim3(B), dim3(64), shm, s, F1, ref, F2, nnratio, checkOri, prev_xy,
+                       prev_stride, lists, list_cap, list_n, matches12, match_stride, nmatches, status);
 }
 
 // Tracking::MonocularInitialization (src/Tracking.cc:573-575): vbPrevMatched[i] = F1.mvKeysUn[i].pt,

@@ -81,6 +81,8 @@ struct orbgpu_ctx {
     DevBuf<uint8_t> in_img;
     // matcher scratch
     DevBuf<uint8_t> mscratch;
+    DevBuf<uint32_t> mlists;  // SearchForInitialization candidate lists {dist:16|i2:16}
+    DevBuf<int> mlist_n;
     StageTimer timer;
     std::string err;
 };
@@ -462,6 +464,8 @@ void orbgpu_destroy(orbgpu_ctx* c)
     release(c->status);
     release(c->in_img);
     release(c->mscratch);
+    release(c->mlists);
+    release(c->mlist_n);
     for (hipEvent_t e : c->timer.ev) hipEventDestroy(e);
     if (c->done) hipEventDestroy(c->done);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -646,7 +650,15 @@ int orbgpu_search_for_initialization(orbgpu_ctx* c, const orbgpu_frame_view* F1,
     og_launch_grid(s, k2, cnts + 1, cap2, G, cs, ci, 1);
     OgFrameDev f1{k1, d1, cnts, nullptr, nullptr, nullptr, cap1};
     OgFrameDev f2{k2, d2, cnts + 1, cs, ci, nullptr, cap2};
-    og_launch_search_init(s, f1, 0, f2, G, nnratio, checkOri, windowSize, pv, 2 * cap1, m12, cap1, nm, 1);
+    int n2oct0 = 0;  // only octave-0 keypoints of F2 can be candidates (level1 == 0)
+    for (int i = 0; i < F2->n; i++) n2oct0 += F2->kps[i].octave == 0;
+    const int list_cap = std::max(n2oct0, 1);
+    HIP_TRY(c, ensure(c->mlists, (size_t)cap1 * list_cap));
+    HIP_TRY(c, ensure(c->mlist_n, (size_t)cap1));
+    HIP_TRY(c, ensure(c->status, 4));
+    HIP_TRY(c, hipMemsetAsync(c->status.p, 0, 16, s));
+    og_launch_search_init(s, f1, 0, f2, G, nnratio, checkOri, windowSize, pv, 2 * cap1, m12, cap1, nm, c->mlists.p,
+                          list_cap, c->mlist_n.p, c->status.p, 1);
     HIP_TRY(c, hipGetLastError());
     int hnm = 0;
     HIP_TRY(c, hipMemcpyAsync(&hnm, nm, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -655,6 +667,8 @@ int orbgpu_search_for_initialization(orbgpu_ctx* c, const orbgpu_frame_view* F1,
         HIP_TRY(c, hipMemcpyAsync(prev_xy, pv, (size_t)F1->n * 8, hipMemcpyDeviceToHost, s));
     }
     HIP_TRY(c, hipStreamSynchronize(s));
+    int r = check_status(c);
+    if (r) return r;
     *nmatches = hnm;
     return ORBGPU_OK;
 }
@@ -675,9 +689,14 @@ int orbgpu_search_for_initialization_batch(orbgpu_ctx* cref, int ref, orbgpu_ctx
     }
     OgFrameDev f1{cref->kps.p, cref->desc.p, cref->counts.p, nullptr, nullptr, nullptr, cref->plan.frame_cap};
     OgFrameDev f2{c->kps.p, c->desc.p, c->counts.p, c->cell_start.p, c->cell_items.p, nullptr, c->plan.frame_cap};
+    const int list_cap = c->plan.lv[0].kcap;  // F2 has at most kcap_0 octave-0 keypoints
+    const size_t cap1 = (size_t)cref->plan.frame_cap;
+    HIP_TRY(c, ensure(c->mlists, (size_t)c->last_B * cap1 * list_cap));
+    HIP_TRY(c, ensure(c->mlist_n, (size_t)c->last_B * cap1));
     timer_mark(c, "match_init");
     og_launch_search_init(s, f1, ref, f2, G, nnratio, checkOri, windowSize, d_prev_xy, 2 * cref->plan.frame_cap,
-                          d_matches12, cref->plan.frame_cap, d_nmatches, c->last_B);
+                          d_matches12, cref->plan.frame_cap, d_nmatches, c->mlists.p, list_cap, c->mlist_n.p,
+                          c->status.p, c->last_B);
     timer_mark(c, "search_init");
     HIP_TRY(c, hipGetLastError());
     return ORBGPU_OK;

@@ -43,7 +43,8 @@ struct OgFrameDev {        // device view of one or many frames (batch stride fr
 
 void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G, float nnratio,
                            int checkOri, int windowSize, float* prev_xy, int prev_stride, int* matches12,
-                           int match_stride, int* nmatches, int B);
+                           int match_stride, int* nmatches, uint32_t* lists, int list_cap, int* list_n, int* status,
+                           int B);
 
 void og_launch_prev_from_frame(hipStream_t s, OgFrameDev F1, int ref, float* prev_xy, int prev_stride, int B);
 
