@@ -159,6 +159,26 @@ int orbgpu_search_by_projection(orbgpu_ctx* ctx, const orbgpu_frame_view* F,
                                 const orbgpu_mappoints_view* mp, float nnratio, float th,
                                 int32_t* owner, int32_t* owner_obs, int* nmatches);
 
+/* ---- stereo ------------------------------------------------------------------------------------- */
+
+/* Replaces void Frame::ComputeStereoMatches() -- src/Frame.cc:466-640, called from the stereo Frame
+ * constructor src/Frame.cc:88.  `left` and `right` are the two extractors (mpORBextractorLeft/Right)
+ * right after orbgpu_extract on the rectified left and right images; both must share image size and
+ * scale pyramid (as constructed in src/Tracking.cc:119-122).  Reads mvKeys/mvKeysRight, both
+ * descriptor sets and both image pyramids from device memory; writes mvuRight (uright) and mvDepth
+ * (depth) for the n left keypoints (-1 where unmatched).  mbf = fx * baseline, mb = baseline.
+ * *nmatches (optional) = number of surviving matches after the 2.1 x median SAD filter.
+ * ORBGPU_ERR_CAPACITY (with *n set) when n > cap. */
+int orbgpu_compute_stereo_matches(orbgpu_ctx* left, orbgpu_ctx* right, float mbf, float mb,
+                                  float* uright, float* depth, int cap, int* n, int* nmatches);
+
+/* Batched device form: frame b of the left batch is paired with frame b of the right batch (both
+ * from orbgpu_extract_batch_device with the same B; the input image buffers must still be alive).
+ * d_uright/d_depth have stride = left frame_cap per frame; d_nmatches one int per frame.  Runs on
+ * the left context's stream after the right context's last batch. */
+int orbgpu_compute_stereo_matches_batch(orbgpu_ctx* left, orbgpu_ctx* right, float mbf, float mb,
+                                        float* d_uright, float* d_depth, int* d_nmatches);
+
 /* ---- stream / timing helpers ------------------------------------------------------------------ */
 
 /* The context's hipStream_t (as void*), e.g. for torch.cuda.ExternalStream. */

@@ -62,6 +62,8 @@ def lib():
         L.oo_features_in_area.argtypes = [vp, f32, f32, f32, i32, i32, vp]
         L.oo_search_for_initialization.restype = i32
         L.oo_search_for_initialization.argtypes = [vp, vp, f32, i32, vp, vp, i32]
+        L.oo_stereo_matches.restype = i32
+        L.oo_stereo_matches.argtypes = [vp, vp, vp, vp, i32, vp, vp, i32, f32, f32, vp, vp]
         L.oo_search_by_projection.restype = i32
         L.oo_search_by_projection.argtypes = [vp, vp, f32, f32, vp, vp]
         _lib = L
@@ -210,6 +212,19 @@ def distribute_octree(xy, resp, minX, maxX, minY, maxY, N):
     orr = np.zeros(cap, np.float32)
     m = lib().oo_distribute_octree(_p(xy), _p(resp), len(resp), minX, maxX, minY, maxY, N, _p(oxy), _p(orr))
     return oxy[:m].copy(), orr[:m].copy()
+
+
+def stereo_matches(exL: "OracleExtractor", exR: "OracleExtractor", kL, dL, kR, dR, mbf, mb):
+    """Frame::ComputeStereoMatches on the two extractors' last pyramids -> (n, uright, depth)."""
+    kL = np.ascontiguousarray(kL)
+    kR = np.ascontiguousarray(kR)
+    dL = np.ascontiguousarray(dL, np.uint8)
+    dR = np.ascontiguousarray(dR, np.uint8)
+    ur = np.zeros(max(len(kL), 1), np.float32)
+    de = np.zeros(max(len(kL), 1), np.float32)
+    n = lib().oo_stereo_matches(exL._h, exR._h, _p(kL), _p(dL), len(kL), _p(kR), _p(dR), len(kR), mbf, mb,
+                                _p(ur), _p(de))
+    return n, ur[:len(kL)].copy(), de[:len(kL)].copy()
 
 
 def descriptor_distance(a, b) -> int:

@@ -951,3 +951,153 @@ int oo_search_by_projection(const oo_frame* F, const oo_mappoints* mp, float nnr
     free(idx);
     return nmatches;
 }
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Frame::ComputeStereoMatches (src/Frame.cc:466-640): left keypoints/descriptors (mvKeys), right      */
+/* keypoints/descriptors (mvKeysRight), both extractors' pyramids (mvImagePyramid).                    */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct { int first, second; } oo_pair;
+static int oo_pair_cmp(const void* a, const void* b)
+{
+    const oo_pair *x = (const oo_pair*)a, *y = (const oo_pair*)b;
+    if (x->first != y->first) return x->first < y->first ? -1 : 1;
+    return x->second < y->second ? -1 : (x->second > y->second);
+}
+
+int oo_stereo_matches(const oo_extractor* EL, const oo_extractor* ER, const oo_keypoint* kL, const uint8_t* dL,
+                      int N, const oo_keypoint* kR, const uint8_t* dR, int Nr, float mbf, float mb,
+                      float* uright, float* depth)
+{
+    for (int i = 0; i < N; i++) { uright[i] = -1.0f; depth[i] = -1.0f; }
+    const int thOrbDist = (OO_TH_HIGH + OO_TH_LOW) / 2;
+    const int nRows = EL->lh[0];
+    int* rowCnt = (int*)calloc((size_t)nRows + 1, sizeof(int));
+    /* row -> right keypoint indices, in iR order (vRowIndices, :476-493) */
+    for (int pass = 0; pass < 2; pass++) {
+        for (int iR = 0; iR < Nr; iR++) {
+            const float kpY = kR[iR].y;
+            const float r = 2.0f * EL->sf[kR[iR].octave];
+            const int maxr = (int)ceilf(kpY + r);
+            const int minr = (int)floorf(kpY - r);
+            for (int yi = minr; yi <= maxr; yi++) {
+                if (yi < 0 || yi >= nRows) continue; /* out of range is UB in the reference */
+                rowCnt[yi]++;
+            }
+        }
+        if (pass == 0) break;
+    }
+    int* rowStart = (int*)malloc(sizeof(int) * ((size_t)nRows + 1));
+    rowStart[0] = 0;
+    for (int y = 0; y < nRows; y++) rowStart[y + 1] = rowStart[y] + rowCnt[y];
+    int* rowItems = (int*)malloc(sizeof(int) * ((size_t)rowStart[nRows] + 1));
+    memset(rowCnt, 0, sizeof(int) * (size_t)nRows);
+    for (int iR = 0; iR < Nr; iR++) {
+        const float kpY = kR[iR].y;
+        const float r = 2.0f * EL->sf[kR[iR].octave];
+        const int maxr = (int)ceilf(kpY + r);
+        const int minr = (int)floorf(kpY - r);
+        for (int yi = minr; yi <= maxr; yi++) {
+            if (yi < 0 || yi >= nRows) continue;
+            rowItems[rowStart[yi] + rowCnt[yi]++] = iR;
+        }
+    }
+    const float minZ = mb;
+    const float minD = 0;
+    const float maxD = mbf / minZ;
+    oo_pair* vDistIdx = (oo_pair*)malloc(sizeof(oo_pair) * ((size_t)N + 1));
+    int nDist = 0;
+    for (int iL = 0; iL < N; iL++) {
+        const oo_keypoint* kpL = &kL[iL];
+        const int levelL = kpL->octave;
+        const float vL = kpL->y, uL = kpL->x;
+        const int row = (int)vL;
+        if (row < 0 || row >= nRows) continue;
+        const int cb = rowStart[row], ce = rowStart[row + 1];
+        if (cb == ce) continue;
+        const float minU = uL - maxD, maxU = uL - minD;
+        if (maxU < 0) continue;
+        int bestDist = OO_TH_HIGH;
+        int bestIdxR = 0;
+        const uint8_t* dl = dL + (size_t)iL * 32;
+        for (int c = cb; c < ce; c++) {
+            const int iR = rowItems[c];
+            const oo_keypoint* kpR = &kR[iR];
+            if (kpR->octave < levelL - 1 || kpR->octave > levelL + 1) continue;
+            const float uR = kpR->x;
+            if (uR >= minU && uR <= maxU) {
+                const int dist = oo_descriptor_distance(dl, dR + (size_t)iR * 32);
+                if (dist < bestDist) { bestDist = dist; bestIdxR = iR; }
+            }
+        }
+        if (bestDist < thOrbDist) {
+            const float uR0 = kR[bestIdxR].x;
+            const float scaleFactor = EL->isf[kpL->octave];
+            const float scaleduL = roundf(kpL->x * scaleFactor);
+            const float scaledvL = roundf(kpL->y * scaleFactor);
+            const float scaleduR0 = roundf(uR0 * scaleFactor);
+            const int w = 5;
+            const int lw = EL->lw[levelL];
+            const uint8_t* IL = EL->lev[levelL];
+            const uint8_t* IRim = ER->lev[levelL];
+            const int rw = ER->lw[levelL];
+            const int ivL = (int)scaledvL, iuL = (int)scaleduL, iuR0 = (int)scaleduR0;
+            const float cL = (float)IL[(size_t)ivL * lw + iuL];
+            int bestD = INT_MAX;
+            int bestincR = 0;
+            const int L = 5;
+            float vDists[11];
+            const float iniu = scaleduR0 + L - w;
+            const float endu = scaleduR0 + L + w + 1;
+            if (iniu < 0 || endu >= rw) continue;
+            for (int incR = -L; incR <= +L; incR++) {
+                const float cR = (float)IRim[(size_t)ivL * rw + iuR0 + incR];
+                double acc = 0; /* cv::norm(IL, IR, NORM_L1) on CV_32F: exact (integer-valued) */
+                for (int yy = -w; yy <= w; yy++)
+                    for (int xx = -w; xx <= w; xx++) {
+                        const float a = (float)IL[(size_t)(ivL + yy) * lw + iuL + xx] - cL;
+                        const float b = (float)IRim[(size_t)(ivL + yy) * rw + iuR0 + incR + xx] - cR;
+                        acc += fabs((double)a - (double)b);
+                    }
+                const float dist = (float)acc;
+                if (dist < bestD) { bestD = (int)dist; bestincR = incR; }
+                vDists[L + incR] = dist;
+            }
+            if (bestincR == -L || bestincR == L) continue;
+            const float dist1 = vDists[L + bestincR - 1];
+            const float dist2 = vDists[L + bestincR];
+            const float dist3 = vDists[L + bestincR + 1];
+            const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+            if (deltaR < -1 || deltaR > 1) continue;
+            float bestuR = EL->sf[kpL->octave] * ((float)scaleduR0 + (float)bestincR + deltaR);
+            float disparity = (uL - bestuR);
+            if (disparity >= minD && disparity < maxD) {
+                if (disparity <= 0) {
+                    disparity = 0.01f;
+                    bestuR = (float)((double)uL - 0.01);
+                }
+                depth[iL] = mbf / disparity;
+                uright[iL] = bestuR;
+                vDistIdx[nDist].first = bestD;
+                vDistIdx[nDist].second = iL;
+                nDist++;
+            }
+        }
+    }
+    int nvalid = nDist;
+    if (nDist > 0) {
+        qsort(vDistIdx, (size_t)nDist, sizeof(oo_pair), oo_pair_cmp);
+        const float median = (float)vDistIdx[nDist / 2].first;
+        const float thDist = 1.5f * 1.4f * median;
+        for (int i = nDist - 1; i >= 0; i--) {
+            if (vDistIdx[i].first < thDist) break;
+            uright[vDistIdx[i].second] = -1;
+            depth[vDistIdx[i].second] = -1;
+            nvalid--;
+        }
+    }
+    free(rowCnt);
+    free(rowStart);
+    free(rowItems);
+    free(vDistIdx);
+    return nvalid;
+}

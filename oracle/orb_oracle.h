@@ -111,6 +111,12 @@ typedef struct {
 int oo_search_by_projection(const oo_frame* f, const oo_mappoints* mp, float nnratio, float th,
                             int* owner, int* owner_obs);
 
+/* Frame::ComputeStereoMatches (src/Frame.cc:466-640) on two oracle extractors' last pyramids.
+ * uright/depth: N floats out.  Returns the number of surviving stereo matches. */
+int oo_stereo_matches(const oo_extractor* EL, const oo_extractor* ER, const oo_keypoint* kL, const uint8_t* dL,
+                      int N, const oo_keypoint* kR, const uint8_t* dR, int Nr, float mbf, float mb,
+                      float* uright, float* depth);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,7 +24,7 @@ EXPORTS = [
     "orbgpu_stage_times", "orbgpu_last_error", "orbgpu_debug_candidates", "orbgpu_debug_octree",
     "orbgpu_device_alloc", "orbgpu_device_free", "orbgpu_memcpy_h2d", "orbgpu_memcpy_d2h",
     "orbgpu_memset_d", "orbgpu_prev_matched_from_frame", "orbgpu_memcpy_d2d_async",
-    "orbgpu_batch_candidate_total",
+    "orbgpu_batch_candidate_total", "orbgpu_compute_stereo_matches", "orbgpu_compute_stereo_matches_batch",
 ]
 
 OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
@@ -98,6 +98,8 @@ def _declare(L):
     L.orbgpu_prev_matched_from_frame.argtypes = [vp, i32, vp, vp]
     L.orbgpu_memcpy_d2d_async.argtypes = [vp, vp, vp, sz]
     L.orbgpu_batch_candidate_total.restype = C.c_longlong
+    L.orbgpu_compute_stereo_matches.argtypes = [vp, vp, f32, f32, vp, vp, i32, C.POINTER(i32), C.POINTER(i32)]
+    L.orbgpu_compute_stereo_matches_batch.argtypes = [vp, vp, f32, f32, vp, vp, vp]
     L.orbgpu_batch_candidate_total.argtypes = [vp]
 
 

@@ -1,0 +1,326 @@
+// orb_stereo.hip -- gfx950 kernels of Frame::ComputeStereoMatches (src/Frame.cc:466-640).
+//
+//   og_stereo_rows_kernel   : vRowIndices (:476-493) as a CSR over image rows, right keypoints of each
+//                             row in index order (one workgroup per frame pair)
+//   og_stereo_match_kernel  : one wave per left keypoint: row-band Hamming search (levels +-1, u-range,
+//                             strict-< first minimum, :504-549), 11x121 SAD sliding window on both
+//                             pyramids with wave reductions (exact integers), parabola sub-pixel fit,
+//                             disparity / depth (:552-622)
+//   og_stereo_filter_kernel : median of the SAD distances by two-pass radix select, 2.1 x median
+//                             rejection (:626-639)
+#include <hip/hip_runtime.h>
+#include <limits.h>
+#include <stdint.h>
+
+#include "orb_math_dev.h"
+#include "orbgpu_internal.h"
+#include "orbgpu_launch.h"
+
+typedef unsigned long long u64;
+
+#define ST_TH_HIGH 100
+#define ST_TH_LOW 50
+#define ST_MAXROWS 8192
+
+__global__ __launch_bounds__(256) void og_stereo_rows_kernel(OgStereoDev S)
+{
+    __shared__ int cnt[ST_MAXROWS + 1];
+    __shared__ int wsum[8];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int Nr = S.R.counts[b];
+    const orbgpu_kp_dev* KR = S.R.kps + (long long)b * S.R.frame_cap;
+    int* RS = S.row_start + (long long)b * (S.nRows + 1);
+    int* RI = S.row_items + (long long)b * S.row_cap;
+    for (int y = tid; y <= S.nRows; y += 256) cnt[y] = 0;
+    __syncthreads();
+    for (int iR = tid; iR < Nr; iR += 256) {
+        const float kpY = KR[iR].y;
+        const float r = 2.0f * S.sf[KR[iR].octave];
+        const int maxr = (int)ceilf(kpY + r), minr = (int)floorf(kpY - r);
+        for (int yi = max(minr, 0); yi <= min(maxr, S.nRows - 1); yi++) atomicAdd(&cnt[yi], 1);
+    }
+    __syncthreads();
+    // exclusive scan of cnt[0..nRows) (serial chunks per thread + one scan of chunk sums)
+    const int per = (S.nRows + 255) / 256;
+    const int lo = tid * per, hi = min(lo + per, S.nRows);
+    int sum = 0;
+    for (int y = lo; y < hi; y++) sum += cnt[y];
+    const int lane = tid & 63, w = tid >> 6;
+    int x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(x, o);
+        if (lane >= o) x += t;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int before = 0;
+    for (int q = 0; q < w; q++) before += wsum[q];
+    int run = before + x - sum;
+    __syncthreads();
+    for (int y = lo; y < hi; y++) {
+        const int c = cnt[y];
+        RS[y] = run;
+        cnt[y] = run;  // cursor
+        run += c;
+    }
+    if (tid == 255) {
+        int tot = 0;
+        for (int q = 0; q < 4; q++) tot += wsum[q];
+        RS[S.nRows] = tot;
+    }
+    __syncthreads();
+    for (int iR = tid; iR < Nr; iR += 256) {
+        const float kpY = KR[iR].y;
+        const float r = 2.0f * S.sf[KR[iR].octave];
+        const int maxr = (int)ceilf(kpY + r), minr = (int)floorf(kpY - r);
+        for (int yi = max(minr, 0); yi <= min(maxr, S.nRows - 1); yi++) {
+            const int pos = atomicAdd(&cnt[yi], 1);
+            if (pos < S.row_cap) RI[pos] = iR;
+        }
+    }
+    __syncthreads();
+    __threadfence_block();
+    // push_back order: ascending iR inside each row
+    for (int y = tid; y < S.nRows; y += 256) {
+        const int b0 = RS[y], e = min(RS[y + 1], S.row_cap);
+        for (int p = b0 + 1; p < e; p++) {
+            const int v = RI[p];
+            int q = p - 1;
+            while (q >= b0 && RI[q] > v) {
+                RI[q + 1] = RI[q];
+                q--;
+            }
+            RI[q + 1] = v;
+        }
+    }
+}
+
+__device__ __forceinline__ int og_wave_isum(int v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void og_stereo_match_kernel(OgStereoDev S)
+{
+    const int b = blockIdx.y, lane = threadIdx.x & 63;
+    const int iL = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int N = S.L.counts[b];
+    if (iL >= N) return;
+    float* UR = S.uright + (long long)b * S.L.frame_cap;
+    float* DE = S.depth + (long long)b * S.L.frame_cap;
+    int* SAD = S.sad + (long long)b * S.L.frame_cap;
+    if (lane == 0) {
+        UR[iL] = -1.0f;
+        DE[iL] = -1.0f;
+        SAD[iL] = -1;
+    }
+    const orbgpu_kp_dev kpL = S.L.kps[(long long)b * S.L.frame_cap + iL];
+    const orbgpu_kp_dev* KR = S.R.kps + (long long)b * S.R.frame_cap;
+    const int levelL = kpL.octave;
+    const float vL = kpL.y, uL = kpL.x;
+    const int row = (int)vL;
+    if (row < 0 || row >= S.nRows) return;
+    const int* RS = S.row_start + (long long)b * (S.nRows + 1);
+    const int* RI = S.row_items + (long long)b * S.row_cap;
+    const int cb = RS[row], ce = min(RS[row + 1], S.row_cap);
+    if (cb == ce) return;
+    const float minZ = S.mb, minD = 0;
+    const float maxD = S.mbf / minZ;
+    const float minU = uL - maxD, maxU = uL - minD;
+    if (maxU < 0) return;
+    // ---- row-band Hamming search: first strict minimum below TH_HIGH in candidate order
+    uint4 da, db;
+    {
+        const uint4* q = (const uint4*)(S.L.desc + ((long long)b * S.L.frame_cap + iL) * 32);
+        da = q[0];
+        db = q[1];
+    }
+    u64 best = ~0ull;
+    for (int c = cb + lane; c - lane < ce; c += 64) {
+        u64 key = ~0ull;
+        if (c < ce) {
+            const int iR = RI[c];
+            const orbgpu_kp_dev kpR = KR[iR];
+            if (!(kpR.octave < levelL - 1 || kpR.octave > levelL + 1)) {
+                const float uR = kpR.x;
+                if (uR >= minU && uR <= maxU) {
+                    const uint4* q = (const uint4*)(S.R.desc + ((long long)b * S.R.frame_cap + iR) * 32);
+                    const int dist = og_hamming(da, db, q[0], q[1]);
+                    if (dist < ST_TH_HIGH) key = ((u64)dist << 32) | ((u64)(c - cb) << 16) | (u64)iR;
+                }
+            }
+        }
+        best = key < best ? key : best;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const u64 w = __shfl_xor(best, o);
+        best = w < best ? w : best;
+    }
+    const int thOrbDist = (ST_TH_HIGH + ST_TH_LOW) / 2;
+    if (best == ~0ull || (int)(best >> 32) >= thOrbDist) return;
+    const int bestIdxR = (int)(best & 0xffff);
+    // ---- SAD sliding window on the keypoint's pyramid level (:552-592)
+    const float uR0 = KR[bestIdxR].x;
+    const float scaleFactor = S.isf[levelL];
+    const float scaleduL = roundf(kpL.x * scaleFactor);
+    const float scaledvL = roundf(kpL.y * scaleFactor);
+    const float scaleduR0 = roundf(uR0 * scaleFactor);
+    const int w = 5, Lw = 5;
+    const float iniu = scaleduR0 + Lw - w;
+    const float endu = scaleduR0 + Lw + w + 1;
+    const int rcols = S.lvl_w[levelL];
+    if (iniu < 0 || endu >= rcols) return;
+    const uint8_t* IL;
+    const uint8_t* IR;
+    long long pl, pr;
+    if (levelL == 0) {
+        IL = S.L0 + (long long)b * S.L0_fstride;
+        pl = S.L0_pitch;
+        IR = S.R0 + (long long)b * S.R0_fstride;
+        pr = S.R0_pitch;
+    } else {
+        IL = S.Lpyr + (long long)b * S.pyr_fstride + S.lvl_off[levelL];
+        IR = S.Rpyr + (long long)b * S.pyr_fstride + S.lvl_off[levelL];
+        pl = pr = S.lvl_pitch[levelL];
+    }
+    const int ivL = (int)scaledvL, iuL = (int)scaleduL, iuR0 = (int)scaleduR0;
+    const int cL = IL[(long long)ivL * pl + iuL];
+    // lane p (< 61) owns window pixels 2p and 2p+1 of the 11x11 patch (121 pixels)
+    int lv[2] = {0, 0}, px[2] = {0, 0}, py[2] = {0, 0};
+    bool has[2] = {false, false};
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int pidx = 2 * lane + k;
+        if (pidx < 121) {
+            has[k] = true;
+            py[k] = pidx / 11 - w;
+            px[k] = pidx % 11 - w;
+            lv[k] = (int)IL[(long long)(ivL + py[k]) * pl + iuL + px[k]] - cL;
+        }
+    }
+    int bestD = INT_MAX, bestincR = 0;
+    float vDists[11];
+#pragma unroll
+    for (int incR = -Lw; incR <= Lw; incR++) {
+        const int cR = IR[(long long)ivL * pr + iuR0 + incR];
+        int part = 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+            if (has[k]) {
+                const int rv = (int)IR[(long long)(ivL + py[k]) * pr + iuR0 + incR + px[k]] - cR;
+                part += abs(lv[k] - rv);
+            }
+        const float dist = (float)og_wave_isum(part);  // cv::norm(IL, IR, NORM_L1): exact integer
+        if (dist < bestD) {
+            bestD = (int)dist;
+            bestincR = incR;
+        }
+        vDists[Lw + incR] = dist;
+    }
+    if (bestincR == -Lw || bestincR == Lw) return;
+    const float dist1 = vDists[Lw + bestincR - 1];
+    const float dist2 = vDists[Lw + bestincR];
+    const float dist3 = vDists[Lw + bestincR + 1];
+    const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+    if (deltaR < -1 || deltaR > 1) return;
+    float bestuR = S.sf[levelL] * ((float)scaleduR0 + (float)bestincR + deltaR);
+    float disparity = (uL - bestuR);
+    if (disparity >= minD && disparity < maxD) {
+        if (disparity <= 0) {
+            disparity = 0.01f;
+            bestuR = (float)((double)uL - 0.01);
+        }
+        if (lane == 0) {
+            DE[iL] = S.mbf / disparity;
+            UR[iL] = bestuR;
+            SAD[iL] = bestD;
+        }
+    }
+}
+
+// median of the valid SAD distances (radix select on 16-bit values: <= 121 * 510 = 61710), then the
+// 1.5 * 1.4 * median rejection, which removes exactly the entries with (float)dist >= thDist (:626-639)
+__global__ __launch_bounds__(256) void og_stereo_filter_kernel(OgStereoDev S)
+{
+    __shared__ int hist[256];
+    __shared__ int sel[4];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int N = S.L.counts[b];
+    float* UR = S.uright + (long long)b * S.L.frame_cap;
+    float* DE = S.depth + (long long)b * S.L.frame_cap;
+    const int* SAD = S.sad + (long long)b * S.L.frame_cap;
+    hist[tid] = 0;
+    if (tid < 4) sel[tid] = 0;
+    __syncthreads();
+    int nv = 0;
+    for (int i = tid; i < N; i += 256) {
+        const int d = SAD[i];
+        if (d >= 0) {
+            atomicAdd(&hist[(d >> 8) & 255], 1);
+            nv++;
+        }
+    }
+    atomicAdd(&sel[0], nv);
+    __syncthreads();
+    const int n = sel[0];
+    if (n == 0) {
+        if (tid == 0) S.nmatches[b] = 0;
+        return;
+    }
+    const int k = n / 2;  // vDistIdx[size/2].first
+    if (tid == 0) {
+        int acc = 0, bin = 0;
+        for (; bin < 256; bin++) {
+            if (acc + hist[bin] > k) break;
+            acc += hist[bin];
+        }
+        sel[1] = bin;
+        sel[2] = k - acc;
+    }
+    __syncthreads();
+    const int hiBin = sel[1], k2 = sel[2];
+    hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < N; i += 256) {
+        const int d = SAD[i];
+        if (d >= 0 && ((d >> 8) & 255) == hiBin) atomicAdd(&hist[d & 255], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0, bin = 0;
+        for (; bin < 256; bin++) {
+            if (acc + hist[bin] > k2) break;
+            acc += hist[bin];
+        }
+        sel[3] = (hiBin << 8) | bin;
+    }
+    __syncthreads();
+    const float median = (float)sel[3];
+    const float thDist = 1.5f * 1.4f * median;
+    int rej = 0;
+    for (int i = tid; i < N; i += 256) {
+        const int d = SAD[i];
+        if (d >= 0 && !((float)d < thDist)) {
+            UR[i] = -1;
+            DE[i] = -1;
+            rej++;
+        }
+    }
+    __shared__ int rsum;
+    if (tid == 0) rsum = 0;
+    __syncthreads();
+    atomicAdd(&rsum, rej);
+    __syncthreads();
+    if (tid == 0) S.nmatches[b] = n - rsum;
+}
+
+void og_launch_stereo(hipStream_t s, const OgStereoDev& S, int B)
+{
+    hipLaunchKernelGGL(og_stereo_rows_kernel, dim3(B), dim3(256), 0, s, S);
+    hipLaunchKernelGGL(og_stereo_match_kernel, dim3((S.L.frame_cap + 3) / 4, B), dim3(256), 0, s, S);
+    hipLaunchKernelGGL(og_stereo_filter_kernel, dim3(B), dim3(256), 0, s, S);
+}

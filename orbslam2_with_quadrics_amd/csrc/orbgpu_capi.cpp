@@ -83,6 +83,9 @@ struct orbgpu_ctx {
     DevBuf<uint8_t> mscratch;
     DevBuf<uint32_t> mlists;  // SearchForInitialization candidate lists {dist:16|i2:16}
     DevBuf<int> mlist_n;
+    // stereo scratch (Frame::ComputeStereoMatches)
+    DevBuf<int> st_row_start, st_row_items, st_sad, st_nm;
+    DevBuf<float> st_out;
     StageTimer timer;
     std::string err;
 };
@@ -466,6 +469,11 @@ void orbgpu_destroy(orbgpu_ctx* c)
     release(c->mscratch);
     release(c->mlists);
     release(c->mlist_n);
+    release(c->st_row_start);
+    release(c->st_row_items);
+    release(c->st_sad);
+    release(c->st_nm);
+    release(c->st_out);
     for (hipEvent_t e : c->timer.ev) hipEventDestroy(e);
     if (c->done) hipEventDestroy(c->done);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -710,6 +718,106 @@ int orbgpu_prev_matched_from_frame(orbgpu_ctx* cref, int ref, orbgpu_ctx* c, flo
     OgFrameDev f1{cref->kps.p, cref->desc.p, cref->counts.p, nullptr, nullptr, nullptr, cref->plan.frame_cap};
     og_launch_prev_from_frame(c->stream, f1, ref, d_prev_xy, 2 * cref->plan.frame_cap, c->last_B);
     HIP_TRY(c, hipGetLastError());
+    return ORBGPU_OK;
+}
+
+// ---- stereo: Frame::ComputeStereoMatches (src/Frame.cc:466-640) -------------------------------------
+static int stereo_launch(orbgpu_ctx* L, orbgpu_ctx* R, float mbf, float mb, float* d_ur, float* d_depth, int* d_nm)
+{
+    if (!L || !R || !L->last_B || !R->last_B || L->last_B != R->last_B) return ORBGPU_ERR_ARG;
+    if (L->W != R->W || L->H != R->H || L->nlevels != R->nlevels || L->sf != R->sf ||
+        L->plan.pyr_per_frame != R->plan.pyr_per_frame) {
+        L->err = "stereo: left and right extractors must share image size and scale pyramid";
+        return ORBGPU_ERR_ARG;
+    }
+    if (!(mb > 0.0f)) {
+        L->err = "stereo: baseline must be positive";
+        return ORBGPU_ERR_ARG;
+    }
+    const int B = L->last_B;
+    const OgPlan& P = L->plan;
+    HIP_TRY(L, hipSetDevice(L->device));
+    hipStream_t s = L->stream;
+    if (R != L) HIP_TRY(L, hipStreamWaitEvent(s, R->done, 0));
+    OgStereoDev S{};
+    S.L = OgFrameDev{L->kps.p, L->desc.p, L->counts.p, nullptr, nullptr, nullptr, P.frame_cap};
+    S.R = OgFrameDev{R->kps.p, R->desc.p, R->counts.p, nullptr, nullptr, nullptr, R->plan.frame_cap};
+    S.L0 = L->last_img;
+    S.R0 = R->last_img;
+    S.L0_pitch = L->last_pitch;
+    S.L0_fstride = L->last_fstride;
+    S.R0_pitch = R->last_pitch;
+    S.R0_fstride = R->last_fstride;
+    S.Lpyr = L->pyr.p;
+    S.Rpyr = R->pyr.p;
+    S.pyr_fstride = P.pyr_per_frame;
+    for (int l = 0; l < P.nlevels; l++) {
+        S.lvl_off[l] = P.lv[l].pyr_off;
+        S.lvl_pitch[l] = P.lv[l].pitch;
+        S.lvl_w[l] = P.lv[l].w;
+        S.sf[l] = L->sf[l];
+        S.isf[l] = L->isf[l];
+    }
+    S.mbf = mbf;
+    S.mb = mb;
+    S.nRows = L->H;
+    if (S.nRows > 8192) {
+        L->err = "stereo: more than 8192 image rows";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
+    // every right keypoint spans at most 2*ceil(2*sf)+2 rows of vRowIndices
+    const int span = 2 * (int)std::ceil(2.0f * L->sf[P.nlevels - 1]) + 2;
+    S.row_cap = R->plan.frame_cap * span;
+    HIP_TRY(L, ensure(L->st_row_start, (size_t)B * (S.nRows + 1)));
+    HIP_TRY(L, ensure(L->st_row_items, (size_t)B * S.row_cap));
+    HIP_TRY(L, ensure(L->st_sad, (size_t)B * P.frame_cap));
+    S.row_start = L->st_row_start.p;
+    S.row_items = L->st_row_items.p;
+    S.sad = L->st_sad.p;
+    S.uright = d_ur;
+    S.depth = d_depth;
+    S.nmatches = d_nm;
+    timer_mark(L, "stereo_in");
+    og_launch_stereo(s, S, B);
+    timer_mark(L, "stereo");
+    HIP_TRY(L, hipGetLastError());
+    return ORBGPU_OK;
+}
+
+int orbgpu_compute_stereo_matches_batch(orbgpu_ctx* left, orbgpu_ctx* right, float mbf, float mb, float* d_uright,
+                                        float* d_depth, int* d_nmatches)
+{
+    if (!d_uright || !d_depth || !d_nmatches) return ORBGPU_ERR_ARG;
+    return stereo_launch(left, right, mbf, mb, d_uright, d_depth, d_nmatches);
+}
+
+int orbgpu_compute_stereo_matches(orbgpu_ctx* left, orbgpu_ctx* right, float mbf, float mb, float* uright,
+                                  float* depth, int cap, int* n, int* nmatches)
+{
+    if (!left || !right || !n) return ORBGPU_ERR_ARG;
+    if (left->last_B != 1 || right->last_B != 1) {
+        left->err = "stereo: host form needs one extracted frame on each side";
+        return ORBGPU_ERR_ARG;
+    }
+    HIP_TRY(left, hipSetDevice(left->device));
+    const int fc = left->plan.frame_cap;
+    HIP_TRY(left, ensure(left->st_out, 2 * (size_t)fc));
+    HIP_TRY(left, ensure(left->st_nm, 4));
+    int r = stereo_launch(left, right, mbf, mb, left->st_out.p, left->st_out.p + fc, left->st_nm.p);
+    if (r) return r;
+    int hc[2] = {0, 0};
+    HIP_TRY(left, hipMemcpyAsync(&hc[0], left->counts.p, sizeof(int), hipMemcpyDeviceToHost, left->stream));
+    HIP_TRY(left, hipMemcpyAsync(&hc[1], left->st_nm.p, sizeof(int), hipMemcpyDeviceToHost, left->stream));
+    HIP_TRY(left, hipStreamSynchronize(left->stream));
+    *n = hc[0];
+    if (nmatches) *nmatches = hc[1];
+    if (hc[0] > cap) return ORBGPU_ERR_CAPACITY;
+    if (hc[0] > 0) {
+        if (uright)
+            HIP_TRY(left, hipMemcpy(uright, left->st_out.p, (size_t)hc[0] * 4, hipMemcpyDeviceToHost));
+        if (depth)
+            HIP_TRY(left, hipMemcpy(depth, left->st_out.p + fc, (size_t)hc[0] * 4, hipMemcpyDeviceToHost));
+    }
     return ORBGPU_OK;
 }
 

@@ -68,3 +68,28 @@ void og_launch_proj_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float
 void og_launch_proj_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp,
                             float nnratio, float th, const int* off, OgProjCand* cands, int* owner, int* owner_obs,
                             int* nmatches);
+
+// stereo (orb_stereo.hip): Frame::ComputeStereoMatches over frame pairs b of two extractor batches
+struct OgStereoDev {
+    OgFrameDev L, R;                 // left / right keypoints + descriptors (level-0 coordinates)
+    const uint8_t* L0;               // level-0 images (the extractors' inputs)
+    const uint8_t* R0;
+    long long L0_pitch, L0_fstride, R0_pitch, R0_fstride;
+    const uint8_t* Lpyr;             // levels >= 1 (same plan on both sides)
+    const uint8_t* Rpyr;
+    long long pyr_fstride;
+    long long lvl_off[OG_MAXLEVELS];
+    int lvl_pitch[OG_MAXLEVELS];
+    int lvl_w[OG_MAXLEVELS];
+    float sf[OG_MAXLEVELS], isf[OG_MAXLEVELS];
+    float mbf, mb;
+    int nRows;                       // level-0 image rows
+    int row_cap;                     // per-frame capacity of row_items
+    int* row_start;                  // per frame nRows+1
+    int* row_items;                  // per frame row_cap
+    float* uright;                   // per frame L.frame_cap
+    float* depth;
+    int* sad;                        // per frame L.frame_cap: SAD distance of a match, -1 otherwise
+    int* nmatches;                   // per frame
+};
+void og_launch_stereo(hipStream_t s, const OgStereoDev& S, int B);

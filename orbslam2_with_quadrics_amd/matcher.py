@@ -36,6 +36,19 @@ class Frame:
         k, d = extractor(image)
         return cls(k, d, image.shape[1], image.shape[0], extractor.GetScaleFactors())
 
+    @classmethod
+    def from_stereo(cls, ex_left: ORBextractor, ex_right: ORBextractor, im_left: np.ndarray,
+                    im_right: np.ndarray, mbf: float, mb: float):
+        """Stereo Frame constructor (src/Frame.cc:52-105, no distortion): extract both images, then
+        ComputeStereoMatches fills mvuRight / mvDepth."""
+        k, d = ex_left(im_left)
+        kr, dr = ex_right(im_right)
+        f = cls(k, d, im_left.shape[1], im_left.shape[0], ex_left.GetScaleFactors())
+        f.mvKeysRight, f.mDescriptorsRight = kr, dr
+        f.mbf, f.mb = float(mbf), float(mb)
+        f.mvuRight, f.mvDepth, f.nStereo = ComputeStereoMatches(ex_left, ex_right, mbf, mb)
+        return f
+
     def view(self) -> _lib.FrameView:
         v = _lib.FrameView()
         v.n = self.N
@@ -108,3 +121,17 @@ class ORBmatcher:
                                                     C.byref(nm))
         _lib.check(ctx, rc, "orbgpu_search_by_projection")
         return nm.value, owner, owner_obs
+
+
+def ComputeStereoMatches(ex_left: ORBextractor, ex_right: ORBextractor, mbf: float, mb: float):
+    """Frame::ComputeStereoMatches (src/Frame.cc:466-640) on the last frame each extractor processed.
+    Returns (mvuRight, mvDepth, nmatches): float32 arrays over the left keypoints, -1 where unmatched."""
+    L = _lib.lib()
+    n, nm = C.c_int(0), C.c_int(0)
+    cap = L.orbgpu_max_keypoints(ex_left.ctx)
+    ur = np.empty(max(cap, 1), np.float32)
+    de = np.empty(max(cap, 1), np.float32)
+    rc = L.orbgpu_compute_stereo_matches(ex_left.ctx, ex_right.ctx, float(mbf), float(mb), _p(ur), _p(de), cap,
+                                         C.byref(n), C.byref(nm))
+    _lib.check(ex_left.ctx, rc, "orbgpu_compute_stereo_matches")
+    return ur[:n.value].copy(), de[:n.value].copy(), nm.value

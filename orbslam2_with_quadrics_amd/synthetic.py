@@ -74,3 +74,23 @@ def flat(height: int, width: int, value: int = 128) -> np.ndarray:
 def pure_noise(seed: int, height: int, width: int) -> np.ndarray:
     rng = np.random.Generator(np.random.PCG64(seed))
     return rng.integers(0, 256, size=(height, width), dtype=np.uint8)
+
+
+def stereo_pair(pair_id: int, height: int, width: int, band: int = 64, dmin: int = 4, dmax: int = 40):
+    """(left, right) rectified pair (config 4): the right image sees the scene point of left column x at
+    column x - d, with d constant inside horizontal bands of `band` rows and drawn in [dmin, dmax]."""
+    scene = make_scene(SEED_BASE + pair_id, height, width)
+    left = render(scene, height, width, 0, 0, noise_seed=SEED_BASE + 7919 * pair_id + 1)
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 104729 * pair_id + 3))
+    nb = (height + band - 1) // band
+    disp = rng.integers(dmin, dmax + 1, size=nb)
+    m = 64
+    shifted = np.empty((height, width), np.float32)
+    for b in range(nb):
+        y0, y1 = b * band, min((b + 1) * band, height)
+        d = int(disp[b])
+        shifted[y0:y1] = scene[m + y0:m + y1, m + d:m + d + width]
+    noise = np.random.Generator(np.random.PCG64(SEED_BASE + 7919 * pair_id + 2))
+    noisy = shifted + noise.normal(0.0, 6.0, size=shifted.shape).astype(np.float32)
+    right = np.ascontiguousarray(np.clip(np.rint(noisy), 0, 255).astype(np.uint8))
+    return left, right, disp

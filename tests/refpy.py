@@ -349,3 +349,95 @@ def fast_score_definition(patch):
         else:
             break
     return best
+
+
+# ---------------------------------------------------------------------------------------------
+# Frame::ComputeStereoMatches, src/Frame.cc:466-640
+# ---------------------------------------------------------------------------------------------
+def stereo_matches(kL, dL, kR, dR, pyrL, pyrR, sf, isf, mbf, mb):
+    """pyrL/pyrR: lists of u8 level images (level 0 = input).  Returns (uright, depth) float32."""
+    N = len(kL)
+    rows = pyrL[0].shape[0]
+    uright = np.full(N, -1.0, np.float32)
+    depth = np.full(N, -1.0, np.float32)
+    row_idx = [[] for _ in range(rows)]
+    for iR, k in enumerate(kR):
+        kpY = F32(k["y"])
+        r = F32(2.0) * F32(sf[k["octave"]])
+        maxr = math.ceil(f32(kpY + r))
+        minr = math.floor(f32(kpY - r))
+        for yi in range(minr, maxr + 1):
+            if 0 <= yi < rows:  # std::vector::operator[] outside the image is UB in the reference
+                row_idx[yi].append(iR)
+    minZ = F32(mb)
+    minD = F32(0)
+    maxD = F32(F32(mbf) / minZ)
+    dist_idx = []
+    for iL in range(N):
+        k = kL[iL]
+        levelL = int(k["octave"])
+        vL, uL = F32(k["y"]), F32(k["x"])
+        cands = row_idx[int(vL)]
+        if not cands:
+            continue
+        minU, maxU = F32(uL - maxD), F32(uL - minD)
+        if maxU < 0:
+            continue
+        bestDist, bestIdxR = 100, 0
+        for iR in cands:
+            kr = kR[iR]
+            if kr["octave"] < levelL - 1 or kr["octave"] > levelL + 1:
+                continue
+            uR = F32(kr["x"])
+            if minU <= uR <= maxU:
+                dist = popcount_dist(dL[iL], dR[iR])
+                if dist < bestDist:
+                    bestDist, bestIdxR = dist, iR
+        if bestDist >= (100 + 50) // 2:
+            continue
+        uR0 = F32(kR[bestIdxR]["x"])
+        s = F32(isf[levelL])
+        suL = _round_half_away(f32(F32(k["x"]) * s))
+        svL = _round_half_away(f32(F32(k["y"]) * s))
+        suR0 = _round_half_away(f32(uR0 * s))
+        w, L = 5, 5
+        IL = pyrL[levelL][svL - w:svL + w + 1, suL - w:suL + w + 1].astype(np.int64)
+        IL = IL - IL[w, w]
+        iniu, endu = suR0 + L - w, suR0 + L + w + 1
+        if iniu < 0 or endu >= pyrR[levelL].shape[1]:
+            continue
+        best, bestinc = 2 ** 31 - 1, 0
+        dists = []
+        for inc in range(-L, L + 1):
+            IR = pyrR[levelL][svL - w:svL + w + 1, suR0 + inc - w:suR0 + inc + w + 1].astype(np.int64)
+            IR = IR - IR[w, w]
+            d = int(np.abs(IL - IR).sum())
+            if d < best:
+                best, bestinc = d, inc
+            dists.append(F32(d))
+        if bestinc in (-L, L):
+            continue
+        d1, d2, d3 = dists[L + bestinc - 1], dists[L + bestinc], dists[L + bestinc + 1]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            deltaR = F32(F32(d1 - d3) / F32(F32(2.0) * F32(F32(d1 + d3) - F32(F32(2.0) * d2))))
+        if deltaR < -1 or deltaR > 1:
+            continue
+        bestuR = F32(F32(sf[levelL]) * F32(F32(F32(suR0) + F32(bestinc)) + deltaR))
+        disparity = F32(uL - bestuR)
+        if minD <= disparity < maxD:
+            if disparity <= 0:
+                disparity = F32(0.01)
+                bestuR = F32(float(uL) - 0.01)
+            depth[iL] = F32(F32(mbf) / disparity)
+            uright[iL] = bestuR
+            dist_idx.append((best, iL))
+    if dist_idx:
+        dist_idx.sort()
+        median = F32(dist_idx[len(dist_idx) // 2][0])
+        thDist = F32(F32(F32(1.5) * F32(1.4)) * median)
+        for d, i in reversed(dist_idx):
+            if F32(d) < thDist:
+                break
+            uright[i] = -1
+            depth[i] = -1
+    return uright, depth
