@@ -159,6 +159,63 @@ int orbgpu_search_by_projection(orbgpu_ctx* ctx, const orbgpu_frame_view* F,
                                 const orbgpu_mappoints_view* mp, float nnratio, float th,
                                 int32_t* owner, int32_t* owner_obs, int* nmatches);
 
+/* ---- projection matchers: isInFrustum (A17) and SearchByProjection(Frame&, const Frame&) (A16) ---- */
+
+/* Pose / intrinsics snapshot of a Frame: mRcw (row-major 3x3), mtcw, mOw (= -Rcw^T tcw, the camera
+ * centre), fx, fy, cx, cy, mbf, mb, mfScaleFactor, mnScaleLevels (src/Frame.cc:253-266, include/Frame.h). */
+typedef struct {
+    float Rcw[9];
+    float tcw[3];
+    float Ow[3];
+    float fx, fy, cx, cy, mbf, mb;
+    float scale_factor;
+    int nlevels;
+} orbgpu_camera;
+
+/* MapPoint geometry Frame::isInFrustum reads (under the per-point mutexes): GetWorldPos(), GetNormal(),
+ * mfMaxDistance, mfMinDistance (src/MapPoint.cc:373-383). */
+typedef struct {
+    int m;
+    const float* pos;       /* m x 3 */
+    const float* normal;    /* m x 3 */
+    const float* max_dist;  /* m */
+    const float* min_dist;  /* m */
+} orbgpu_mappoint_geom_view;
+
+/* Replaces the per-point bool Frame::isInFrustum(MapPoint*, float viewingCosLimit) -- src/Frame.cc:269-325,
+ * with MapPoint::PredictScale(dist, Frame*) src/MapPoint.cc:402-417 -- for all m points at once, as
+ * Tracking::SearchLocalPoints calls it (src/Tracking.cc:1167-1180).  `bounds` = mnMinX/mnMaxX/mnMinY/
+ * mnMaxY (grid fields ignored).  Writes mbTrackInView (track_in_view) and, for points in view,
+ * mTrackProjX/Y/XR, mnTrackScaleLevel, mTrackViewCos; those arrays feed orbgpu_mappoints_view
+ * directly.  *n_in_view (optional) = number of points in view. */
+int orbgpu_is_in_frustum(orbgpu_ctx* ctx, const orbgpu_camera* cam, orbgpu_grid_geom bounds,
+                         const orbgpu_mappoint_geom_view* mp, float viewingCosLimit, uint8_t* track_in_view,
+                         float* proj_x, float* proj_y, float* proj_xr, int32_t* level, float* view_cos,
+                         int* n_in_view);
+
+/* LastFrame snapshot for the motion-model matcher. */
+typedef struct {
+    int n;                         /* LastFrame.N */
+    const orbgpu_keypoint* kps;    /* mvKeysUn (octave and angle equal mvKeys') */
+    const uint8_t* has_mp;         /* mvpMapPoints[i] != NULL */
+    const uint8_t* outlier;        /* mvbOutlier[i] */
+    const float* pos;              /* n x 3: mvpMapPoints[i]->GetWorldPos() */
+    const int32_t* n_obs;          /* mvpMapPoints[i]->Observations() */
+    const uint8_t* desc;           /* n x 32: mvpMapPoints[i]->GetDescriptor() */
+} orbgpu_last_frame_view;
+
+/* Replaces int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th,
+ * const bool bMono) -- src/ORBmatcher.cc:1328-1470, include/ORBmatcher.h:56; called from
+ * Tracking::TrackWithMotionModel (src/Tracking.cc:869-891).  F = CurrentFrame (kps, desc, uright,
+ * bounds/grid, scale factors), cur/last = the two frames' poses (cur also gives K, mbf, mb).
+ * owner (F.n ints, in/out) = CurrentFrame.mvpMapPoints as LastFrame keypoint indices (-1 == NULL,
+ * values >= LF.n = claims from other map points); owner_obs (in/out) = Observations()>0 of the claimant.
+ * checkOri = the matcher's mbCheckOrientation. */
+int orbgpu_search_by_projection_last_frame(orbgpu_ctx* ctx, const orbgpu_frame_view* F,
+                                           const orbgpu_camera* cur, const orbgpu_camera* last,
+                                           const orbgpu_last_frame_view* LF, float th, int bMono, int checkOri,
+                                           int32_t* owner, int32_t* owner_obs, int* nmatches);
+
 /* ---- stereo ------------------------------------------------------------------------------------- */
 
 /* Replaces void Frame::ComputeStereoMatches() -- src/Frame.cc:466-640, called from the stereo Frame

@@ -15,6 +15,11 @@
  *    follows the machine code of libm.so.6's FMA variant (constants read from its table) and is
  *    pinned by an exhaustive comparison against the container's libm over every float in [0, 8)
  *    (tools/verify_sincosf.c, tests/test_oracle_pins.py).
+ *  - oo_logf: glibc 2.35 logf (16-entry table, degree-3 polynomial in double).  The reference calls
+ *    std::log(float) -- `using namespace std` is global via Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:36
+ *    -- in MapPoint::PredictScale (src/MapPoint.cc:410) and Frame (src/Frame.cc:71).  Pinned by an
+ *    exhaustive comparison against the container's libm over every positive normal float
+ *    (tools/verify_logf.c).
  */
 #ifndef OO_MATH_H
 #define OO_MATH_H
@@ -105,6 +110,51 @@ static inline int oo_sincosf(float y, float* sinp, float* cosp)
     if (n & 1) { *sinp = co; *cosp = so; }
     else       { *sinp = so; *cosp = co; }
     return 1;
+}
+
+/* glibc logf data: (invc, logc) per 16 subintervals of [0x1.66p-1, 0x1.66p0), ln2, polynomial */
+static const double oo_logf_tab[16][2] = {
+    {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
+    {0x1.49539f0f010bp+0, -0x1.01eae7f513a67p-2},  {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
+    {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8eap+0, -0x1.1aa2bc79c81p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
+    {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1p+0, 0x0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5},  {0x1.ca4b31f026aap-1, 0x1.c5e53aa362eb4p-4},
+    {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3},  {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d22477p-3},
+    {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2},  {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2},
+};
+static const double oo_logf_ln2 = 0x1.62e42fefa39efp-1;
+static const double oo_logf_poly[3] = {-0x1.00ea348b88334p-2, 0x1.5575b0be00b6ap-2, -0x1.ffffef20a4123p-2};
+
+/* logf for positive normal x (the only inputs PredictScale produces); other inputs follow IEEE limits */
+static inline float oo_logf(float x)
+{
+    uint32_t ix;
+    memcpy(&ix, &x, 4);
+    if (ix == 0x3f800000u) return 0.0f;
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+        if (ix * 2 == 0) return -INFINITY;
+        if (ix == 0x7f800000u) return x;
+        if ((ix & 0x80000000u) || ix * 2 >= 0xff000000u) return NAN;
+        /* subnormal: normalise */
+        const float xs = x * 0x1p23f;
+        memcpy(&ix, &xs, 4);
+        ix -= 23u << 23;
+    }
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> 19) % 16);
+    const int k = (int32_t)tmp >> 23;
+    const uint32_t iz = ix - (tmp & 0xff800000u);
+    float zf;
+    memcpy(&zf, &iz, 4);
+    const double z = zf, invc = oo_logf_tab[i][0], logc = oo_logf_tab[i][1];
+    const double r = fma(z, invc, -1.0);
+    const double y0 = logc + (double)k * oo_logf_ln2;
+    const double r2 = r * r;
+    double y = fma(oo_logf_poly[1], r, oo_logf_poly[2]);
+    y = fma(oo_logf_poly[0], r2, y);
+    y = fma(y, r2, y0 + r);
+    return (float)y;
 }
 
 #endif

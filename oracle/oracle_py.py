@@ -66,6 +66,10 @@ def lib():
         L.oo_stereo_matches.argtypes = [vp, vp, vp, vp, i32, vp, vp, i32, f32, f32, vp, vp]
         L.oo_search_by_projection.restype = i32
         L.oo_search_by_projection.argtypes = [vp, vp, f32, f32, vp, vp]
+        L.oo_is_in_frustum.restype = i32
+        L.oo_is_in_frustum.argtypes = [vp, vp, f32, vp, vp, vp, vp, vp, vp]
+        L.oo_search_by_projection_last.restype = i32
+        L.oo_search_by_projection_last.argtypes = [vp, vp, vp, vp, f32, i32, i32, vp, vp]
         _lib = L
     return _lib
 
@@ -201,6 +205,79 @@ def search_by_projection(f: OracleFrame, mp: dict, nnratio=0.8, th=3.0, owner=No
     for k, v in arrs.items():
         setattr(s, k, _p(v).value)
     nm = lib().oo_search_by_projection(C.byref(f._s), C.byref(s), nnratio, th, _p(owner), _p(owner_obs))
+    return nm, owner, owner_obs
+
+
+class _OOCamera(C.Structure):
+    _fields_ = [("Rcw", C.c_float * 9), ("tcw", C.c_float * 3), ("Ow", C.c_float * 3), ("fx", C.c_float),
+                ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("mbf", C.c_float), ("mb", C.c_float),
+                ("scale_factor", C.c_float), ("nlevels", C.c_int), ("minX", C.c_float), ("maxX", C.c_float),
+                ("minY", C.c_float), ("maxY", C.c_float)]
+
+
+def _camera(cam: dict) -> _OOCamera:
+    """cam: Rcw (3x3), tcw (3), Ow (3), fx, fy, cx, cy, mbf, mb, scale_factor, nlevels, cols, rows."""
+    c = _OOCamera()
+    c.Rcw[:] = [float(v) for v in np.asarray(cam["Rcw"], np.float32).reshape(9)]
+    c.tcw[:] = [float(v) for v in np.asarray(cam["tcw"], np.float32).reshape(3)]
+    c.Ow[:] = [float(v) for v in np.asarray(cam.get("Ow", np.zeros(3)), np.float32).reshape(3)]
+    for k in ("fx", "fy", "cx", "cy", "mbf", "mb", "scale_factor"):
+        setattr(c, k, float(cam[k]))
+    c.nlevels = int(cam["nlevels"])
+    vals = [C.c_float() for _ in range(6)]
+    lib().oo_grid_params(int(cam["cols"]), int(cam["rows"]), *[C.byref(v) for v in vals])
+    c.minX, c.minY, c.maxX, c.maxY = vals[0].value, vals[1].value, vals[2].value, vals[3].value
+    return c
+
+
+class _OOMapPointGeom(C.Structure):
+    _fields_ = [("m", C.c_int), ("pos", C.c_void_p), ("normal", C.c_void_p), ("max_dist", C.c_void_p),
+                ("min_dist", C.c_void_p)]
+
+
+def is_in_frustum(cam: dict, pos, normal, max_dist, min_dist, viewing_cos_limit=0.5):
+    """Frame::isInFrustum + PredictScale for every point -> dict of the mTrack* SoA fields."""
+    pos = np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
+    normal = np.ascontiguousarray(normal, np.float32).reshape(-1, 3)
+    mx = np.ascontiguousarray(max_dist, np.float32)
+    mn = np.ascontiguousarray(min_dist, np.float32)
+    m = len(pos)
+    g = _OOMapPointGeom(m, _p(pos).value, _p(normal).value, _p(mx).value, _p(mn).value)
+    out = dict(track_in_view=np.zeros(max(m, 1), np.uint8), proj_x=np.zeros(max(m, 1), np.float32),
+               proj_y=np.zeros(max(m, 1), np.float32), proj_xr=np.zeros(max(m, 1), np.float32),
+               level=np.zeros(max(m, 1), np.int32), view_cos=np.zeros(max(m, 1), np.float32))
+    c = _camera(cam)
+    n = lib().oo_is_in_frustum(C.byref(c), C.byref(g), viewing_cos_limit, _p(out["track_in_view"]),
+                               _p(out["proj_x"]), _p(out["proj_y"]), _p(out["proj_xr"]), _p(out["level"]),
+                               _p(out["view_cos"]))
+    return n, {k: v[:m].copy() for k, v in out.items()}
+
+
+class _OOLastFrame(C.Structure):
+    _fields_ = [("n", C.c_int), ("kps", C.c_void_p), ("has_mp", C.c_void_p), ("outlier", C.c_void_p),
+                ("pos", C.c_void_p), ("n_obs", C.c_void_p), ("desc", C.c_void_p)]
+
+
+def search_by_projection_last(f: OracleFrame, cur: dict, last: dict, lf: dict, th=7.0, mono=True, check_ori=True,
+                              owner=None, owner_obs=None):
+    """SearchByProjection(CurrentFrame, LastFrame, th, bMono).  lf: kps, has_mp, outlier, pos, n_obs, desc."""
+    n = len(f.kps)
+    owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+    owner_obs = (np.zeros(n, np.int32) if owner_obs is None
+                 else np.ascontiguousarray(owner_obs, np.int32).copy())
+    arrs = dict(kps=np.ascontiguousarray(lf["kps"]), has_mp=np.ascontiguousarray(lf["has_mp"], np.uint8),
+                outlier=np.ascontiguousarray(lf["outlier"], np.uint8),
+                pos=np.ascontiguousarray(lf["pos"], np.float32).reshape(-1, 3),
+                n_obs=np.ascontiguousarray(lf["n_obs"], np.int32),
+                desc=np.ascontiguousarray(lf["desc"], np.uint8))
+    s = _OOLastFrame()
+    s.n = len(arrs["kps"])
+    for k, v in arrs.items():
+        setattr(s, k, _p(v).value if v.size else None)
+    cc, cl = _camera(cur), _camera(last)
+    nm = lib().oo_search_by_projection_last(C.byref(f._s), C.byref(cc), C.byref(cl), C.byref(s), th, int(mono),
+                                            int(check_ori), _p(owner) if n else None,
+                                            _p(owner_obs) if n else None)
     return nm, owner, owner_obs
 
 

@@ -1101,3 +1101,154 @@ int oo_stereo_matches(const oo_extractor* EL, const oo_extractor* ER, const oo_k
     free(vDistIdx);
     return nvalid;
 }
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Projection helpers.  cv::Mat float algebra of the reference, pinned (OpenCV internals are not     */
+/* available here): R*x + t as ((r0*x0 + r1*x1) + r2*x2) + t in float (OpenCV's     */
+/* small-matrix gemm path; OpenCV is not built with FMA); the reference's own expressions contract   */
+/* into fma under GCC -O3 -march=native (tools/probe_contraction_proj.cc).                            */
+/* ------------------------------------------------------------------------------------------------ */
+static void oo_rx_plus_t(const float* R, const float* x, const float* t, float* out)
+{
+    for (int r = 0; r < 3; r++) {
+        float s = R[3 * r] * x[0];
+        s = s + R[3 * r + 1] * x[1];
+        s = s + R[3 * r + 2] * x[2];
+        out[r] = s + t[r];
+    }
+}
+
+/* Frame::isInFrustum (src/Frame.cc:269-325) + MapPoint::PredictScale (src/MapPoint.cc:402-417) */
+int oo_is_in_frustum(const oo_camera* cam, const oo_mappoint_geom* mp, float viewingCosLimit, uint8_t* in_view,
+                     float* proj_x, float* proj_y, float* proj_xr, int* level, float* view_cos)
+{
+    const float logsf = oo_logf(cam->scale_factor);  /* mfLogScaleFactor = log(mfScaleFactor), :71 */
+    int nin = 0;
+    for (int m = 0; m < mp->m; m++) {
+        in_view[m] = 0;
+        const float* P = mp->pos + 3 * (size_t)m;
+        float Pc[3];
+        oo_rx_plus_t(cam->Rcw, P, cam->tcw, Pc);
+        if (Pc[2] < 0.0f) continue;
+        const float invz = 1.0f / Pc[2];
+        const float u = fmaf(cam->fx * Pc[0], invz, cam->cx);
+        const float v = fmaf(cam->fy * Pc[1], invz, cam->cy);
+        if (u < cam->minX || u > cam->maxX) continue;
+        if (v < cam->minY || v > cam->maxY) continue;
+        const float maxDistance = 1.2f * mp->max_dist[m];  /* GetMaxDistanceInvariance, src/MapPoint.cc:379 */
+        const float minDistance = 0.8f * mp->min_dist[m];  /* GetMinDistanceInvariance, :373 */
+        const float PO[3] = {P[0] - cam->Ow[0], P[1] - cam->Ow[1], P[2] - cam->Ow[2]};
+        /* cv::norm(PO): NORM_L2 of 32F accumulates squares in double, sqrt in double */
+        double ss = 0.0;
+        for (int k = 0; k < 3; k++) ss += (double)PO[k] * (double)PO[k];
+        const float dist = (float)sqrt(ss);
+        if (dist < minDistance || dist > maxDistance) continue;
+        /* PO.dot(Pn): double accumulation of float products; /dist in double */
+        const float* Pn = mp->normal + 3 * (size_t)m;
+        double dot = 0.0;
+        for (int k = 0; k < 3; k++) dot += (double)PO[k] * (double)Pn[k];
+        const float viewCos = (float)(dot / (double)dist);
+        if (viewCos < viewingCosLimit) continue;
+        /* PredictScale: ratio = mfMaxDistance/currentDist; ceil(log(ratio)/mfLogScaleFactor), clamp */
+        const float ratio = mp->max_dist[m] / dist;
+        int nScale = (int)ceilf(oo_logf(ratio) / logsf);
+        if (nScale < 0) nScale = 0;
+        else if (nScale >= cam->nlevels) nScale = cam->nlevels - 1;
+        in_view[m] = 1;
+        proj_x[m] = u;
+        proj_xr[m] = fmaf(-cam->mbf, invz, u);
+        proj_y[m] = v;
+        level[m] = nScale;
+        view_cos[m] = viewCos;
+        nin++;
+    }
+    return nin;
+}
+
+/* ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) (src/ORBmatcher.cc:1328-1470) */
+int oo_search_by_projection_last(const oo_frame* F, const oo_camera* cur, const oo_camera* last,
+                                 const oo_last_frame* LF, float th, int bMono, int checkOri, int* owner,
+                                 int* owner_obs)
+{
+    int nmatches = 0;
+    const float factor = 1.0f / OO_HISTO;
+    int hlen[OO_HISTO] = {0};
+    int* hist = (int*)malloc(sizeof(int) * OO_HISTO * (size_t)(LF->n + 1));
+    int* idx = (int*)malloc(sizeof(int) * (size_t)(F->n + 1));
+    /* twc = -Rcw^T tcw ; tlc = Rlw*twc + tlw  (:1338-1346) */
+    float twc[3], tlc[3];
+    for (int j = 0; j < 3; j++) {
+        float s = cur->Rcw[j] * cur->tcw[0];
+        s = s + cur->Rcw[3 + j] * cur->tcw[1];
+        s = s + cur->Rcw[6 + j] * cur->tcw[2];
+        twc[j] = -s;
+    }
+    oo_rx_plus_t(last->Rcw, twc, last->tcw, tlc);
+    const int bForward = tlc[2] > cur->mb && !bMono;
+    const int bBackward = -tlc[2] > cur->mb && !bMono;
+    for (int i = 0; i < LF->n; i++) {
+        if (!LF->has_mp[i] || LF->outlier[i]) continue;
+        float x3Dc[3];
+        oo_rx_plus_t(cur->Rcw, LF->pos + 3 * (size_t)i, cur->tcw, x3Dc);
+        const float xc = x3Dc[0], yc = x3Dc[1];
+        const float invzc = (float)(1.0 / (double)x3Dc[2]);
+        if (invzc < 0) continue;
+        const float u = fmaf(cur->fx * xc, invzc, cur->cx);
+        const float v = fmaf(cur->fy * yc, invzc, cur->cy);
+        if (u < F->minX || u > F->maxX) continue;
+        if (v < F->minY || v > F->maxY) continue;
+        if (u != u || v != v) continue;  /* zc == 0 with xc == 0: undefined in the reference */
+        const int nLastOctave = LF->kps[i].octave;
+        const float radius = th * F->scale_factors[nLastOctave];
+        int nc;
+        if (bForward) nc = oo_features_in_area(F, u, v, radius, nLastOctave, -1, idx);
+        else if (bBackward) nc = oo_features_in_area(F, u, v, radius, 0, nLastOctave, idx);
+        else nc = oo_features_in_area(F, u, v, radius, nLastOctave - 1, nLastOctave + 1, idx);
+        if (nc == 0) continue;
+        const uint8_t* dMP = LF->desc + 32 * (size_t)i;
+        int bestDist = 256, bestIdx2 = -1;
+        for (int c = 0; c < nc; c++) {
+            const int i2 = idx[c];
+            if (owner[i2] >= 0 && owner_obs[i2]) continue;
+            if (F->uright && F->uright[i2] > 0) {
+                const float ur = fmaf(-cur->mbf, invzc, u);
+                const float er = fabsf(ur - F->uright[i2]);
+                if (er > radius) continue;
+            }
+            const int dist = oo_descriptor_distance(dMP, F->desc + 32 * (size_t)i2);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx2 = i2;
+            }
+        }
+        if (bestDist <= OO_TH_HIGH) {
+            owner[bestIdx2] = i;
+            owner_obs[bestIdx2] = LF->n_obs[i] > 0;
+            nmatches++;
+            if (checkOri) {
+                float rot = LF->kps[i].angle - F->kps[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == OO_HISTO) bin = 0;
+                assert(bin >= 0 && bin < OO_HISTO);
+                hist[bin * (LF->n + 1) + hlen[bin]++] = bestIdx2;
+            }
+        }
+    }
+    if (checkOri) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        oo_three_maxima(hlen, OO_HISTO, &ind1, &ind2, &ind3);
+        for (int b = 0; b < OO_HISTO; b++) {
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            for (int j = 0; j < hlen[b]; j++) {
+                const int i2 = hist[b * (LF->n + 1) + j];
+                owner[i2] = -1;
+                owner_obs[i2] = 0;
+                nmatches--;
+            }
+        }
+    }
+    free(hist);
+    free(idx);
+    return nmatches;
+}

@@ -117,6 +117,49 @@ int oo_stereo_matches(const oo_extractor* EL, const oo_extractor* ER, const oo_k
                       int N, const oo_keypoint* kR, const uint8_t* dR, int Nr, float mbf, float mb,
                       float* uright, float* depth);
 
+/* Camera / pose snapshot of a Frame: mRcw (row-major), mtcw, mOw, intrinsics, mbf, mb, mfScaleFactor,
+ * mnScaleLevels, image bounds mnMinX.. (src/Frame.cc:253-266, include/Frame.h). */
+typedef struct {
+    float Rcw[9], tcw[3], Ow[3];
+    float fx, fy, cx, cy, mbf, mb;
+    float scale_factor;
+    int nlevels;
+    float minX, maxX, minY, maxY;
+} oo_camera;
+
+/* MapPoint geometry read by Frame::isInFrustum: GetWorldPos, GetNormal, mfMaxDistance, mfMinDistance */
+typedef struct {
+    int m;
+    const float* pos;      /* m x 3 */
+    const float* normal;   /* m x 3 */
+    const float* max_dist; /* mfMaxDistance */
+    const float* min_dist; /* mfMinDistance */
+} oo_mappoint_geom;
+
+/* Frame::isInFrustum (src/Frame.cc:269-325) + MapPoint::PredictScale (src/MapPoint.cc:402-417) for every
+ * map point; writes the mTrack* fields (SoA, m entries each).  Returns the number in view. */
+int oo_is_in_frustum(const oo_camera* cam, const oo_mappoint_geom* mp, float viewingCosLimit, uint8_t* in_view,
+                     float* proj_x, float* proj_y, float* proj_xr, int* level, float* view_cos);
+
+/* LastFrame snapshot for SearchByProjection(Frame&, const Frame&, th, bMono) */
+typedef struct {
+    int n;
+    const oo_keypoint* kps;  /* mvKeysUn (octave, angle; octave == mvKeys[i].octave) */
+    const uint8_t* has_mp;   /* mvpMapPoints[i] != NULL */
+    const uint8_t* outlier;  /* mvbOutlier[i] */
+    const float* pos;        /* n x 3, GetWorldPos() */
+    const int* n_obs;        /* Observations() */
+    const uint8_t* desc;     /* n x 32, GetDescriptor() */
+} oo_last_frame;
+
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)
+ * (src/ORBmatcher.cc:1328-1470).  owner (F.n ints, in/out): last-frame index whose map point claims
+ * the keypoint, or -1 (values >= LF.n denote pre-existing claims); owner_obs: Observations()>0 of
+ * the claimant.  Returns nmatches. */
+int oo_search_by_projection_last(const oo_frame* F, const oo_camera* cur, const oo_camera* last,
+                                 const oo_last_frame* LF, float th, int bMono, int checkOri, int* owner,
+                                 int* owner_obs);
+
 #ifdef __cplusplus
 }
 #endif

@@ -25,6 +25,7 @@ EXPORTS = [
     "orbgpu_device_alloc", "orbgpu_device_free", "orbgpu_memcpy_h2d", "orbgpu_memcpy_d2h",
     "orbgpu_memset_d", "orbgpu_prev_matched_from_frame", "orbgpu_memcpy_d2d_async",
     "orbgpu_batch_candidate_total", "orbgpu_compute_stereo_matches", "orbgpu_compute_stereo_matches_batch",
+    "orbgpu_is_in_frustum", "orbgpu_search_by_projection_last_frame",
 ]
 
 OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
@@ -50,6 +51,22 @@ class MapPointsView(C.Structure):
                 ("level", C.c_void_p), ("view_cos", C.c_void_p), ("proj_x", C.c_void_p),
                 ("proj_y", C.c_void_p), ("proj_xr", C.c_void_p), ("n_obs", C.c_void_p),
                 ("desc", C.c_void_p)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("Rcw", C.c_float * 9), ("tcw", C.c_float * 3), ("Ow", C.c_float * 3), ("fx", C.c_float),
+                ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("mbf", C.c_float), ("mb", C.c_float),
+                ("scale_factor", C.c_float), ("nlevels", C.c_int)]
+
+
+class MapPointGeomView(C.Structure):
+    _fields_ = [("m", C.c_int), ("pos", C.c_void_p), ("normal", C.c_void_p), ("max_dist", C.c_void_p),
+                ("min_dist", C.c_void_p)]
+
+
+class LastFrameView(C.Structure):
+    _fields_ = [("n", C.c_int), ("kps", C.c_void_p), ("has_mp", C.c_void_p), ("outlier", C.c_void_p),
+                ("pos", C.c_void_p), ("n_obs", C.c_void_p), ("desc", C.c_void_p)]
 
 
 _lib = None
@@ -101,6 +118,11 @@ def _declare(L):
     L.orbgpu_compute_stereo_matches.argtypes = [vp, vp, f32, f32, vp, vp, i32, C.POINTER(i32), C.POINTER(i32)]
     L.orbgpu_compute_stereo_matches_batch.argtypes = [vp, vp, f32, f32, vp, vp, vp]
     L.orbgpu_batch_candidate_total.argtypes = [vp]
+    L.orbgpu_is_in_frustum.argtypes = [vp, C.POINTER(Camera), GridGeom, C.POINTER(MapPointGeomView), f32, vp, vp,
+                                       vp, vp, vp, vp, C.POINTER(i32)]
+    L.orbgpu_search_by_projection_last_frame.argtypes = [vp, C.POINTER(FrameView), C.POINTER(Camera),
+                                                         C.POINTER(Camera), C.POINTER(LastFrameView), f32, i32, i32,
+                                                         vp, vp, C.POINTER(i32)]
 
 
 def lib(load_torch_first: bool = True):

@@ -496,3 +496,262 @@ void og_launch_proj_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const flo
 }
 
 size_t og_proj_cand_size() { return sizeof(OgProjCand); }
+
+// ------------------------------------------------------------------------------------------------
+// Frame::isInFrustum + MapPoint::PredictScale (src/Frame.cc:269-325, src/MapPoint.cc:402-417), one thread
+// per map point.  cv::Mat algebra as pinned in DESIGN.md §3 (R*x + t left to right in float; norm
+// and dot accumulate in double); the reference's own u/v/ur expressions are GCC-contracted FMAs.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void og_rx_t(const float* R, const float* x, const float* t, float* o)
+{
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        float s = __fmul_rn(R[3 * r], x[0]);
+        s = __fadd_rn(s, __fmul_rn(R[3 * r + 1], x[1]));
+        s = __fadd_rn(s, __fmul_rn(R[3 * r + 2], x[2]));
+        o[r] = __fadd_rn(s, t[r]);
+    }
+}
+
+__global__ __launch_bounds__(256) void og_frustum_kernel(OgCameraDev cam, OgMapGeomDev mp, float limit,
+                                                         OgFrustumOut out)
+{
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= mp.m) return;
+    bool in = false;
+    float u = 0, v = 0, ur = 0, vc = 0;
+    int lvl = 0;
+    do {
+        const float P[3] = {mp.pos[3 * m], mp.pos[3 * m + 1], mp.pos[3 * m + 2]};
+        float Pc[3];
+        og_rx_t(cam.R, P, cam.t, Pc);
+        if (Pc[2] < 0.0f) break;
+        const float invz = __fdiv_rn(1.0f, Pc[2]);
+        u = __fmaf_rn(__fmul_rn(cam.fx, Pc[0]), invz, cam.cx);
+        v = __fmaf_rn(__fmul_rn(cam.fy, Pc[1]), invz, cam.cy);
+        if (u < cam.minX || u > cam.maxX) break;
+        if (v < cam.minY || v > cam.maxY) break;
+        const float maxD = __fmul_rn(1.2f, mp.max_dist[m]);
+        const float minD = __fmul_rn(0.8f, mp.min_dist[m]);
+        const float PO[3] = {__fsub_rn(P[0], cam.Ow[0]), __fsub_rn(P[1], cam.Ow[1]), __fsub_rn(P[2], cam.Ow[2])};
+        double ss = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) ss = __dadd_rn(ss, __dmul_rn((double)PO[k], (double)PO[k]));
+        const float dist = (float)__dsqrt_rn(ss);
+        if (dist < minD || dist > maxD) break;
+        double dot = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) dot = __dadd_rn(dot, __dmul_rn((double)PO[k], (double)mp.normal[3 * m + k]));
+        vc = (float)__ddiv_rn(dot, (double)dist);
+        if (vc < limit) break;
+        const float ratio = __fdiv_rn(mp.max_dist[m], dist);
+        int ns = (int)ceilf(__fdiv_rn(og_logf(ratio), og_logf(cam.scale_factor)));
+        ns = ns < 0 ? 0 : (ns >= cam.nlevels ? cam.nlevels - 1 : ns);
+        lvl = ns;
+        ur = __fmaf_rn(-cam.mbf, invz, u);
+        in = true;
+    } while (0);
+    out.in_view[m] = in ? 1 : 0;
+    if (in) {
+        out.proj_x[m] = u;
+        out.proj_y[m] = v;
+        out.proj_xr[m] = ur;
+        out.level[m] = lvl;
+        out.view_cos[m] = vc;
+    }
+    if (out.n_in_view) {
+        const u64 b = __ballot(in);
+        if ((threadIdx.x & 63) == 0 && b) atomicAdd(out.n_in_view, __popcll(b));
+    }
+}
+
+void og_launch_frustum(hipStream_t s, OgCameraDev cam, OgMapGeomDev mp, float viewingCosLimit, OgFrustumOut out)
+{
+    if (mp.m > 0)
+        hipLaunchKernelGGL(og_frustum_kernel, dim3((mp.m + 255) / 256), dim3(256), 0, s, cam, mp, viewingCosLimit,
+                           out);
+}
+
+// ------------------------------------------------------------------------------------------------
+// ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)
+// (src/ORBmatcher.cc:1328-1470).  Projection + GetFeaturesInArea + static filters (stereo check) +
+// distances in parallel per last-frame point; the claim order (:1384-1386, :1411) and the rotation
+// histogram (:1414-1443) replay in one ordered pass.
+// ------------------------------------------------------------------------------------------------
+template <bool FILL>
+__device__ int og_last_enum(const OgFrameDev& F, const OgGridGeom& G, const float* sf, const OgCameraDev& cam,
+                            const OgLastFrameDev& LF, int i, float th, int mode, OgLastCand* out)
+{
+    if (!LF.has_mp[i] || LF.outlier[i]) return 0;
+    const float P[3] = {LF.pos[3 * i], LF.pos[3 * i + 1], LF.pos[3 * i + 2]};
+    float x3[3];
+    og_rx_t(cam.R, P, cam.t, x3);
+    const float invzc = (float)__ddiv_rn(1.0, (double)x3[2]);
+    if (invzc < 0) return 0;
+    const float u = __fmaf_rn(__fmul_rn(cam.fx, x3[0]), invzc, cam.cx);
+    const float v = __fmaf_rn(__fmul_rn(cam.fy, x3[1]), invzc, cam.cy);
+    if (u < G.minX || u > G.maxX) return 0;
+    if (v < G.minY || v > G.maxY) return 0;
+    if (u != u || v != v) return 0;
+    const int o = LF.kps[i].octave;
+    const float radius = __fmul_rn(th, sf[o]);
+    int minLevel, maxLevel;
+    if (mode == 1) minLevel = o, maxLevel = -1;
+    else if (mode == 2) minLevel = 0, maxLevel = o;
+    else minLevel = o - 1, maxLevel = o + 1;
+    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    const OgCellRange cr = og_cell_range(G, u, v, radius);
+    if (cr.x0 > cr.x1) return 0;
+    const float ur = __fmaf_rn(-cam.mbf, invzc, u);
+    uint4 da, db;
+    if (FILL) og_load_desc(LF.desc + (long long)i * 32, da, db);
+    int n = 0;
+    for (int ix = cr.x0; ix <= cr.x1; ix++)
+        for (int iy = cr.y0; iy <= cr.y1; iy++) {
+            const int cell = ix * OG_GRID_ROWS + iy;
+            for (int j = F.cell_start[cell]; j < F.cell_start[cell + 1]; j++) {
+                const int idx = F.cell_items[j];
+                const orbgpu_kp_dev kp = F.kps[idx];
+                if (bCheckLevels) {
+                    if (kp.octave < minLevel) continue;
+                    if (maxLevel >= 0 && kp.octave > maxLevel) continue;
+                }
+                const float distx = __fsub_rn(kp.x, u), disty = __fsub_rn(kp.y, v);
+                if (!(fabsf(distx) < radius && fabsf(disty) < radius)) continue;
+                if (F.uright && F.uright[idx] > 0) {
+                    if (fabsf(__fsub_rn(ur, F.uright[idx])) > radius) continue;
+                }
+                if (FILL) {
+                    uint4 ea, eb;
+                    og_load_desc(F.desc + (long long)idx * 32, ea, eb);
+                    out[n] = OgLastCand{idx, og_hamming(da, db, ea, eb)};
+                }
+                n++;
+            }
+        }
+    return n;
+}
+
+__global__ __launch_bounds__(256) void og_last_count_kernel(OgFrameDev F, OgGridGeom G, const float* sf,
+                                                            OgCameraDev cam, OgLastFrameDev LF, float th, int mode,
+                                                            int* cnt)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= LF.n) return;
+    cnt[i] = og_last_enum<false>(F, G, sf, cam, LF, i, th, mode, nullptr);
+}
+
+__global__ __launch_bounds__(256) void og_last_fill_kernel(OgFrameDev F, OgGridGeom G, const float* sf,
+                                                           OgCameraDev cam, OgLastFrameDev LF, float th, int mode,
+                                                           const int* off, OgLastCand* cands)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= LF.n) return;
+    og_last_enum<true>(F, G, sf, cam, LF, i, th, mode, cands + off[i]);
+}
+
+// ORBmatcher::ComputeThreeMaxima (src/ORBmatcher.cc:1601-1642)
+__device__ void og_three_maxima(const int* h, int& ind1, int& ind2, int& ind3)
+{
+    int max1 = 0, max2 = 0, max3 = 0;
+    ind1 = ind2 = ind3 = -1;
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+        const int s = h[i];
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+            max3 = s;
+            ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+}
+
+// ent: LF.n ints -- the rotation-histogram pushes in order, packed (bin << 24) | keypoint index
+__global__ __launch_bounds__(64) void og_last_resolve_kernel(OgFrameDev F, OgLastFrameDev LF, int checkOri,
+                                                             const int* off, const OgLastCand* cands, int* ent,
+                                                             int* owner, int* owner_obs, int* nmatches)
+{
+    __shared__ int hist[HISTO_LENGTH];
+    __shared__ int sh[4];
+    const int lane = threadIdx.x;
+    if (lane < HISTO_LENGTH) hist[lane] = 0;
+    __syncthreads();
+    if (lane == 0) {
+        int nm = 0, ne = 0;
+        const float factor = 1.0f / HISTO_LENGTH;
+        for (int i = 0; i < LF.n; i++) {
+            const int b = off[i], e = off[i + 1];
+            if (b == e) continue;
+            int bestDist = 256, bestIdx2 = -1;
+            for (int c = b; c < e; c++) {
+                const OgLastCand cc = cands[c];
+                if (owner[cc.idx] >= 0 && owner_obs[cc.idx]) continue;
+                if (cc.dist < bestDist) {
+                    bestDist = cc.dist;
+                    bestIdx2 = cc.idx;
+                }
+            }
+            if (bestDist <= TH_HIGH) {
+                owner[bestIdx2] = i;
+                owner_obs[bestIdx2] = LF.n_obs[i] > 0;
+                nm++;
+                if (checkOri) {
+                    float rot = __fsub_rn(LF.kps[i].angle, F.kps[bestIdx2].angle);
+                    if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+                    int bin = (int)roundf(__fmul_rn(rot, factor));
+                    if (bin == HISTO_LENGTH) bin = 0;
+                    hist[bin]++;
+                    ent[ne++] = (bin << 24) | bestIdx2;
+                }
+            }
+        }
+        sh[0] = nm;
+        sh[1] = ne;
+        int i1 = -1, i2 = -1, i3 = -1;
+        if (checkOri) og_three_maxima(hist, i1, i2, i3);
+        sh[2] = i1;
+        sh[3] = (i2 & 0xffff) | (i3 << 16);
+    }
+    __syncthreads();
+    int culled = 0;
+    if (checkOri) {
+        const int ne = sh[1], i1 = sh[2], i2 = (short)(sh[3] & 0xffff), i3 = sh[3] >> 16;
+        for (int k = lane; k < ne; k += 64) {
+            const int v = ent[k], bin = v >> 24, idx = v & 0xffffff;
+            if (bin != i1 && bin != i2 && bin != i3) {
+                owner[idx] = -1;  // all writes are NULL: order-free
+                owner_obs[idx] = 0;
+                culled++;
+            }
+        }
+    }
+    culled = og_wave_sum(culled);
+    if (lane == 0) *nmatches = sh[0] - culled;
+}
+
+void og_launch_last_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
+                          OgLastFrameDev LF, float th, int mode, int* cnt, int* off)
+{
+    const int blocks = (LF.n + 255) / 256;
+    if (blocks > 0)
+        hipLaunchKernelGGL(og_last_count_kernel, dim3(blocks), dim3(256), 0, s, F, G, sf, cam, LF, th, mode, cnt);
+    hipLaunchKernelGGL(og_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, LF.n, off);
+}
+
+void og_launch_last_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
+                            OgLastFrameDev LF, float th, int mode, int checkOri, const int* off, OgLastCand* cands,
+                            int* ent, int* owner, int* owner_obs, int* nmatches)
+{
+    const int blocks = (LF.n + 255) / 256;
+    if (blocks > 0)
+        hipLaunchKernelGGL(og_last_fill_kernel, dim3(blocks), dim3(256), 0, s, F, G, sf, cam, LF, th, mode, off,
+                           cands);
+    hipLaunchKernelGGL(og_last_resolve_kernel, dim3(1), dim3(64), 0, s, F, LF, checkOri, off, cands, ent, owner,
+                       owner_obs, nmatches);
+}

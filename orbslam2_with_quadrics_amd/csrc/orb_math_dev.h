@@ -83,3 +83,40 @@ __device__ __forceinline__ int og_hamming(const uint4 a0, const uint4 a1, const 
     return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
+
+// glibc 2.35 logf (the reference's std::log(float) in MapPoint::PredictScale, src/MapPoint.cc:410, and
+// Frame's mfLogScaleFactor, src/Frame.cc:71): 16-entry (1/c, log c) table + degree-3 polynomial in
+// double, the libm operation sequence (pinned exhaustively against the host libm).
+__constant__ const double og_logf_tab[16][2] = {
+    {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
+    {0x1.49539f0f010bp+0, -0x1.01eae7f513a67p-2},  {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
+    {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8eap+0, -0x1.1aa2bc79c81p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
+    {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1p+0, 0x0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5},  {0x1.ca4b31f026aap-1, 0x1.c5e53aa362eb4p-4},
+    {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3},  {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d22477p-3},
+    {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2},  {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2},
+};
+
+__device__ __forceinline__ float og_logf(float x)
+{
+    uint32_t ix = __float_as_uint(x);
+    if (ix == 0x3f800000u) return 0.0f;
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+        if (ix * 2 == 0) return -__builtin_inff();
+        if (ix == 0x7f800000u) return x;
+        if ((ix & 0x80000000u) || ix * 2 >= 0xff000000u) return __builtin_nanf("");
+        ix = __float_as_uint(x * 0x1p23f) - (23u << 23);  // subnormal
+    }
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> 19) & 15);
+    const int k = (int32_t)tmp >> 23;
+    const double z = (double)__uint_as_float(ix - (tmp & 0xff800000u));
+    const double r = __fma_rn(z, og_logf_tab[i][0], -1.0);
+    const double y0 = __dadd_rn(og_logf_tab[i][1], __dmul_rn((double)k, 0x1.62e42fefa39efp-1));
+    const double r2 = __dmul_rn(r, r);
+    double y = __fma_rn(0x1.5575b0be00b6ap-2, r, -0x1.ffffef20a4123p-2);
+    y = __fma_rn(-0x1.00ea348b88334p-2, r2, y);
+    y = __fma_rn(y, r2, __dadd_rn(y0, r));
+    return (float)y;
+}

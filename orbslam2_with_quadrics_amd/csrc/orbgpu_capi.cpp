@@ -83,6 +83,7 @@ struct orbgpu_ctx {
     DevBuf<uint8_t> mscratch;
     DevBuf<uint32_t> mlists;  // SearchForInitialization candidate lists {dist:16|i2:16}
     DevBuf<int> mlist_n;
+    DevBuf<uint8_t> mcands;   // projection-matcher candidate lists (grown on demand, kept)
     // stereo scratch (Frame::ComputeStereoMatches)
     DevBuf<int> st_row_start, st_row_items, st_sad, st_nm;
     DevBuf<float> st_out;
@@ -311,7 +312,7 @@ static void timer_mark(orbgpu_ctx* c, const char* name)
         if (hipEventCreate(&e) != hipSuccess) return;
         t.ev.push_back(e);
     }
-    hipEventRecord(t.ev[t.used++], c->stream);
+    (void)hipEventRecord(t.ev[t.used++], c->stream);
     t.names.push_back(name);
 }
 
@@ -362,7 +363,7 @@ static int collect_timer(orbgpu_ctx* c)
     t.last_names.clear();
     for (int i = 1; i < t.used; i++) {
         float ms = 0;
-        hipEventElapsedTime(&ms, t.ev[i - 1], t.ev[i]);
+        (void)hipEventElapsedTime(&ms, t.ev[i - 1], t.ev[i]);
         t.last_ms.push_back(ms);
         t.last_names.push_back(t.names[i]);
     }
@@ -448,8 +449,8 @@ orbgpu_ctx* orbgpu_create(int device, int nfeatures, float scaleFactor, int nlev
 void orbgpu_destroy(orbgpu_ctx* c)
 {
     if (!c) return;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     release(c->cells);
     release(c->tabs);
     release(c->pyr);
@@ -469,14 +470,15 @@ void orbgpu_destroy(orbgpu_ctx* c)
     release(c->mscratch);
     release(c->mlists);
     release(c->mlist_n);
+    release(c->mcands);
     release(c->st_row_start);
     release(c->st_row_items);
     release(c->st_sad);
     release(c->st_nm);
     release(c->st_out);
-    for (hipEvent_t e : c->timer.ev) hipEventDestroy(e);
-    if (c->done) hipEventDestroy(c->done);
-    if (c->stream) hipStreamDestroy(c->stream);
+    for (hipEvent_t e : c->timer.ev) (void)hipEventDestroy(e);
+    if (c->done) (void)hipEventDestroy(c->done);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -613,6 +615,9 @@ int orbgpu_descriptor_distance(const uint8_t* a, const uint8_t* b)
 }
 
 // ---- matchers -----------------------------------------------------------------------------------
+// every scratch_carve rounds its region up to 256 B: kCarvePad covers the rounding of up to 64 carves
+static constexpr size_t kCarvePad = 64 * 256;
+
 static uint8_t* scratch_carve(uint8_t*& cur, size_t bytes)
 {
     uint8_t* p = cur;
@@ -628,7 +633,7 @@ int orbgpu_search_for_initialization(orbgpu_ctx* c, const orbgpu_frame_view* F1,
     if ((F1->n && (!F1->kps || !F1->desc)) || (F2->n && (!F2->kps || !F2->desc))) return ORBGPU_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     const int cap1 = std::max(F1->n, 1), cap2 = std::max(F2->n, 1);
-    const size_t need = 8 * 256 + (size_t)cap1 * (28 + 32 + 8 + 4) + (size_t)cap2 * (28 + 32 + 4) +
+    const size_t need = kCarvePad + (size_t)cap1 * (28 + 32 + 8 + 4) + (size_t)cap2 * (28 + 32 + 4) +
                         (OG_GRID_CELLS + 1) * 4 + 16;
     HIP_TRY(c, ensure(c->mscratch, need));
     uint8_t* cur = c->mscratch.p;
@@ -824,13 +829,14 @@ int orbgpu_compute_stereo_matches(orbgpu_ctx* left, orbgpu_ctx* right, float mbf
 int orbgpu_search_by_projection(orbgpu_ctx* c, const orbgpu_frame_view* F, const orbgpu_mappoints_view* mp,
                                 float nnratio, float th, int32_t* owner, int32_t* owner_obs, int* nmatches)
 {
-    if (!c || !F || !mp || !owner || !owner_obs || !nmatches || F->n < 0 || mp->m < 0) return ORBGPU_ERR_ARG;
+    if (!c || !F || !mp || !nmatches || F->n < 0 || mp->m < 0) return ORBGPU_ERR_ARG;
+    if (F->n && (!owner || !owner_obs)) return ORBGPU_ERR_ARG;
     if (!F->scale_factors || F->nlevels < 1) return ORBGPU_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     const int n = std::max(F->n, 1), m = std::max(mp->m, 1);
     // generous bound for the candidate lists: every map point may see every keypoint of its levels;
     // the count pass gives the exact total, so size the list region after it
-    const size_t fixed = 16 * 256 + (size_t)n * (28 + 32 + 4 + 4 + 4 + 4) + (OG_GRID_CELLS + 1) * 4 +
+    const size_t fixed = kCarvePad + (size_t)n * (28 + 32 + 4 + 4 + 4 + 4) + (OG_GRID_CELLS + 1) * 4 +
                          (size_t)m * (1 + 1 + 4 + 4 + 4 + 4 + 4 + 4 + 32 + 4 + 4 + 4) + 64 + F->nlevels * 4;
     HIP_TRY(c, ensure(c->mscratch, fixed));
     uint8_t* cur = c->mscratch.p;
@@ -886,9 +892,8 @@ int orbgpu_search_by_projection(orbgpu_ctx* c, const orbgpu_frame_view* F, const
     int total = 0;
     HIP_TRY(c, hipMemcpyAsync(&total, off + mp->m, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
-    DevBuf<uint8_t> lists;
-    HIP_TRY(c, ensure(lists, (size_t)std::max(total, 1) * og_proj_cand_size()));
-    og_launch_proj_resolve(s, fd, G, sfd, mpd, nnratio, th, off, (OgProjCand*)lists.p, own, obs, nm);
+    HIP_TRY(c, ensure(c->mcands, (size_t)std::max(total, 1) * og_proj_cand_size()));
+    og_launch_proj_resolve(s, fd, G, sfd, mpd, nnratio, th, off, (OgProjCand*)c->mcands.p, own, obs, nm);
     HIP_TRY(c, hipGetLastError());
     int hnm = 0;
     HIP_TRY(c, hipMemcpyAsync(&hnm, nm, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -897,7 +902,181 @@ int orbgpu_search_by_projection(orbgpu_ctx* c, const orbgpu_frame_view* F, const
         HIP_TRY(c, hipMemcpyAsync(owner_obs, obs, (size_t)F->n * 4, hipMemcpyDeviceToHost, s));
     }
     HIP_TRY(c, hipStreamSynchronize(s));
-    release(lists);
+    *nmatches = hnm;
+    return ORBGPU_OK;
+}
+
+static OgCameraDev camera_dev(const orbgpu_camera* cam, float minX, float maxX, float minY, float maxY)
+{
+    OgCameraDev d{};
+    std::memcpy(d.R, cam->Rcw, sizeof(d.R));
+    std::memcpy(d.t, cam->tcw, sizeof(d.t));
+    std::memcpy(d.Ow, cam->Ow, sizeof(d.Ow));
+    d.fx = cam->fx;
+    d.fy = cam->fy;
+    d.cx = cam->cx;
+    d.cy = cam->cy;
+    d.mbf = cam->mbf;
+    d.mb = cam->mb;
+    d.scale_factor = cam->scale_factor;
+    d.nlevels = cam->nlevels;
+    d.minX = minX;
+    d.maxX = maxX;
+    d.minY = minY;
+    d.maxY = maxY;
+    return d;
+}
+
+int orbgpu_is_in_frustum(orbgpu_ctx* c, const orbgpu_camera* cam, orbgpu_grid_geom bounds,
+                         const orbgpu_mappoint_geom_view* mp, float viewingCosLimit, uint8_t* track_in_view,
+                         float* proj_x, float* proj_y, float* proj_xr, int32_t* level, float* view_cos,
+                         int* n_in_view)
+{
+    if (!c || !cam || !mp || mp->m < 0 || cam->nlevels < 1 || !(cam->scale_factor > 0)) return ORBGPU_ERR_ARG;
+    if (mp->m && (!mp->pos || !mp->normal || !mp->max_dist || !mp->min_dist || !track_in_view || !proj_x ||
+                  !proj_y || !proj_xr || !level || !view_cos))
+        return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t m = (size_t)std::max(mp->m, 1);
+    HIP_TRY(c, ensure(c->mscratch, kCarvePad + m * (12 + 12 + 4 + 4 + 1 + 4 * 5) + 64));
+    uint8_t* cur = c->mscratch.p;
+    float* pos = (float*)scratch_carve(cur, m * 12);
+    float* nrm = (float*)scratch_carve(cur, m * 12);
+    float* mxd = (float*)scratch_carve(cur, m * 4);
+    float* mnd = (float*)scratch_carve(cur, m * 4);
+    uint8_t* iv = scratch_carve(cur, m);
+    float* px = (float*)scratch_carve(cur, m * 4);
+    float* py = (float*)scratch_carve(cur, m * 4);
+    float* pxr = (float*)scratch_carve(cur, m * 4);
+    int* lv = (int*)scratch_carve(cur, m * 4);
+    float* vc = (float*)scratch_carve(cur, m * 4);
+    int* nin = (int*)scratch_carve(cur, 16);
+    hipStream_t s = c->stream;
+    const size_t M = (size_t)mp->m;
+    if (M) {
+        HIP_TRY(c, hipMemcpyAsync(pos, mp->pos, M * 12, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(nrm, mp->normal, M * 12, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(mxd, mp->max_dist, M * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(mnd, mp->min_dist, M * 4, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(c, hipMemsetAsync(nin, 0, 4, s));
+    og_launch_frustum(s, camera_dev(cam, bounds.minX, bounds.maxX, bounds.minY, bounds.maxY),
+                      OgMapGeomDev{mp->m, pos, nrm, mxd, mnd}, viewingCosLimit,
+                      OgFrustumOut{iv, px, py, pxr, lv, vc, nin});
+    HIP_TRY(c, hipGetLastError());
+    int hn = 0;
+    HIP_TRY(c, hipMemcpyAsync(&hn, nin, 4, hipMemcpyDeviceToHost, s));
+    if (M) {
+        HIP_TRY(c, hipMemcpyAsync(track_in_view, iv, M, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipMemcpyAsync(proj_x, px, M * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipMemcpyAsync(proj_y, py, M * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipMemcpyAsync(proj_xr, pxr, M * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipMemcpyAsync(level, lv, M * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipMemcpyAsync(view_cos, vc, M * 4, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if (n_in_view) *n_in_view = hn;
+    return ORBGPU_OK;
+}
+
+// bForward / bBackward of SearchByProjection(Frame&, const Frame&) (src/ORBmatcher.cc:1338-1349):
+// twc = -Rcw^T tcw, tlc = Rlw*twc + tlw, float, left to right (pinned as in the oracle)
+static int last_frame_mode(const orbgpu_camera* cur, const orbgpu_camera* last, int bMono)
+{
+    float twc[3], tlc[3];
+    for (int j = 0; j < 3; j++) {
+        float s = cur->Rcw[j] * cur->tcw[0];
+        s = s + cur->Rcw[3 + j] * cur->tcw[1];
+        s = s + cur->Rcw[6 + j] * cur->tcw[2];
+        twc[j] = -s;
+    }
+    for (int r = 0; r < 3; r++) {
+        float s = last->Rcw[3 * r] * twc[0];
+        s = s + last->Rcw[3 * r + 1] * twc[1];
+        s = s + last->Rcw[3 * r + 2] * twc[2];
+        tlc[r] = s + last->tcw[r];
+    }
+    if (tlc[2] > cur->mb && !bMono) return 1;
+    if (-tlc[2] > cur->mb && !bMono) return 2;
+    return 0;
+}
+
+int orbgpu_search_by_projection_last_frame(orbgpu_ctx* c, const orbgpu_frame_view* F, const orbgpu_camera* curc,
+                                           const orbgpu_camera* lastc, const orbgpu_last_frame_view* LF, float th,
+                                           int bMono, int checkOri, int32_t* owner, int32_t* owner_obs,
+                                           int* nmatches)
+{
+    if (!c || !F || !curc || !lastc || !LF || !nmatches || F->n < 0 || LF->n < 0) return ORBGPU_ERR_ARG;
+    if (F->n && (!owner || !owner_obs)) return ORBGPU_ERR_ARG;
+    if (!F->scale_factors || F->nlevels < 1) return ORBGPU_ERR_ARG;
+    if (LF->n && (!LF->kps || !LF->has_mp || !LF->outlier || !LF->pos || !LF->n_obs || !LF->desc))
+        return ORBGPU_ERR_ARG;
+    if (LF->n >= (1 << 24) || F->n >= (1 << 24)) return ORBGPU_ERR_UNSUPPORTED;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const int n = std::max(F->n, 1), L = std::max(LF->n, 1);
+    const size_t fixed = kCarvePad + (size_t)n * (28 + 32 + 4 + 4 + 4 + 4) + (OG_GRID_CELLS + 1) * 4 +
+                         (size_t)L * (28 + 1 + 1 + 12 + 4 + 32 + 4 + 4 + 4) + 64 + F->nlevels * 4;
+    HIP_TRY(c, ensure(c->mscratch, fixed));
+    uint8_t* cur = c->mscratch.p;
+    orbgpu_kp_dev* k = (orbgpu_kp_dev*)scratch_carve(cur, (size_t)n * 28);
+    uint8_t* d = scratch_carve(cur, (size_t)n * 32);
+    float* ur = (float*)scratch_carve(cur, (size_t)n * 4);
+    int* own = (int*)scratch_carve(cur, (size_t)n * 4);
+    int* obs = (int*)scratch_carve(cur, (size_t)n * 4);
+    int* cnts = (int*)scratch_carve(cur, 16);
+    int* cs = (int*)scratch_carve(cur, (OG_GRID_CELLS + 1) * 4);
+    int* ci = (int*)scratch_carve(cur, (size_t)n * 4);
+    float* sfd = (float*)scratch_carve(cur, (size_t)F->nlevels * 4);
+    orbgpu_kp_dev* lk = (orbgpu_kp_dev*)scratch_carve(cur, (size_t)L * 28);
+    uint8_t* hm = scratch_carve(cur, (size_t)L);
+    uint8_t* ol = scratch_carve(cur, (size_t)L);
+    float* lp = (float*)scratch_carve(cur, (size_t)L * 12);
+    int* lo = (int*)scratch_carve(cur, (size_t)L * 4);
+    uint8_t* ld = scratch_carve(cur, (size_t)L * 32);
+    int* cnt = (int*)scratch_carve(cur, (size_t)L * 4);
+    int* off = (int*)scratch_carve(cur, (size_t)(L + 1) * 4);
+    int* ent = (int*)scratch_carve(cur, (size_t)L * 4);
+    int* nm = (int*)scratch_carve(cur, 16);
+    hipStream_t s = c->stream;
+    if (F->n) {
+        HIP_TRY(c, hipMemcpyAsync(k, F->kps, (size_t)F->n * 28, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(d, F->desc, (size_t)F->n * 32, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(own, owner, (size_t)F->n * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(obs, owner_obs, (size_t)F->n * 4, hipMemcpyHostToDevice, s));
+        if (F->uright) HIP_TRY(c, hipMemcpyAsync(ur, F->uright, (size_t)F->n * 4, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(c, hipMemcpyAsync(sfd, F->scale_factors, (size_t)F->nlevels * 4, hipMemcpyHostToDevice, s));
+    if (LF->n) {
+        HIP_TRY(c, hipMemcpyAsync(lk, LF->kps, (size_t)LF->n * 28, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(hm, LF->has_mp, (size_t)LF->n, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(ol, LF->outlier, (size_t)LF->n, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(lp, LF->pos, (size_t)LF->n * 12, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(lo, LF->n_obs, (size_t)LF->n * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(ld, LF->desc, (size_t)LF->n * 32, hipMemcpyHostToDevice, s));
+    }
+    int hc = F->n;
+    HIP_TRY(c, hipMemcpyAsync(cnts, &hc, sizeof(int), hipMemcpyHostToDevice, s));
+    const OgGridGeom G{F->grid.minX, F->grid.minY, F->grid.maxX, F->grid.maxY, F->grid.invW, F->grid.invH};
+    og_launch_grid(s, k, cnts, n, G, cs, ci, 1);
+    OgFrameDev fd{k, d, cnts, cs, ci, F->uright ? ur : nullptr, n};
+    OgLastFrameDev lfd{LF->n, lk, hm, ol, lp, lo, ld};
+    const OgCameraDev cam = camera_dev(curc, G.minX, G.maxX, G.minY, G.maxY);
+    const int mode = last_frame_mode(curc, lastc, bMono);
+    og_launch_last_count(s, fd, G, sfd, cam, lfd, th, mode, cnt, off);
+    int total = 0;
+    HIP_TRY(c, hipMemcpyAsync(&total, off + LF->n, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    HIP_TRY(c, ensure(c->mcands, (size_t)std::max(total, 1) * sizeof(OgLastCand)));
+    og_launch_last_resolve(s, fd, G, sfd, cam, lfd, th, mode, checkOri, off, (OgLastCand*)c->mcands.p, ent, own, obs,
+                           nm);
+    HIP_TRY(c, hipGetLastError());
+    int hnm = 0;
+    HIP_TRY(c, hipMemcpyAsync(&hnm, nm, sizeof(int), hipMemcpyDeviceToHost, s));
+    if (F->n) {
+        HIP_TRY(c, hipMemcpyAsync(owner, own, (size_t)F->n * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipMemcpyAsync(owner_obs, obs, (size_t)F->n * 4, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(c, hipStreamSynchronize(s));
     *nmatches = hnm;
     return ORBGPU_OK;
 }

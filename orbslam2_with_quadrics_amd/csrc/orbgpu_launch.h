@@ -93,3 +93,49 @@ struct OgStereoDev {
     int* nmatches;                   // per frame
 };
 void og_launch_stereo(hipStream_t s, const OgStereoDev& S, int B);
+
+// projection matchers (orb_match.hip): Frame::isInFrustum (A17) and SearchByProjection(F, LastFrame) (A16)
+struct OgCameraDev {          // Frame pose / intrinsics snapshot
+    float R[9], t[3], Ow[3];  // mRcw (row-major), mtcw, mOw
+    float fx, fy, cx, cy, mbf, mb;
+    float scale_factor;       // mfScaleFactor (mfLogScaleFactor = logf of it, taken on the device)
+    int nlevels;              // mnScaleLevels
+    float minX, maxX, minY, maxY;
+};
+struct OgMapGeomDev {
+    int m;
+    const float* pos;      // m x 3
+    const float* normal;   // m x 3
+    const float* max_dist; // mfMaxDistance
+    const float* min_dist; // mfMinDistance
+};
+struct OgFrustumOut {
+    uint8_t* in_view;
+    float* proj_x;
+    float* proj_y;
+    float* proj_xr;
+    int* level;
+    float* view_cos;
+    int* n_in_view;        // optional counter (nullptr = skip)
+};
+void og_launch_frustum(hipStream_t s, OgCameraDev cam, OgMapGeomDev mp, float viewingCosLimit, OgFrustumOut out);
+
+struct OgLastFrameDev {
+    int n;
+    const orbgpu_kp_dev* kps;  // mvKeysUn (octave, angle)
+    const uint8_t* has_mp;
+    const uint8_t* outlier;
+    const float* pos;          // n x 3
+    const int* n_obs;
+    const uint8_t* desc;       // n x 32
+};
+struct OgLastCand {
+    int idx;
+    int dist;
+};
+// mode: 0 = levels [o-1, o+1], 1 = forward [o, any), 2 = backward [0, o]
+void og_launch_last_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
+                          OgLastFrameDev LF, float th, int mode, int* cnt, int* off);
+void og_launch_last_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
+                            OgLastFrameDev LF, float th, int mode, int checkOri, const int* off, OgLastCand* cands,
+                            int* ent, int* owner, int* owner_obs, int* nmatches);

@@ -122,6 +122,59 @@ class ORBmatcher:
         _lib.check(ctx, rc, "orbgpu_search_by_projection")
         return nm.value, owner, owner_obs
 
+    def IsInFrustum(self, F: Frame, cam: dict, geom: dict, viewingCosLimit: float = 0.5):
+        """Frame::isInFrustum (src/Frame.cc:269-325) + PredictScale for every map point of `geom` (pos, normal,
+        max_dist, min_dist).  Returns (n_in_view, dict of the mTrack* fields as SearchByProjection inputs)."""
+        pos = np.ascontiguousarray(geom["pos"], np.float32).reshape(-1, 3)
+        nrm = np.ascontiguousarray(geom["normal"], np.float32).reshape(-1, 3)
+        mx = np.ascontiguousarray(geom["max_dist"], np.float32)
+        mn = np.ascontiguousarray(geom["min_dist"], np.float32)
+        m = len(pos)
+        v = _lib.MapPointGeomView(m, _p(pos).value if m else None, _p(nrm).value if m else None,
+                                  _p(mx).value if m else None, _p(mn).value if m else None)
+        out = dict(track_in_view=np.zeros(max(m, 1), np.uint8), proj_x=np.zeros(max(m, 1), np.float32),
+                   proj_y=np.zeros(max(m, 1), np.float32), proj_xr=np.zeros(max(m, 1), np.float32),
+                   level=np.zeros(max(m, 1), np.int32), view_cos=np.zeros(max(m, 1), np.float32))
+        nin = C.c_int(0)
+        c = camera_struct(cam)
+        ctx = self._ex.ctx
+        rc = _lib.lib().orbgpu_is_in_frustum(ctx, C.byref(c), F.grid, C.byref(v), float(viewingCosLimit),
+                                             _p(out["track_in_view"]), _p(out["proj_x"]), _p(out["proj_y"]),
+                                             _p(out["proj_xr"]), _p(out["level"]), _p(out["view_cos"]), C.byref(nin))
+        _lib.check(ctx, rc, "orbgpu_is_in_frustum")
+        return nin.value, {k: a[:m].copy() for k, a in out.items()}
+
+
+    def SearchByProjectionLastFrame(self, CurrentFrame: Frame, cur: dict, LastFrame: dict, last: dict, th: float,
+                                   bMono: bool, owner=None, owner_obs=None):
+        """ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)
+        (src/ORBmatcher.cc:1328-1470).  LastFrame: dict of kps, has_mp, outlier, pos, n_obs, desc; cur/last: the
+        two frames' pose dicts.  Returns (nmatches, owner, owner_obs) -- owner = LastFrame keypoint index."""
+        n = CurrentFrame.N
+        owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+        owner_obs = (np.zeros(n, np.int32) if owner_obs is None
+                     else np.ascontiguousarray(owner_obs, np.int32).copy())
+        arrs = dict(kps=np.ascontiguousarray(LastFrame["kps"], KP_DTYPE),
+                    has_mp=np.ascontiguousarray(LastFrame["has_mp"], np.uint8),
+                    outlier=np.ascontiguousarray(LastFrame["outlier"], np.uint8),
+                    pos=np.ascontiguousarray(LastFrame["pos"], np.float32).reshape(-1, 3),
+                    n_obs=np.ascontiguousarray(LastFrame["n_obs"], np.int32),
+                    desc=np.ascontiguousarray(LastFrame["desc"], np.uint8))
+        lv = _lib.LastFrameView()
+        lv.n = len(arrs["kps"])
+        for k, a in arrs.items():
+            setattr(lv, k, _p(a).value if a.size else None)
+        fv = CurrentFrame.view()
+        cc, cl = camera_struct(cur), camera_struct(last)
+        nm = C.c_int(0)
+        ctx = self._ex.ctx
+        rc = _lib.lib().orbgpu_search_by_projection_last_frame(ctx, C.byref(fv), C.byref(cc), C.byref(cl), C.byref(lv),
+                                                               float(th), int(bMono), int(self.mbCheckOrientation),
+                                                               _p(owner) if n else None, _p(owner_obs) if n else None,
+                                                               C.byref(nm))
+        _lib.check(ctx, rc, "orbgpu_search_by_projection_last_frame")
+        return nm.value, owner, owner_obs
+
 
 def ComputeStereoMatches(ex_left: ORBextractor, ex_right: ORBextractor, mbf: float, mb: float):
     """Frame::ComputeStereoMatches (src/Frame.cc:466-640) on the last frame each extractor processed.
@@ -135,3 +188,17 @@ def ComputeStereoMatches(ex_left: ORBextractor, ex_right: ORBextractor, mbf: flo
                                          C.byref(n), C.byref(nm))
     _lib.check(ex_left.ctx, rc, "orbgpu_compute_stereo_matches")
     return ur[:n.value].copy(), de[:n.value].copy(), nm.value
+
+
+def camera_struct(cam: dict) -> _lib.Camera:
+    """orbgpu_camera from a pose/intrinsics dict (synthetic.camera layout: Rcw, tcw, Ow, fx, fy, cx, cy, mbf,
+    mb, scale_factor, nlevels)."""
+    c = _lib.Camera()
+    c.Rcw[:] = [float(v) for v in np.asarray(cam["Rcw"], np.float32).reshape(9)]
+    c.tcw[:] = [float(v) for v in np.asarray(cam["tcw"], np.float32).reshape(3)]
+    c.Ow[:] = [float(v) for v in np.asarray(cam["Ow"], np.float32).reshape(3)]
+    for k in ("fx", "fy", "cx", "cy", "mbf", "mb", "scale_factor"):
+        setattr(c, k, float(np.float32(cam[k])))
+    c.nlevels = int(cam["nlevels"])
+    return c
+

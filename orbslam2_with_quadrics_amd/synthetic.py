@@ -94,3 +94,80 @@ def stereo_pair(pair_id: int, height: int, width: int, band: int = 64, dmin: int
     noisy = shifted + noise.normal(0.0, 6.0, size=shifted.shape).astype(np.float32)
     right = np.ascontiguousarray(np.clip(np.rint(noisy), 0, 255).astype(np.uint8))
     return left, right, disp
+
+
+# ---- 3-D scenarios for the projection matchers -----------------
+def rotation(rx: float, ry: float, rz: float) -> np.ndarray:
+    """Rz @ Ry @ Rx (radians), float64."""
+    cx, sx, cy, sy, cz, sz = np.cos(rx), np.sin(rx), np.cos(ry), np.sin(ry), np.cos(rz), np.sin(rz)
+    Rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    Rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    return Rz @ Ry @ Rx
+
+
+def camera(cols: int, rows: int, Rcw=None, tcw=None, fx=None, fy=None, cx=None, cy=None, bf=None,
+           scale_factor: float = 1.2, nlevels: int = 8) -> dict:
+    """Frame camera snapshot (mRcw, mtcw, mOw = -Rcw^T tcw, K, mbf, mb, scale pyramid, image size) as float32."""
+    Rcw = np.eye(3) if Rcw is None else np.asarray(Rcw, np.float64)
+    tcw = np.zeros(3) if tcw is None else np.asarray(tcw, np.float64)
+    fx = fx if fx is not None else 0.73 * cols
+    fy = fy if fy is not None else fx
+    cx = cx if cx is not None else cols / 2.0 - 0.37
+    cy = cy if cy is not None else rows / 2.0 + 0.21
+    bf = bf if bf is not None else 0.54 * fx
+    R32 = Rcw.astype(np.float32)
+    t32 = tcw.astype(np.float32)
+    Ow = (-(R32.astype(np.float64).T @ t32.astype(np.float64))).astype(np.float32)
+    return dict(Rcw=R32, tcw=t32, Ow=Ow, fx=np.float32(fx), fy=np.float32(fy), cx=np.float32(cx), cy=np.float32(cy),
+                mbf=np.float32(bf), mb=np.float32(np.float32(bf) / np.float32(fx)), scale_factor=np.float32(scale_factor),
+                nlevels=int(nlevels), cols=int(cols), rows=int(rows))
+
+
+def last_frame_points(seed: int, kps, desc, cam_last: dict, depth=(2.0, 9.0), p_no_mp=0.1, p_outlier=0.05,
+                      p_flip=0.03, n_obs_zero=0.2) -> dict:
+    """LastFrame snapshot for SearchByProjection(Frame&, const Frame&): every keypoint back-projected at a
+    random depth through the last camera (world positions), descriptors = keypoint descriptors with bits
+    flipped at p_flip; some keypoints without map point, some outliers, some points with 0 observations."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n = len(kps)
+    z = rng.uniform(depth[0], depth[1], n)
+    fx, fy, cx, cy = (float(cam_last[k]) for k in ("fx", "fy", "cx", "cy"))
+    Xc = np.stack([(kps["x"].astype(np.float64) - cx) * z / fx, (kps["y"].astype(np.float64) - cy) * z / fy, z], 1)
+    R = cam_last["Rcw"].astype(np.float64)
+    t = cam_last["tcw"].astype(np.float64)
+    Xw = (Xc - t) @ R  # R^T (Xc - t)
+    flips = rng.random((n, 256)) < p_flip
+    bits = np.unpackbits(np.asarray(desc, np.uint8).reshape(n, 32), axis=1, bitorder="little") ^ flips
+    d = np.packbits(bits.astype(np.uint8), axis=1, bitorder="little")
+    return dict(kps=np.ascontiguousarray(kps), has_mp=(rng.random(n) >= p_no_mp).astype(np.uint8),
+                outlier=(rng.random(n) < p_outlier).astype(np.uint8), pos=Xw.astype(np.float32),
+                n_obs=np.where(rng.random(n) < n_obs_zero, 0, rng.integers(1, 6, n)).astype(np.int32),
+                desc=np.ascontiguousarray(d))
+
+
+def local_map_points(seed: int, m: int, cam: dict, nlevels: int = 8, scale_factor: float = 1.2) -> dict:
+    """Map-point geometry for Frame::isInFrustum: points spread over a frustum-shaped volume of `cam`
+    (plus points behind it and outside the image), unit normals from a reference camera centre, and the
+    distance bounds UpdateNormalAndDepth would set (mfMaxDistance = dist * sf^level, mfMinDistance =
+    mfMaxDistance / sf^(nlevels-1))."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    fx, fy, cx, cy = (float(cam[k]) for k in ("fx", "fy", "cx", "cy"))
+    W, H = cam["cols"], cam["rows"]
+    z = rng.uniform(-1.0, 12.0, m)
+    u = rng.uniform(-0.1 * W, 1.1 * W, m)
+    v = rng.uniform(-0.1 * H, 1.1 * H, m)
+    Xc = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)
+    R = cam["Rcw"].astype(np.float64)
+    t = cam["tcw"].astype(np.float64)
+    Xw = (Xc - t) @ R
+    ref_c = -(R.T @ t) + rng.normal(0, 0.6, (m, 3))
+    nrm = Xw - ref_c
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    nrm = np.where(rng.random((m, 1)) < 0.1, -nrm, nrm)  # some points seen from the other side
+    dref = np.linalg.norm(Xw - ref_c, axis=1) * rng.uniform(0.7, 1.4, m)
+    lvl = rng.integers(0, nlevels, m)
+    mx = dref * scale_factor ** lvl
+    mn = mx / scale_factor ** (nlevels - 1)
+    return dict(pos=Xw.astype(np.float32), normal=nrm.astype(np.float32), max_dist=mx.astype(np.float32),
+                min_dist=mn.astype(np.float32))

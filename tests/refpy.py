@@ -441,3 +441,167 @@ def stereo_matches(kL, dL, kR, dR, pyrL, pyrR, sf, isf, mbf, mb):
             uright[i] = -1
             depth[i] = -1
     return uright, depth
+
+
+# ---------------------------------------------------------------------------------------------
+# Projection matchers: Frame::isInFrustum + MapPoint::PredictScale (src/Frame.cc:269-325,
+# src/MapPoint.cc:402-417) and SearchByProjection(Frame&, const Frame&) (src/ORBmatcher.cc:1328-1470)
+# ---------------------------------------------------------------------------------------------
+def _libm_logf():
+    import ctypes
+
+    m = ctypes.CDLL("libm.so.6")
+    m.logf.restype = ctypes.c_float
+    m.logf.argtypes = [ctypes.c_float]
+    return m.logf
+
+
+def fmaf(a, b, c):
+    """Correctly rounded float32 fma (exact rational arithmetic, no double rounding)."""
+    from fractions import Fraction
+
+    ex = Fraction(float(F32(a))) * Fraction(float(F32(b))) + Fraction(float(F32(c)))
+    d = float(ex)                                  # correctly rounded double
+    f = F32(d)
+    # double -> float rounding is wrong only when d sits exactly on a float32 midpoint
+    lo, hi = (np.nextafter(f, F32(-np.inf)), f) if float(f) > d else (f, np.nextafter(f, F32(np.inf)))
+    if float(lo) != float(hi) and Fraction(float(lo)) + Fraction(float(hi)) == 2 * Fraction(d):
+        f = hi if ex > Fraction(d) else lo if ex < Fraction(d) else f
+    return F32(f)
+
+
+def _rx_t(R, x, t):
+    out = []
+    for r in range(3):
+        s = F32(F32(R[r][0]) * F32(x[0]))
+        s = F32(s + F32(F32(R[r][1]) * F32(x[1])))
+        s = F32(s + F32(F32(R[r][2]) * F32(x[2])))
+        out.append(F32(s + F32(t[r])))
+    return out
+
+
+def is_in_frustum(cam, pos, normal, max_dist, min_dist, limit=0.5):
+    logf = _libm_logf()
+    lsf = F32(logf(float(cam["scale_factor"])))
+    R = np.asarray(cam["Rcw"], np.float32).reshape(3, 3)
+    t = np.asarray(cam["tcw"], np.float32)
+    Ow = np.asarray(cam["Ow"], np.float32)
+    fx, fy, cx, cy, mbf = (F32(cam[k]) for k in ("fx", "fy", "cx", "cy", "mbf"))
+    W, H = F32(cam["cols"]), F32(cam["rows"])
+    m = len(pos)
+    out = dict(track_in_view=np.zeros(m, np.uint8), proj_x=np.zeros(m, np.float32),
+               proj_y=np.zeros(m, np.float32), proj_xr=np.zeros(m, np.float32), level=np.zeros(m, np.int32),
+               view_cos=np.zeros(m, np.float32))
+    for i in range(m):
+        P = np.asarray(pos[i], np.float32)
+        Pc = _rx_t(R, P, t)
+        if Pc[2] < 0:
+            continue
+        invz = F32(F32(1.0) / Pc[2])
+        u = fmaf(F32(fx * Pc[0]), invz, cx)
+        v = fmaf(F32(fy * Pc[1]), invz, cy)
+        if u < 0 or u > W or v < 0 or v > H:
+            continue
+        maxD = F32(F32(1.2) * F32(max_dist[i]))
+        minD = F32(F32(0.8) * F32(min_dist[i]))
+        PO = [F32(P[k] - Ow[k]) for k in range(3)]
+        ss = 0.0
+        for k in range(3):
+            ss += float(PO[k]) * float(PO[k])
+        dist = F32(math.sqrt(ss))
+        if dist < minD or dist > maxD:
+            continue
+        dot = 0.0
+        for k in range(3):
+            dot += float(PO[k]) * float(F32(normal[i][k]))
+        vc = F32(dot / float(dist))
+        if vc < F32(limit):
+            continue
+        ratio = F32(F32(max_dist[i]) / dist)
+        ns = int(math.ceil(F32(F32(logf(float(ratio))) / lsf)))
+        ns = min(max(ns, 0), int(cam["nlevels"]) - 1)
+        out["track_in_view"][i] = 1
+        out["proj_x"][i] = u
+        out["proj_y"][i] = v
+        out["proj_xr"][i] = fmaf(-mbf, invz, u)
+        out["level"][i] = ns
+        out["view_cos"][i] = vc
+    return out
+
+
+def search_by_projection_last(F, cur, last, lf, th, mono, check_ori, owner=None, owner_obs=None):
+    """F: PyFrame (current).  Returns (nmatches, owner, owner_obs)."""
+    n = len(F.kps)
+    owner = [-1] * n if owner is None else list(owner)
+    owner_obs = [0] * n if owner_obs is None else list(owner_obs)
+    Rc = np.asarray(cur["Rcw"], np.float32).reshape(3, 3)
+    tc = np.asarray(cur["tcw"], np.float32)
+    Rl = np.asarray(last["Rcw"], np.float32).reshape(3, 3)
+    tl = np.asarray(last["tcw"], np.float32)
+    twc = []
+    for j in range(3):
+        s = F32(Rc[0][j] * tc[0])
+        s = F32(s + F32(Rc[1][j] * tc[1]))
+        s = F32(s + F32(Rc[2][j] * tc[2]))
+        twc.append(F32(-s))
+    tlc = _rx_t(Rl, twc, tl)
+    mb, mbf = F32(cur["mb"]), F32(cur["mbf"])
+    bForward = tlc[2] > mb and not mono
+    bBackward = -tlc[2] > mb and not mono
+    fx, fy, cx, cy = (F32(cur[k]) for k in ("fx", "fy", "cx", "cy"))
+    hist = [[] for _ in range(30)]
+    nm = 0
+    for i in range(len(lf["kps"])):
+        if not lf["has_mp"][i] or lf["outlier"][i]:
+            continue
+        x3 = _rx_t(Rc, np.asarray(lf["pos"][i], np.float32), tc)
+        invzc = F32(1.0 / float(x3[2]))
+        if invzc < 0:
+            continue
+        u = fmaf(F32(fx * x3[0]), invzc, cx)
+        v = fmaf(F32(fy * x3[1]), invzc, cy)
+        if u < F.minX or u > F.maxX or v < F.minY or v > F.maxY:
+            continue
+        o = int(lf["kps"][i]["octave"])
+        radius = F32(F32(th) * F.sf[o])
+        if bForward:
+            cands = F.features_in_area(u, v, radius, o, -1)
+        elif bBackward:
+            cands = F.features_in_area(u, v, radius, 0, o)
+        else:
+            cands = F.features_in_area(u, v, radius, o - 1, o + 1)
+        if not cands:
+            continue
+        best, bi = 256, -1
+        for i2 in cands:
+            if owner[i2] >= 0 and owner_obs[i2]:
+                continue
+            if F.uright is not None and F.uright[i2] > 0:
+                ur = fmaf(-mbf, invzc, u)
+                if abs(F32(ur - F32(F.uright[i2]))) > radius:
+                    continue
+            d = popcount_dist(lf["desc"][i], F.desc[i2])
+            if d < best:
+                best, bi = d, i2
+        if best <= 100:
+            owner[bi] = i
+            owner_obs[bi] = int(lf["n_obs"][i] > 0)
+            nm += 1
+            if check_ori:
+                rot = F32(F32(lf["kps"][i]["angle"]) - F32(F.kps[bi]["angle"]))
+                if rot < 0.0:
+                    rot = F32(rot + F32(360.0))
+                b = _round_half_away(f32(rot * F32(F32(1.0) / F32(30))))
+                if b == 30:
+                    b = 0
+                hist[b].append(bi)
+    if check_ori:
+        i1, i2_, i3 = three_maxima([len(h) for h in hist])
+        for b in range(30):
+            if b in (i1, i2_, i3):
+                continue
+            for k in hist[b]:
+                owner[k] = -1
+                owner_obs[k] = 0
+                nm -= 1
+    return nm, owner, owner_obs

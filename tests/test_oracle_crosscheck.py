@@ -162,3 +162,59 @@ def test_stereo_matches_python_restatement(oracle, pid, shape):
     assert n > 0
     np.testing.assert_array_equal(ur.view(np.uint32), wur.view(np.uint32))
     np.testing.assert_array_equal(de.view(np.uint32), wde.view(np.uint32))
+
+
+def _pose_pair(seed, cols, rows, mono=True):
+    from orbslam2_with_quadrics_amd import synthetic
+
+    rng = np.random.default_rng(seed)
+    R0 = synthetic.rotation(*rng.uniform(-0.05, 0.05, 3))
+    t0 = rng.uniform(-0.3, 0.3, 3)
+    dR = synthetic.rotation(*rng.uniform(-0.01, 0.01, 3))
+    tz = [0.0, 0.8, -0.8][seed % 3] if not mono else 0.0
+    last = synthetic.camera(cols, rows, R0, t0)
+    cur = synthetic.camera(cols, rows, dR @ R0, dR @ t0 + np.array([-0.02, -0.01, tz]))
+    return last, cur
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_is_in_frustum_python_restatement(oracle, seed):
+    from orbslam2_with_quadrics_amd import synthetic
+
+    cols, rows = (640, 480) if seed % 2 else (1920, 1080)
+    _, cam = _pose_pair(seed, cols, rows)
+    mp = synthetic.local_map_points(seed, 1500, cam)
+    n, got = oracle.is_in_frustum(cam, mp["pos"], mp["normal"], mp["max_dist"], mp["min_dist"], 0.5)
+    want = refpy.is_in_frustum(cam, mp["pos"], mp["normal"], mp["max_dist"], mp["min_dist"], 0.5)
+    assert n == int(want["track_in_view"].sum()) and n > 200
+    assert len(set(got["level"][got["track_in_view"] == 1].tolist())) >= 4
+    for k in want:
+        np.testing.assert_array_equal(got[k].view(np.uint8), want[k].view(np.uint8), err_msg=k)
+
+
+@pytest.mark.parametrize("seed,mono", [(0, True), (1, True), (2, False), (3, False), (4, False)])
+def test_search_by_projection_last_python_restatement(oracle, seed, mono):
+    from orbslam2_with_quadrics_amd import synthetic
+
+    rows, cols = 480, 640
+    f1, f2 = synthetic.frame_pair(60 + seed, rows, cols, (5, 2))
+    ex = oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+    k1, d1 = ex(f1)
+    k2, d2 = ex(f2)
+    sf = ex.tables()["scale"]
+    last, cur = _pose_pair(seed, cols, rows, mono)
+    lf = synthetic.last_frame_points(seed, k1, d1, last)
+    rng = np.random.default_rng(seed)
+    uright = None if mono else np.where(rng.random(len(k2)) < 0.5, k2["x"] - rng.uniform(1, 40, len(k2)),
+                                        -1).astype(np.float32)
+    Fo = oracle.OracleFrame(k2, d2, cols, rows, sf, uright)
+    Fp = refpy.PyFrame(k2, d2, cols, rows, sf, uright)
+    owner0 = np.full(len(k2), -1, np.int32)
+    obs0 = np.zeros(len(k2), np.int32)
+    owner0[::17] = len(k1)  # pre-existing claims
+    obs0[::34] = 1
+    for th, ori in ((7.0, True), (15.0, False)):
+        n, ow, ob = oracle.search_by_projection_last(Fo, cur, last, lf, th, mono, ori, owner0, obs0)
+        wn, wow, wob = refpy.search_by_projection_last(Fp, cur, last, lf, th, mono, ori, owner0, obs0)
+        assert n == wn and n > 20
+        assert ow.tolist() == wow and ob.tolist() == wob

@@ -73,6 +73,28 @@ def test_sincosf_restatement_exhaustive_sample(tmp_path):
     assert out.strip().endswith("mismatches 0"), out
 
 
+def test_logf_restatement_exhaustive_sample(tmp_path):
+    """oracle glibc-logf restatement (PredictScale) vs this host's libm (every 7th positive float)."""
+    exe = tmp_path / "verify_logf"
+    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-fopenmp",
+                           os.path.join(ROOT, "tools", "verify_logf.c"), "-o", str(exe), "-lm"])
+    out = subprocess.check_output([str(exe), "7"]).decode()
+    assert out.strip().endswith("mismatches 0"), out
+
+
+def test_projection_contraction_probe(tmp_path):
+    """GCC -O3 -march=native contracts the isInFrustum / SearchByProjection projections into the FMA
+    forms the oracle pins (u = fma(fx*X, invz, cx), ur = fma(-mbf, invz, u))."""
+    exe = tmp_path / "probe_proj"
+    subprocess.check_call(["g++", "-O3", "-march=native", os.path.join(ROOT, "tools", "probe_contraction_proj.cc"),
+                           "-o", str(exe)])
+    out = subprocess.check_output([str(exe)]).decode().split()
+    vals = dict(zip(out[2::2], out[3::2]))
+    if "fma" not in open("/proc/cpuinfo").read():
+        pytest.skip("host without FMA: the reference build would not contract")
+    assert vals["u!=fma(fx*X,invz,cx)"] == "0" and vals["ur!=fma(-mbf,invz,u)"] == "0", out
+
+
 def test_sincos_golden_vectors(oracle):
     """Golden (angle -> sin, cos) pairs produced by libm sincosf (tests/golden/make_golden.py)."""
     g = json.load(open(os.path.join(GOLDEN, "sincosf.json")))
