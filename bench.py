@@ -7,8 +7,10 @@ One step = one batch of B synthetic 1920x1080 frames already resident in HBM, pe
     frame b (src/ORBmatcher.cc:405-520; window 100, ratio 0.9, orientation check, src/Tracking.cc:599-600);
   * (N > 1) RCCL all-gather of the per-frame keypoint counts (the only collective of the path).
 Frames are independent, so N GPUs run N frame shards ("scaling": "weak"; value = all frames / max time).
+Within a GPU the B frames are split over S extractor contexts (--streams, one HIP stream each) whose
+kernels run concurrently.
 
-python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--streams S]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 from __future__ import annotations
@@ -138,6 +140,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=128, help="frames per step per GPU")
+    ap.add_argument("--streams", type=int, default=2, help="concurrent extractor contexts (HIP streams) per GPU")
     ap.add_argument("--rows", type=int, default=1080)
     ap.add_argument("--cols", type=int, default=1920)
     ap.add_argument("--nfeatures", type=int, default=2000)
@@ -167,49 +170,66 @@ def main():
     frames = np.stack([uniq[i % nuniq] for i in range(B)])
     log(f"rank {rank}: generated {B} frames ({nuniq} distinct) in {time.time() - t:.1f}s")
 
+    S = args.streams
+    if B % S:
+        raise SystemExit(f"--batch {B} must be a multiple of --streams {S}")
+    Bs = B // S
     ex_ref = ORBextractor(NF, 1.2, 8, 20, 7, device=dev)
-    ex = ORBextractor(NF, 1.2, 8, 20, 7, device=dev)
+    # S extractor contexts = S HIP streams, each extracting and matching B/S frames: the latency-bound
+    # stages of one stream (octree, describe, ordered matcher pass) overlap another stream's FAST/pyramid
+    exs = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev) for _ in range(S)]
+    ex = exs[0]
     d_f1 = ex_ref.device_alloc(f1.nbytes)
     d_frames = ex.device_alloc(frames.nbytes)
     ex_ref.h2d(d_f1, f1)
     ex.h2d(d_frames, frames)
+    fbytes = rows * cols
     grid = _lib.GridGeom()
     L.orbgpu_grid_geom_for_image(cols, rows, C.byref(grid))
     # plan + output capacities (one untimed extraction)
     ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
-    ex.extract_batch_device(d_frames, B, cols, rows, cols, rows * cols)
-    ex.synchronize()
-    _, _, d_counts, cap = ex.batch_outputs()
-    d_prev = ex.device_alloc(B * cap * 2 * 4)
-    d_m12 = ex.device_alloc(B * cap * 4)
-    d_nm = ex.device_alloc(B * 4)
+    for s_, e in enumerate(exs):
+        e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
+        e.synchronize()
+    outs = [e.batch_outputs() for e in exs]
+    cap = outs[0][3]
+    d_prev = [e.device_alloc(Bs * cap * 2 * 4) for e in exs]
+    d_m12 = [e.device_alloc(Bs * cap * 4) for e in exs]
+    d_nm = [e.device_alloc(Bs * 4) for e in exs]
     counts_t = torch.zeros(B, dtype=torch.int32, device=f"cuda:{dev}")
 
     def step():
         ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
-        ex.extract_batch_device(d_frames, B, cols, rows, cols, rows * cols)
-        _lib.check(ex.ctx, L.orbgpu_prev_matched_from_frame(ex_ref.ctx, 0, ex.ctx, C.c_void_p(d_prev)), "prev")
-        _lib.check(ex.ctx, L.orbgpu_search_for_initialization_batch(ex_ref.ctx, 0, ex.ctx, grid, 0.9, 1, 100,
-                                                                      C.c_void_p(d_prev), C.c_void_p(d_m12),
-                                                                      C.c_void_p(d_nm)), "search_init")
-        if dist is not None:
-            _lib.check(ex.ctx, L.orbgpu_memcpy_d2d_async(ex.ctx, C.c_void_p(counts_t.data_ptr()),
-                                                         C.c_void_p(d_counts), B * 4), "d2d")
-        ex.synchronize()
+        for s_, e in enumerate(exs):
+            e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
+        for s_, e in enumerate(exs):
+            _lib.check(e.ctx, L.orbgpu_prev_matched_from_frame(ex_ref.ctx, 0, e.ctx, C.c_void_p(d_prev[s_])),
+                       "prev")
+            _lib.check(e.ctx, L.orbgpu_search_for_initialization_batch(ex_ref.ctx, 0, e.ctx, grid, 0.9, 1, 100,
+                                                                         C.c_void_p(d_prev[s_]),
+                                                                         C.c_void_p(d_m12[s_]),
+                                                                         C.c_void_p(d_nm[s_])), "search_init")
+            if dist is not None:
+                _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C.c_void_p(counts_t.data_ptr() + 4 * s_ * Bs),
+                                                            C.c_void_p(outs[s_][2]), Bs * 4), "d2d")
+        for e in exs:
+            e.synchronize()
         if dist is not None:
             allgather_counts(dist, counts_t, world)
 
     stage_acc = {}
 
     def collect():
-        for name, ms in ex.stage_times():
-            a = stage_acc.setdefault(name, [0.0, 0])
-            a[0] += ms
-            a[1] += 1
+        for e in exs:
+            for name, ms in e.stage_times():
+                a = stage_acc.setdefault(name, [0.0, 0])
+                a[0] += ms
+                a[1] += 1
 
     for i in range(args.warmup):
         step()
-    ex.set_stage_timing(True)
+    for e in exs:
+        e.set_stage_timing(True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -224,27 +244,35 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     dt = max_over_ranks(dist, dt, device=f"cuda:{dev}")
-    ex.set_stage_timing(False)
+    for e in exs:
+        e.set_stage_timing(False)
 
     # ---- per-stage averages and the dominant kernel's roofline
-    cand_total = L.orbgpu_batch_candidate_total(ex.ctx)
-    counts = np.zeros(B, np.int32)
-    ex.d2h(counts, d_counts)
-    kp_total = int(counts.sum())
-    nm = np.zeros(B, np.int32)
-    ex.d2h(nm, d_nm)
+    # per-launch quantities: one launch processes one stream's Bs frames (stage times are per launch)
+    cand_total = sum(L.orbgpu_batch_candidate_total(e.ctx) for e in exs) / S
+    counts = np.zeros(Bs, np.int32)
+    nm = np.zeros(Bs, np.int32)
+    kp_all, nm_all = 0, 0
+    for s_, e in enumerate(exs):
+        e.d2h(counts, outs[s_][2])
+        e.d2h(nm, d_nm[s_])
+        kp_all += int(counts.sum())
+        nm_all += int(nm.sum())
+    kp_total = kp_all / S
     P = level_pixels(cols, rows, ex.GetInverseScaleFactors())
     stages = {k: v[0] / max(v[1], 1) for k, v in stage_acc.items()}
     kernels = {k: v for k, v in stages.items() if k not in ("pyramid", "match_init")}
     dom = max(kernels, key=kernels.get)
     dom_ms = kernels[dom]
-    dom_bytes = stage_bytes(dom, B, P, cand_total, kp_total)
+    dom_bytes = stage_bytes(dom, Bs, P, cand_total, kp_total)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.pmc_json):
         try:
             pmc = json.load(open(args.pmc_json))
             traffic = pmc.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+            if traffic is not None and pmc.get("batch", Bs) != Bs:  # per-frame linear in the batch
+                traffic = int(traffic * Bs / pmc["batch"])
         except Exception:
             traffic = None
 
@@ -267,11 +295,13 @@ def main():
             "workload": f"config 3: {cols}x{rows} mono, {NF} features, ORB extract + SearchForInitialization "
                         f"(window 100, ratio 0.9, checkOri) of every frame against an initial frame",
             "frames_per_step_per_gpu": B,
+            "streams_per_gpu": S,
+            "frames_per_launch": Bs,
             "resolution": f"{cols}x{rows}",
             "nfeatures": NF,
-            "parallelism": f"frame-sharded x{world} (RCCL all-gather of keypoint counts only)",
-            "mean_keypoints_per_frame": round(kp_total / B, 1),
-            "mean_init_matches_per_frame": round(float(nm.mean()), 1),
+            "parallelism": f"frame-sharded x{world} GPUs, {S} streams per GPU (RCCL all-gather of keypoint counts only)",
+            "mean_keypoints_per_frame": round(kp_all / B, 1),
+            "mean_init_matches_per_frame": round(nm_all / B, 1),
         },
         "roofline": {
             "bound": "hbm",
@@ -284,15 +314,17 @@ def main():
             "algorithmic_bytes_per_launch": int(dom_bytes),
             "avg_launch_ms": round(dom_ms, 4),
         },
-        "stages_ms_per_batch": {k: round(v, 4) for k, v in stages.items()},
+        "stages_ms_per_launch": {k: round(v, 4) for k, v in stages.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("timing the CPU baseline (oracle, 1 thread)")
         out["cpu_baseline"] = cpu_baseline(rows, cols, NF, args.cpu_seconds)
     elif rank == 0:
         out["cpu_baseline"] = None
-    for p in (d_prev, d_m12, d_nm, d_frames):
-        ex.device_free(p)
+    for s_, e in enumerate(exs):
+        for p in (d_prev[s_], d_m12[s_], d_nm[s_]):
+            e.device_free(p)
+    ex.device_free(d_frames)
     ex_ref.device_free(d_f1)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liborbgpu.so")
+# ORBGPU_LIB selects an experiment build of the same library (tools/fast_variants.py); default in-tree
+LIB_PATH = os.environ.get("ORBGPU_LIB") or os.path.join(HERE, "liborbgpu.so")
 
 # Every symbol include/orbgpu.h declares (checked by tests/test_lib_abi.py).
 EXPORTS = [

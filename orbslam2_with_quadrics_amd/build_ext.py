@@ -40,25 +40,28 @@ def _stale() -> bool:
     return False
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None) -> str:
+    """Build liborbgpu.so (or, with `out`/`defines`, an experiment variant of it, e.g. tools/fast_variants.py)."""
+    target = out or LIB
+    if not force and out is None and not _stale():
         return LIB
     objs = []
     cc = hipcc()
-    tmp = os.path.join(HERE, "build")
+    tmp = os.path.join(HERE, "build", os.path.basename(target))
     os.makedirs(tmp, exist_ok=True)
     for src in SOURCES:
         obj = os.path.join(tmp, src + ".o")
-        cmd = [cc, f"--offload-arch={ARCH}", *FLAGS, "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [cc, f"--offload-arch={ARCH}", *FLAGS, *[f"-D{d}" for d in defines], "-x", "hip", "-c",
+               os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
         objs.append(obj)
-    out_tmp = LIB + ".tmp"
+    out_tmp = target + ".tmp"
     cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out_tmp, *objs]
     subprocess.check_call(cmd)
-    os.replace(out_tmp, LIB)
-    return LIB
+    os.replace(out_tmp, target)
+    return target
 
 
 if __name__ == "__main__":

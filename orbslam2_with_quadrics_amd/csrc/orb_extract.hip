@@ -183,11 +183,12 @@ __device__ __forceinline__ int og_fast_M_tile(const uint8_t* p) { return og_fast
 
 // OpenCV FAST_t quick rejection (src: cv::FAST, pairs {k, k+8}): a pixel can only be a corner at
 // threshold t if for every opposite pair one pixel is darker than v-t (resp. brighter than v+t).
-// Necessary condition => every pixel that fails it has M <= t.
+// Necessary condition => every pixel that fails it has M <= t.  Restated threshold-free:
+//   dark(t)   <=>  max_k min(c_k, c_k+8) < v - t,   bright(t) <=> min_k max(c_k, c_k+8) > v + t,
+// (16 byte loads, 8 min + 8 max reductions, 2 compares).
 __device__ __forceinline__ bool og_fast_quick(const uint8_t* p, int t)
 {
     const int v = p[0];
-    const int lo = v - t, hi = v + t;
     int c[16];
     c[0] = p[3 * OG_RS];
     c[1] = p[1 + 3 * OG_RS];
@@ -205,37 +206,41 @@ __device__ __forceinline__ bool og_fast_quick(const uint8_t* p, int t)
     c[13] = p[-3 + 1 * OG_RS];
     c[14] = p[-2 + 2 * OG_RS];
     c[15] = p[-1 + 3 * OG_RS];
-    bool dark = true, bright = true;
+    int md = 0, mb = 255;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        dark &= (c[k] < lo) | (c[k + 8] < lo);
-        bright &= (c[k] > hi) | (c[k + 8] > hi);
+        md = max(md, min(c[k], c[k + 8]));
+        mb = min(mb, max(c[k], c[k + 8]));
     }
-    return dark | bright;
+    return (md < v - t) | (mb > v + t);
 }
 
-__device__ __forceinline__ bool og_nms_keep(const uint8_t* Ms, int i, int j, int dw, int dh, int t)
+// cell-local 3x3 NMS at two thresholds at once: keep iff M > t and (M-1) > every neighbour's score, a
+// neighbour's score being M'-1 if it is a corner at t (M' > t) inside the detection area, else 0
+__device__ __forceinline__ void og_nms_keep2(const uint8_t* Ms, int i, int j, int dw, int dh, int ta, int tb,
+                                             bool& ka, bool& kb)
 {
     const int m = Ms[i * OG_MAX_CELL_W + j];
-    if (m <= t) return false;
-    const int s = m - 1;
+    int na = 0, nb = 0;
 #pragma unroll
     for (int di = -1; di <= 1; di++)
 #pragma unroll
         for (int dj = -1; dj <= 1; dj++) {
             if (di == 0 && dj == 0) continue;
             const int ii = i + di, jj = j + dj;
-            int nb = 0;
-            if (ii >= 0 && ii < dh && jj >= 0 && jj < dw) {
-                const int mn = Ms[ii * OG_MAX_CELL_W + jj];
-                nb = mn > t ? mn - 1 : 0;
-            }
-            if (!(s > nb)) return false;
+            const bool in = ii >= 0 && ii < dh && jj >= 0 && jj < dw;
+            const int mn = in ? (int)Ms[ii * OG_MAX_CELL_W + jj] : 0;
+            na = max(na, mn > ta ? mn - 1 : 0);
+            nb = max(nb, mn > tb ? mn - 1 : 0);
         }
-    return true;
+    ka = m > ta && m - 1 > na;
+    kb = m > tb && m - 1 > nb;
 }
 
 #define FAST_NT 256
+#ifndef OG_EXP_FAST_STOP
+#define OG_EXP_FAST_STOP 0
+#endif
 
 // One 256-thread workgroup (4 waves) per FAST cell: the cell's ROI, score map and survivor list live in
 // LDS shared by the four waves (full occupancy at ~17 KB per workgroup).
@@ -248,7 +253,7 @@ __global__ __launch_bounds__(FAST_NT, 8) void og_fast_cells_kernel(OgPlan P, con
     __shared__ __attribute__((aligned(16))) uint8_t roi[OG_ROI_MAX * OG_RS + 16];
     __shared__ __attribute__((aligned(16))) uint8_t Ms[OG_MAX_CELL_W * OG_MAX_CELL_W];
     __shared__ uint16_t lst[OG_MAX_CELL_W * OG_MAX_CELL_W];
-    __shared__ int sh_n[4];  // 0: survivors, 1: keep count, 2: emission base, 3: emission cursor
+    __shared__ int sh_n[6];  // 0: survivors, 1/4: keep count at t1/t2, 2: emission base, 3: cursor
     const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int f = (int)(lin / gridDim.x);
     const OgCell cd = cells[lin % gridDim.x];
@@ -267,7 +272,7 @@ __global__ __launch_bounds__(FAST_NT, 8) void og_fast_cells_kernel(OgPlan P, con
     const int rw = cd.x1 - cd.x0, rh = cd.y1 - cd.y0;
     const int dw = rw - 6, dh = rh - 6;
     if (dw <= 0 || dh <= 0) return;
-    if (tid < 4) sh_n[tid] = 0;
+    if (tid < 6) sh_n[tid] = 0;
     // ---- ROI -> LDS.  Fast path: 4-byte aligned rows -> whole dwords land at roi + r*OG_RS + 4q and
     // the ROI origin sits `mis` bytes into every LDS row.
     const uint8_t* row0 = img + (long long)cd.y0 * pitch + cd.x0;
@@ -300,9 +305,14 @@ __global__ __launch_bounds__(FAST_NT, 8) void og_fast_cells_kernel(OgPlan P, con
     }
     for (int idx = tid * 4; idx < dh * OG_MAX_CELL_W; idx += FAST_NT * 4) *(uint32_t*)&Ms[idx] = 0u;
     __syncthreads();
+#if OG_EXP_FAST_STOP == 1  // timing experiments only (tools/fast_variants.py): results are wrong
+    if (roi[tid] == 255 && roi[tid + 1] == 254) cand_count[0] = 1;
+    return;
+#endif
     const int t1 = min(max(P.iniTh, 0), 255), t2 = min(max(P.minTh, 0), 255);
     const int tq = min(t1, t2);
-    // ---- stage 1: quick test on every detection pixel, ballot-compacted survivor list
+    // ---- stage 1: quick test on every detection pixel at the weaker threshold, ballot-compacted
+    // survivor list (u16 pixel index; bits 12/13 later carry the NMS keep flags)
     {
         const bool two = dw <= 32;
         const int rowsPer = two ? FAST_NT / 32 : FAST_NT / 64;
@@ -316,43 +326,51 @@ __global__ __launch_bounds__(FAST_NT, 8) void og_fast_cells_kernel(OgPlan P, con
                 int base = 0;
                 if (lane == 0) base = atomicAdd(&sh_n[0], __popcll(mask));
                 base = __shfl(base, 0);
-                if (sv) lst[base + __popcll(mask & ((1ull << lane) - 1ull))] = (uint16_t)(i * OG_MAX_CELL_W + j);
+                if (sv)
+                    lst[base + __popcll(mask & ((1ull << lane) - 1ull))] =
+                        (uint16_t)(i * OG_MAX_CELL_W + j);
             }
         }
     }
     __syncthreads();
     const int nsurv = sh_n[0];
+#if OG_EXP_FAST_STOP == 2
+    if (nsurv == 12345) cand_count[0] = 1;
+    return;
+#endif
     if (nsurv == 0) return;
-    // ---- stage 2: exact M for the survivors only
+    // ---- stage 2: exact M for every survivor of the weaker threshold
     for (int e = tid; e < nsurv; e += FAST_NT) {
-        const int pix = lst[e];
+        const int pix = lst[e] & 0xfff;
         const int i = pix / OG_MAX_CELL_W, j = pix % OG_MAX_CELL_W;
         Ms[pix] = (uint8_t)og_fast_M_tile(&T[(i + 3) * OG_RS + (j + 3)]);
     }
     __syncthreads();
-    // ---- stage 3: NMS at iniThFAST; if the cell is empty, at minThFAST (src/ORBextractor.cc:809-816)
-    auto count_keep = [&](int tt) {
-        int c = 0;
+    // ---- stage 3: NMS at iniThFAST and at minThFAST in one pass (src/ORBextractor.cc:809-816 keeps the
+    // first unless the cell is empty at it); the keep bits are stored in the list entry (bits 12, 13)
+    {
+        int c1 = 0, c2 = 0;
         for (int e = tid; e - tid < nsurv; e += FAST_NT) {
-            bool keep = false;
+            bool k1 = false, k2 = false;
             if (e < nsurv) {
-                const int pix = lst[e];
-                keep = og_nms_keep(Ms, pix / OG_MAX_CELL_W, pix % OG_MAX_CELL_W, dw, dh, tt);
+                const int pix = lst[e] & 0xfff;
+                og_nms_keep2(Ms, pix / OG_MAX_CELL_W, pix % OG_MAX_CELL_W, dw, dh, t1, t2, k1, k2);
+                lst[e] = (uint16_t)(pix | (k1 ? 0x1000 : 0) | (k2 ? 0x2000 : 0));
             }
-            c += __popcll(__ballot(keep));
+            c1 += __popcll(__ballot(k1));
+            c2 += __popcll(__ballot(k2));
         }
-        if (lane == 0 && c) atomicAdd(&sh_n[1], c);
-        __syncthreads();
-        return sh_n[1];
-    };
-    int t = t1;
-    int cnt = count_keep(t);
-    if (cnt == 0) {
-        t = t2;
-        __syncthreads();  // every wave has read the zero count before it changes
-        cnt = count_keep(t);
+        if (lane == 0 && c1) atomicAdd(&sh_n[1], c1);
+        if (lane == 0 && c2) atomicAdd(&sh_n[4], c2);
     }
+    __syncthreads();
+    const int cnt = sh_n[1] ? sh_n[1] : sh_n[4];
+    const int kbit = sh_n[1] ? 0x1000 : 0x2000;
     if (cnt == 0) return;
+#if OG_EXP_FAST_STOP == 3
+    if (cnt == 12345) cand_count[0] = 1;
+    return;
+#endif
     if (tid == 0) {
         const int base = atomicAdd(&cand_count[f * P.nlevels + l], cnt);
         sh_n[2] = base;
@@ -364,18 +382,16 @@ __global__ __launch_bounds__(FAST_NT, 8) void og_fast_cells_kernel(OgPlan P, con
     u64* out = cand + (long long)f * P.cand_per_frame + L.cand_off + base;
     const int ox = cd.x0 - L.minB + 3, oy = cd.y0 - L.minB + 3;
     for (int e = tid; e - tid < nsurv; e += FAST_NT) {
-        bool keep = false;
-        int pix = 0;
-        if (e < nsurv) {
-            pix = lst[e];
-            keep = og_nms_keep(Ms, pix / OG_MAX_CELL_W, pix % OG_MAX_CELL_W, dw, dh, t);
-        }
+        int ent = 0;
+        if (e < nsurv) ent = lst[e];
+        const bool keep = (ent & kbit) != 0;
         const u64 mask = __ballot(keep);
         if (mask) {
             int wb = 0;
             if (lane == 0) wb = atomicAdd(&sh_n[3], __popcll(mask));
             wb = __shfl(wb, 0);
             if (keep) {
+                const int pix = ent & 0xfff;
                 const int pos = wb + __popcll(mask & ((1ull << lane) - 1ull));
                 out[pos] = og_pack_cand(ox + pix % OG_MAX_CELL_W, oy + pix / OG_MAX_CELL_W, Ms[pix] - 1);
             }

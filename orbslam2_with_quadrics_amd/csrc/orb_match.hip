@@ -11,6 +11,8 @@
 //       the precomputed lists.
 #include <hip/hip_runtime.h>
 #include <limits.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "orb_math_dev.h"
@@ -22,6 +24,29 @@ typedef unsigned long long u64;
 #define TH_HIGH 100
 #define TH_LOW 50
 #define HISTO_LENGTH 30
+
+// ORBmatcher::ComputeThreeMaxima (src/ORBmatcher.cc:1601-1642) -> (ind1, ind2, ind3), -1 = none
+__device__ __forceinline__ int3 og_three_maxima(const int* h)
+{
+    int max1 = 0, max2 = 0, max3 = 0;
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+        const int s = h[i];
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+            max3 = s;
+            ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+    return make_int3(ind1, ind2, ind3);
+}
 
 struct OgCellRange {
     int x0, x1, y0, y1;  // inclusive; empty if x0 > x1
@@ -156,136 +181,249 @@ __global__ __launch_bounds__(256) void og_init_cand_kernel(OgFrameDev F1, int re
     if (lane == 0) NC[i1] = min(n, list_cap) | (n > list_cap ? (int)0x80000000 : 0);
 }
 
-__global__ __launch_bounds__(64) void og_init_resolve_kernel(OgFrameDev F1, int ref, OgFrameDev F2, float nnratio,
-                                                             int checkOri, float* __restrict__ prev_xy,
-                                                             int prev_stride, const uint32_t* __restrict__ lists,
-                                                             int list_cap, const int* __restrict__ list_n,
-                                                             int* __restrict__ matches12, int match_stride,
-                                                             int* __restrict__ nmatches, int* __restrict__ status)
+// wave-wide min of a u32 (all 64 lanes active): DPP row_shr prefix minima inside each 16-lane row, then
+// the four row results via readlane -- no LDS round trips (ds_bpermute) on the sequential critical path
+__device__ __forceinline__ uint32_t og_wave_min_u32(uint32_t v)
+{
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    return min(min(a, b), min(c, d));
+}
+
+#define INIT_NT 256
+
+// One workgroup per pair.  All four waves stage the pair's candidate lists (compacted), the keypoint
+// angles and the per-query offsets into LDS; wave 0 then replays the reference's ordered loop
+// (src/ORBmatcher.cc:418-487).  The only state a later query reads is vMatchedDistance (:444), so the
+// loop keeps just that (u16 in LDS, 0xffff == INT_MAX) and logs every accepted match (i1, i2); the
+// next query's entries and their vMatchedDistance values are loaded one query ahead and the single
+// entry the current match changes is patched in registers.  Steals (:463-470), the final
+// vnMatches12, nmatches and the rotation histogram (including stolen matches' stale entries, :478)
+// follow from the log in a parallel pass: vnMatches12[i1] = i2 iff i1 is the last claimant of i2.
+__global__ __launch_bounds__(INIT_NT) void og_init_resolve_kernel(
+    OgFrameDev F1, int ref, OgFrameDev F2, float nnratio, int checkOri, float* __restrict__ prev_xy,
+    int prev_stride, const uint32_t* __restrict__ lists, int list_cap, const int* __restrict__ list_n,
+    int* __restrict__ matches12, int match_stride, int* __restrict__ nmatches, int* __restrict__ status, int ecap)
 {
     extern __shared__ __attribute__((aligned(16))) int smem[];
-    const int b = blockIdx.x, lane = threadIdx.x;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n1 = F1.counts[ref];
     const int n2 = F2.counts[b];
-    int* vMD = smem;                  // vMatchedDistance [cap2]
-    int* v21 = vMD + F2.frame_cap;    // vnMatches21      [cap2]
-    int* m12 = v21 + F2.frame_cap;    // vnMatches12      [cap1]
-    int* binOf = m12 + F1.frame_cap;  // rot-hist bin the match was pushed to, -1 = none [cap1]
+    const int c1 = F1.frame_cap, c2 = F2.frame_cap;
+    float* a1 = (float*)smem;                   // F1 angles               [c1]
+    float* a2 = a1 + c1;                        // F2 angles               [c2]
+    int* offs = (int*)(a2 + c2);                // list offsets of the active queries [c1 + 1]
+    int* own = offs + c1 + 1;                   // last log entry claiming i2 [c2]
+    uint32_t* E = (uint32_t*)(own + c2);        // staged entries          [ecap]
+    uint16_t* vMD = (uint16_t*)(E + ecap);      // vMatchedDistance        [c2]
+    short* m12 = (short*)(vMD + c2);            // vnMatches12             [c1]
+    short* log1 = m12 + c1;                     // match log: i1           [c1]
+    short* log2 = log1 + c1;                    // match log: i2           [c1]
+    short* act = log2 + c1;                     // active queries (F1 indices) [c1]
+    signed char* binOf = (signed char*)(act + c1);  // rot-hist bin of i1's match, -1 = none [c1]
     __shared__ int hist[HISTO_LENGTH];
-    for (int i = lane; i < n2; i += 64) {
-        vMD[i] = INT_MAX;
-        v21[i] = -1;
+    __shared__ int wsum[INIT_NT / 64];
+    __shared__ int wact[INIT_NT / 64];
+    __shared__ int sh_nlog;
+    const orbgpu_kp_dev* K1 = F1.kps + (long long)ref * c1;
+    const orbgpu_kp_dev* K2 = F2.kps + (long long)b * c2;
+    const int* NC = list_n + (long long)b * c1;
+    const uint32_t* LB = lists + (long long)b * c1 * list_cap;
+    for (int i = tid; i < n2; i += INIT_NT) {
+        vMD[i] = 0xffff;
+        own[i] = -1;
+        a2[i] = K2[i].angle;
     }
-    for (int i = lane; i < n1; i += 64) {
+    for (int i = tid; i < n1; i += INIT_NT) {
         m12[i] = -1;
         binOf[i] = -1;
+        a1[i] = K1[i].angle;
     }
-    if (lane < HISTO_LENGTH) hist[lane] = 0;
+    if (tid < HISTO_LENGTH) hist[tid] = 0;
+    // the queries that have candidates (octave-0 F1 keypoints with a non-empty window), in order, with
+    // the exclusive prefix of their list lengths (overflowed lists count 0 and are reported)
+    int na;
+    {
+        int carry = 0, acarry = 0;
+        for (int base = 0; base < n1; base += INIT_NT) {
+            const int i = base + tid;
+            int v = 0;
+            if (i < n1) {
+                const int raw = NC[i];
+                if (raw < 0) atomicOr(status, 16);
+                v = raw < 0 ? 0 : raw;
+            }
+            const u64 am = __ballot(v > 0);
+            int x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o);
+                if (lane >= o) x += y;
+            }
+            if (lane == 63) wsum[wv] = x;
+            if (lane == 0) wact[wv] = __popcll(am);
+            __syncthreads();
+            int before = carry, abefore = acarry;
+            for (int q = 0; q < wv; q++) before += wsum[q], abefore += wact[q];
+            if (v > 0) {
+                const int k = abefore + __popcll(am & ((1ull << lane) - 1ull));
+                act[k] = (short)i;
+                offs[k] = before + x - v;
+            }
+            int tot = 0, atot = 0;
+            for (int q = 0; q < INIT_NT / 64; q++) tot += wsum[q], atot += wact[q];
+            __syncthreads();
+            carry += tot;
+            acarry += atot;
+        }
+        na = acarry;
+        if (tid == 0) offs[na] = carry;
+    }
     __syncthreads();
-    const orbgpu_kp_dev* K1 = F1.kps + (long long)ref * F1.frame_cap;
-    const orbgpu_kp_dev* K2 = F2.kps + (long long)b * F2.frame_cap;
-    const int* NC = list_n + (long long)b * F1.frame_cap;
-    const uint32_t* LB = lists + (long long)b * F1.frame_cap * list_cap;
-    float* PV = prev_xy + (long long)b * prev_stride;
-    const float factor = 1.0f / HISTO_LENGTH;
-    int nm = 0;
-    // software pipeline: the first chunk of query i1+1 is in flight while query i1 is resolved
-    int ncNext = n1 > 0 ? NC[0] : 0;
-    uint32_t entNext = (n1 > 0 && lane < (ncNext & 0x7fffffff)) ? LB[lane] : 0u;
-    for (int i1 = 0; i1 < n1; i1++) {
-        const int ncRaw = ncNext;
-        const uint32_t ent0 = entNext;
-        if (i1 + 1 < n1) {
-            ncNext = NC[i1 + 1];
-            entNext = lane < (ncNext & 0x7fffffff) ? LB[(long long)(i1 + 1) * list_cap + lane] : 0u;
+    int nlog = 0;  // wave 0's register copy of the log length
+    // chunks of queries whose entries fit the LDS staging buffer (one list never exceeds ecap)
+    for (int qa = 0; qa < na;) {
+        int qb;
+        {
+            int lo = qa, hi = na;  // largest qb with offs[qb] - offs[qa] <= ecap
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (offs[mid] - offs[qa] <= ecap) lo = mid;
+                else hi = mid - 1;
+            }
+            qb = lo;
         }
-        if (ncRaw < 0) {  // candidate list overflowed its slot: reported, never silent
-            if (lane == 0) atomicOr(status, 16);
-            continue;
+        const int ebase = offs[qa], tot = offs[qb] - ebase;
+        auto src_of = [&](int t) -> long long {  // list slot of staged element t (last q with offs[q] <= g)
+            const int g = ebase + t;
+            int lo = qa, hi = qb - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (offs[mid] <= g) lo = mid;
+                else hi = mid - 1;
+            }
+            return (long long)act[lo] * list_cap + (g - offs[lo]);
+        };
+        for (int t0 = 0; t0 < tot; t0 += INIT_NT * 4) {
+            const int ta = t0 + tid, tb = ta + INIT_NT, tc = tb + INIT_NT, td = tc + INIT_NT;
+            const long long sa = ta < tot ? src_of(ta) : 0, sb = tb < tot ? src_of(tb) : 0;
+            const long long sc = tc < tot ? src_of(tc) : 0, sd = td < tot ? src_of(td) : 0;
+            const uint32_t va = ta < tot ? LB[sa] : 0u, vb = tb < tot ? LB[sb] : 0u;
+            const uint32_t vc = tc < tot ? LB[sc] : 0u, vd = td < tot ? LB[sd] : 0u;
+            if (ta < tot) E[ta] = va;
+            if (tb < tot) E[tb] = vb;
+            if (tc < tot) E[tc] = vc;
+            if (td < tot) E[td] = vd;
         }
-        const int nc = ncRaw;
-        if (nc == 0) continue;
-        u64 best1 = ~0ull, best2 = ~0ull;  // lane-local two smallest (dist, list position, i2)
-        for (int e0 = 0; e0 < nc; e0 += 64) {
-            const int e = e0 + lane;
-            if (e < nc) {
-                const uint32_t ent = e0 == 0 ? ent0 : LB[(long long)i1 * list_cap + e];
-                const int i2 = (int)(ent & 0xffff), dist = (int)(ent >> 16);
-                if (!(vMD[i2] <= dist)) {  // src/ORBmatcher.cc:444
-                    const u64 key = ((u64)dist << 32) | ((u64)e << 16) | (u64)i2;
-                    if (key < best1) {
-                        best2 = best1;
-                        best1 = key;
-                    } else if (key < best2) {
-                        best2 = key;
+        __syncthreads();
+        if (wv == 0 && qa < qb) {
+            // pipeline registers of the next query: its first 64 entries and their vMatchedDistance
+            int nOff = offs[qa] - ebase, nCnt = offs[qa + 1] - offs[qa];
+            uint32_t nEnt = lane < nCnt ? E[nOff + lane] : 0u;
+            int nVmd = lane < nCnt ? (int)vMD[nEnt & 0xffff] : 0;
+            int nI1 = act[qa];
+            for (int k = qa; k < qb; k++) {
+                const int i1 = nI1, eo = nOff, nc = nCnt;
+                const uint32_t ent0 = nEnt;
+                const int vmd0 = nVmd;
+                if (k + 1 < qb) {
+                    nI1 = act[k + 1];
+                    nOff = offs[k + 1] - ebase;
+                    nCnt = offs[k + 2] - offs[k + 1];
+                    nEnt = lane < nCnt ? E[nOff + lane] : 0u;
+                    nVmd = lane < nCnt ? (int)vMD[nEnt & 0xffff] : 0;
+                }
+                uint32_t best1 = 0xffffffffu, best2 = 0xffffffffu;  // lane-local two smallest (dist:16 | pos:16)
+                int best1i2 = 0;
+                for (int e0 = 0; e0 < nc; e0 += 64) {
+                    const int e = e0 + lane;
+                    if (e < nc) {
+                        const uint32_t ent = e0 == 0 ? ent0 : E[eo + e];
+                        const int i2 = (int)(ent & 0xffff), dist = (int)(ent >> 16);
+                        const int vmd = e0 == 0 ? vmd0 : (int)vMD[i2];
+                        if (!(vmd <= dist)) {  // src/ORBmatcher.cc:444 (0xffff == INT_MAX)
+                            const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)e;
+                            if (key < best1) {
+                                best2 = best1;
+                                best1 = key;
+                                best1i2 = i2;
+                            } else if (key < best2) {
+                                best2 = key;
+                            }
+                        }
                     }
                 }
+                const uint32_t gbest = og_wave_min_u32(best1);
+                if (gbest == 0xffffffffu) continue;
+                const uint32_t gsecond = og_wave_min_u32(best1 == gbest ? best2 : best1);
+                const int bestDist = (int)(gbest >> 16);
+                const int bestDist2 = gsecond == 0xffffffffu ? INT_MAX : (int)(gsecond >> 16);
+                if (bestDist <= TH_LOW && bestDist < (float)bestDist2 * nnratio) {
+                    const int bestIdx2 = __builtin_amdgcn_readlane(best1i2, (int)(gbest & 63));
+                    if (lane == 0) {
+                        vMD[bestIdx2] = (uint16_t)bestDist;
+                        log1[nlog] = (short)i1;
+                        log2[nlog] = (short)bestIdx2;
+                    }
+                    nlog++;
+                    if (lane < nCnt && (int)(nEnt & 0xffff) == bestIdx2) nVmd = bestDist;
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
             }
         }
-        const u64 gbest = og_wave_min_u64(best1);
-        if (gbest == ~0ull) continue;
-        const u64 mine2 = (best1 == gbest) ? best2 : best1;
-        const u64 gsecond = og_wave_min_u64(mine2);
-        const int bestIdx2 = (int)(gbest & 0xffff);
-        const int bestDist = (int)(gbest >> 32);
-        const int bestDist2 = gsecond == ~0ull ? INT_MAX : (int)(gsecond >> 32);
-        if (bestDist <= TH_LOW && bestDist < (float)bestDist2 * nnratio) {
-            if (lane == 0) {
-                const int prev = v21[bestIdx2];
-                if (prev >= 0) {
-                    m12[prev] = -1;
-                    nm--;
-                }
-                m12[i1] = bestIdx2;
-                v21[bestIdx2] = i1;
-                vMD[bestIdx2] = bestDist;
-                nm++;
-                if (checkOri) {
-                    float rot = K1[i1].angle - K2[bestIdx2].angle;
-                    if (rot < 0.0) rot += 360.0f;
-                    int bin = (int)roundf(rot * factor);
-                    if (bin == HISTO_LENGTH) bin = 0;
-                    binOf[i1] = bin;
-                    hist[bin]++;
-                }
-            }
-            __syncthreads();
+        __syncthreads();
+        qa = qb;
+    }
+    if (tid == 0) sh_nlog = nlog;
+    __syncthreads();
+    nlog = sh_nlog;
+    // ---- replay the log in parallel: last claimant per i2, rotation histogram of every match
+    const float factor = 1.0f / HISTO_LENGTH;
+    for (int j = tid; j < nlog; j += INIT_NT) {
+        atomicMax(&own[log2[j]], j);
+        if (checkOri) {
+            const int i1 = log1[j], i2 = log2[j];
+            float rot = a1[i1] - a2[i2];
+            if (rot < 0.0) rot += 360.0f;
+            int bin = (int)roundf(rot * factor);
+            if (bin == HISTO_LENGTH) bin = 0;
+            binOf[i1] = (signed char)bin;
+            atomicAdd(&hist[bin], 1);
         }
     }
     __syncthreads();
-    nm = __shfl(nm, 0);
-    if (checkOri) {
-        // ComputeThreeMaxima (src/ORBmatcher.cc:1601-1642)
-        int ind1 = -1, ind2 = -1, ind3 = -1;
-        int max1 = 0, max2 = 0, max3 = 0;
-        for (int i = 0; i < HISTO_LENGTH; i++) {
-            const int s = hist[i];
-            if (s > max1) {
-                max3 = max2; max2 = max1; max1 = s;
-                ind3 = ind2; ind2 = ind1; ind1 = i;
-            } else if (s > max2) {
-                max3 = max2; max2 = s;
-                ind3 = ind2; ind2 = i;
-            } else if (s > max3) {
-                max3 = s;
-                ind3 = i;
-            }
+    int live = 0;
+    for (int j = tid; j < nlog; j += INIT_NT) {
+        const int i2 = log2[j];
+        if (own[i2] == j) {
+            m12[log1[j]] = (short)i2;
+            live++;
         }
-        if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
-        else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-        int dropped = 0;
-        for (int i = lane; i < n1; i += 64) {
-            const int bin = binOf[i];
-            if (bin >= 0 && bin != ind1 && bin != ind2 && bin != ind3 && m12[i] >= 0) {
-                m12[i] = -1;
-                dropped++;
-            }
-        }
-        nm -= og_wave_sum(dropped);
     }
+    __syncthreads();
+    if (checkOri) {
+        const int3 im = og_three_maxima(hist);
+        for (int i = tid; i < n1; i += INIT_NT) {
+            const int bin = binOf[i];
+            if (bin >= 0 && bin != im.x && bin != im.y && bin != im.z && m12[i] >= 0) {
+                m12[i] = -1;
+                live--;
+            }
+        }
+    }
+    live = og_wave_sum(live);
+    if (lane == 0) wsum[wv] = live;
     __syncthreads();
     int* M = matches12 + (long long)b * match_stride;
-    for (int i = lane; i < n1; i += 64) {
+    float* PV = prev_xy + (long long)b * prev_stride;
+    for (int i = tid; i < n1; i += INIT_NT) {
         const int j = m12[i];
         M[i] = j;
         if (j >= 0) {  // update vbPrevMatched (src/ORBmatcher.cc:515-517)
@@ -293,7 +431,15 @@ __global__ __launch_bounds__(64) void og_init_resolve_kernel(OgFrameDev F1, int 
             PV[2 * i + 1] = K2[j].y;
         }
     }
-    if (lane == 0) nmatches[b] = nm;
+    if (tid == 0) nmatches[b] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+size_t og_init_resolve_lds(int cap1, int cap2, int ecap)
+{
+    // a1, a2, offs, own, E, vMD, m12, log1, log2, act, binOf (see og_init_resolve_kernel), 16-B aligned
+    const size_t b = 4 * (size_t)cap1 + 4 * (size_t)cap2 + 4 * ((size_t)cap1 + 1) + 4 * (size_t)cap2 +
+                     4 * (size_t)ecap + 2 * (size_t)cap2 + 4 * 2 * (size_t)cap1 + (size_t)cap1;
+    return (b + 15) & ~(size_t)15;
 }
 
 void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G, float nnratio,
@@ -303,9 +449,18 @@ void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2,
 {
     hipLaunchKernelGGL(og_init_cand_kernel, dim3((F1.frame_cap + 3) / 4, B), dim3(256), 0, s, F1, ref, F2, G,
                        windowSize, prev_xy, prev_stride, lists, list_cap, list_n);
-    const size_t shm = sizeof(int) * (2 * (size_t)F2.frame_cap + 2 * (size_t)F1.frame_cap);
-    hipLaunchKernelGGL(og_init_resolve_kernel, dim3(B), dim3(64), shm, s, F1, ref, F2, nnratio, checkOri, prev_xy,
-                       prev_stride, lists, list_cap, list_n, matches12, match_stride, nmatches, status);
+    static bool lds_attr = false;  // allow more than the default dynamic LDS per workgroup (benign race)
+    if (!lds_attr) {
+        (void)hipFuncSetAttribute((const void*)og_init_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  OG_INIT_LDS_MAX);
+        lds_attr = true;
+    }
+    const size_t fixed = og_init_resolve_lds(F1.frame_cap, F2.frame_cap, 0);
+    const int ecap = (int)std::min<size_t>(16384, (OG_INIT_LDS_MAX - fixed) / 4);
+    const size_t shm = og_init_resolve_lds(F1.frame_cap, F2.frame_cap, ecap);
+    hipLaunchKernelGGL(og_init_resolve_kernel, dim3(B), dim3(INIT_NT), shm, s, F1, ref, F2, nnratio, checkOri,
+                       prev_xy, prev_stride, lists, list_cap, list_n, matches12, match_stride, nmatches, status,
+                       ecap);
 }
 
 // Tracking::MonocularInitialization (src/Tracking.cc:573-575): vbPrevMatched[i] = F1.mvKeysUn[i].pt,
@@ -650,28 +805,6 @@ __global__ __launch_bounds__(256) void og_last_fill_kernel(OgFrameDev F, OgGridG
     og_last_enum<true>(F, G, sf, cam, LF, i, th, mode, cands + off[i]);
 }
 
-// ORBmatcher::ComputeThreeMaxima (src/ORBmatcher.cc:1601-1642)
-__device__ void og_three_maxima(const int* h, int& ind1, int& ind2, int& ind3)
-{
-    int max1 = 0, max2 = 0, max3 = 0;
-    ind1 = ind2 = ind3 = -1;
-    for (int i = 0; i < HISTO_LENGTH; i++) {
-        const int s = h[i];
-        if (s > max1) {
-            max3 = max2; max2 = max1; max1 = s;
-            ind3 = ind2; ind2 = ind1; ind1 = i;
-        } else if (s > max2) {
-            max3 = max2; max2 = s;
-            ind3 = ind2; ind2 = i;
-        } else if (s > max3) {
-            max3 = s;
-            ind3 = i;
-        }
-    }
-    if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
-    else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-}
-
 // ent: LF.n ints -- the rotation-histogram pushes in order, packed (bin << 24) | keypoint index
 __global__ __launch_bounds__(64) void og_last_resolve_kernel(OgFrameDev F, OgLastFrameDev LF, int checkOri,
                                                              const int* off, const OgLastCand* cands, int* ent,
@@ -714,7 +847,10 @@ __global__ __launch_bounds__(64) void og_last_resolve_kernel(OgFrameDev F, OgLas
         sh[0] = nm;
         sh[1] = ne;
         int i1 = -1, i2 = -1, i3 = -1;
-        if (checkOri) og_three_maxima(hist, i1, i2, i3);
+        if (checkOri) {
+            const int3 im = og_three_maxima(hist);
+            i1 = im.x, i2 = im.y, i3 = im.z;
+        }
         sh[2] = i1;
         sh[3] = (i2 & 0xffff) | (i3 << 16);
     }

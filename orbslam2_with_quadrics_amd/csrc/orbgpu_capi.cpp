@@ -666,6 +666,10 @@ int orbgpu_search_for_initialization(orbgpu_ctx* c, const orbgpu_frame_view* F1,
     int n2oct0 = 0;  // only octave-0 keypoints of F2 can be candidates (level1 == 0)
     for (int i = 0; i < F2->n; i++) n2oct0 += F2->kps[i].octave == 0;
     const int list_cap = std::max(n2oct0, 1);
+    if (og_init_resolve_lds(cap1, cap2, list_cap) > OG_INIT_LDS_MAX) {
+        c->err = "SearchForInitialization: frames too large for the LDS-resident ordered pass";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
     HIP_TRY(c, ensure(c->mlists, (size_t)cap1 * list_cap));
     HIP_TRY(c, ensure(c->mlist_n, (size_t)cap1));
     HIP_TRY(c, ensure(c->status, 4));
@@ -704,6 +708,10 @@ int orbgpu_search_for_initialization_batch(orbgpu_ctx* cref, int ref, orbgpu_ctx
     OgFrameDev f2{c->kps.p, c->desc.p, c->counts.p, c->cell_start.p, c->cell_items.p, nullptr, c->plan.frame_cap};
     const int list_cap = c->plan.lv[0].kcap;  // F2 has at most kcap_0 octave-0 keypoints
     const size_t cap1 = (size_t)cref->plan.frame_cap;
+    if (og_init_resolve_lds((int)cap1, c->plan.frame_cap, list_cap) > OG_INIT_LDS_MAX) {
+        c->err = "SearchForInitialization: frames too large for the LDS-resident ordered pass";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
     HIP_TRY(c, ensure(c->mlists, (size_t)c->last_B * cap1 * list_cap));
     HIP_TRY(c, ensure(c->mlist_n, (size_t)c->last_B * cap1));
     timer_mark(c, "match_init");

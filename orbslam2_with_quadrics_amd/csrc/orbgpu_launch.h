@@ -46,6 +46,11 @@ void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2,
                            int match_stride, int* nmatches, uint32_t* lists, int list_cap, int* list_n, int* status,
                            int B);
 
+// LDS bytes of the ordered SearchForInitialization pass for frame capacities cap1/cap2 and `ecap` staged
+// candidate entries; the pass needs og_init_resolve_lds(cap1, cap2, list_cap) <= OG_INIT_LDS_MAX
+#define OG_INIT_LDS_MAX (150 * 1024)
+size_t og_init_resolve_lds(int cap1, int cap2, int ecap);
+
 void og_launch_prev_from_frame(hipStream_t s, OgFrameDev F1, int ref, float* prev_xy, int prev_stride, int B);
 
 struct OgMapPointsDev {

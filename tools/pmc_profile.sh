@@ -3,7 +3,7 @@
 # Usage (on the GPU box, from the repo root): bash tools/pmc_profile.sh <outdir> [bench args...]
 set -e
 OUT=${1:-gpurun_out/pmc}; shift || true
-ARGS=${@:---steps 3 --warmup 1 --batch 64 --no-cpu-baseline}
+ARGS=${@:---steps 3 --warmup 1 --no-cpu-baseline}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 ROOT=$(pwd)

@@ -2,7 +2,8 @@
 per-launch metrics.  HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reads 1/2 of the bytes
 of wide coalesced streams on gfx950 -> doubled ("corrected"); WRITE_SIZE (KB) taken as is.
 
-python tools/pmc_summary.py <pmc dir> [--json out.json] [--md out.md]
+python tools/pmc_summary.py <pmc dir> [--json out.json] [--md out.md] [--batch B]
+(--batch = frames per launch of the profiled bench run; bench.py rescales traffic if its batch differs)
 """
 import csv
 import glob
@@ -54,7 +55,8 @@ def main():
         if "SQ_WAIT_ANY" in m and m.get("SQ_WAVE_CYCLES"):
             e["wait_frac"] = m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"]
         out[STAGE.get(k, k)] = e
-    js = {"source": d, "note": "per-launch averages over the B-frame launches; FETCH_SIZE doubled per the "
+    batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else 128
+    js = {"source": d, "batch": batch, "note": "per-launch averages over the B-frame launches; FETCH_SIZE doubled per the "
                                 "gfx950 correction (uncalibrated for non-16B accesses)", "kernels": out}
     if "--json" in sys.argv:
         json.dump(js, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
