@@ -236,6 +236,11 @@ int orbgpu_compute_stereo_matches(orbgpu_ctx* left, orbgpu_ctx* right, float mbf
 int orbgpu_compute_stereo_matches_batch(orbgpu_ctx* left, orbgpu_ctx* right, float mbf, float mb,
                                         float* d_uright, float* d_depth, int* d_nmatches);
 
+/* Experiment builds only (OG_OCT_PROFILE=1, tools/octree_profile.py): per-round clock64 stamps and list
+ * sizes of the octree workgroup of (frame 0, level 0) of the last batch.  ORBGPU_ERR_UNSUPPORTED in the
+ * product build. */
+int orbgpu_debug_octree_profile(orbgpu_ctx* ctx, unsigned long long* out, int n);
+
 /* ---- stream / timing helpers ------------------------------------------------------------------ */
 
 /* The context's hipStream_t (as void*), e.g. for torch.cuda.ExternalStream. */
@@ -247,6 +252,10 @@ int orbgpu_synchronize(orbgpu_ctx* ctx);
  * number of stages. */
 int orbgpu_set_stage_timing(orbgpu_ctx* ctx, int on);
 int orbgpu_stage_times(orbgpu_ctx* ctx, const char** names, float* ms, int cap);
+/* The same marks as absolute times: milliseconds from `ref`'s first mark of its last batch to each mark
+ * of ctx's (both contexts on one device, timing on).  Lets a caller measure the union of a stage's
+ * busy intervals across concurrently running contexts.  Returns the number of marks written. */
+int orbgpu_stage_marks(orbgpu_ctx* ctx, orbgpu_ctx* ref, const char** names, float* t_ms, int cap);
 /* Human-readable message for the last error on this context (static storage, never NULL). */
 const char* orbgpu_last_error(const orbgpu_ctx* ctx);
 

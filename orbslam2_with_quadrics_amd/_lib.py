@@ -26,7 +26,8 @@ EXPORTS = [
     "orbgpu_device_alloc", "orbgpu_device_free", "orbgpu_memcpy_h2d", "orbgpu_memcpy_d2h",
     "orbgpu_memset_d", "orbgpu_prev_matched_from_frame", "orbgpu_memcpy_d2d_async",
     "orbgpu_batch_candidate_total", "orbgpu_compute_stereo_matches", "orbgpu_compute_stereo_matches_batch",
-    "orbgpu_is_in_frustum", "orbgpu_search_by_projection_last_frame",
+    "orbgpu_is_in_frustum", "orbgpu_search_by_projection_last_frame", "orbgpu_debug_octree_profile",
+    "orbgpu_stage_marks",
 ]
 
 OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
@@ -116,6 +117,8 @@ def _declare(L):
     L.orbgpu_prev_matched_from_frame.argtypes = [vp, i32, vp, vp]
     L.orbgpu_memcpy_d2d_async.argtypes = [vp, vp, vp, sz]
     L.orbgpu_batch_candidate_total.restype = C.c_longlong
+    L.orbgpu_debug_octree_profile.argtypes = [vp, vp, i32]
+    L.orbgpu_stage_marks.argtypes = [vp, vp, C.POINTER(C.c_char_p), C.POINTER(f32), i32]
     L.orbgpu_compute_stereo_matches.argtypes = [vp, vp, f32, f32, vp, vp, i32, C.POINTER(i32), C.POINTER(i32)]
     L.orbgpu_compute_stereo_matches_batch.argtypes = [vp, vp, f32, f32, vp, vp, vp]
     L.orbgpu_batch_candidate_total.argtypes = [vp]

@@ -471,6 +471,21 @@ __device__ __forceinline__ unsigned og_cand_order(int x, int y, const OgLevel& L
 
 #define OCT_U 8  // candidates per thread per pass with all loads hoisted (latency batching)
 
+#ifndef OG_OCT_PROFILE
+#define OG_OCT_PROFILE 0
+#endif
+#if OG_OCT_PROFILE  // experiment builds only (tools/fast_variants.py): per-round clocks of (frame 0, level 0)
+__device__ unsigned long long og_oct_prof[256];
+#define OCT_PROF(slot, v)                                                              \
+    do {                                                                               \
+        if (tid == 0 && f == 0 && l == 0 && (slot) < 256) og_oct_prof[(slot)] = (v); \
+    } while (0)
+#else
+#define OCT_PROF(slot, v) \
+    do {                  \
+    } while (0)
+#endif
+
 __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* __restrict__ cand,
                                                            const int* __restrict__ cand_count,
                                                            uint16_t* __restrict__ node_of,
@@ -499,6 +514,8 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
     const int nIni = L.nIni;
     const int H = L.maxBY - L.minB;
 
+    OCT_PROF(0, clock64());
+    OCT_PROF(1, (unsigned long long)C);
     // ---- roots (src/ORBextractor.cc:552-585)
     for (int r = tid; r < nIni; r += OCT_NT) childCnt[1][r] = 0;
     __syncthreads();
@@ -575,9 +592,12 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
     }
     __syncthreads();
 
+    OCT_PROF(2, clock64());
     for (int round = 0; round < 4096; round++) {
         if (sv[3]) break;
         const int Ln = sv[0], mode = sv[1], cur = sv[4], cc = sv[7];
+        OCT_PROF(8 + 4 * round, clock64());
+        OCT_PROF(9 + 4 * round, (unsigned long long)Ln | ((unsigned long long)mode << 32));
         OctNode* cn = nodes[cur];
         uint8_t* cf = fresh[cur];
         OctNode* nn = nodes[cur ^ 1];
@@ -701,6 +721,8 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
         if (done)
             for (int q = tid; q < Lnew; q += OCT_NT) best[q] = 0ull;
         __syncthreads();
+        OCT_PROF(10 + 4 * round, clock64());
+        OCT_PROF(11 + 4 * round, (unsigned long long)S | ((unsigned long long)A << 32));
         // ---- one pass over the keys: move to the new list position, and either count the children of
         // the next round's split candidates or (last round) keep the best key per node (:744-760)
         for (int base = tid; base < C; base += OCT_NT * OCT_U) {
@@ -746,6 +768,7 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
         __syncthreads();
     }
     __syncthreads();
+    OCT_PROF(3, clock64());
     const int Ln = sv[0];
     if (!sv[8]) {  // finished without a final key pass (empty split set): one pass for the best key
         for (int n = tid; n < Ln; n += OCT_NT) best[n] = 0ull;
@@ -789,6 +812,8 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
         oct_count[f * P.nlevels + l] = nout;
         if (Ln > L.kcap) atomicOr(status, 4);
     }
+    OCT_PROF(4, clock64());
+    OCT_PROF(5, (unsigned long long)Ln);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1030,6 +1055,17 @@ hipError_t og_upload_pattern(int device)
                                      hipMemcpyHostToDevice);
     if (e == hipSuccess && device >= 0 && device < 64) g_pattern_uploaded_dev[device] = true;
     return e;
+}
+
+hipError_t og_read_oct_prof(unsigned long long* out, int n)
+{
+#if OG_OCT_PROFILE
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(og_oct_prof), sizeof(unsigned long long) * (size_t)std::min(n, 256));
+#else
+    (void)out;
+    (void)n;
+    return hipErrorNotSupported;
+#endif
 }
 
 void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,

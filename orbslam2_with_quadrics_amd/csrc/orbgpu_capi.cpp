@@ -1119,6 +1119,17 @@ int orbgpu_debug_octree(orbgpu_ctx* c, int b, int level, uint32_t* xy, uint8_t* 
     return n;
 }
 
+int orbgpu_debug_octree_profile(orbgpu_ctx* c, unsigned long long* out, int n)
+{
+    if (!c || !out || n <= 0) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const hipError_t e = og_read_oct_prof(out, n);
+    if (e == hipErrorNotSupported) return ORBGPU_ERR_UNSUPPORTED;
+    HIP_TRY(c, e);
+    return ORBGPU_OK;
+}
+
 void* orbgpu_stream(orbgpu_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int orbgpu_synchronize(orbgpu_ctx* c)
@@ -1142,6 +1153,24 @@ int orbgpu_stage_times(orbgpu_ctx* c, const char** names, float* ms, int cap)
     for (int i = 0; i < n && i < cap; i++) {
         if (names) names[i] = c->timer.last_names[i];
         if (ms) ms[i] = c->timer.last_ms[i];
+    }
+    return n;
+}
+
+int orbgpu_stage_marks(orbgpu_ctx* c, orbgpu_ctx* ref, const char** names, float* t_ms, int cap)
+{
+    if (!c || !ref || !names || !t_ms || cap < 0) return ORBGPU_ERR_ARG;
+    StageTimer& t = c->timer;
+    StageTimer& r = ref->timer;
+    if (!t.on || !r.on || t.used < 1 || r.used < 1) return 0;
+    HIP_TRY(c, hipEventSynchronize(t.ev[t.used - 1]));
+    HIP_TRY(c, hipEventSynchronize(r.ev[0]));
+    const int n = std::min(cap, t.used);
+    for (int i = 0; i < n; i++) {
+        float ms = 0;
+        HIP_TRY(c, hipEventElapsedTime(&ms, r.ev[0], t.ev[i]));
+        t_ms[i] = ms;
+        names[i] = t.names[i];
     }
     return n;
 }

@@ -22,6 +22,7 @@ void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, lo
 void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,
                     long long fstride0, const uint8_t* pyr, unsigned long long* cand, int* cand_count, int* status,
                     int B);
+hipError_t og_read_oct_prof(unsigned long long* out, int n);  // OG_OCT_PROFILE builds only
 void og_launch_octree(hipStream_t s, const OgPlan& P, const unsigned long long* cand, const int* cand_count,
                       uint16_t* node_of, uint32_t* oct_xy, uint8_t* oct_resp, int* oct_count, int* status, int B);
 void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, long long pitch0, long long fstride0,

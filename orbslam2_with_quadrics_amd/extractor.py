@@ -148,6 +148,13 @@ class ORBextractor:
         n = self._L.orbgpu_stage_times(self._ctx, names, ms, 32)
         return [(names[i].decode(), ms[i]) for i in range(min(n, 32))]
 
+    def stage_marks(self, ref: "ORBextractor"):
+        """[(mark name, ms since ref's first mark)] of the last batch (stage timing on for both)."""
+        names = (C.c_char_p * 64)()
+        t = (C.c_float * 64)()
+        n = self._L.orbgpu_stage_marks(self._ctx, ref.ctx, names, t, 64)
+        return [(names[i].decode(), t[i]) for i in range(max(n, 0))]
+
     # ---- introspection for parity tests
     def debug_candidates(self, b: int, level: int) -> np.ndarray:
         n = self._L.orbgpu_debug_candidates(self._ctx, b, level, None, 0)

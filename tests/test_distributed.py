@@ -68,3 +68,13 @@ def test_stage_bytes_formula():
     P = bench.level_pixels(1920, 1080, inv)
     assert P[0] == 1920 * 1080 and P[1] == 1600 * 900
     assert sum(P) == pytest.approx(6_419_321, abs=2000)
+
+
+def test_interval_union():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.interval_union([]) == 0.0
+    assert bench.interval_union([(0.0, 2.0), (1.0, 3.0)]) == 3.0
+    assert bench.interval_union([(5.0, 6.0), (0.0, 1.0), (0.5, 0.75)]) == 2.0
+    assert bench.interval_union([(-1.0, 1.0), (1.0, 2.0)]) == 3.0

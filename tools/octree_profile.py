@@ -1,0 +1,58 @@
+"""Per-round timeline of the level-0 octree workgroup (test infrastructure).
+
+python tools/octree_profile.py --build     # here: variant library with OG_OCT_PROFILE=1
+python tools/octree_profile.py --run       # GPU box: one 64-frame 1080p batch, prints per-round cycles
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+VLIB = os.path.join(ROOT, "orbslam2_with_quadrics_amd", "variants", "liborbgpu_octprof.so")
+
+
+def build():
+    from orbslam2_with_quadrics_amd import build_ext
+
+    os.makedirs(os.path.dirname(VLIB), exist_ok=True)
+    print(build_ext.build(force=True, defines=["OG_OCT_PROFILE=1"], out=VLIB))
+
+
+def run():
+    os.environ["ORBGPU_LIB"] = VLIB
+    import torch  # noqa: F401
+
+    from orbslam2_with_quadrics_amd import ORBextractor, _lib, synthetic
+
+    rows, cols, B = 1080, 1920, 64
+    frames = np.stack([synthetic.frame(i % 8, rows, cols) for i in range(B)])
+    ex = ORBextractor(2000, 1.2, 8, 20, 7)
+    d = ex.device_alloc(frames.nbytes)
+    ex.h2d(d, frames)
+    for _ in range(3):
+        ex.extract_batch_device(d, B, cols, rows, cols, rows * cols)
+        ex.synchronize()
+    buf = np.zeros(256, np.uint64)
+    _lib.check(ex.ctx, _lib.lib().orbgpu_debug_octree_profile(ex.ctx, buf.ctypes.data, 256), "prof")
+    t0 = int(buf[0])
+    print("candidates", int(buf[1]), "final list", int(buf[5]))
+    print("roots+remap  ", int(buf[2]) - t0, "cycles")
+    r = 0
+    prev = int(buf[2])
+    while 8 + 4 * r < 256 and int(buf[8 + 4 * r]) > 0 and int(buf[8 + 4 * r]) >= t0:
+        ts, info, tm, sa = (int(v) for v in buf[8 + 4 * r: 12 + 4 * r])
+        nxt = int(buf[8 + 4 * (r + 1)]) if int(buf[8 + 4 * (r + 1)]) >= ts else int(buf[3])
+        print(f"round {r}: Ln={info & 0xffffffff} mode={info >> 32} S={sa & 0xffffffff} A={sa >> 32} "
+              f"plan={tm - ts} keypass={nxt - tm} cycles")
+        r += 1
+    print("tail (final best pass + output)", int(buf[4]) - int(buf[3]), "cycles; total", int(buf[4]) - t0)
+    ex.device_free(d)
+
+
+if __name__ == "__main__":
+    if "--build" in sys.argv:
+        build()
+    if "--run" in sys.argv:
+        run()

@@ -3,7 +3,8 @@ per-launch metrics.  HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB)
 of wide coalesced streams on gfx950 -> doubled ("corrected"); WRITE_SIZE (KB) taken as is.
 
 python tools/pmc_summary.py <pmc dir> [--json out.json] [--md out.md] [--batch B]
-(--batch = frames per launch of the profiled bench run; bench.py rescales traffic if its batch differs)
+(--batch = frames per launch of the profiled bench run = batch / streams; bench.py rescales traffic if its
+per-launch frame count differs)
 """
 import csv
 import glob
