@@ -159,6 +159,29 @@ int orbgpu_search_by_projection(orbgpu_ctx* ctx, const orbgpu_frame_view* F,
                                 const orbgpu_mappoints_view* mp, float nnratio, float th,
                                 int32_t* owner, int32_t* owner_obs, int* nmatches);
 
+/* ---- Frame post-processing: UndistortKeyPoints / ComputeImageBounds ---------------------------- */
+
+/* Replaces void Frame::UndistortKeyPoints() -- src/Frame.cc:404-434: mvKeysUn from mvKeys through
+ * cv::undistortPoints(mat, mat, mK, mDistCoef, Mat(), mK) (OpenCV 3.4, 5 iterations).  K4 = fx, fy, cx, cy;
+ * dist = k1, k2, p1, p2[, k3], ndist 0..5.  When k1 == 0 the keypoints are copied (the reference's
+ * `mDistCoef.at<float>(0)==0.0` shortcut).  in/out may alias. */
+int orbgpu_undistort_keypoints(orbgpu_ctx* ctx, const float* K4, const float* dist, int ndist,
+                               const orbgpu_keypoint* in, orbgpu_keypoint* out, int n);
+
+/* Replaces void Frame::ComputeImageBounds(const cv::Mat&) -- src/Frame.cc:436-461 -- and fills the grid
+ * scales mfGridElementWidthInv/HeightInv (src/Frame.cc:103-104). */
+int orbgpu_compute_image_bounds(orbgpu_ctx* ctx, const float* K4, const float* dist, int ndist, int cols,
+                                int rows, orbgpu_grid_geom* g);
+
+/* Device-resident Frame post-processing for batches: from the next batch on, every extracted frame also
+ * gets mvKeysUn on the device, and the batch grid, orbgpu_prev_matched_from_frame and the batched
+ * SearchForInitialization use mvKeysUn with the undistorted image bounds (as Frame does, src/Frame.cc:
+ * 180-207).  ndist == 0 or k1 == 0 switches it off (mvKeysUn == mvKeys). */
+int orbgpu_set_undistortion(orbgpu_ctx* ctx, const float* K4, const float* dist, int ndist);
+/* Device pointer of the last batch's mvKeysUn (== the keypoints when undistortion is off; stride
+ * frame_cap per frame) and the image bounds/grid scales in use. */
+int orbgpu_batch_outputs_undistorted(orbgpu_ctx* ctx, orbgpu_keypoint** d_kps_un, orbgpu_grid_geom* bounds);
+
 /* ---- projection matchers: isInFrustum (A17) and SearchByProjection(Frame&, const Frame&) (A16) ---- */
 
 /* Pose / intrinsics snapshot of a Frame: mRcw (row-major 3x3), mtcw, mOw (= -Rcw^T tcw, the camera

@@ -68,6 +68,9 @@ def lib():
         L.oo_search_by_projection.argtypes = [vp, vp, f32, f32, vp, vp]
         L.oo_is_in_frustum.restype = i32
         L.oo_is_in_frustum.argtypes = [vp, vp, f32, vp, vp, vp, vp, vp, vp]
+        L.oo_undistort_points.argtypes = [vp, vp, i32, vp, vp, i32]
+        L.oo_undistort_keypoints.argtypes = [vp, vp, i32, vp, vp, i32]
+        L.oo_compute_image_bounds.argtypes = [vp, vp, i32, i32, i32] + [C.POINTER(f32)] * 6
         L.oo_search_by_projection_last.restype = i32
         L.oo_search_by_projection_last.argtypes = [vp, vp, vp, vp, f32, i32, i32, vp, vp]
         _lib = L
@@ -140,7 +143,8 @@ class _OOFrame(C.Structure):
 class OracleFrame:
     """Snapshot of the Frame fields the matchers read (mvKeysUn, mDescriptors, mvuRight, grid)."""
 
-    def __init__(self, kps, desc, cols, rows, scale_factors, uright=None):
+    def __init__(self, kps, desc, cols, rows, scale_factors, uright=None, bounds=None):
+        """bounds: (minX, maxX, minY, maxY, invW, invH) of Frame::ComputeImageBounds; default = image rect."""
         L = lib()
         self.kps = np.ascontiguousarray(kps)
         self.desc = np.ascontiguousarray(desc, dtype=np.uint8)
@@ -150,7 +154,10 @@ class OracleFrame:
         self.cell_items = np.zeros(max(len(self.kps), 1), np.int32)
         vals = [C.c_float() for _ in range(6)]
         L.oo_grid_params(cols, rows, *[C.byref(v) for v in vals])
-        self.bounds = [v.value for v in vals]
+        self.bounds = [v.value for v in vals]  # minX, minY, maxX, maxY, invW, invH
+        if bounds is not None:
+            mnx, mxx, mny, mxy, iw, ih = bounds
+            self.bounds = [mnx, mny, mxx, mxy, iw, ih]
         s = _OOFrame()
         s.n = len(self.kps)
         s.kps = _p(self.kps).value
@@ -279,6 +286,25 @@ def search_by_projection_last(f: OracleFrame, cur: dict, last: dict, lf: dict, t
                                             int(check_ori), _p(owner) if n else None,
                                             _p(owner_obs) if n else None)
     return nm, owner, owner_obs
+
+
+def undistort_keypoints(K4, dist, kps):
+    """Frame::UndistortKeyPoints -> mvKeysUn (copy of kps with undistorted pt)."""
+    K4 = np.ascontiguousarray(K4, np.float32)
+    dist = np.ascontiguousarray(dist, np.float32)
+    kps = np.ascontiguousarray(kps)
+    out = kps.copy()
+    lib().oo_undistort_keypoints(_p(K4), _p(dist), len(dist), _p(kps), _p(out), len(kps))
+    return out
+
+
+def compute_image_bounds(K4, dist, cols, rows):
+    """Frame::ComputeImageBounds + grid scales -> (minX, maxX, minY, maxY, invW, invH)."""
+    K4 = np.ascontiguousarray(K4, np.float32)
+    dist = np.ascontiguousarray(dist, np.float32)
+    v = [C.c_float() for _ in range(6)]
+    lib().oo_compute_image_bounds(_p(K4), _p(dist), len(dist), cols, rows, *[C.byref(x) for x in v])
+    return tuple(x.value for x in v)
 
 
 def distribute_octree(xy, resp, minX, maxX, minY, maxY, N):

@@ -1252,3 +1252,69 @@ int oo_search_by_projection_last(const oo_frame* F, const oo_camera* cur, const 
     free(idx);
     return nmatches;
 }
+
+/* ------------------------------------------------------------------------------------------------ */
+/* cv::undistortPoints(src, dst, K, D, noArray(), K) as Frame::UndistortKeyPoints (src/Frame.cc:404-434)  */
+/* and Frame::ComputeImageBounds (:436-461) call it.  OpenCV 3.4 cvUndistortPointsInternal with the     */
+/* default TermCriteria(COUNT, 5, 0.01): 5 fixed-point iterations in double; R = I, P = K; the tilt and */
+/* thin-prism terms are identity / +0.0 for <= 5 coefficients.  OpenCV's baseline build has no FMA.     */
+/* ------------------------------------------------------------------------------------------------ */
+void oo_undistort_points(const float* K4, const float* dist, int ndist, const float* xy, float* out, int n)
+{
+    double k[5] = {0, 0, 0, 0, 0};
+    for (int i = 0; i < ndist && i < 5; i++) k[i] = (double)dist[i];
+    const double fx = K4[0], fy = K4[1], cx = K4[2], cy = K4[3];
+    const double ifx = 1. / fx, ify = 1. / fy;
+    for (int i = 0; i < n; i++) {
+        double x = xy[2 * i], y = xy[2 * i + 1];
+        x = (x - cx) * ifx;
+        y = (y - cy) * ify;
+        const double x0 = x, y0 = y;
+        for (int j = 0; j < 5; j++) {
+            const double r2 = x * x + y * y;
+            const double icdist = 1. / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+            const double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x);
+            const double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y;
+            x = (x0 - deltaX) * icdist;
+            y = (y0 - deltaY) * icdist;
+        }
+        /* P = K, R = I: xx = fx*x + 0*y + cx, yy = 0*x + fy*y + cy, ww = 1/(0*x + 0*y + 1) */
+        out[2 * i] = (float)(fx * x + cx);
+        out[2 * i + 1] = (float)(fy * y + cy);
+    }
+}
+
+void oo_undistort_keypoints(const float* K4, const float* dist, int ndist, const oo_keypoint* in, oo_keypoint* out,
+                            int n)
+{
+    for (int i = 0; i < n; i++) out[i] = in[i];
+    if (ndist < 1 || dist[0] == 0.0f) return;  /* mDistCoef.at<float>(0)==0.0: mvKeysUn = mvKeys */
+    for (int i = 0; i < n; i++) {
+        float p[2] = {in[i].x, in[i].y}, q[2];
+        oo_undistort_points(K4, dist, ndist, p, q, 1);
+        out[i].x = q[0];
+        out[i].y = q[1];
+    }
+}
+
+/* Frame::ComputeImageBounds (src/Frame.cc:436-461) + the grid scales (src/Frame.cc:103-104) */
+void oo_compute_image_bounds(const float* K4, const float* dist, int ndist, int cols, int rows, float* minX,
+                             float* maxX, float* minY, float* maxY, float* invW, float* invH)
+{
+    if (ndist >= 1 && dist[0] != 0.0f) {
+        const float c[8] = {0.0f, 0.0f, (float)cols, 0.0f, 0.0f, (float)rows, (float)cols, (float)rows};
+        float u[8];
+        oo_undistort_points(K4, dist, ndist, c, u, 4);
+        *minX = fminf(u[0], u[4]);
+        *maxX = fmaxf(u[2], u[6]);
+        *minY = fminf(u[1], u[3]);
+        *maxY = fmaxf(u[5], u[7]);
+    } else {
+        *minX = 0.0f;
+        *maxX = (float)cols;
+        *minY = 0.0f;
+        *maxY = (float)rows;
+    }
+    *invW = (float)OO_GRID_COLS / (*maxX - *minX);
+    *invH = (float)OO_GRID_ROWS / (*maxY - *minY);
+}

@@ -160,6 +160,16 @@ int oo_search_by_projection_last(const oo_frame* F, const oo_camera* cur, const 
                                  const oo_last_frame* LF, float th, int bMono, int checkOri, int* owner,
                                  int* owner_obs);
 
+/* cv::undistortPoints(src, dst, K, D, noArray(), K) (OpenCV 3.4, 5 iterations) on n points (x, y interleaved);
+ * K4 = fx, fy, cx, cy; dist = k1, k2, p1, p2[, k3] (ndist 4 or 5). */
+void oo_undistort_points(const float* K4, const float* dist, int ndist, const float* xy, float* out, int n);
+/* Frame::UndistortKeyPoints (src/Frame.cc:404-434): copies when k1 == 0. */
+void oo_undistort_keypoints(const float* K4, const float* dist, int ndist, const oo_keypoint* in, oo_keypoint* out,
+                            int n);
+/* Frame::ComputeImageBounds (src/Frame.cc:436-461) and mfGridElementWidthInv/HeightInv. */
+void oo_compute_image_bounds(const float* K4, const float* dist, int ndist, int cols, int rows, float* minX,
+                             float* maxX, float* minY, float* maxY, float* invW, float* invH);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,7 +27,8 @@ EXPORTS = [
     "orbgpu_memset_d", "orbgpu_prev_matched_from_frame", "orbgpu_memcpy_d2d_async",
     "orbgpu_batch_candidate_total", "orbgpu_compute_stereo_matches", "orbgpu_compute_stereo_matches_batch",
     "orbgpu_is_in_frustum", "orbgpu_search_by_projection_last_frame", "orbgpu_debug_octree_profile",
-    "orbgpu_stage_marks",
+    "orbgpu_stage_marks", "orbgpu_undistort_keypoints", "orbgpu_compute_image_bounds", "orbgpu_set_undistortion",
+    "orbgpu_batch_outputs_undistorted",
 ]
 
 OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
@@ -118,6 +119,10 @@ def _declare(L):
     L.orbgpu_memcpy_d2d_async.argtypes = [vp, vp, vp, sz]
     L.orbgpu_batch_candidate_total.restype = C.c_longlong
     L.orbgpu_debug_octree_profile.argtypes = [vp, vp, i32]
+    L.orbgpu_undistort_keypoints.argtypes = [vp, vp, vp, i32, vp, vp, i32]
+    L.orbgpu_compute_image_bounds.argtypes = [vp, vp, vp, i32, i32, i32, C.POINTER(GridGeom)]
+    L.orbgpu_set_undistortion.argtypes = [vp, vp, vp, i32]
+    L.orbgpu_batch_outputs_undistorted.argtypes = [vp, C.POINTER(vp), C.POINTER(GridGeom)]
     L.orbgpu_stage_marks.argtypes = [vp, vp, C.POINTER(C.c_char_p), C.POINTER(f32), i32]
     L.orbgpu_compute_stereo_matches.argtypes = [vp, vp, f32, f32, vp, vp, i32, C.POINTER(i32), C.POINTER(i32)]
     L.orbgpu_compute_stereo_matches_batch.argtypes = [vp, vp, f32, f32, vp, vp, vp]

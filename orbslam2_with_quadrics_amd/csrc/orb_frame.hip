@@ -1,0 +1,63 @@
+// orb_frame.hip -- gfx950 kernels of the Frame post-processing on the feature path:
+//   og_undistort_kernel : Frame::UndistortKeyPoints (src/Frame.cc:404-434) = cv::undistortPoints(src, dst, K,
+//                         D, noArray(), K) of OpenCV 3.4 with its default TermCriteria(COUNT, 5, 0.01): five
+//                         fixed-point iterations in double, R = I, P = K.  One thread per keypoint; the same
+//                         double operation order as OpenCV's scalar loop (no contraction: -ffp-contract=off).
+// Also used on the 4 image corners for Frame::ComputeImageBounds (src/Frame.cc:436-461).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "orbgpu_internal.h"
+#include "orbgpu_launch.h"
+
+__device__ __forceinline__ void og_undistort_pt(const OgUndistort& U, float px, float py, float& ox, float& oy)
+{
+    const double fx = U.K[0], fy = U.K[1], cx = U.K[2], cy = U.K[3];
+    const double k0 = U.d[0], k1 = U.d[1], k2 = U.d[2], k3 = U.d[3], k4 = U.d[4];
+    const double ifx = 1. / fx, ify = 1. / fy;
+    double x = ((double)px - cx) * ifx;
+    double y = ((double)py - cy) * ify;
+    const double x0 = x, y0 = y;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const double r2 = x * x + y * y;
+        const double icdist = 1. / (1 + ((k4 * r2 + k1) * r2 + k0) * r2);
+        const double deltaX = 2 * k2 * x * y + k3 * (r2 + 2 * x * x);
+        const double deltaY = k2 * (r2 + 2 * y * y) + 2 * k3 * x * y;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    ox = (float)(fx * x + cx);
+    oy = (float)(fy * y + cy);
+}
+
+__global__ __launch_bounds__(256) void og_undistort_kernel(const orbgpu_kp_dev* __restrict__ in,
+                                                           orbgpu_kp_dev* __restrict__ out, const int* counts,
+                                                           int n_fixed, int frame_cap, OgUndistort U)
+{
+    const int b = blockIdx.y;
+    const int n = counts ? counts[b] : n_fixed;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        orbgpu_kp_dev kp = in[(long long)b * frame_cap + i];
+        og_undistort_pt(U, kp.x, kp.y, kp.x, kp.y);
+        out[(long long)b * frame_cap + i] = kp;
+    }
+}
+
+__global__ void og_undistort_points_kernel(const float* __restrict__ xy, float* __restrict__ out, int n, OgUndistort U)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) og_undistort_pt(U, xy[2 * i], xy[2 * i + 1], out[2 * i], out[2 * i + 1]);
+}
+
+void og_launch_undistort(hipStream_t s, const orbgpu_kp_dev* in, orbgpu_kp_dev* out, const int* counts, int n_fixed,
+                         int frame_cap, const OgUndistort& U, int B)
+{
+    const int gx = counts ? (frame_cap + 255) / 256 : (n_fixed + 255) / 256;
+    if (gx > 0) hipLaunchKernelGGL(og_undistort_kernel, dim3(gx, B), dim3(256), 0, s, in, out, counts, n_fixed, frame_cap, U);
+}
+
+void og_launch_undistort_points(hipStream_t s, const float* xy, float* out, int n, const OgUndistort& U)
+{
+    if (n > 0) hipLaunchKernelGGL(og_undistort_points_kernel, dim3((n + 63) / 64), dim3(64), 0, s, xy, out, n, U);
+}

@@ -84,6 +84,12 @@ struct orbgpu_ctx {
     DevBuf<uint32_t> mlists;  // SearchForInitialization candidate lists {dist:16|i2:16}
     DevBuf<int> mlist_n;
     DevBuf<uint8_t> mcands;   // projection-matcher candidate lists (grown on demand, kept)
+    // Frame::UndistortKeyPoints on the device (set by orbgpu_set_undistortion): batches then also hold
+    // mvKeysUn, and the grid and the matchers use it with the undistorted image bounds
+    bool undist = false;
+    OgUndistort und{};
+    DevBuf<orbgpu_kp_dev> kps_un;
+    DevBuf<float> und_pts;
     // stereo scratch (Frame::ComputeStereoMatches)
     DevBuf<int> st_row_start, st_row_items, st_sad, st_nm;
     DevBuf<float> st_out;
@@ -120,6 +126,33 @@ static void release(DevBuf<T>& b)
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.n = 0;
+}
+
+// Frame::ComputeImageBounds (src/Frame.cc:436-461) + mfGridElementWidthInv/HeightInv (:103-104): the
+// undistorted corners (on the device, same kernel as the keypoints) or the plain image rectangle
+static int image_bounds(orbgpu_ctx* c, bool undist, const OgUndistort& U, int cols, int rows, OgGridGeom* G)
+{
+    if (!undist) {
+        orbgpu_grid_geom g;
+        orbgpu_grid_geom_for_image(cols, rows, &g);
+        *G = OgGridGeom{g.minX, g.minY, g.maxX, g.maxY, g.invW, g.invH};
+        return ORBGPU_OK;
+    }
+    const float corners[8] = {0.0f, 0.0f, (float)cols, 0.0f, 0.0f, (float)rows, (float)cols, (float)rows};
+    float u[8];
+    HIP_TRY(c, ensure(c->und_pts, 16));
+    HIP_TRY(c, hipMemcpyAsync(c->und_pts.p, corners, sizeof(corners), hipMemcpyHostToDevice, c->stream));
+    og_launch_undistort_points(c->stream, c->und_pts.p, c->und_pts.p + 8, 4, U);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipMemcpyAsync(u, c->und_pts.p + 8, sizeof(u), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    G->minX = std::min(u[0], u[4]);
+    G->maxX = std::max(u[2], u[6]);
+    G->minY = std::min(u[1], u[3]);
+    G->maxY = std::max(u[5], u[7]);
+    G->invW = (float)OG_GRID_COLS / (G->maxX - G->minX);
+    G->invH = (float)OG_GRID_ROWS / (G->maxY - G->minY);
+    return ORBGPU_OK;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -269,10 +302,7 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
     c->H = H;
     c->planned = true;
     c->Bcap = 0;  // batch buffers must be re-sized for the new plan
-    orbgpu_grid_geom g;
-    orbgpu_grid_geom_for_image(W, H, &g);
-    c->grid_geom = OgGridGeom{g.minX, g.minY, g.maxX, g.maxY, g.invW, g.invH};
-    return ORBGPU_OK;
+    return image_bounds(c, c->undist, c->und, W, H, &c->grid_geom);
 }
 
 static int ensure_batch(orbgpu_ctx* c, int B)
@@ -288,6 +318,7 @@ static int ensure_batch(orbgpu_ctx* c, int B)
     HIP_TRY(c, ensure(c->oct_resp, Bn * (size_t)P.kcap_total));
     HIP_TRY(c, ensure(c->oct_count, Bn * (size_t)P.nlevels));
     HIP_TRY(c, ensure(c->kps, Bn * (size_t)P.frame_cap));
+    HIP_TRY(c, ensure(c->kps_un, Bn * (size_t)P.frame_cap));
     HIP_TRY(c, ensure(c->desc, Bn * (size_t)P.frame_cap * 32));
     HIP_TRY(c, ensure(c->counts, Bn));
     HIP_TRY(c, ensure(c->cell_start, Bn * (OG_GRID_CELLS + 1)));
@@ -316,6 +347,9 @@ static void timer_mark(orbgpu_ctx* c, const char* name)
     t.names.push_back(name);
 }
 
+// the keypoints the Frame-level code reads (mvKeysUn): undistorted when the context has a distortion model
+static const orbgpu_kp_dev* kps_match(const orbgpu_ctx* c) { return c->undist ? c->kps_un.p : c->kps.p; }
+
 static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitch, long long fstride)
 {
     const OgPlan& P = c->plan;
@@ -343,7 +377,8 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
     og_launch_describe(s, P, d_imgs, pitch, fstride, c->pyr.p, c->oct_xy.p, c->oct_resp.p, c->oct_count.p, c->kps.p,
                        c->desc.p, c->counts.p, B);
     timer_mark(c, "describe");
-    og_launch_grid(s, c->kps.p, c->counts.p, P.frame_cap, c->grid_geom, c->cell_start.p, c->cell_items.p, B);
+    if (c->undist) og_launch_undistort(s, c->kps.p, c->kps_un.p, c->counts.p, 0, P.frame_cap, c->und, B);
+    og_launch_grid(s, kps_match(c), c->counts.p, P.frame_cap, c->grid_geom, c->cell_start.p, c->cell_items.p, B);
     timer_mark(c, "grid");
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(c->done, s));
@@ -471,6 +506,8 @@ void orbgpu_destroy(orbgpu_ctx* c)
     release(c->mlists);
     release(c->mlist_n);
     release(c->mcands);
+    release(c->kps_un);
+    release(c->und_pts);
     release(c->st_row_start);
     release(c->st_row_items);
     release(c->st_sad);
@@ -702,10 +739,11 @@ int orbgpu_search_for_initialization_batch(orbgpu_ctx* cref, int ref, orbgpu_ctx
     const OgGridGeom G{grid.minX, grid.minY, grid.maxX, grid.maxY, grid.invW, grid.invH};
     if (std::memcmp(&G, &c->grid_geom, sizeof(G)) != 0) {
         c->grid_geom = G;
-        og_launch_grid(s, c->kps.p, c->counts.p, c->plan.frame_cap, G, c->cell_start.p, c->cell_items.p, c->last_B);
+        og_launch_grid(s, kps_match(c), c->counts.p, c->plan.frame_cap, G, c->cell_start.p, c->cell_items.p,
+                       c->last_B);
     }
-    OgFrameDev f1{cref->kps.p, cref->desc.p, cref->counts.p, nullptr, nullptr, nullptr, cref->plan.frame_cap};
-    OgFrameDev f2{c->kps.p, c->desc.p, c->counts.p, c->cell_start.p, c->cell_items.p, nullptr, c->plan.frame_cap};
+    OgFrameDev f1{kps_match(cref), cref->desc.p, cref->counts.p, nullptr, nullptr, nullptr, cref->plan.frame_cap};
+    OgFrameDev f2{kps_match(c), c->desc.p, c->counts.p, c->cell_start.p, c->cell_items.p, nullptr, c->plan.frame_cap};
     const int list_cap = c->plan.lv[0].kcap;  // F2 has at most kcap_0 octave-0 keypoints
     const size_t cap1 = (size_t)cref->plan.frame_cap;
     if (og_init_resolve_lds((int)cap1, c->plan.frame_cap, list_cap) > OG_INIT_LDS_MAX) {
@@ -728,9 +766,88 @@ int orbgpu_prev_matched_from_frame(orbgpu_ctx* cref, int ref, orbgpu_ctx* c, flo
     if (!cref || !c || !cref->last_B || !c->last_B || ref < 0 || ref >= cref->last_B || !d_prev_xy) return ORBGPU_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     if (cref != c) HIP_TRY(c, hipStreamWaitEvent(c->stream, cref->done, 0));
-    OgFrameDev f1{cref->kps.p, cref->desc.p, cref->counts.p, nullptr, nullptr, nullptr, cref->plan.frame_cap};
+    OgFrameDev f1{kps_match(cref), cref->desc.p, cref->counts.p, nullptr, nullptr, nullptr, cref->plan.frame_cap};
     og_launch_prev_from_frame(c->stream, f1, ref, d_prev_xy, 2 * cref->plan.frame_cap, c->last_B);
     HIP_TRY(c, hipGetLastError());
+    return ORBGPU_OK;
+}
+
+// ---- Frame::UndistortKeyPoints / ComputeImageBounds (src/Frame.cc:404-461) ------------------------------
+static int parse_undistort(const float* K4, const float* dist, int ndist, OgUndistort* U, bool* active)
+{
+    if (!K4 || ndist < 0 || ndist > 5 || (ndist > 0 && !dist)) return ORBGPU_ERR_ARG;
+    *U = OgUndistort{};
+    for (int i = 0; i < 4; i++) U->K[i] = K4[i];
+    for (int i = 0; i < ndist; i++) U->d[i] = dist[i];
+    *active = ndist >= 1 && dist[0] != 0.0f;  // mDistCoef.at<float>(0)==0.0 -> mvKeysUn = mvKeys
+    return ORBGPU_OK;
+}
+
+int orbgpu_set_undistortion(orbgpu_ctx* c, const float* K4, const float* dist, int ndist)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    OgUndistort U;
+    bool active = false;
+    int r = parse_undistort(K4, dist, ndist, &U, &active);
+    if (r) return r;
+    HIP_TRY(c, hipSetDevice(c->device));
+    c->undist = active;
+    c->und = U;
+    if (c->planned) return image_bounds(c, c->undist, c->und, c->W, c->H, &c->grid_geom);
+    return ORBGPU_OK;
+}
+
+int orbgpu_undistort_keypoints(orbgpu_ctx* c, const float* K4, const float* dist, int ndist,
+                               const orbgpu_keypoint* in, orbgpu_keypoint* out, int n)
+{
+    if (!c || n < 0 || (n && (!in || !out))) return ORBGPU_ERR_ARG;
+    OgUndistort U;
+    bool active = false;
+    int r = parse_undistort(K4, dist, ndist, &U, &active);
+    if (r) return r;
+    if (n == 0) return ORBGPU_OK;
+    if (!active) {
+        if (out != in) std::memcpy(out, in, (size_t)n * sizeof(orbgpu_keypoint));
+        return ORBGPU_OK;
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, ensure(c->mscratch, kCarvePad + (size_t)n * 56));
+    uint8_t* cur = c->mscratch.p;
+    orbgpu_kp_dev* din = (orbgpu_kp_dev*)scratch_carve(cur, (size_t)n * 28);
+    orbgpu_kp_dev* dout = (orbgpu_kp_dev*)scratch_carve(cur, (size_t)n * 28);
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(din, in, (size_t)n * 28, hipMemcpyHostToDevice, s));
+    og_launch_undistort(s, din, dout, nullptr, n, n, U, 1);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipMemcpyAsync(out, dout, (size_t)n * 28, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    return ORBGPU_OK;
+}
+
+int orbgpu_compute_image_bounds(orbgpu_ctx* c, const float* K4, const float* dist, int ndist, int cols, int rows,
+                                orbgpu_grid_geom* g)
+{
+    if (!c || !g || cols <= 0 || rows <= 0) return ORBGPU_ERR_ARG;
+    OgUndistort U;
+    bool active = false;
+    int r = parse_undistort(K4, dist, ndist, &U, &active);
+    if (r) return r;
+    HIP_TRY(c, hipSetDevice(c->device));
+    OgGridGeom G;
+    r = image_bounds(c, active, U, cols, rows, &G);
+    if (r) return r;
+    *g = orbgpu_grid_geom{G.minX, G.minY, G.maxX, G.maxY, G.invW, G.invH};
+    return ORBGPU_OK;
+}
+
+int orbgpu_batch_outputs_undistorted(orbgpu_ctx* c, orbgpu_keypoint** d_kps_un, orbgpu_grid_geom* bounds)
+{
+    if (!c || !c->planned || !c->last_B) return ORBGPU_ERR_ARG;
+    if (d_kps_un) *d_kps_un = (orbgpu_keypoint*)kps_match(c);
+    if (bounds) {
+        const OgGridGeom& G = c->grid_geom;
+        *bounds = orbgpu_grid_geom{G.minX, G.minY, G.maxX, G.maxY, G.invW, G.invH};
+    }
     return ORBGPU_OK;
 }
 

@@ -145,3 +145,13 @@ void og_launch_last_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float
 void og_launch_last_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
                             OgLastFrameDev LF, float th, int mode, int checkOri, const int* off, OgLastCand* cands,
                             int* ent, int* owner, int* owner_obs, int* nmatches);
+
+// Frame post-processing (orb_frame.hip): cv::undistortPoints of Frame::UndistortKeyPoints
+struct OgUndistort {
+    float K[4];  // fx, fy, cx, cy (mK)
+    float d[5];  // k1, k2, p1, p2, k3 (mDistCoef, k3 = 0 when absent)
+};
+// counts == nullptr: n_fixed keypoints in one frame
+void og_launch_undistort(hipStream_t s, const orbgpu_kp_dev* in, orbgpu_kp_dev* out, const int* counts, int n_fixed,
+                         int frame_cap, const OgUndistort& U, int B);
+void og_launch_undistort_points(hipStream_t s, const float* xy, float* out, int n, const OgUndistort& U);

@@ -124,6 +124,21 @@ class ORBextractor:
                                                             C.byref(cap)), "orbgpu_batch_outputs")
         return kp.value, de.value, cn.value, cap.value
 
+    def set_undistortion(self, K4, dist):
+        """Device-resident Frame::UndistortKeyPoints for the coming batches (mvKeysUn + undistorted grid)."""
+        K4 = np.ascontiguousarray(K4, np.float32)
+        dist = np.ascontiguousarray(dist, np.float32)
+        _lib.check(self._ctx, self._L.orbgpu_set_undistortion(self._ctx, _p(K4), _p(dist) if dist.size else None,
+                                                                int(dist.size)), "orbgpu_set_undistortion")
+
+    def batch_outputs_undistorted(self):
+        """(device pointer of mvKeysUn, GridGeom bounds) of the last batch."""
+        kp = C.c_void_p()
+        g = _lib.GridGeom()
+        _lib.check(self._ctx, self._L.orbgpu_batch_outputs_undistorted(self._ctx, C.byref(kp), C.byref(g)),
+                   "orbgpu_batch_outputs_undistorted")
+        return kp.value, g
+
     def batch_download(self, b: int):
         cap = self._L.orbgpu_max_keypoints(self._ctx)
         kps = np.zeros(max(cap, 1), KP_DTYPE)

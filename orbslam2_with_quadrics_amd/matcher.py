@@ -20,21 +20,28 @@ class Frame:
     """The subset of ORB_SLAM2::Frame the hot path produces and the matchers consume: mvKeysUn (no
     distortion -> == mvKeys), mDescriptors, mvuRight, mvScaleFactors and the image bounds/grid scales."""
 
-    def __init__(self, keypoints, descriptors, cols: int, rows: int, scale_factors, uright=None):
-        self.mvKeysUn = np.ascontiguousarray(keypoints, dtype=KP_DTYPE)
-        self.mvKeys = self.mvKeysUn
+    def __init__(self, keypoints, descriptors, cols: int, rows: int, scale_factors, uright=None, keys_un=None,
+                 grid=None):
+        self.mvKeys = np.ascontiguousarray(keypoints, dtype=KP_DTYPE)
+        self.mvKeysUn = self.mvKeys if keys_un is None else np.ascontiguousarray(keys_un, dtype=KP_DTYPE)
         self.mDescriptors = np.ascontiguousarray(descriptors, dtype=np.uint8)
         self.mvScaleFactors = np.ascontiguousarray(scale_factors, dtype=np.float32)
         self.N = len(self.mvKeysUn)
         self.mvuRight = None if uright is None else np.ascontiguousarray(uright, np.float32)
-        g = _lib.GridGeom()
-        _lib.check(None, _lib.lib().orbgpu_grid_geom_for_image(cols, rows, C.byref(g)), "grid_geom")
-        self.grid = g
+        if grid is None:  # no distortion: the image rectangle (Frame::ComputeImageBounds, k1 == 0)
+            grid = _lib.GridGeom()
+            _lib.check(None, _lib.lib().orbgpu_grid_geom_for_image(cols, rows, C.byref(grid)), "grid_geom")
+        self.grid = grid
 
     @classmethod
-    def from_image(cls, extractor: ORBextractor, image: np.ndarray):
+    def from_image(cls, extractor: ORBextractor, image: np.ndarray, K4=None, dist=None):
+        """Monocular Frame constructor (src/Frame.cc:161-210): extract, UndistortKeyPoints, image bounds."""
         k, d = extractor(image)
-        return cls(k, d, image.shape[1], image.shape[0], extractor.GetScaleFactors())
+        if K4 is None or dist is None:
+            return cls(k, d, image.shape[1], image.shape[0], extractor.GetScaleFactors())
+        ku = UndistortKeyPoints(extractor, K4, dist, k)
+        g = ComputeImageBounds(extractor, K4, dist, image.shape[1], image.shape[0])
+        return cls(k, d, image.shape[1], image.shape[0], extractor.GetScaleFactors(), keys_un=ku, grid=g)
 
     @classmethod
     def from_stereo(cls, ex_left: ORBextractor, ex_right: ORBextractor, im_left: np.ndarray,
@@ -202,3 +209,27 @@ def camera_struct(cam: dict) -> _lib.Camera:
     c.nlevels = int(cam["nlevels"])
     return c
 
+
+
+def UndistortKeyPoints(extractor: ORBextractor, K4, dist, keypoints):
+    """Frame::UndistortKeyPoints (src/Frame.cc:404-434) on the GPU -> mvKeysUn."""
+    K4 = np.ascontiguousarray(K4, np.float32)
+    dist = np.ascontiguousarray(dist, np.float32)
+    kin = np.ascontiguousarray(keypoints, KP_DTYPE)
+    out = np.empty_like(kin)
+    n = len(kin)
+    rc = _lib.lib().orbgpu_undistort_keypoints(extractor.ctx, _p(K4), _p(dist) if dist.size else None, int(dist.size),
+                                               _p(kin) if n else None, _p(out) if n else None, n)
+    _lib.check(extractor.ctx, rc, "orbgpu_undistort_keypoints")
+    return out
+
+
+def ComputeImageBounds(extractor: ORBextractor, K4, dist, cols: int, rows: int) -> _lib.GridGeom:
+    """Frame::ComputeImageBounds (src/Frame.cc:436-461) + grid scales, on the GPU."""
+    K4 = np.ascontiguousarray(K4, np.float32)
+    dist = np.ascontiguousarray(dist, np.float32)
+    g = _lib.GridGeom()
+    rc = _lib.lib().orbgpu_compute_image_bounds(extractor.ctx, _p(K4), _p(dist) if dist.size else None,
+                                                int(dist.size), cols, rows, C.byref(g))
+    _lib.check(extractor.ctx, rc, "orbgpu_compute_image_bounds")
+    return g

@@ -605,3 +605,26 @@ def search_by_projection_last(F, cur, last, lf, th, mono, check_ori, owner=None,
                 owner_obs[k] = 0
                 nm -= 1
     return nm, owner, owner_obs
+
+
+# ---------------------------------------------------------------------------------------------
+# Frame::UndistortKeyPoints / ComputeImageBounds via cv::undistortPoints (OpenCV 3.4, 5 iterations)
+# ---------------------------------------------------------------------------------------------
+def undistort_point(K4, dist, px, py):
+    k = [float(F32(v)) for v in dist] + [0.0] * (5 - len(dist))
+    fx, fy, cx, cy = (float(F32(v)) for v in K4)
+    ifx, ify = 1.0 / fx, 1.0 / fy
+    x = (float(F32(px)) - cx) * ifx
+    y = (float(F32(py)) - cy) * ify
+    x0, y0 = x, y
+    for _ in range(5):
+        r2 = x * x + y * y
+        icdist = (1 + ((0.0 * r2 + 0.0) * r2 + 0.0) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2)
+        dx = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + 0.0 * r2 + 0.0 * r2 * r2
+        dy = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + 0.0 * r2 + 0.0 * r2 * r2
+        x = (x0 - dx) * icdist
+        y = (y0 - dy) * icdist
+    xx = fx * x + 0.0 * y + cx
+    yy = 0.0 * x + fy * y + cy
+    ww = 1.0 / (0.0 * x + 0.0 * y + 1.0)
+    return F32(xx * ww), F32(yy * ww)

@@ -1,0 +1,99 @@
+"""GPU parity tests of the Frame post-processing rows: Frame::UndistortKeyPoints and
+Frame::ComputeImageBounds (src/Frame.cc:404-461) through the C ABI vs the CPU oracle, and the
+device-resident form (mvKeysUn + undistorted grid inside a batch) feeding the batched
+SearchForInitialization, against the oracle chain extract -> undistort -> grid -> match."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from orbslam2_with_quadrics_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+
+TUM1 = dict(K4=[517.306408, 516.469215, 318.643040, 255.313989],
+            dist=[0.262383, -0.953104, -0.005358, 0.002628, 1.163314])
+TUM2 = dict(K4=[520.908620, 521.007327, 325.141442, 249.701764],
+            dist=[0.231222, -0.784899, -0.003257, -0.000105, 0.917205])
+TUM3 = dict(K4=[535.4, 539.2, 320.1, 247.6], dist=[0.0, 0.0, 0.0, 0.0])
+
+
+@pytest.mark.parametrize("cam", [TUM1, TUM2, dict(TUM1, dist=TUM1["dist"][:4]), TUM3])
+def test_undistort_keypoints_vs_oracle(gpu, oracle, cam):
+    ex = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    k, _ = ex(synthetic.frame(11, 480, 640))
+    rng = np.random.default_rng(1)
+    extra = np.zeros(500, gpu.KP_DTYPE)  # border and outside points too
+    extra["x"] = rng.uniform(-20, 660, 500).astype(np.float32)
+    extra["y"] = rng.uniform(-20, 500, 500).astype(np.float32)
+    kps = np.concatenate([k, extra])
+    got = gpu.UndistortKeyPoints(ex, cam["K4"], cam["dist"], kps)
+    want = oracle.undistort_keypoints(cam["K4"], cam["dist"], kps)
+    assert got.tobytes() == want.tobytes()
+    g = gpu.ComputeImageBounds(ex, cam["K4"], cam["dist"], 640, 480)
+    wb = oracle.compute_image_bounds(cam["K4"], cam["dist"], 640, 480)
+    assert (g.minX, g.maxX, g.minY, g.maxY, g.invW, g.invH) == wb
+
+
+def test_batch_undistortion_feeds_search_for_initialization(gpu, oracle):
+    from orbslam2_with_quadrics_amd import _lib
+
+    rows, cols, B = 480, 640, 6
+    pairs = [synthetic.frame_pair(120 + b, rows, cols, (5, 3)) for b in range(B)]
+    f1 = pairs[0][0]
+    frames = np.stack([p[1] for p in pairs])
+    ex_ref = gpu.ORBextractor(2000, 1.2, 8, 20, 7)  # the init extractor uses 2x features (src/Tracking.cc:125)
+    ex = gpu.ORBextractor(2000, 1.2, 8, 20, 7)
+    for e in (ex_ref, ex):
+        e.set_undistortion(TUM1["K4"], TUM1["dist"])
+    d1 = ex_ref.device_alloc(f1.nbytes)
+    dB = ex.device_alloc(frames.nbytes)
+    try:
+        ex_ref.h2d(d1, f1)
+        ex.h2d(dB, frames)
+        ex_ref.extract_batch_device(d1, 1, cols, rows, cols, f1.nbytes)
+        ex.extract_batch_device(dB, B, cols, rows, cols, rows * cols)
+        _, _, d_counts, cap = ex.batch_outputs()
+        d_prev = ex.device_alloc(B * cap * 8)
+        d_m12 = ex.device_alloc(B * cap * 4)
+        d_nm = ex.device_alloc(B * 4)
+        L = _lib.lib()
+        _lib.check(ex.ctx, L.orbgpu_prev_matched_from_frame(ex_ref.ctx, 0, ex.ctx, C.c_void_p(d_prev)), "prev")
+        _, bounds = ex.batch_outputs_undistorted()
+        _lib.check(ex.ctx, L.orbgpu_search_for_initialization_batch(ex_ref.ctx, 0, ex.ctx, bounds, 0.9, 1, 100,
+                                                                      C.c_void_p(d_prev), C.c_void_p(d_m12),
+                                                                      C.c_void_p(d_nm)), "search_init")
+        ex.synchronize()
+        d_un, _ = ex.batch_outputs_undistorted()
+        nm = np.zeros(B, np.int32)
+        m12 = np.zeros((B, cap), np.int32)
+        kun = np.zeros((B, cap), gpu.KP_DTYPE)
+        cnt = np.zeros(B, np.int32)
+        ex.d2h(nm, d_nm)
+        ex.d2h(m12, d_m12)
+        ex.d2h(kun, d_un)
+        ex.d2h(cnt, d_counts)
+        # oracle chain
+        oe = oracle.OracleExtractor(2000, 1.2, 8, 20, 7)
+        k1, dd1 = oe(f1)
+        k1u = oracle.undistort_keypoints(TUM1["K4"], TUM1["dist"], k1)
+        wb = oracle.compute_image_bounds(TUM1["K4"], TUM1["dist"], cols, rows)
+        assert (bounds.minX, bounds.maxX, bounds.minY, bounds.maxY, bounds.invW, bounds.invH) == wb
+        sf = oe.tables()["scale"]
+        F1 = oracle.OracleFrame(k1u, dd1, cols, rows, sf, bounds=wb)
+        total = 0
+        for b in range(B):
+            k2, dd2 = oe(frames[b])
+            k2u = oracle.undistort_keypoints(TUM1["K4"], TUM1["dist"], k2)
+            assert cnt[b] == len(k2) and kun[b, :cnt[b]].tobytes() == k2u.tobytes()
+            F2 = oracle.OracleFrame(k2u, dd2, cols, rows, sf, bounds=wb)
+            prev = np.stack([k1u["x"], k1u["y"]], 1).astype(np.float32)
+            n, mo, _ = oracle.search_for_initialization(F1, F2, prev, 0.9, True, 100)
+            assert nm[b] == n and np.array_equal(m12[b, :len(k1)], mo)
+            total += n
+        assert total > 50
+        for p in (d_prev, d_m12, d_nm):
+            ex.device_free(p)
+    finally:
+        ex_ref.device_free(d1)
+        ex.device_free(dB)

@@ -218,3 +218,48 @@ def test_search_by_projection_last_python_restatement(oracle, seed, mono):
         wn, wow, wob = refpy.search_by_projection_last(Fp, cur, last, lf, th, mono, ori, owner0, obs0)
         assert n == wn and n > 20
         assert ow.tolist() == wow and ob.tolist() == wob
+
+
+TUM1 = dict(K4=[517.306408, 516.469215, 318.643040, 255.313989],
+            dist=[0.262383, -0.953104, -0.005358, 0.002628, 1.163314])  # Examples/Monocular/TUM1.yaml
+TUM2 = dict(K4=[520.908620, 521.007327, 325.141442, 249.701764],
+            dist=[0.231222, -0.784899, -0.003257, -0.000105, 0.917205])
+
+
+@pytest.mark.parametrize("cam", [TUM1, TUM2, dict(TUM1, dist=TUM1["dist"][:4])])
+def test_undistort_python_restatement(oracle, cam):
+    rng = np.random.default_rng(3)
+    from orbslam2_with_quadrics_amd.extractor import KP_DTYPE
+
+    kps = np.zeros(4000, KP_DTYPE)
+    kps["x"] = rng.uniform(-5, 645, 4000).astype(np.float32)
+    kps["y"] = rng.uniform(-5, 485, 4000).astype(np.float32)
+    kps["octave"] = rng.integers(0, 8, 4000)
+    kps["angle"] = rng.uniform(0, 360, 4000).astype(np.float32)
+    out = oracle.undistort_keypoints(cam["K4"], cam["dist"], kps)
+    for i in range(0, 4000, 7):
+        wx, wy = refpy.undistort_point(cam["K4"], cam["dist"], kps["x"][i], kps["y"][i])
+        assert out["x"][i] == wx and out["y"][i] == wy, i
+    assert np.array_equal(out["octave"], kps["octave"]) and np.array_equal(out["angle"], kps["angle"])
+    moved = np.abs(out["x"] - kps["x"]) + np.abs(out["y"] - kps["y"])
+    assert moved.max() > 1.0  # TUM distortion moves border points by pixels
+
+
+def test_undistort_k1_zero_is_copy(oracle):
+    from orbslam2_with_quadrics_amd.extractor import KP_DTYPE
+
+    kps = np.zeros(10, KP_DTYPE)
+    kps["x"] = np.arange(10, dtype=np.float32) * 50
+    kps["y"] = 100
+    out = oracle.undistort_keypoints(TUM1["K4"], [0.0, -0.9, 0.01, 0.01], kps)  # k1 == 0: mvKeysUn = mvKeys
+    assert out.tobytes() == kps.tobytes()
+    b = oracle.compute_image_bounds(TUM1["K4"], [0.0, 0.1, 0, 0], 640, 480)
+    assert b[:4] == (0.0, 640.0, 0.0, 480.0)
+
+
+def test_image_bounds_python_restatement(oracle):
+    b = oracle.compute_image_bounds(TUM1["K4"], TUM1["dist"], 640, 480)
+    c = [refpy.undistort_point(TUM1["K4"], TUM1["dist"], x, y) for x, y in ((0, 0), (640, 0), (0, 480), (640, 480))]
+    want = (min(c[0][0], c[2][0]), max(c[1][0], c[3][0]), min(c[0][1], c[1][1]), max(c[2][1], c[3][1]))
+    assert b[:4] == tuple(float(v) for v in want)
+    assert b[4] == float(np.float32(64) / np.float32(np.float32(b[1]) - np.float32(b[0])))
