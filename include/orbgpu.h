@@ -239,6 +239,27 @@ int orbgpu_search_by_projection_last_frame(orbgpu_ctx* ctx, const orbgpu_frame_v
                                            const orbgpu_last_frame_view* LF, float th, int bMono, int checkOri,
                                            int32_t* owner, int32_t* owner_obs, int* nmatches);
 
+/* KeyFrame snapshot for the relocalisation / loop matcher. */
+typedef struct {
+    int n;                         /* pKF->GetMapPointMatches().size() */
+    const orbgpu_keypoint* kps;    /* pKF->mvKeysUn (angle) */
+    const uint8_t* valid;          /* pMP && !pMP->isBad() && !sAlreadyFound.count(pMP) */
+    const float* pos;              /* n x 3: GetWorldPos() */
+    const float* max_dist;         /* mfMaxDistance */
+    const float* min_dist;         /* mfMinDistance */
+    const uint8_t* desc;           /* n x 32: GetDescriptor() */
+} orbgpu_keyframe_view;
+
+/* Replaces int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>&
+ * sAlreadyFound, const float th, const int ORBdist) -- src/ORBmatcher.cc:1472-1599, include/ORBmatcher.h:59;
+ * called from Tracking::Relocalization (src/Tracking.cc:1433,1467).  owner (F.n ints, in/out) =
+ * CurrentFrame.mvpMapPoints as keyframe indices (-1 == NULL, values >= KF.n = other claims; any claim
+ * blocks the keypoint).  `cur` gives the current pose (Tcw) and intrinsics; cur->Ow is not read (the
+ * matcher recomputes Ow = -Rcw^T tcw, :1478). */
+int orbgpu_search_by_projection_keyframe(orbgpu_ctx* ctx, const orbgpu_frame_view* F, const orbgpu_camera* cur,
+                                         const orbgpu_keyframe_view* KF, float th, int ORBdist, int checkOri,
+                                         int32_t* owner, int* nmatches);
+
 /* ---- stereo ------------------------------------------------------------------------------------- */
 
 /* Replaces void Frame::ComputeStereoMatches() -- src/Frame.cc:466-640, called from the stereo Frame

@@ -68,6 +68,8 @@ def lib():
         L.oo_search_by_projection.argtypes = [vp, vp, f32, f32, vp, vp]
         L.oo_is_in_frustum.restype = i32
         L.oo_is_in_frustum.argtypes = [vp, vp, f32, vp, vp, vp, vp, vp, vp]
+        L.oo_search_by_projection_kf.restype = i32
+        L.oo_search_by_projection_kf.argtypes = [vp, vp, vp, f32, i32, i32, vp]
         L.oo_undistort_points.argtypes = [vp, vp, i32, vp, vp, i32]
         L.oo_undistort_keypoints.argtypes = [vp, vp, i32, vp, vp, i32]
         L.oo_compute_image_bounds.argtypes = [vp, vp, i32, i32, i32] + [C.POINTER(f32)] * 6
@@ -286,6 +288,31 @@ def search_by_projection_last(f: OracleFrame, cur: dict, last: dict, lf: dict, t
                                             int(check_ori), _p(owner) if n else None,
                                             _p(owner_obs) if n else None)
     return nm, owner, owner_obs
+
+
+class _OOKeyFrame(C.Structure):
+    _fields_ = [("n", C.c_int), ("kps", C.c_void_p), ("valid", C.c_void_p), ("pos", C.c_void_p),
+                ("max_dist", C.c_void_p), ("min_dist", C.c_void_p), ("desc", C.c_void_p)]
+
+
+def search_by_projection_kf(f: OracleFrame, cur: dict, kf: dict, th=10.0, orbdist=100, check_ori=True, owner=None):
+    """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist).  kf: kps, valid, pos, max_dist,
+    min_dist, desc.  Returns (nmatches, owner)."""
+    n = len(f.kps)
+    owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+    arrs = dict(kps=np.ascontiguousarray(kf["kps"]), valid=np.ascontiguousarray(kf["valid"], np.uint8),
+                pos=np.ascontiguousarray(kf["pos"], np.float32).reshape(-1, 3),
+                max_dist=np.ascontiguousarray(kf["max_dist"], np.float32),
+                min_dist=np.ascontiguousarray(kf["min_dist"], np.float32),
+                desc=np.ascontiguousarray(kf["desc"], np.uint8))
+    s = _OOKeyFrame()
+    s.n = len(arrs["kps"])
+    for k, v in arrs.items():
+        setattr(s, k, _p(v).value if v.size else None)
+    c = _camera(cur)
+    nm = lib().oo_search_by_projection_kf(C.byref(f._s), C.byref(c), C.byref(s), th, int(orbdist), int(check_ori),
+                                          _p(owner) if n else None)
+    return nm, owner
 
 
 def undistort_keypoints(K4, dist, kps):

@@ -1318,3 +1318,86 @@ void oo_compute_image_bounds(const float* K4, const float* dist, int ndist, int 
     *invW = (float)OO_GRID_COLS / (*maxX - *minX);
     *invH = (float)OO_GRID_ROWS / (*maxY - *minY);
 }
+
+/* ORBmatcher::SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)
+ * (src/ORBmatcher.cc:1472-1599): relocalisation / loop matcher of the map points of one keyframe */
+int oo_search_by_projection_kf(const oo_frame* F, const oo_camera* cur, const oo_keyframe* KF, float th, int ORBdist,
+                               int checkOri, int* owner)
+{
+    int nmatches = 0;
+    const float factor = 1.0f / OO_HISTO;
+    int hlen[OO_HISTO] = {0};
+    int* hist = (int*)malloc(sizeof(int) * OO_HISTO * (size_t)(KF->n + 1));
+    int* idx = (int*)malloc(sizeof(int) * (size_t)(F->n + 1));
+    const float logsf = oo_logf(cur->scale_factor);
+    float Ow[3];  /* Ow = -Rcw^T tcw (:1478), pinned like twc in oo_search_by_projection_last */
+    for (int j = 0; j < 3; j++) {
+        float s = cur->Rcw[j] * cur->tcw[0];
+        s = s + cur->Rcw[3 + j] * cur->tcw[1];
+        s = s + cur->Rcw[6 + j] * cur->tcw[2];
+        Ow[j] = -s;
+    }
+    for (int i = 0; i < KF->n; i++) {
+        if (!KF->valid[i]) continue;
+        const float* X = KF->pos + 3 * (size_t)i;
+        float x3Dc[3];
+        oo_rx_plus_t(cur->Rcw, X, cur->tcw, x3Dc);
+        const float xc = x3Dc[0], yc = x3Dc[1];
+        const float invzc = (float)(1.0 / (double)x3Dc[2]);
+        const float u = fmaf(cur->fx * xc, invzc, cur->cx);
+        const float v = fmaf(cur->fy * yc, invzc, cur->cy);
+        if (u < F->minX || u > F->maxX) continue;
+        if (v < F->minY || v > F->maxY) continue;
+        if (u != u || v != v) continue;  /* zc == 0 with xc == 0: undefined in the reference */
+        const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
+        double ss = 0.0;
+        for (int k = 0; k < 3; k++) ss += (double)PO[k] * (double)PO[k];
+        const float dist3D = (float)sqrt(ss);
+        const float maxDistance = 1.2f * KF->max_dist[i];
+        const float minDistance = 0.8f * KF->min_dist[i];
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        int nPredictedLevel = (int)ceilf(oo_logf(KF->max_dist[i] / dist3D) / logsf);
+        if (nPredictedLevel < 0) nPredictedLevel = 0;
+        else if (nPredictedLevel >= cur->nlevels) nPredictedLevel = cur->nlevels - 1;
+        const float radius = th * F->scale_factors[nPredictedLevel];
+        const int nc = oo_features_in_area(F, u, v, radius, nPredictedLevel - 1, nPredictedLevel + 1, idx);
+        if (nc == 0) continue;
+        const uint8_t* dMP = KF->desc + 32 * (size_t)i;
+        int bestDist = 256, bestIdx2 = -1;
+        for (int c = 0; c < nc; c++) {
+            const int i2 = idx[c];
+            if (owner[i2] >= 0) continue;
+            const int dist = oo_descriptor_distance(dMP, F->desc + 32 * (size_t)i2);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx2 = i2;
+            }
+        }
+        if (bestDist <= ORBdist) {
+            owner[bestIdx2] = i;
+            nmatches++;
+            if (checkOri) {
+                float rot = KF->kps[i].angle - F->kps[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == OO_HISTO) bin = 0;
+                assert(bin >= 0 && bin < OO_HISTO);
+                hist[bin * (KF->n + 1) + hlen[bin]++] = bestIdx2;
+            }
+        }
+    }
+    if (checkOri) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        oo_three_maxima(hlen, OO_HISTO, &ind1, &ind2, &ind3);
+        for (int b = 0; b < OO_HISTO; b++) {
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            for (int j = 0; j < hlen[b]; j++) {
+                owner[hist[b * (KF->n + 1) + j]] = -1;
+                nmatches--;
+            }
+        }
+    }
+    free(hist);
+    free(idx);
+    return nmatches;
+}

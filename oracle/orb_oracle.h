@@ -160,6 +160,23 @@ int oo_search_by_projection_last(const oo_frame* F, const oo_camera* cur, const 
                                  const oo_last_frame* LF, float th, int bMono, int checkOri, int* owner,
                                  int* owner_obs);
 
+/* KeyFrame snapshot for the relocalisation matcher */
+typedef struct {
+    int n;                   /* pKF->GetMapPointMatches().size() */
+    const oo_keypoint* kps;  /* pKF->mvKeysUn (angle) */
+    const uint8_t* valid;    /* pMP && !pMP->isBad() && !sAlreadyFound.count(pMP) */
+    const float* pos;        /* n x 3 */
+    const float* max_dist;   /* mfMaxDistance */
+    const float* min_dist;   /* mfMinDistance */
+    const uint8_t* desc;     /* n x 32 */
+} oo_keyframe;
+
+/* ORBmatcher::SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)
+ * (src/ORBmatcher.cc:1472-1599).  owner (F.n ints, in/out): keyframe index claiming the keypoint, -1 = NULL,
+ * >= KF.n = other claims.  Returns nmatches. */
+int oo_search_by_projection_kf(const oo_frame* F, const oo_camera* cur, const oo_keyframe* KF, float th, int ORBdist,
+                               int checkOri, int* owner);
+
 /* cv::undistortPoints(src, dst, K, D, noArray(), K) (OpenCV 3.4, 5 iterations) on n points (x, y interleaved);
  * K4 = fx, fy, cx, cy; dist = k1, k2, p1, p2[, k3] (ndist 4 or 5). */
 void oo_undistort_points(const float* K4, const float* dist, int ndist, const float* xy, float* out, int n);

@@ -28,7 +28,7 @@ EXPORTS = [
     "orbgpu_batch_candidate_total", "orbgpu_compute_stereo_matches", "orbgpu_compute_stereo_matches_batch",
     "orbgpu_is_in_frustum", "orbgpu_search_by_projection_last_frame", "orbgpu_debug_octree_profile",
     "orbgpu_stage_marks", "orbgpu_undistort_keypoints", "orbgpu_compute_image_bounds", "orbgpu_set_undistortion",
-    "orbgpu_batch_outputs_undistorted",
+    "orbgpu_batch_outputs_undistorted", "orbgpu_search_by_projection_keyframe",
 ]
 
 OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
@@ -70,6 +70,11 @@ class MapPointGeomView(C.Structure):
 class LastFrameView(C.Structure):
     _fields_ = [("n", C.c_int), ("kps", C.c_void_p), ("has_mp", C.c_void_p), ("outlier", C.c_void_p),
                 ("pos", C.c_void_p), ("n_obs", C.c_void_p), ("desc", C.c_void_p)]
+
+
+class KeyFrameView(C.Structure):
+    _fields_ = [("n", C.c_int), ("kps", C.c_void_p), ("valid", C.c_void_p), ("pos", C.c_void_p),
+                ("max_dist", C.c_void_p), ("min_dist", C.c_void_p), ("desc", C.c_void_p)]
 
 
 _lib = None
@@ -119,6 +124,8 @@ def _declare(L):
     L.orbgpu_memcpy_d2d_async.argtypes = [vp, vp, vp, sz]
     L.orbgpu_batch_candidate_total.restype = C.c_longlong
     L.orbgpu_debug_octree_profile.argtypes = [vp, vp, i32]
+    L.orbgpu_search_by_projection_keyframe.argtypes = [vp, C.POINTER(FrameView), C.POINTER(Camera),
+                                                       C.POINTER(KeyFrameView), f32, i32, i32, vp, C.POINTER(i32)]
     L.orbgpu_undistort_keypoints.argtypes = [vp, vp, vp, i32, vp, vp, i32]
     L.orbgpu_compute_image_bounds.argtypes = [vp, vp, vp, i32, i32, i32, C.POINTER(GridGeom)]
     L.orbgpu_set_undistortion.argtypes = [vp, vp, vp, i32]

@@ -806,9 +806,12 @@ __global__ __launch_bounds__(256) void og_last_fill_kernel(OgFrameDev F, OgGridG
 }
 
 // ent: LF.n ints -- the rotation-histogram pushes in order, packed (bin << 24) | keypoint index
+// blockAny: any claim blocks a keypoint (relocalisation, :1543-1544) instead of claims by map points with
+// observations (:1384-1386); thAccept: TH_HIGH or the caller's ORBdist; owner_obs may be nullptr.
 __global__ __launch_bounds__(64) void og_last_resolve_kernel(OgFrameDev F, OgLastFrameDev LF, int checkOri,
-                                                             const int* off, const OgLastCand* cands, int* ent,
-                                                             int* owner, int* owner_obs, int* nmatches)
+                                                             int blockAny, int thAccept, const int* off,
+                                                             const OgLastCand* cands, int* ent, int* owner,
+                                                             int* owner_obs, int* nmatches)
 {
     __shared__ int hist[HISTO_LENGTH];
     __shared__ int sh[4];
@@ -824,15 +827,15 @@ __global__ __launch_bounds__(64) void og_last_resolve_kernel(OgFrameDev F, OgLas
             int bestDist = 256, bestIdx2 = -1;
             for (int c = b; c < e; c++) {
                 const OgLastCand cc = cands[c];
-                if (owner[cc.idx] >= 0 && owner_obs[cc.idx]) continue;
+                if (owner[cc.idx] >= 0 && (blockAny || owner_obs[cc.idx])) continue;
                 if (cc.dist < bestDist) {
                     bestDist = cc.dist;
                     bestIdx2 = cc.idx;
                 }
             }
-            if (bestDist <= TH_HIGH) {
+            if (bestDist <= thAccept) {
                 owner[bestIdx2] = i;
-                owner_obs[bestIdx2] = LF.n_obs[i] > 0;
+                if (owner_obs) owner_obs[bestIdx2] = LF.n_obs ? LF.n_obs[i] > 0 : 1;
                 nm++;
                 if (checkOri) {
                     float rot = __fsub_rn(LF.kps[i].angle, F.kps[bestIdx2].angle);
@@ -862,7 +865,7 @@ __global__ __launch_bounds__(64) void og_last_resolve_kernel(OgFrameDev F, OgLas
             const int v = ent[k], bin = v >> 24, idx = v & 0xffffff;
             if (bin != i1 && bin != i2 && bin != i3) {
                 owner[idx] = -1;  // all writes are NULL: order-free
-                owner_obs[idx] = 0;
+                if (owner_obs) owner_obs[idx] = 0;
                 culled++;
             }
         }
@@ -888,6 +891,103 @@ void og_launch_last_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const flo
     if (blocks > 0)
         hipLaunchKernelGGL(og_last_fill_kernel, dim3(blocks), dim3(256), 0, s, F, G, sf, cam, LF, th, mode, off,
                            cands);
-    hipLaunchKernelGGL(og_last_resolve_kernel, dim3(1), dim3(64), 0, s, F, LF, checkOri, off, cands, ent, owner,
-                       owner_obs, nmatches);
+    hipLaunchKernelGGL(og_last_resolve_kernel, dim3(1), dim3(64), 0, s, F, LF, checkOri, 0, TH_HIGH, off, cands, ent,
+                       owner, owner_obs, nmatches);
+}
+
+// ------------------------------------------------------------------------------------------------
+// ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>& sAlreadyFound,
+// th, ORBdist) (src/ORBmatcher.cc:1472-1599): the keyframe's map points projected into the frame (no depth
+// sign test), PredictScale on ||X - Ow|| picks the level window; any claim blocks; accept <= ORBdist.
+// ------------------------------------------------------------------------------------------------
+template <bool FILL>
+__device__ int og_kf_enum(const OgFrameDev& F, const OgGridGeom& G, const float* sf, const OgCameraDev& cam,
+                          const float* Ow, const OgLastFrameDev& KF, const float* max_dist, const float* min_dist,
+                          int i, float th, OgLastCand* out)
+{
+    if (!KF.has_mp[i]) return 0;
+    const float X[3] = {KF.pos[3 * i], KF.pos[3 * i + 1], KF.pos[3 * i + 2]};
+    float x3[3];
+    og_rx_t(cam.R, X, cam.t, x3);
+    const float invzc = (float)__ddiv_rn(1.0, (double)x3[2]);
+    const float u = __fmaf_rn(__fmul_rn(cam.fx, x3[0]), invzc, cam.cx);
+    const float v = __fmaf_rn(__fmul_rn(cam.fy, x3[1]), invzc, cam.cy);
+    if (u < G.minX || u > G.maxX) return 0;
+    if (v < G.minY || v > G.maxY) return 0;
+    if (u != u || v != v) return 0;
+    const float PO[3] = {__fsub_rn(X[0], Ow[0]), __fsub_rn(X[1], Ow[1]), __fsub_rn(X[2], Ow[2])};
+    double ss = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) ss = __dadd_rn(ss, __dmul_rn((double)PO[k], (double)PO[k]));
+    const float dist3D = (float)__dsqrt_rn(ss);
+    const float maxD = __fmul_rn(1.2f, max_dist[i]), minD = __fmul_rn(0.8f, min_dist[i]);
+    if (dist3D < minD || dist3D > maxD) return 0;
+    int lvl = (int)ceilf(__fdiv_rn(og_logf(__fdiv_rn(max_dist[i], dist3D)), og_logf(cam.scale_factor)));
+    lvl = lvl < 0 ? 0 : (lvl >= cam.nlevels ? cam.nlevels - 1 : lvl);
+    const float radius = __fmul_rn(th, sf[lvl]);
+    const int minLevel = lvl - 1, maxLevel = lvl + 1;
+    const OgCellRange cr = og_cell_range(G, u, v, radius);
+    if (cr.x0 > cr.x1) return 0;
+    uint4 da, db;
+    if (FILL) og_load_desc(KF.desc + (long long)i * 32, da, db);
+    int n = 0;
+    for (int ix = cr.x0; ix <= cr.x1; ix++)
+        for (int iy = cr.y0; iy <= cr.y1; iy++) {
+            const int cell = ix * OG_GRID_ROWS + iy;
+            for (int j = F.cell_start[cell]; j < F.cell_start[cell + 1]; j++) {
+                const int idx = F.cell_items[j];
+                const orbgpu_kp_dev kp = F.kps[idx];
+                if (kp.octave < minLevel || kp.octave > maxLevel) continue;  // bCheckLevels (maxLevel >= 0)
+                const float distx = __fsub_rn(kp.x, u), disty = __fsub_rn(kp.y, v);
+                if (!(fabsf(distx) < radius && fabsf(disty) < radius)) continue;
+                if (FILL) {
+                    uint4 ea, eb;
+                    og_load_desc(F.desc + (long long)idx * 32, ea, eb);
+                    out[n] = OgLastCand{idx, og_hamming(da, db, ea, eb)};
+                }
+                n++;
+            }
+        }
+    return n;
+}
+
+__global__ __launch_bounds__(256) void og_kf_count_kernel(OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
+                                                          OgLastFrameDev KF, const float* max_dist,
+                                                          const float* min_dist, float th, int* cnt)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= KF.n) return;
+    cnt[i] = og_kf_enum<false>(F, G, sf, cam, cam.Ow, KF, max_dist, min_dist, i, th, nullptr);
+}
+
+__global__ __launch_bounds__(256) void og_kf_fill_kernel(OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
+                                                         OgLastFrameDev KF, const float* max_dist,
+                                                         const float* min_dist, float th, const int* off,
+                                                         OgLastCand* cands)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= KF.n) return;
+    og_kf_enum<true>(F, G, sf, cam, cam.Ow, KF, max_dist, min_dist, i, th, cands + off[i]);
+}
+
+void og_launch_kf_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
+                        OgLastFrameDev KF, const float* max_dist, const float* min_dist, float th, int* cnt, int* off)
+{
+    const int blocks = (KF.n + 255) / 256;
+    if (blocks > 0)
+        hipLaunchKernelGGL(og_kf_count_kernel, dim3(blocks), dim3(256), 0, s, F, G, sf, cam, KF, max_dist, min_dist,
+                           th, cnt);
+    hipLaunchKernelGGL(og_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, KF.n, off);
+}
+
+void og_launch_kf_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
+                          OgLastFrameDev KF, const float* max_dist, const float* min_dist, float th, int ORBdist,
+                          int checkOri, const int* off, OgLastCand* cands, int* ent, int* owner, int* nmatches)
+{
+    const int blocks = (KF.n + 255) / 256;
+    if (blocks > 0)
+        hipLaunchKernelGGL(og_kf_fill_kernel, dim3(blocks), dim3(256), 0, s, F, G, sf, cam, KF, max_dist, min_dist,
+                           th, off, cands);
+    hipLaunchKernelGGL(og_last_resolve_kernel, dim3(1), dim3(64), 0, s, F, KF, checkOri, 1, ORBdist, off, cands, ent,
+                       owner, (int*)nullptr, nmatches);
 }

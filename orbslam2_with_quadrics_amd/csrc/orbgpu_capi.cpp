@@ -1206,6 +1206,83 @@ int orbgpu_search_by_projection_last_frame(orbgpu_ctx* c, const orbgpu_frame_vie
     return ORBGPU_OK;
 }
 
+int orbgpu_search_by_projection_keyframe(orbgpu_ctx* c, const orbgpu_frame_view* F, const orbgpu_camera* curc,
+                                         const orbgpu_keyframe_view* KF, float th, int ORBdist, int checkOri,
+                                         int32_t* owner, int* nmatches)
+{
+    if (!c || !F || !curc || !KF || !nmatches || F->n < 0 || KF->n < 0) return ORBGPU_ERR_ARG;
+    if (F->n && !owner) return ORBGPU_ERR_ARG;
+    if (!F->scale_factors || F->nlevels < 1) return ORBGPU_ERR_ARG;
+    if (KF->n && (!KF->kps || !KF->valid || !KF->pos || !KF->max_dist || !KF->min_dist || !KF->desc))
+        return ORBGPU_ERR_ARG;
+    if (KF->n >= (1 << 24) || F->n >= (1 << 24)) return ORBGPU_ERR_UNSUPPORTED;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const int n = std::max(F->n, 1), L = std::max(KF->n, 1);
+    const size_t fixed = kCarvePad + (size_t)n * (28 + 32 + 4 + 4) + (OG_GRID_CELLS + 1) * 4 +
+                         (size_t)L * (28 + 1 + 12 + 4 + 4 + 32 + 4 + 4 + 4) + 64 + F->nlevels * 4;
+    HIP_TRY(c, ensure(c->mscratch, fixed));
+    uint8_t* cur = c->mscratch.p;
+    orbgpu_kp_dev* k = (orbgpu_kp_dev*)scratch_carve(cur, (size_t)n * 28);
+    uint8_t* d = scratch_carve(cur, (size_t)n * 32);
+    int* own = (int*)scratch_carve(cur, (size_t)n * 4);
+    int* cnts = (int*)scratch_carve(cur, 16);
+    int* cs = (int*)scratch_carve(cur, (OG_GRID_CELLS + 1) * 4);
+    int* ci = (int*)scratch_carve(cur, (size_t)n * 4);
+    float* sfd = (float*)scratch_carve(cur, (size_t)F->nlevels * 4);
+    orbgpu_kp_dev* kk = (orbgpu_kp_dev*)scratch_carve(cur, (size_t)L * 28);
+    uint8_t* kv = scratch_carve(cur, (size_t)L);
+    float* kp3 = (float*)scratch_carve(cur, (size_t)L * 12);
+    float* kmx = (float*)scratch_carve(cur, (size_t)L * 4);
+    float* kmn = (float*)scratch_carve(cur, (size_t)L * 4);
+    uint8_t* kd = scratch_carve(cur, (size_t)L * 32);
+    int* cnt = (int*)scratch_carve(cur, (size_t)L * 4);
+    int* off = (int*)scratch_carve(cur, (size_t)(L + 1) * 4);
+    int* ent = (int*)scratch_carve(cur, (size_t)L * 4);
+    int* nm = (int*)scratch_carve(cur, 16);
+    hipStream_t s = c->stream;
+    if (F->n) {
+        HIP_TRY(c, hipMemcpyAsync(k, F->kps, (size_t)F->n * 28, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(d, F->desc, (size_t)F->n * 32, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(own, owner, (size_t)F->n * 4, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(c, hipMemcpyAsync(sfd, F->scale_factors, (size_t)F->nlevels * 4, hipMemcpyHostToDevice, s));
+    if (KF->n) {
+        HIP_TRY(c, hipMemcpyAsync(kk, KF->kps, (size_t)KF->n * 28, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(kv, KF->valid, (size_t)KF->n, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(kp3, KF->pos, (size_t)KF->n * 12, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(kmx, KF->max_dist, (size_t)KF->n * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(kmn, KF->min_dist, (size_t)KF->n * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(kd, KF->desc, (size_t)KF->n * 32, hipMemcpyHostToDevice, s));
+    }
+    int hc = F->n;
+    HIP_TRY(c, hipMemcpyAsync(cnts, &hc, sizeof(int), hipMemcpyHostToDevice, s));
+    const OgGridGeom G{F->grid.minX, F->grid.minY, F->grid.maxX, F->grid.maxY, F->grid.invW, F->grid.invH};
+    og_launch_grid(s, k, cnts, n, G, cs, ci, 1);
+    OgFrameDev fd{k, d, cnts, cs, ci, nullptr, n};
+    OgLastFrameDev kfd{KF->n, kk, kv, nullptr, kp3, nullptr, kd};
+    OgCameraDev cam = camera_dev(curc, G.minX, G.maxX, G.minY, G.maxY);
+    for (int j = 0; j < 3; j++) {  // Ow = -Rcw^T tcw as the matcher computes it (src/ORBmatcher.cc:1478)
+        float t = curc->Rcw[j] * curc->tcw[0];
+        t = t + curc->Rcw[3 + j] * curc->tcw[1];
+        t = t + curc->Rcw[6 + j] * curc->tcw[2];
+        cam.Ow[j] = -t;
+    }
+    og_launch_kf_count(s, fd, G, sfd, cam, kfd, kmx, kmn, th, cnt, off);
+    int total = 0;
+    HIP_TRY(c, hipMemcpyAsync(&total, off + KF->n, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    HIP_TRY(c, ensure(c->mcands, (size_t)std::max(total, 1) * sizeof(OgLastCand)));
+    og_launch_kf_resolve(s, fd, G, sfd, cam, kfd, kmx, kmn, th, ORBdist, checkOri, off, (OgLastCand*)c->mcands.p,
+                         ent, own, nm);
+    HIP_TRY(c, hipGetLastError());
+    int hnm = 0;
+    HIP_TRY(c, hipMemcpyAsync(&hnm, nm, sizeof(int), hipMemcpyDeviceToHost, s));
+    if (F->n) HIP_TRY(c, hipMemcpyAsync(owner, own, (size_t)F->n * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    *nmatches = hnm;
+    return ORBGPU_OK;
+}
+
 int orbgpu_debug_candidates(orbgpu_ctx* c, int b, int level, uint64_t* out, int cap)
 {
     if (!c || !c->last_B || b < 0 || b >= c->last_B || level < 0 || level >= c->nlevels) return ORBGPU_ERR_ARG;

@@ -146,6 +146,14 @@ void og_launch_last_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const flo
                             OgLastFrameDev LF, float th, int mode, int checkOri, const int* off, OgLastCand* cands,
                             int* ent, int* owner, int* owner_obs, int* nmatches);
 
+// relocalisation SearchByProjection(F, pKF, sAlreadyFound, th, ORBdist): KF.has_mp = valid flag, KF.outlier and
+// KF.n_obs unused; cam.Ow = -Rcw^T tcw of the current frame as the reference computes it (:1478)
+void og_launch_kf_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
+                        OgLastFrameDev KF, const float* max_dist, const float* min_dist, float th, int* cnt, int* off);
+void og_launch_kf_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
+                          OgLastFrameDev KF, const float* max_dist, const float* min_dist, float th, int ORBdist,
+                          int checkOri, const int* off, OgLastCand* cands, int* ent, int* owner, int* nmatches);
+
 // Frame post-processing (orb_frame.hip): cv::undistortPoints of Frame::UndistortKeyPoints
 struct OgUndistort {
     float K[4];  // fx, fy, cx, cy (mK)

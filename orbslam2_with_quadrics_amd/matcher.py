@@ -152,6 +152,32 @@ class ORBmatcher:
         return nin.value, {k: a[:m].copy() for k, a in out.items()}
 
 
+    def SearchByProjectionKeyFrame(self, CurrentFrame: Frame, cur: dict, KF: dict, th: float, ORBdist: int,
+                                   owner=None):
+        """ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>& sAlreadyFound,
+        th, ORBdist) (src/ORBmatcher.cc:1472-1599).  KF: dict of kps, valid, pos, max_dist, min_dist, desc.
+        Returns (nmatches, owner) -- owner = keyframe map-point index per keypoint, -1 = NULL."""
+        n = CurrentFrame.N
+        owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+        arrs = dict(kps=np.ascontiguousarray(KF["kps"], KP_DTYPE), valid=np.ascontiguousarray(KF["valid"], np.uint8),
+                    pos=np.ascontiguousarray(KF["pos"], np.float32).reshape(-1, 3),
+                    max_dist=np.ascontiguousarray(KF["max_dist"], np.float32),
+                    min_dist=np.ascontiguousarray(KF["min_dist"], np.float32),
+                    desc=np.ascontiguousarray(KF["desc"], np.uint8))
+        kv = _lib.KeyFrameView()
+        kv.n = len(arrs["kps"])
+        for k, a in arrs.items():
+            setattr(kv, k, _p(a).value if a.size else None)
+        fv = CurrentFrame.view()
+        cc = camera_struct(cur)
+        nm = C.c_int(0)
+        ctx = self._ex.ctx
+        rc = _lib.lib().orbgpu_search_by_projection_keyframe(ctx, C.byref(fv), C.byref(cc), C.byref(kv), float(th),
+                                                             int(ORBdist), int(self.mbCheckOrientation),
+                                                             _p(owner) if n else None, C.byref(nm))
+        _lib.check(ctx, rc, "orbgpu_search_by_projection_keyframe")
+        return nm.value, owner
+
     def SearchByProjectionLastFrame(self, CurrentFrame: Frame, cur: dict, LastFrame: dict, last: dict, th: float,
                                    bMono: bool, owner=None, owner_obs=None):
         """ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)

@@ -171,3 +171,20 @@ def local_map_points(seed: int, m: int, cam: dict, nlevels: int = 8, scale_facto
     mn = mx / scale_factor ** (nlevels - 1)
     return dict(pos=Xw.astype(np.float32), normal=nrm.astype(np.float32), max_dist=mx.astype(np.float32),
                 min_dist=mn.astype(np.float32))
+
+
+def keyframe_points(seed: int, kps, desc, cam_kf: dict, depth=(2.0, 9.0), p_invalid=0.1, p_flip=0.03,
+                    scale_factor: float = 1.2, nlevels: int = 8) -> dict:
+    """KeyFrame snapshot for the relocalisation SearchByProjection(F, pKF, sAlreadyFound, th, ORBdist): the
+    keyframe's keypoints back-projected at random depths (world positions), descriptors with bits flipped,
+    the distance bounds UpdateNormalAndDepth sets (mfMaxDistance = dist * sf^octave), and a validity flag
+    (map point present, not bad, not already found)."""
+    lf = last_frame_points(seed, kps, desc, cam_kf, depth, p_no_mp=0.0, p_outlier=0.0, p_flip=p_flip)
+    rng = np.random.Generator(np.random.PCG64(seed + 77))
+    n = len(kps)
+    Ow = cam_kf["Ow"].astype(np.float64)
+    d = np.linalg.norm(lf["pos"].astype(np.float64) - Ow, axis=1) * rng.uniform(0.85, 1.15, n)
+    mx = d * scale_factor ** np.asarray(kps["octave"], np.float64)
+    mn = mx / scale_factor ** (nlevels - 1)
+    return dict(kps=lf["kps"], valid=(rng.random(n) >= p_invalid).astype(np.uint8), pos=lf["pos"],
+                max_dist=mx.astype(np.float32), min_dist=mn.astype(np.float32), desc=lf["desc"])

@@ -628,3 +628,72 @@ def undistort_point(K4, dist, px, py):
     yy = 0.0 * x + fy * y + cy
     ww = 1.0 / (0.0 * x + 0.0 * y + 1.0)
     return F32(xx * ww), F32(yy * ww)
+
+
+def search_by_projection_kf(F, cur, kf, th, orbdist, check_ori, owner=None):
+    """SearchByProjection(Frame&, KeyFrame*, set<MapPoint*>&, th, ORBdist) (src/ORBmatcher.cc:1472-1599)."""
+    logf = _libm_logf()
+    n = len(F.kps)
+    owner = [-1] * n if owner is None else list(owner)
+    Rc = np.asarray(cur["Rcw"], np.float32).reshape(3, 3)
+    tc = np.asarray(cur["tcw"], np.float32)
+    Ow = []
+    for j in range(3):
+        s = F32(Rc[0][j] * tc[0])
+        s = F32(s + F32(Rc[1][j] * tc[1]))
+        s = F32(s + F32(Rc[2][j] * tc[2]))
+        Ow.append(F32(-s))
+    lsf = F32(logf(float(cur["scale_factor"])))
+    fx, fy, cx, cy = (F32(cur[k]) for k in ("fx", "fy", "cx", "cy"))
+    hist = [[] for _ in range(30)]
+    nm = 0
+    for i in range(len(kf["kps"])):
+        if not kf["valid"][i]:
+            continue
+        X = np.asarray(kf["pos"][i], np.float32)
+        x3 = _rx_t(Rc, X, tc)
+        invzc = F32(1.0 / float(x3[2]))
+        u = fmaf(F32(fx * x3[0]), invzc, cx)
+        v = fmaf(F32(fy * x3[1]), invzc, cy)
+        if u < F.minX or u > F.maxX or v < F.minY or v > F.maxY:
+            continue
+        PO = [F32(X[k] - Ow[k]) for k in range(3)]
+        ss = 0.0
+        for k in range(3):
+            ss += float(PO[k]) * float(PO[k])
+        d3 = F32(math.sqrt(ss))
+        if d3 < F32(F32(0.8) * F32(kf["min_dist"][i])) or d3 > F32(F32(1.2) * F32(kf["max_dist"][i])):
+            continue
+        lvl = int(math.ceil(F32(F32(logf(float(F32(F32(kf["max_dist"][i]) / d3)))) / lsf)))
+        lvl = min(max(lvl, 0), int(cur["nlevels"]) - 1)
+        radius = F32(F32(th) * F.sf[lvl])
+        cands = F.features_in_area(u, v, radius, lvl - 1, lvl + 1)
+        if not cands:
+            continue
+        best, bi = 256, -1
+        for i2 in cands:
+            if owner[i2] >= 0:
+                continue
+            d = popcount_dist(kf["desc"][i], F.desc[i2])
+            if d < best:
+                best, bi = d, i2
+        if best <= orbdist:
+            owner[bi] = i
+            nm += 1
+            if check_ori:
+                rot = F32(F32(kf["kps"][i]["angle"]) - F32(F.kps[bi]["angle"]))
+                if rot < 0.0:
+                    rot = F32(rot + F32(360.0))
+                b = _round_half_away(f32(rot * F32(F32(1.0) / F32(30))))
+                if b == 30:
+                    b = 0
+                hist[b].append(bi)
+    if check_ori:
+        i1, i2_, i3 = three_maxima([len(h) for h in hist])
+        for b in range(30):
+            if b in (i1, i2_, i3):
+                continue
+            for k in hist[b]:
+                owner[k] = -1
+                nm -= 1
+    return nm, owner

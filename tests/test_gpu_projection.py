@@ -151,3 +151,26 @@ def test_tiny_inputs_all_host_matchers(gpu, oracle):
     wn, wown, _ = oracle.search_by_projection_last(oracle.OracleFrame(k2, d2, cols, rows, sf), cur, last, lf, 7.0,
                                                    True, True)
     assert gn == wn and np.array_equal(gown, wown)
+
+
+@pytest.mark.parametrize("seed,shape,nf", [(0, (480, 640), 1000), (1, (480, 640), 1000), (2, (1080, 1920), 2000)])
+def test_search_by_projection_keyframe_vs_oracle(gpu, oracle, seed, shape, nf):
+    """Relocalisation SearchByProjection(F, pKF, sAlreadyFound, th, ORBdist) (src/ORBmatcher.cc:1472-1599)
+    with the calls of Tracking::Relocalization: (th 10, ORBdist 100) then (th 3, ORBdist 64)."""
+    rows, cols = shape
+    f1, f2 = synthetic.frame_pair(130 + seed, rows, cols, (4, -2))
+    ex = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
+    k1, d1 = ex(f1)
+    k2, d2 = ex(f2)
+    sf = ex.GetScaleFactors()
+    kfcam, cur = _poses(seed, cols, rows)
+    kf = synthetic.keyframe_points(seed, k1, d1, kfcam)
+    F = gpu.Frame(k2, d2, cols, rows, sf)
+    Fo = oracle.OracleFrame(k2, d2, cols, rows, sf)
+    owner0 = np.full(len(k2), -1, np.int32)
+    owner0[::13] = len(k1)
+    for th, orbdist, ori in ((10.0, 100, True), (3.0, 64, True), (10.0, 50, False)):
+        gn, gown = gpu.ORBmatcher(0.9, ori, context=ex).SearchByProjectionKeyFrame(F, cur, kf, th, orbdist, owner0)
+        wn, wown = oracle.search_by_projection_kf(Fo, cur, kf, th, orbdist, ori, owner0)
+        assert gn == wn and gn > 10
+        assert np.array_equal(gown, wown)

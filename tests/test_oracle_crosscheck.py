@@ -263,3 +263,26 @@ def test_image_bounds_python_restatement(oracle):
     want = (min(c[0][0], c[2][0]), max(c[1][0], c[3][0]), min(c[0][1], c[1][1]), max(c[2][1], c[3][1]))
     assert b[:4] == tuple(float(v) for v in want)
     assert b[4] == float(np.float32(64) / np.float32(np.float32(b[1]) - np.float32(b[0])))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_search_by_projection_kf_python_restatement(oracle, seed):
+    from orbslam2_with_quadrics_amd import synthetic
+
+    rows, cols = 480, 640
+    f1, f2 = synthetic.frame_pair(70 + seed, rows, cols, (4, -2))
+    ex = oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+    k1, d1 = ex(f1)
+    k2, d2 = ex(f2)
+    sf = ex.tables()["scale"]
+    kfcam, cur = _pose_pair(seed, cols, rows)
+    kf = synthetic.keyframe_points(seed, k1, d1, kfcam)
+    Fo = oracle.OracleFrame(k2, d2, cols, rows, sf)
+    Fp = refpy.PyFrame(k2, d2, cols, rows, sf)
+    owner0 = np.full(len(k2), -1, np.int32)
+    owner0[::13] = len(k1)  # keypoints already matched (mvpMapPoints set) block candidates
+    for th, orbdist, ori in ((10.0, 100, True), (3.0, 50, True), (10.0, 64, False)):
+        n, ow = oracle.search_by_projection_kf(Fo, cur, kf, th, orbdist, ori, owner0)
+        wn, wow = refpy.search_by_projection_kf(Fp, cur, kf, th, orbdist, ori, owner0)
+        assert n == wn and ow.tolist() == wow
+        assert n > 10
