@@ -285,6 +285,21 @@ int orbgpu_compute_stereo_matches_batch(orbgpu_ctx* left, orbgpu_ctx* right, flo
  * product build. */
 int orbgpu_debug_octree_profile(orbgpu_ctx* ctx, unsigned long long* out, int n);
 
+/* ---- RGB-D ------------------------------------------------------------------------------------------ */
+
+/* Replaces void Frame::ComputeStereoFromRGBD(const cv::Mat& imDepth) -- src/Frame.cc:643-664, called from the
+ * RGB-D Frame constructor (src/Frame.cc:161) -- for the frame the context extracted last (mvKeys for the
+ * lookup, mvKeysUn when orbgpu_set_undistortion is active).  depth: CV_32F (is_u16 = 0) or the raw CV_16U
+ * image with Tracking::GrabImageRGBD's convertTo(CV_32F, mDepthMapFactor) fused in (is_u16 = 1, factor =
+ * mDepthMapFactor; src/Tracking.cc:227-228).  Writes mvuRight / mvDepth (-1 where the depth is <= 0). */
+int orbgpu_compute_stereo_from_rgbd(orbgpu_ctx* ctx, const void* depth, int is_u16, float factor, size_t step_bytes,
+                                    float mbf, float* uright, float* depth_out, int cap, int* n);
+/* Batched device form over the context's last batch: depth frame b at d_depth + b*frame_stride_bytes;
+ * outputs at stride frame_cap per frame. */
+int orbgpu_compute_stereo_from_rgbd_batch(orbgpu_ctx* ctx, const void* d_depth, int is_u16, float factor,
+                                          size_t pitch_bytes, size_t frame_stride_bytes, float mbf, float* d_uright,
+                                          float* d_depth_out);
+
 /* ---- stream / timing helpers ------------------------------------------------------------------ */
 
 /* The context's hipStream_t (as void*), e.g. for torch.cuda.ExternalStream. */

@@ -70,6 +70,8 @@ def lib():
         L.oo_is_in_frustum.argtypes = [vp, vp, f32, vp, vp, vp, vp, vp, vp]
         L.oo_search_by_projection_kf.restype = i32
         L.oo_search_by_projection_kf.argtypes = [vp, vp, vp, f32, i32, i32, vp]
+        L.oo_stereo_from_rgbd.argtypes = [vp, vp, i32, vp, i32, f32, vp, vp]
+        L.oo_depth_u16_to_f32.argtypes = [vp, i32, f32, vp]
         L.oo_undistort_points.argtypes = [vp, vp, i32, vp, vp, i32]
         L.oo_undistort_keypoints.argtypes = [vp, vp, i32, vp, vp, i32]
         L.oo_compute_image_bounds.argtypes = [vp, vp, i32, i32, i32] + [C.POINTER(f32)] * 6
@@ -313,6 +315,25 @@ def search_by_projection_kf(f: OracleFrame, cur: dict, kf: dict, th=10.0, orbdis
     nm = lib().oo_search_by_projection_kf(C.byref(f._s), C.byref(c), C.byref(s), th, int(orbdist), int(check_ori),
                                           _p(owner) if n else None)
     return nm, owner
+
+
+def depth_u16_to_f32(depth_u16, factor):
+    src = np.ascontiguousarray(depth_u16, np.uint16)
+    out = np.zeros(src.shape, np.float32)
+    lib().oo_depth_u16_to_f32(_p(src), src.size, factor, _p(out))
+    return out
+
+
+def stereo_from_rgbd(kps, kps_un, depth_f32, mbf):
+    """Frame::ComputeStereoFromRGBD -> (uright, depth)."""
+    kps = np.ascontiguousarray(kps)
+    kps_un = np.ascontiguousarray(kps_un)
+    dep = np.ascontiguousarray(depth_f32, np.float32)
+    n = len(kps)
+    ur = np.zeros(max(n, 1), np.float32)
+    de = np.zeros(max(n, 1), np.float32)
+    lib().oo_stereo_from_rgbd(_p(kps), _p(kps_un), n, _p(dep), dep.shape[1], mbf, _p(ur), _p(de))
+    return ur[:n].copy(), de[:n].copy()
 
 
 def undistort_keypoints(K4, dist, kps):

@@ -1401,3 +1401,26 @@ int oo_search_by_projection_kf(const oo_frame* F, const oo_camera* cur, const oo
     free(idx);
     return nmatches;
 }
+
+/* Frame::ComputeStereoFromRGBD (src/Frame.cc:643-664) on a float depth map (imDepth after
+ * Tracking::GrabImageRGBD's convertTo(CV_32F, mDepthMapFactor), src/Tracking.cc:227-228).  step in floats. */
+void oo_stereo_from_rgbd(const oo_keypoint* kps, const oo_keypoint* kps_un, int n, const float* depth, int step,
+                         float mbf, float* uright, float* depth_out)
+{
+    for (int i = 0; i < n; i++) {
+        uright[i] = -1;
+        depth_out[i] = -1;
+        const int v = (int)kps[i].y, u = (int)kps[i].x;  /* imDepth.at<float>(v,u): float -> int */
+        const float d = depth[(size_t)v * step + u];
+        if (d > 0) {
+            depth_out[i] = d;
+            uright[i] = kps_un[i].x - mbf / d;
+        }
+    }
+}
+
+/* imDepth.convertTo(imDepth, CV_32F, mDepthMapFactor) for a CV_16U depth image (shift 0: one product) */
+void oo_depth_u16_to_f32(const uint16_t* src, int n, float factor, float* dst)
+{
+    for (int i = 0; i < n; i++) dst[i] = (float)src[i] * factor;
+}

@@ -177,6 +177,11 @@ typedef struct {
 int oo_search_by_projection_kf(const oo_frame* F, const oo_camera* cur, const oo_keyframe* KF, float th, int ORBdist,
                                int checkOri, int* owner);
 
+/* Frame::ComputeStereoFromRGBD (src/Frame.cc:643-664): depth = float map (step in floats). */
+void oo_stereo_from_rgbd(const oo_keypoint* kps, const oo_keypoint* kps_un, int n, const float* depth, int step,
+                         float mbf, float* uright, float* depth_out);
+void oo_depth_u16_to_f32(const uint16_t* src, int n, float factor, float* dst);
+
 /* cv::undistortPoints(src, dst, K, D, noArray(), K) (OpenCV 3.4, 5 iterations) on n points (x, y interleaved);
  * K4 = fx, fy, cx, cy; dist = k1, k2, p1, p2[, k3] (ndist 4 or 5). */
 void oo_undistort_points(const float* K4, const float* dist, int ndist, const float* xy, float* out, int n);

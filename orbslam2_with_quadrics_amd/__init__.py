@@ -5,7 +5,8 @@ The compute path is the gfx950 HIP library liborbgpu.so (C ABI: include/orbgpu.h
 are thin mirrors of the reference C++ classes for Python callers, tests and the bench.
 """
 from .extractor import KP_DTYPE, ORBextractor  # noqa: F401
-from .matcher import ComputeImageBounds, ComputeStereoMatches, Frame, ORBmatcher, UndistortKeyPoints  # noqa: F401
+from .matcher import (ComputeImageBounds, ComputeStereoFromRGBD, ComputeStereoMatches, Frame, ORBmatcher,  # noqa: F401
+                      UndistortKeyPoints)
 
 __all__ = ["ORBextractor", "ORBmatcher", "Frame", "ComputeStereoMatches", "UndistortKeyPoints", "ComputeImageBounds",
-           "KP_DTYPE"]
+           "ComputeStereoFromRGBD", "KP_DTYPE"]

@@ -29,6 +29,7 @@ EXPORTS = [
     "orbgpu_is_in_frustum", "orbgpu_search_by_projection_last_frame", "orbgpu_debug_octree_profile",
     "orbgpu_stage_marks", "orbgpu_undistort_keypoints", "orbgpu_compute_image_bounds", "orbgpu_set_undistortion",
     "orbgpu_batch_outputs_undistorted", "orbgpu_search_by_projection_keyframe",
+    "orbgpu_compute_stereo_from_rgbd", "orbgpu_compute_stereo_from_rgbd_batch",
 ]
 
 OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
@@ -126,6 +127,8 @@ def _declare(L):
     L.orbgpu_debug_octree_profile.argtypes = [vp, vp, i32]
     L.orbgpu_search_by_projection_keyframe.argtypes = [vp, C.POINTER(FrameView), C.POINTER(Camera),
                                                        C.POINTER(KeyFrameView), f32, i32, i32, vp, C.POINTER(i32)]
+    L.orbgpu_compute_stereo_from_rgbd.argtypes = [vp, vp, i32, f32, sz, f32, vp, vp, i32, C.POINTER(i32)]
+    L.orbgpu_compute_stereo_from_rgbd_batch.argtypes = [vp, vp, i32, f32, sz, sz, f32, vp, vp]
     L.orbgpu_undistort_keypoints.argtypes = [vp, vp, vp, i32, vp, vp, i32]
     L.orbgpu_compute_image_bounds.argtypes = [vp, vp, vp, i32, i32, i32, C.POINTER(GridGeom)]
     L.orbgpu_set_undistortion.argtypes = [vp, vp, vp, i32]

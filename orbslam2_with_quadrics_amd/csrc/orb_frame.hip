@@ -61,3 +61,41 @@ void og_launch_undistort_points(hipStream_t s, const float* xy, float* out, int 
 {
     if (n > 0) hipLaunchKernelGGL(og_undistort_points_kernel, dim3((n + 63) / 64), dim3(64), 0, s, xy, out, n, U);
 }
+
+// Frame::ComputeStereoFromRGBD (src/Frame.cc:643-664): mvDepth = imDepth.at<float>(v, u) at the distorted
+// keypoint (float -> int truncation), mvuRight = kpU.x - mbf/d where d > 0.  The depth map is either the
+// CV_32F image the reference receives, or the raw CV_16U image with Tracking::GrabImageRGBD's
+// convertTo(CV_32F, mDepthMapFactor) fused in (src/Tracking.cc:227-228: one product per sample).
+__global__ __launch_bounds__(256) void og_rgbd_kernel(const orbgpu_kp_dev* __restrict__ kps,
+                                                      const orbgpu_kp_dev* __restrict__ kps_un, const int* counts,
+                                                      int n_fixed, int frame_cap, const uint8_t* __restrict__ depth,
+                                                      int is_u16, float factor, long long pitch, long long fstride,
+                                                      float mbf, float* __restrict__ uright, float* __restrict__ dout)
+{
+    const int b = blockIdx.y;
+    const int n = counts ? counts[b] : n_fixed;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const long long o = (long long)b * frame_cap + i;
+        const orbgpu_kp_dev kp = kps[o];
+        const int v = (int)kp.y, u = (int)kp.x;
+        const uint8_t* row = depth + (long long)b * fstride + (long long)v * pitch;
+        const float d = is_u16 ? __fmul_rn((float)((const uint16_t*)row)[u], factor) : ((const float*)row)[u];
+        float ur = -1.0f, de = -1.0f;
+        if (d > 0) {
+            de = d;
+            ur = __fsub_rn(kps_un[o].x, __fdiv_rn(mbf, d));
+        }
+        uright[o] = ur;
+        dout[o] = de;
+    }
+}
+
+void og_launch_rgbd(hipStream_t s, const orbgpu_kp_dev* kps, const orbgpu_kp_dev* kps_un, const int* counts,
+                    int n_fixed, int frame_cap, const uint8_t* depth, int is_u16, float factor, long long pitch,
+                    long long fstride, float mbf, float* uright, float* dout, int B)
+{
+    const int gx = counts ? (frame_cap + 255) / 256 : (n_fixed + 255) / 256;
+    if (gx > 0)
+        hipLaunchKernelGGL(og_rgbd_kernel, dim3(gx, B), dim3(256), 0, s, kps, kps_un, counts, n_fixed, frame_cap, depth,
+                           is_u16, factor, pitch, fstride, mbf, uright, dout);
+}

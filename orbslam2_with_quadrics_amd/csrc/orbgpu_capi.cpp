@@ -851,6 +851,58 @@ int orbgpu_batch_outputs_undistorted(orbgpu_ctx* c, orbgpu_keypoint** d_kps_un, 
     return ORBGPU_OK;
 }
 
+// ---- Frame::ComputeStereoFromRGBD (src/Frame.cc:643-664) ---------------------------------------------------
+int orbgpu_compute_stereo_from_rgbd_batch(orbgpu_ctx* c, const void* d_depth, int is_u16, float factor,
+                                          size_t pitch_bytes, size_t frame_stride_bytes, float mbf, float* d_uright,
+                                          float* d_depth_out)
+{
+    if (!c || !c->last_B || !d_depth || !d_uright || !d_depth_out) return ORBGPU_ERR_ARG;
+    const size_t px = is_u16 ? 2 : 4;
+    if (pitch_bytes < (size_t)c->W * px || pitch_bytes % px) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    timer_mark(c, "rgbd_in");
+    og_launch_rgbd(c->stream, c->kps.p, kps_match(c), c->counts.p, 0, c->plan.frame_cap, (const uint8_t*)d_depth,
+                   is_u16 ? 1 : 0, factor, (long long)pitch_bytes, (long long)frame_stride_bytes, mbf, d_uright,
+                   d_depth_out, c->last_B);
+    timer_mark(c, "rgbd");
+    HIP_TRY(c, hipGetLastError());
+    return ORBGPU_OK;
+}
+
+int orbgpu_compute_stereo_from_rgbd(orbgpu_ctx* c, const void* depth, int is_u16, float factor, size_t step_bytes,
+                                    float mbf, float* uright, float* depth_out, int cap, int* n)
+{
+    if (!c || !depth || !n) return ORBGPU_ERR_ARG;
+    if (c->last_B != 1) {
+        c->err = "ComputeStereoFromRGBD: host form needs one extracted frame";
+        return ORBGPU_ERR_ARG;
+    }
+    const size_t px = is_u16 ? 2 : 4;
+    if (step_bytes < (size_t)c->W * px) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t pitch = ((size_t)c->W * px + 255) & ~(size_t)255;
+    const int fc = c->plan.frame_cap;
+    HIP_TRY(c, ensure(c->mscratch, kCarvePad + pitch * (size_t)c->H + (size_t)fc * 8));
+    uint8_t* cur = c->mscratch.p;
+    uint8_t* dd = scratch_carve(cur, pitch * (size_t)c->H);
+    float* ur = (float*)scratch_carve(cur, (size_t)fc * 4);
+    float* de = (float*)scratch_carve(cur, (size_t)fc * 4);
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpy2DAsync(dd, pitch, depth, step_bytes, (size_t)c->W * px, (size_t)c->H, hipMemcpyHostToDevice, s));
+    int r = orbgpu_compute_stereo_from_rgbd_batch(c, dd, is_u16, factor, pitch, pitch * (size_t)c->H, mbf, ur, de);
+    if (r) return r;
+    int cnt = 0;
+    HIP_TRY(c, hipMemcpyAsync(&cnt, c->counts.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    *n = cnt;
+    if (cnt > cap) return ORBGPU_ERR_CAPACITY;
+    if (cnt > 0) {
+        if (uright) HIP_TRY(c, hipMemcpy(uright, ur, (size_t)cnt * 4, hipMemcpyDeviceToHost));
+        if (depth_out) HIP_TRY(c, hipMemcpy(depth_out, de, (size_t)cnt * 4, hipMemcpyDeviceToHost));
+    }
+    return ORBGPU_OK;
+}
+
 // ---- stereo: Frame::ComputeStereoMatches (src/Frame.cc:466-640) -------------------------------------
 static int stereo_launch(orbgpu_ctx* L, orbgpu_ctx* R, float mbf, float mb, float* d_ur, float* d_depth, int* d_nm)
 {

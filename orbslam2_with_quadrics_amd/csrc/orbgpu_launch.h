@@ -163,3 +163,8 @@ struct OgUndistort {
 void og_launch_undistort(hipStream_t s, const orbgpu_kp_dev* in, orbgpu_kp_dev* out, const int* counts, int n_fixed,
                          int frame_cap, const OgUndistort& U, int B);
 void og_launch_undistort_points(hipStream_t s, const float* xy, float* out, int n, const OgUndistort& U);
+// Frame::ComputeStereoFromRGBD over B frames (counts == nullptr: one frame of n_fixed keypoints); depth rows
+// are `pitch` bytes apart, frames `fstride` bytes; is_u16: raw CV_16U scaled by `factor`, else CV_32F
+void og_launch_rgbd(hipStream_t s, const orbgpu_kp_dev* kps, const orbgpu_kp_dev* kps_un, const int* counts,
+                    int n_fixed, int frame_cap, const uint8_t* depth, int is_u16, float factor, long long pitch,
+                    long long fstride, float mbf, float* uright, float* dout, int B);

@@ -259,3 +259,20 @@ def ComputeImageBounds(extractor: ORBextractor, K4, dist, cols: int, rows: int) 
                                                 int(dist.size), cols, rows, C.byref(g))
     _lib.check(extractor.ctx, rc, "orbgpu_compute_image_bounds")
     return g
+
+
+def ComputeStereoFromRGBD(extractor: ORBextractor, depth: np.ndarray, mbf: float, depth_map_factor: float = 1.0):
+    """Frame::ComputeStereoFromRGBD (src/Frame.cc:643-664) for the frame `extractor` processed last.
+    depth: float32 map (as Frame receives it) or the raw uint16 image, scaled by mDepthMapFactor =
+    1/DepthMapFactor as Tracking::GrabImageRGBD does (src/Tracking.cc:227-228).  Returns (mvuRight, mvDepth)."""
+    is_u16 = depth.dtype == np.uint16
+    dep = np.ascontiguousarray(depth, np.uint16 if is_u16 else np.float32)
+    L = _lib.lib()
+    cap = L.orbgpu_max_keypoints(extractor.ctx)
+    ur = np.empty(max(cap, 1), np.float32)
+    de = np.empty(max(cap, 1), np.float32)
+    n = C.c_int(0)
+    rc = L.orbgpu_compute_stereo_from_rgbd(extractor.ctx, _p(dep), int(is_u16), float(depth_map_factor),
+                                           dep.strides[0], float(mbf), _p(ur), _p(de), cap, C.byref(n))
+    _lib.check(extractor.ctx, rc, "orbgpu_compute_stereo_from_rgbd")
+    return ur[:n.value].copy(), de[:n.value].copy()

@@ -188,3 +188,18 @@ def keyframe_points(seed: int, kps, desc, cam_kf: dict, depth=(2.0, 9.0), p_inva
     mn = mx / scale_factor ** (nlevels - 1)
     return dict(kps=lf["kps"], valid=(rng.random(n) >= p_invalid).astype(np.uint8), pos=lf["pos"],
                 max_dist=mx.astype(np.float32), min_dist=mn.astype(np.float32), desc=lf["desc"])
+
+
+def depth_u16(seed: int, height: int, width: int, p_hole: float = 0.08) -> np.ndarray:
+    """TUM-style raw depth (uint16, DepthMapFactor 5000 => 0.5-8 m as 2500-40000): smooth slanted planes
+    plus blocky objects, with missing-depth holes (0)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    yy, xx = np.mgrid[0:height, 0:width].astype(np.float32)
+    d = 2.0 + 3.0 * yy / height + 0.5 * np.sin(xx / 57.0)
+    for _ in range(20):
+        w, h = int(rng.integers(20, 200)), int(rng.integers(20, 200))
+        x, y = int(rng.integers(0, width)), int(rng.integers(0, height))
+        d[y:y + h, x:x + w] = rng.uniform(0.5, 8.0)
+    raw = np.clip(np.rint(d * 5000.0), 0, 65535).astype(np.uint16)
+    raw[rng.random((height, width)) < p_hole] = 0
+    return raw

@@ -97,3 +97,60 @@ def test_batch_undistortion_feeds_search_for_initialization(gpu, oracle):
     finally:
         ex_ref.device_free(d1)
         ex.device_free(dB)
+
+
+@pytest.mark.parametrize("u16,undist", [(True, True), (False, True), (True, False)])
+def test_stereo_from_rgbd_vs_oracle(gpu, oracle, u16, undist):
+    img = synthetic.frame(21, 480, 640)
+    raw = synthetic.depth_u16(21, 480, 640)
+    factor = float(np.float32(1.0) / np.float32(5000.0))
+    mbf = 40.0
+    ex = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    if undist:
+        ex.set_undistortion(TUM1["K4"], TUM1["dist"])
+    k, _ = ex(img)
+    dep_f = oracle.depth_u16_to_f32(raw, factor)
+    ur, de = gpu.ComputeStereoFromRGBD(ex, raw if u16 else dep_f, mbf, factor)
+    ku = oracle.undistort_keypoints(TUM1["K4"], TUM1["dist"], k) if undist else k
+    wur, wde = oracle.stereo_from_rgbd(k, ku, dep_f, mbf)
+    assert ur.tobytes() == wur.tobytes() and de.tobytes() == wde.tobytes()
+    assert (de > 0).sum() > 100
+
+
+def test_stereo_from_rgbd_batch_vs_oracle(gpu, oracle):
+    import ctypes as C
+
+    from orbslam2_with_quadrics_amd import _lib
+
+    B, rows, cols = 4, 480, 640
+    imgs = np.stack([synthetic.frame(40 + b, rows, cols) for b in range(B)])
+    deps = np.stack([synthetic.depth_u16(40 + b, rows, cols) for b in range(B)])
+    factor = float(np.float32(1.0) / np.float32(5000.0))
+    ex = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    ex.set_undistortion(TUM2["K4"], TUM2["dist"])
+    di = ex.device_alloc(imgs.nbytes)
+    dd = ex.device_alloc(deps.nbytes)
+    try:
+        ex.h2d(di, imgs)
+        ex.h2d(dd, deps)
+        ex.extract_batch_device(di, B, cols, rows, cols, rows * cols)
+        _, _, d_counts, cap = ex.batch_outputs()
+        dout = ex.device_alloc(B * cap * 8)
+        _lib.check(ex.ctx, _lib.lib().orbgpu_compute_stereo_from_rgbd_batch(
+            ex.ctx, C.c_void_p(dd), 1, factor, cols * 2, rows * cols * 2, 40.0, C.c_void_p(dout),
+            C.c_void_p(dout + B * cap * 4)), "rgbd_batch")
+        ex.synchronize()
+        ur = np.zeros((B, cap), np.float32)
+        de = np.zeros((B, cap), np.float32)
+        ex.d2h(ur, dout)
+        ex.d2h(de, dout + B * cap * 4)
+        oe = oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+        for b in range(B):
+            k, _ = oe(imgs[b])
+            ku = oracle.undistort_keypoints(TUM2["K4"], TUM2["dist"], k)
+            wur, wde = oracle.stereo_from_rgbd(k, ku, oracle.depth_u16_to_f32(deps[b], factor), 40.0)
+            assert ur[b, :len(k)].tobytes() == wur.tobytes() and de[b, :len(k)].tobytes() == wde.tobytes()
+        ex.device_free(dout)
+    finally:
+        ex.device_free(di)
+        ex.device_free(dd)

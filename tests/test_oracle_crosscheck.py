@@ -286,3 +286,25 @@ def test_search_by_projection_kf_python_restatement(oracle, seed):
         wn, wow = refpy.search_by_projection_kf(Fp, cur, kf, th, orbdist, ori, owner0)
         assert n == wn and ow.tolist() == wow
         assert n > 10
+
+
+def test_stereo_from_rgbd_restatement(oracle):
+    from orbslam2_with_quadrics_amd import synthetic
+
+    img = synthetic.frame(9, 480, 640)
+    ex = oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+    k, _ = ex(img)
+    ku = oracle.undistort_keypoints(TUM1["K4"], TUM1["dist"], k)
+    raw = synthetic.depth_u16(9, 480, 640)
+    factor = np.float32(1.0) / np.float32(5000.0)
+    dep = oracle.depth_u16_to_f32(raw, float(factor))
+    assert np.array_equal(dep, raw.astype(np.float32) * factor)
+    mbf = np.float32(40.0)
+    ur, de = oracle.stereo_from_rgbd(k, ku, dep, float(mbf))
+    for i in range(len(k)):
+        d = dep[int(np.float32(k["y"][i])), int(np.float32(k["x"][i]))]
+        if d > 0:
+            assert de[i] == d and ur[i] == np.float32(ku["x"][i] - np.float32(mbf / d))
+        else:
+            assert de[i] == -1 and ur[i] == -1
+    assert (de > 0).sum() > len(k) // 2 and (de == -1).sum() > 0
