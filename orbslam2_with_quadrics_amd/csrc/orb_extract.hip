@@ -1,9 +1,9 @@
 // orb_extract.hip -- gfx950 kernels of ORBextractor::operator() (src/ORBextractor.cc:1043-1105).
 //
 //   k1 og_resize_kernel    : one chained pyramid level (cv::resize INTER_LINEAR 8U, scalar form)
-//   k2 og_fast_cells_kernel: one 64-lane wave per FAST cell: ROI -> LDS, FAST-9 score, cell-local
-//                            3x3 NMS, the reference's 20 -> 7 threshold fallback, ballot/mbcnt
-//                            compaction into the (frame, level) candidate slots
+//   k2 og_fast_blocks_kernel: one 512-thread workgroup per block of up to 2x2 FAST cells: ROI -> LDS,
+//                            threshold-free quick test, FAST-9 score, same-cell 3x3 NMS, the reference's
+//                            per-cell 20 -> 7 fallback, ballot compaction into the (frame, level) slots
 //   k3 og_octree_kernel    : one 1024-thread workgroup per (frame, level): the DistributeOctTree list
 //                            simulation as data-parallel rounds (LDS node table, block scans)
 //   k4 og_describe_kernel  : one wave per keypoint: 43x43 raw patch -> LDS, IC angle, fused 7x7
@@ -175,37 +175,33 @@ __device__ __forceinline__ int og_fast_M(const uint8_t* p, int st)
     return M > 0 ? M : 0;
 }
 
-#define OG_ROI_MAX (OG_MAX_CELL_W + 6)
-#define OG_RS 72  // LDS row stride of the ROI tile: circle offsets become compile-time immediates
-
-// exact M of the pixel at p (ROI tile with stride OG_RS)
-__device__ __forceinline__ int og_fast_M_tile(const uint8_t* p) { return og_fast_M(p, OG_RS); }
 
 // OpenCV FAST_t quick rejection (src: cv::FAST, pairs {k, k+8}): a pixel can only be a corner at
 // threshold t if for every opposite pair one pixel is darker than v-t (resp. brighter than v+t).
 // Necessary condition => every pixel that fails it has M <= t.  Restated threshold-free:
 //   dark(t)   <=>  max_k min(c_k, c_k+8) < v - t,   bright(t) <=> min_k max(c_k, c_k+8) > v + t,
 // (16 byte loads, 8 min + 8 max reductions, 2 compares).
+template <int RS>
 __device__ __forceinline__ bool og_fast_quick(const uint8_t* p, int t)
 {
     const int v = p[0];
     int c[16];
-    c[0] = p[3 * OG_RS];
-    c[1] = p[1 + 3 * OG_RS];
-    c[2] = p[2 + 2 * OG_RS];
-    c[3] = p[3 + 1 * OG_RS];
+    c[0] = p[3 * RS];
+    c[1] = p[1 + 3 * RS];
+    c[2] = p[2 + 2 * RS];
+    c[3] = p[3 + 1 * RS];
     c[4] = p[3];
-    c[5] = p[3 - 1 * OG_RS];
-    c[6] = p[2 - 2 * OG_RS];
-    c[7] = p[1 - 3 * OG_RS];
-    c[8] = p[-3 * OG_RS];
-    c[9] = p[-1 - 3 * OG_RS];
-    c[10] = p[-2 - 2 * OG_RS];
-    c[11] = p[-3 - 1 * OG_RS];
+    c[5] = p[3 - 1 * RS];
+    c[6] = p[2 - 2 * RS];
+    c[7] = p[1 - 3 * RS];
+    c[8] = p[-3 * RS];
+    c[9] = p[-1 - 3 * RS];
+    c[10] = p[-2 - 2 * RS];
+    c[11] = p[-3 - 1 * RS];
     c[12] = p[-3];
-    c[13] = p[-3 + 1 * OG_RS];
-    c[14] = p[-2 + 2 * OG_RS];
-    c[15] = p[-1 + 3 * OG_RS];
+    c[13] = p[-3 + 1 * RS];
+    c[14] = p[-2 + 2 * RS];
+    c[15] = p[-1 + 3 * RS];
     int md = 0, mb = 255;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
@@ -215,12 +211,32 @@ __device__ __forceinline__ bool og_fast_quick(const uint8_t* p, int t)
     return (md < v - t) | (mb > v + t);
 }
 
-// cell-local 3x3 NMS at two thresholds at once: keep iff M > t and (M-1) > every neighbour's score, a
-// neighbour's score being M'-1 if it is a corner at t (M' > t) inside the detection area, else 0
-__device__ __forceinline__ void og_nms_keep2(const uint8_t* Ms, int i, int j, int dw, int dh, int ta, int tb,
-                                             bool& ka, bool& kb)
+#ifndef OG_EXP_FAST_STOP
+#define OG_EXP_FAST_STOP 0
+#endif
+
+// ------------------------------------------------------------------------------------------------
+// k2': FAST over blocks of up to 2x2 cells.  The cells' detection areas tile a level without overlap
+// (cell j covers [minB + j*wCell + 3, minB + (j+1)*wCell + 3); only the last row/column is clipped), so a
+// block's detection area is the union and a pixel's cell is (i >= hCell, j >= wCell).  Every per-cell rule
+// of src/ORBextractor.cc:789-829 + cv::FAST is kept: the NMS only sees corners of the same cell, and each
+// cell falls back to minThFAST on its own.  One 512-thread workgroup per block: 4x fewer workgroups, one
+// global reservation per block, 15 % less halo than per-cell ROIs.
+// ------------------------------------------------------------------------------------------------
+#define FB_NT 512
+#define FB_RS 92                 // ROI row stride in LDS (>= 86 columns + 3 misalignment, dword multiple)
+#define FB_ROWS 86               // ROI rows (detection <= 80 + 6)
+#define FB_MW 80                 // detection width/height capacity of a block (2 x 40 or 1 x 64)
+#define FB_DW ((FB_RS / 4) < 32 ? (FB_RS / 4) : 32)
+
+__device__ __forceinline__ int og_fast_M_blk(const uint8_t* p) { return og_fast_M(p, FB_RS); }
+
+// cell-local 3x3 NMS at two thresholds, neighbours outside the pixel's cell count as 0
+__device__ __forceinline__ void og_nms_keep2_blk(const uint8_t* Ms, int i, int j, int dw, int dh, int wC, int hC,
+                                                 int ta, int tb, bool& ka, bool& kb)
 {
-    const int m = Ms[i * OG_MAX_CELL_W + j];
+    const int m = Ms[i * FB_MW + j];
+    const int ci = i >= hC, cj = j >= wC;
     int na = 0, nb = 0;
 #pragma unroll
     for (int di = -1; di <= 1; di++)
@@ -228,8 +244,8 @@ __device__ __forceinline__ void og_nms_keep2(const uint8_t* Ms, int i, int j, in
         for (int dj = -1; dj <= 1; dj++) {
             if (di == 0 && dj == 0) continue;
             const int ii = i + di, jj = j + dj;
-            const bool in = ii >= 0 && ii < dh && jj >= 0 && jj < dw;
-            const int mn = in ? (int)Ms[ii * OG_MAX_CELL_W + jj] : 0;
+            const bool in = ii >= 0 && ii < dh && jj >= 0 && jj < dw && (ii >= hC) == ci && (jj >= wC) == cj;
+            const int mn = in ? (int)Ms[ii * FB_MW + jj] : 0;
             na = max(na, mn > ta ? mn - 1 : 0);
             nb = max(nb, mn > tb ? mn - 1 : 0);
         }
@@ -237,29 +253,23 @@ __device__ __forceinline__ void og_nms_keep2(const uint8_t* Ms, int i, int j, in
     kb = m > tb && m - 1 > nb;
 }
 
-#define FAST_NT 256
-#ifndef OG_EXP_FAST_STOP
-#define OG_EXP_FAST_STOP 0
-#endif
-
-// One 256-thread workgroup (4 waves) per FAST cell: the cell's ROI, score map and survivor list live in
-// LDS shared by the four waves (full occupancy at ~17 KB per workgroup).
-__global__ __launch_bounds__(FAST_NT, 8) void og_fast_cells_kernel(OgPlan P, const OgCell* __restrict__ cells,
-                                                                const uint8_t* __restrict__ img0, long long pitch0,
-                                                                long long fstride0, const uint8_t* __restrict__ pyr,
-                                                                u64* __restrict__ cand, int* __restrict__ cand_count,
-                                                                int* __restrict__ status)
+__global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_fast_blocks_kernel(OgPlan P, const OgCell* __restrict__ blocks,
+                                                               const uint8_t* __restrict__ img0, long long pitch0,
+                                                               long long fstride0, const uint8_t* __restrict__ pyr,
+                                                               u64* __restrict__ cand, int* __restrict__ cand_count,
+                                                               int* __restrict__ status)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t roi[OG_ROI_MAX * OG_RS + 16];
-    __shared__ __attribute__((aligned(16))) uint8_t Ms[OG_MAX_CELL_W * OG_MAX_CELL_W];
-    __shared__ uint16_t lst[OG_MAX_CELL_W * OG_MAX_CELL_W];
-    __shared__ int sh_n[6];  // 0: survivors, 1/4: keep count at t1/t2, 2: emission base, 3: cursor
+    __shared__ __attribute__((aligned(16))) uint8_t roi[FB_ROWS * FB_RS + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t Ms[FB_MW * FB_MW];
+    __shared__ uint16_t lst[FB_MW * FB_MW];
+    __shared__ int sh_n[4];        // 0: survivors, 1: total kept, 2: emission base, 3: cursor
+    __shared__ int cnt1[4], cnt2[4];
     const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int f = (int)(lin / gridDim.x);
-    const OgCell cd = cells[lin % gridDim.x];
+    const OgCell cd = blocks[lin % gridDim.x];
     const int l = cd.level;
     const OgLevel& L = P.lv[l];
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint8_t* img;
     long long pitch;
     if (l == 0) {
@@ -271,39 +281,38 @@ __global__ __launch_bounds__(FAST_NT, 8) void og_fast_cells_kernel(OgPlan P, con
     }
     const int rw = cd.x1 - cd.x0, rh = cd.y1 - cd.y0;
     const int dw = rw - 6, dh = rh - 6;
+    const int wC = L.wCell, hC = L.hCell;
     if (dw <= 0 || dh <= 0) return;
-    if (tid < 6) sh_n[tid] = 0;
-    // ---- ROI -> LDS.  Fast path: 4-byte aligned rows -> whole dwords land at roi + r*OG_RS + 4q and
-    // the ROI origin sits `mis` bytes into every LDS row.
+    if (tid < 4) {
+        sh_n[tid] = 0;
+        cnt1[tid] = 0;
+        cnt2[tid] = 0;
+    }
+    // ---- ROI -> LDS (dword loads of 4-byte aligned rows, all issued before the LDS stores)
     const uint8_t* row0 = img + (long long)cd.y0 * pitch + cd.x0;
     const int mis = (int)((uintptr_t)row0 & 3);
     const bool aligned_rows = ((pitch & 3) == 0);
-    uint8_t* T = roi + (aligned_rows ? mis : 0);  // T[r*OG_RS + c] = ROI pixel (r, c)
+    uint8_t* T = roi + (aligned_rows ? mis : 0);  // T[r*FB_RS + c] = ROI pixel (r, c)
     if (aligned_rows) {
-        // all loads of a thread issued before any LDS store: one memory latency, not five
         const int nd = (rw + mis + 3) >> 2;
-        uint32_t buf[5][2];
+        uint32_t buf[6];
 #pragma unroll
-        for (int k = 0; k < 5; k++)
+        for (int k = 0; k < 6; k++) {
+            const int r = (tid >> 5) + 16 * k, q = tid & 31;
+            buf[k] = (r < rh && q < nd) ? ((const uint32_t*)(row0 + (long long)r * pitch - mis))[q] : 0u;
+        }
 #pragma unroll
-            for (int qq = 0; qq < 2; qq++) {
-                const int r = (tid >> 4) + 16 * k, q = (tid & 15) + 16 * qq;
-                buf[k][qq] = (r < rh && q < nd) ? ((const uint32_t*)(row0 + (long long)r * pitch - mis))[q] : 0u;
-            }
-#pragma unroll
-        for (int k = 0; k < 5; k++)
-#pragma unroll
-            for (int qq = 0; qq < 2; qq++) {
-                const int r = (tid >> 4) + 16 * k, q = (tid & 15) + 16 * qq;
-                if (r < rh && q < nd) *(uint32_t*)&roi[r * OG_RS + 4 * q] = buf[k][qq];
-            }
+        for (int k = 0; k < 6; k++) {
+            const int r = (tid >> 5) + 16 * k, q = tid & 31;
+            if (r < rh && q < nd) *(uint32_t*)&roi[r * FB_RS + 4 * q] = buf[k];
+        }
     } else {
-        for (int r = tid >> 6; r < rh; r += FAST_NT / 64) {
+        for (int r = wv; r < rh; r += FB_NT / 64) {
             const uint8_t* src = row0 + (long long)r * pitch;
-            for (int c = lane; c < rw; c += 64) roi[r * OG_RS + c] = src[c];
+            for (int c = lane; c < rw; c += 64) roi[r * FB_RS + c] = src[c];
         }
     }
-    for (int idx = tid * 4; idx < dh * OG_MAX_CELL_W; idx += FAST_NT * 4) *(uint32_t*)&Ms[idx] = 0u;
+    for (int idx = tid * 4; idx < dh * FB_MW; idx += FB_NT * 4) *(uint32_t*)&Ms[idx] = 0u;
     __syncthreads();
 #if OG_EXP_FAST_STOP == 1  // timing experiments only (tools/fast_variants.py): results are wrong
     if (roi[tid] == 255 && roi[tid + 1] == 254) cand_count[0] = 1;
@@ -311,24 +320,17 @@ __global__ __launch_bounds__(FAST_NT, 8) void og_fast_cells_kernel(OgPlan P, con
 #endif
     const int t1 = min(max(P.iniTh, 0), 255), t2 = min(max(P.minTh, 0), 255);
     const int tq = min(t1, t2);
-    // ---- stage 1: quick test on every detection pixel at the weaker threshold, ballot-compacted
-    // survivor list (u16 pixel index; bits 12/13 later carry the NMS keep flags)
-    {
-        const bool two = dw <= 32;
-        const int rowsPer = two ? FAST_NT / 32 : FAST_NT / 64;
-        const int li = two ? (tid >> 5) : (tid >> 6), lj = two ? (tid & 31) : lane;
-        for (int i0 = 0; i0 < dh; i0 += rowsPer) {
-            const int i = i0 + li, j = lj;
-            bool sv = false;
-            if (i < dh && j < dw) sv = og_fast_quick(&T[(i + 3) * OG_RS + (j + 3)], tq);
+    // ---- stage 1: quick test on every detection pixel (one row per wave, lanes over columns)
+    for (int i = wv; i < dh; i += FB_NT / 64) {
+        for (int j0 = 0; j0 < dw; j0 += 64) {
+            const int j = j0 + lane;
+            const bool sv = j < dw && og_fast_quick<FB_RS>(&T[(i + 3) * FB_RS + (j + 3)], tq);
             const u64 mask = __ballot(sv);
             if (mask) {
                 int base = 0;
                 if (lane == 0) base = atomicAdd(&sh_n[0], __popcll(mask));
                 base = __shfl(base, 0);
-                if (sv)
-                    lst[base + __popcll(mask & ((1ull << lane) - 1ull))] =
-                        (uint16_t)(i * OG_MAX_CELL_W + j);
+                if (sv) lst[base + __popcll(mask & ((1ull << lane) - 1ull))] = (uint16_t)(i * FB_MW + j);
             }
         }
     }
@@ -339,33 +341,35 @@ __global__ __launch_bounds__(FAST_NT, 8) void og_fast_cells_kernel(OgPlan P, con
     return;
 #endif
     if (nsurv == 0) return;
-    // ---- stage 2: exact M for every survivor of the weaker threshold
-    for (int e = tid; e < nsurv; e += FAST_NT) {
-        const int pix = lst[e] & 0xfff;
-        const int i = pix / OG_MAX_CELL_W, j = pix % OG_MAX_CELL_W;
-        Ms[pix] = (uint8_t)og_fast_M_tile(&T[(i + 3) * OG_RS + (j + 3)]);
+    // ---- stage 2: exact M for every survivor (eager: ~92 % of 2x2 blocks hold a cell that falls back to
+    // minThFAST, so a lazy second pass costs more than it saves)
+    for (int e = tid; e < nsurv; e += FB_NT) {
+        const int pix = lst[e] & 0x1fff;
+        const int i = pix / FB_MW, j = pix % FB_MW;
+        Ms[pix] = (uint8_t)og_fast_M_blk(&T[(i + 3) * FB_RS + (j + 3)]);
     }
     __syncthreads();
-    // ---- stage 3: NMS at iniThFAST and at minThFAST in one pass (src/ORBextractor.cc:809-816 keeps the
-    // first unless the cell is empty at it); the keep bits are stored in the list entry (bits 12, 13)
-    {
-        int c1 = 0, c2 = 0;
-        for (int e = tid; e - tid < nsurv; e += FAST_NT) {
-            bool k1 = false, k2 = false;
-            if (e < nsurv) {
-                const int pix = lst[e] & 0xfff;
-                og_nms_keep2(Ms, pix / OG_MAX_CELL_W, pix % OG_MAX_CELL_W, dw, dh, t1, t2, k1, k2);
-                lst[e] = (uint16_t)(pix | (k1 ? 0x1000 : 0) | (k2 ? 0x2000 : 0));
-            }
-            c1 += __popcll(__ballot(k1));
-            c2 += __popcll(__ballot(k2));
-        }
-        if (lane == 0 && c1) atomicAdd(&sh_n[1], c1);
-        if (lane == 0 && c2) atomicAdd(&sh_n[4], c2);
+    // ---- stage 3: same-cell NMS at both thresholds; keep bits in the entry (13: t1, 14: t2), counts per cell
+    for (int e = tid; e < nsurv; e += FB_NT) {
+        const int pix = lst[e] & 0x1fff;
+        const int i = pix / FB_MW, j = pix % FB_MW;
+        bool k1, k2;
+        og_nms_keep2_blk(Ms, i, j, dw, dh, wC, hC, t1, t2, k1, k2);
+        lst[e] = (uint16_t)(pix | (k1 ? 0x2000 : 0) | (k2 ? 0x4000 : 0));
+        const int cell = (i >= hC) * 2 + (j >= wC);
+        if (k1) atomicAdd(&cnt1[cell], 1);
+        if (k2) atomicAdd(&cnt2[cell], 1);
     }
     __syncthreads();
-    const int cnt = sh_n[1] ? sh_n[1] : sh_n[4];
-    const int kbit = sh_n[1] ? 0x1000 : 0x2000;
+    // per cell: iniThFAST unless the cell is empty at it (src/ORBextractor.cc:809-816)
+    int cnt = 0;
+    unsigned useT2 = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int a = cnt1[c];
+        cnt += a ? a : cnt2[c];
+        useT2 |= (a ? 0u : 1u) << c;
+    }
     if (cnt == 0) return;
 #if OG_EXP_FAST_STOP == 3
     if (cnt == 12345) cand_count[0] = 1;
@@ -381,19 +385,21 @@ __global__ __launch_bounds__(FAST_NT, 8) void og_fast_cells_kernel(OgPlan P, con
     if (base + cnt > L.cand_cap) return;
     u64* out = cand + (long long)f * P.cand_per_frame + L.cand_off + base;
     const int ox = cd.x0 - L.minB + 3, oy = cd.y0 - L.minB + 3;
-    for (int e = tid; e - tid < nsurv; e += FAST_NT) {
+    for (int e = tid; e - tid < nsurv; e += FB_NT) {
         int ent = 0;
         if (e < nsurv) ent = lst[e];
-        const bool keep = (ent & kbit) != 0;
+        const int pix = ent & 0x1fff;
+        const int i = pix / FB_MW, j = pix % FB_MW;
+        const int cell = (i >= hC) * 2 + (j >= wC);
+        const bool keep = e < nsurv && ((ent & (((useT2 >> cell) & 1u) ? 0x4000 : 0x2000)) != 0);
         const u64 mask = __ballot(keep);
         if (mask) {
             int wb = 0;
             if (lane == 0) wb = atomicAdd(&sh_n[3], __popcll(mask));
             wb = __shfl(wb, 0);
             if (keep) {
-                const int pix = ent & 0xfff;
                 const int pos = wb + __popcll(mask & ((1ull << lane) - 1ull));
-                out[pos] = og_pack_cand(ox + pix % OG_MAX_CELL_W, oy + pix / OG_MAX_CELL_W, Ms[pix] - 1);
+                out[pos] = og_pack_cand(ox + j, oy + i, Ms[pix] - 1);
             }
         }
     }
@@ -1080,8 +1086,8 @@ void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, lo
 void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,
                     long long fstride0, const uint8_t* pyr, u64* cand, int* cand_count, int* status, int B)
 {
-    hipLaunchKernelGGL(og_fast_cells_kernel, dim3(P.total_cells, B), dim3(FAST_NT), 0, s, P, cells, img0, pitch0, fstride0,
-                       pyr, cand, cand_count, status);
+    hipLaunchKernelGGL(og_fast_blocks_kernel, dim3(P.total_cells, B), dim3(FB_NT), 0, s, P, cells, img0, pitch0,
+                       fstride0, pyr, cand, cand_count, status);
 }
 
 void og_launch_octree(hipStream_t s, const OgPlan& P, const u64* cand, const int* cand_count, uint16_t* node_of,

@@ -227,6 +227,34 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
                 cap += (long long)((dw + 1) / 2) * ((dh + 1) / 2);  // NMS keeps an independent set
             }
         }
+        // FAST blocks of up to 2x2 valid cells (og_fast_blocks_kernel); the valid cells form a rectangle
+        // (the skip tests depend on the row or the column only)
+        {
+            std::vector<OgCell> lc(cells.begin() + L.cell_base, cells.end());
+            cells.resize(L.cell_base);
+            int nr = 0, ncl = 0;
+            for (const OgCell& cc : lc) {
+                nr = std::max(nr, (int)cc.i + 1);
+                ncl = std::max(ncl, (int)cc.j + 1);
+            }
+            if ((int)lc.size() != nr * ncl) {
+                c->err = "FAST cells do not form a rectangle";
+                return ORBGPU_ERR_INTERNAL;
+            }
+            const int bs = (L.wCell <= 40 && L.hCell <= 40) ? 2 : 1;
+            for (int bi = 0; bi < nr; bi += bs)
+                for (int bj = 0; bj < ncl; bj += bs) {
+                    const int ni = std::min(bs, nr - bi), nj = std::min(bs, ncl - bj);
+                    const OgCell& a = lc[bi * ncl + bj];
+                    const OgCell& right = lc[bi * ncl + bj + nj - 1];
+                    const OgCell& below = lc[(bi + ni - 1) * ncl + bj];
+                    OgCell blk = a;
+                    blk.pad = (short)((ni << 8) | nj);
+                    blk.x1 = right.x1;
+                    blk.y1 = below.y1;
+                    cells.push_back(blk);
+                }
+        }
         L.ncells = (int)cells.size() - L.cell_base;
         L.cand_off = cand_off;
         L.cand_cap = (int)std::max<long long>(cap, 1);

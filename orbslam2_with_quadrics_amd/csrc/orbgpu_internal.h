@@ -44,8 +44,8 @@ struct OgLevel {
     int patch_size;        // (int)(PATCH_SIZE * mvScaleFactor[l])
 };
 
-struct OgCell {            // one FAST cell ROI, src/ORBextractor.cc:789-829
-    short level, i, j, pad;
+struct OgCell {            // one FAST block of up to 2x2 cells (ROI union), src/ORBextractor.cc:789-829
+    short level, i, j, pad;   // first cell (row i, column j); pad = (cell rows << 8) | cell columns
     short x0, y0, x1, y1;  // ROI [x0,x1) x [y0,y1) in level pixels
 };
 
