@@ -475,7 +475,7 @@ __device__ __forceinline__ unsigned og_cand_order(int x, int y, const OgLevel& L
     return (unsigned)(((ci * L.nCols + cj) * L.hCell + ly) * L.wCell + lx);
 }
 
-#define OCT_U 8  // candidates per thread per pass with all loads hoisted (latency batching)
+#define OCT_U 4  // candidates per thread per pass with all loads hoisted (latency batching)
 
 #ifndef OG_OCT_PROFILE
 #define OG_OCT_PROFILE 0
@@ -492,7 +492,7 @@ __device__ unsigned long long og_oct_prof[256];
     } while (0)
 #endif
 
-__global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* __restrict__ cand,
+__global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_octree_kernel(OgPlan P, const u64* __restrict__ cand,
                                                            const int* __restrict__ cand_count,
                                                            uint16_t* __restrict__ node_of,
                                                            uint32_t* __restrict__ oct_xy,
@@ -505,9 +505,12 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
     __shared__ int splitNode[OG_OCT_MAXL];
     __shared__ int newPos[OG_OCT_MAXL];
     __shared__ int aux[OG_OCT_MAXL];
-    __shared__ __attribute__((aligned(16))) int childCnt[2][4 * OG_OCT_MAXL];  // indexed 4*node + quadrant
+    // child counts, indexed 4*node + quadrant: one buffer -- a round's counts are consumed (split set,
+    // children) before the key pass accumulates the next round's, with barriers in between; the last key
+    // pass keeps the best key per node in the same storage.  ~74 KB of LDS in total: 2 workgroups per CU.
+    __shared__ __attribute__((aligned(16))) int childCnt[4 * OG_OCT_MAXL];
     __shared__ uint16_t childPos[4 * OG_OCT_MAXL];
-    __shared__ u64 best[OG_OCT_MAXL];
+    u64* best = (u64*)childCnt;  // [OG_OCT_MAXL], final key pass only
     __shared__ int wsum[32];
     __shared__ int sv[16];
 
@@ -523,7 +526,7 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
     OCT_PROF(0, clock64());
     OCT_PROF(1, (unsigned long long)C);
     // ---- roots (src/ORBextractor.cc:552-585)
-    for (int r = tid; r < nIni; r += OCT_NT) childCnt[1][r] = 0;
+    for (int r = tid; r < nIni; r += OCT_NT) childCnt[r] = 0;
     __syncthreads();
     for (int base = tid; base < C; base += OCT_NT * OCT_U) {
         u64 kv[OCT_U];
@@ -539,7 +542,7 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
                 int r = (int)((float)(int)(kv[u] & 0xffff) / L.hX);
                 r = min(r, nIni - 1);
                 NO[k] = (uint16_t)r;
-                atomicAdd(&childCnt[1][r], 1);
+                atomicAdd(&childCnt[r], 1);
             }
         }
     }
@@ -547,7 +550,7 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
     if (tid == 0) {
         int Ln = 0;
         for (int r = 0; r < nIni; r++) {
-            const int c = childCnt[1][r];
+            const int c = childCnt[r];
             if (c > 0) {
                 OctNode n;
                 n.x0 = (short)(int)(L.hX * (float)r);
@@ -568,11 +571,10 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
         sv[2] = nIni;    // next creation id
         sv[3] = Ln == 0; // done (an empty list can never grow)
         sv[4] = 0;       // current node buffer
-        sv[7] = 0;       // current child-count buffer
         sv[8] = 0;       // `best` filled by a key pass
     }
     __syncthreads();
-    for (int q = tid; q < 4 * OG_OCT_MAXL; q += OCT_NT) childCnt[0][q] = 0;
+    for (int q = tid; q < 4 * OG_OCT_MAXL; q += OCT_NT) childCnt[q] = 0;
     __syncthreads();
     // remap keys to root positions and count the children of the first pass's splits (cnt > 1)
     for (int base = tid; base < C; base += OCT_NT * OCT_U) {
@@ -592,7 +594,7 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
                 NO[k] = (uint16_t)n;
                 const OctNode& nd = nodes[0][n];
                 if (nd.cnt > 1)
-                    atomicAdd(&childCnt[0][4 * n + og_quadrant((int)(kv[u] & 0xffff), (int)((kv[u] >> 16) & 0xffff), nd)], 1);
+                    atomicAdd(&childCnt[4 * n + og_quadrant((int)(kv[u] & 0xffff), (int)((kv[u] >> 16) & 0xffff), nd)], 1);
             }
         }
     }
@@ -601,15 +603,15 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
     OCT_PROF(2, clock64());
     for (int round = 0; round < 4096; round++) {
         if (sv[3]) break;
-        const int Ln = sv[0], mode = sv[1], cur = sv[4], cc = sv[7];
+        const int Ln = sv[0], mode = sv[1], cur = sv[4];
         OCT_PROF(8 + 4 * round, clock64());
         OCT_PROF(9 + 4 * round, (unsigned long long)Ln | ((unsigned long long)mode << 32));
         OctNode* cn = nodes[cur];
         uint8_t* cf = fresh[cur];
         OctNode* nn = nodes[cur ^ 1];
         uint8_t* nf = fresh[cur ^ 1];
-        const int* CC = childCnt[cc];
-        int* NCC = childCnt[cc ^ 1];
+        const int* CC = childCnt;
+        int* NCC = childCnt;
         __syncthreads();
         // ---- the split set of this round and its order
         const int i = tid;
@@ -768,7 +770,6 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_kernel(OgPlan P, const u64* 
             sv[2] += T;
             sv[3] = done;
             sv[4] = cur ^ 1;
-            sv[7] = cc ^ 1;
             sv[8] = done;  // `best` is valid
         }
         __syncthreads();
