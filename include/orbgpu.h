@@ -300,6 +300,36 @@ int orbgpu_compute_stereo_from_rgbd_batch(orbgpu_ctx* ctx, const void* d_depth, 
                                           size_t pitch_bytes, size_t frame_stride_bytes, float mbf, float* d_uright,
                                           float* d_depth_out);
 
+/* ---- Bag of words: Frame::ComputeBoW ---------------------------------------------------------------- */
+
+/* A DBoW2 vocabulary (ORBVocabulary = TemplatedVocabulary<FORB::TDescriptor, FORB>, include/ORBVocabulary.h)
+ * resident on the context's device. */
+typedef struct orbgpu_vocabulary orbgpu_vocabulary;
+
+/* Replaces TemplatedVocabulary::loadFromTextFile (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1420, called
+ * at src/System.cc:65): header "k L scoring weighting", then one line per node "parent isLeaf d0..d31 weight".
+ * NULL on failure (message in orbgpu_last_error(ctx)). */
+orbgpu_vocabulary* orbgpu_vocabulary_load_text(orbgpu_ctx* ctx, const char* path);
+/* The same from arrays: nn nodes 1..nn in file order (node 0 is the root). */
+orbgpu_vocabulary* orbgpu_vocabulary_create(orbgpu_ctx* ctx, int k, int L, int scoring, int weighting, int nn,
+                                            const int* parent, const uint8_t* is_leaf, const uint8_t* desc,
+                                            const double* weight);
+void orbgpu_vocabulary_destroy(orbgpu_vocabulary* voc);
+int orbgpu_vocabulary_info(const orbgpu_vocabulary* voc, int* k, int* L, int* nodes, int* words);
+
+/* Replaces void Frame::ComputeBoW() -- src/Frame.cc:395-402 --
+ * mpORBvocabulary->transform(Converter::toDescriptorVector(mDescriptors), mBowVec, mFeatVec, levelsup = 4).
+ * mBowVec as (*nwords) ascending word ids + double values; mFeatVec as (*nnodes) ascending node ids, offsets
+ * node_off[0..nnodes] into feats (feature indices in feature order).  Capacities: n each (n+1 for node_off). */
+int orbgpu_compute_bow(orbgpu_ctx* ctx, const orbgpu_vocabulary* voc, const uint8_t* desc, int n, int levelsup,
+                       int32_t* words, double* values, int* nwords, int32_t* nodes, int32_t* node_off,
+                       int32_t* feats, int* nnodes);
+/* Batched device form over the context's last batch (descriptors in HBM): per frame b, outputs at stride
+ * frame_cap (node_off: frame_cap + 1), counts in d_nwords[b] / d_nnodes[b]. */
+int orbgpu_compute_bow_batch(orbgpu_ctx* ctx, const orbgpu_vocabulary* voc, int levelsup, int32_t* d_words,
+                             double* d_values, int32_t* d_nwords, int32_t* d_nodes, int32_t* d_node_off,
+                             int32_t* d_feats, int32_t* d_nnodes);
+
 /* ---- stream / timing helpers ------------------------------------------------------------------ */
 
 /* The context's hipStream_t (as void*), e.g. for torch.cuda.ExternalStream. */

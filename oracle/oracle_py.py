@@ -72,6 +72,14 @@ def lib():
         L.oo_search_by_projection_kf.argtypes = [vp, vp, vp, f32, i32, i32, vp]
         L.oo_stereo_from_rgbd.argtypes = [vp, vp, i32, vp, i32, f32, vp, vp]
         L.oo_depth_u16_to_f32.argtypes = [vp, i32, f32, vp]
+        L.oo_vocab_from_arrays.restype = vp
+        L.oo_vocab_from_arrays.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp]
+        L.oo_vocab_load_text.restype = vp
+        L.oo_vocab_load_text.argtypes = [C.c_char_p]
+        L.oo_vocab_free.argtypes = [vp]
+        L.oo_vocab_nodes.argtypes = [vp]
+        L.oo_vocab_words.argtypes = [vp]
+        L.oo_bow_transform.argtypes = [vp, vp, i32, i32, vp, vp, C.POINTER(i32), vp, vp, vp, C.POINTER(i32)]
         L.oo_undistort_points.argtypes = [vp, vp, i32, vp, vp, i32]
         L.oo_undistort_keypoints.argtypes = [vp, vp, i32, vp, vp, i32]
         L.oo_compute_image_bounds.argtypes = [vp, vp, i32, i32, i32] + [C.POINTER(f32)] * 6
@@ -334,6 +342,45 @@ def stereo_from_rgbd(kps, kps_un, depth_f32, mbf):
     de = np.zeros(max(n, 1), np.float32)
     lib().oo_stereo_from_rgbd(_p(kps), _p(kps_un), n, _p(dep), dep.shape[1], mbf, _p(ur), _p(de))
     return ur[:n].copy(), de[:n].copy()
+
+
+class OracleVocabulary:
+    """DBoW2 TemplatedVocabulary<FORB> (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h) restated in C."""
+
+    def __init__(self, voc: dict = None, path: str = None):
+        L = lib()
+        if path is not None:
+            self._h = L.oo_vocab_load_text(path.encode())
+        else:
+            par = np.ascontiguousarray(voc["parent"], np.int32)
+            leaf = np.ascontiguousarray(voc["is_leaf"], np.uint8)
+            desc = np.ascontiguousarray(voc["desc"], np.uint8)
+            w = np.ascontiguousarray(voc["weight"], np.float64)
+            self._h = L.oo_vocab_from_arrays(voc["k"], voc["L"], voc["scoring"], voc["weighting"], len(par), _p(par),
+                                             _p(leaf), _p(desc), _p(w))
+        if not self._h:
+            raise ValueError("vocabulary rejected")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().oo_vocab_free(self._h)
+            self._h = None
+
+    def transform(self, desc, levelsup=4):
+        """-> (BowVector {word: value} as (words, values) ascending, FeatureVector as (nodes, offsets, features))."""
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(desc)
+        words = np.zeros(max(n, 1), np.int32)
+        values = np.zeros(max(n, 1), np.float64)
+        nodes = np.zeros(max(n, 1), np.int32)
+        off = np.zeros(n + 1, np.int32)
+        feats = np.zeros(max(n, 1), np.int32)
+        nw, nn = C.c_int(0), C.c_int(0)
+        lib().oo_bow_transform(self._h, _p(desc), n, levelsup, _p(words), _p(values), C.byref(nw), _p(nodes), _p(off),
+                               _p(feats), C.byref(nn))
+        m = int(off[nn.value]) if nn.value else 0
+        return ((words[:nw.value].copy(), values[:nw.value].copy()),
+                (nodes[:nn.value].copy(), off[:nn.value + 1].copy(), feats[:m].copy()))
 
 
 def undistort_keypoints(K4, dist, kps):

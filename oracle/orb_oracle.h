@@ -182,6 +182,17 @@ void oo_stereo_from_rgbd(const oo_keypoint* kps, const oo_keypoint* kps_un, int 
                          float mbf, float* uright, float* depth_out);
 void oo_depth_u16_to_f32(const uint16_t* src, int n, float factor, float* dst);
 
+/* DBoW2 vocabulary + transform (oracle/oo_bow.c): Frame::ComputeBoW, src/Frame.cc:395-402 */
+typedef struct oo_vocab oo_vocab;
+oo_vocab* oo_vocab_from_arrays(int k, int L, int scoring, int weighting, int nn, const int* parent,
+                               const uint8_t* is_leaf, const uint8_t* desc, const double* weight);
+oo_vocab* oo_vocab_load_text(const char* path);
+void oo_vocab_free(oo_vocab* v);
+int oo_vocab_nodes(const oo_vocab* v);
+int oo_vocab_words(const oo_vocab* v);
+int oo_bow_transform(const oo_vocab* v, const uint8_t* desc, int n, int levelsup, int* words, double* values,
+                     int* nwords, int* nodes, int* node_off, int* feat_idx, int* nnodes);
+
 /* cv::undistortPoints(src, dst, K, D, noArray(), K) (OpenCV 3.4, 5 iterations) on n points (x, y interleaved);
  * K4 = fx, fy, cx, cy; dist = k1, k2, p1, p2[, k3] (ndist 4 or 5). */
 void oo_undistort_points(const float* K4, const float* dist, int ndist, const float* xy, float* out, int n);

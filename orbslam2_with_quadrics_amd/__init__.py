@@ -7,6 +7,7 @@ are thin mirrors of the reference C++ classes for Python callers, tests and the 
 from .extractor import KP_DTYPE, ORBextractor  # noqa: F401
 from .matcher import (ComputeImageBounds, ComputeStereoFromRGBD, ComputeStereoMatches, Frame, ORBmatcher,  # noqa: F401
                       UndistortKeyPoints)
+from .vocabulary import ComputeBoW, ORBVocabulary  # noqa: F401
 
 __all__ = ["ORBextractor", "ORBmatcher", "Frame", "ComputeStereoMatches", "UndistortKeyPoints", "ComputeImageBounds",
-           "ComputeStereoFromRGBD", "KP_DTYPE"]
+           "ComputeStereoFromRGBD", "ORBVocabulary", "ComputeBoW", "KP_DTYPE"]

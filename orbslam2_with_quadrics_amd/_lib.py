@@ -30,6 +30,8 @@ EXPORTS = [
     "orbgpu_stage_marks", "orbgpu_undistort_keypoints", "orbgpu_compute_image_bounds", "orbgpu_set_undistortion",
     "orbgpu_batch_outputs_undistorted", "orbgpu_search_by_projection_keyframe",
     "orbgpu_compute_stereo_from_rgbd", "orbgpu_compute_stereo_from_rgbd_batch",
+    "orbgpu_vocabulary_load_text", "orbgpu_vocabulary_create", "orbgpu_vocabulary_destroy", "orbgpu_vocabulary_info",
+    "orbgpu_compute_bow", "orbgpu_compute_bow_batch",
 ]
 
 OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
@@ -129,6 +131,14 @@ def _declare(L):
                                                        C.POINTER(KeyFrameView), f32, i32, i32, vp, C.POINTER(i32)]
     L.orbgpu_compute_stereo_from_rgbd.argtypes = [vp, vp, i32, f32, sz, f32, vp, vp, i32, C.POINTER(i32)]
     L.orbgpu_compute_stereo_from_rgbd_batch.argtypes = [vp, vp, i32, f32, sz, sz, f32, vp, vp]
+    L.orbgpu_vocabulary_load_text.restype = vp
+    L.orbgpu_vocabulary_load_text.argtypes = [vp, C.c_char_p]
+    L.orbgpu_vocabulary_create.restype = vp
+    L.orbgpu_vocabulary_create.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp]
+    L.orbgpu_vocabulary_destroy.argtypes = [vp]
+    L.orbgpu_vocabulary_info.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
+    L.orbgpu_compute_bow.argtypes = [vp, vp, vp, i32, i32, vp, vp, C.POINTER(i32), vp, vp, vp, C.POINTER(i32)]
+    L.orbgpu_compute_bow_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]
     L.orbgpu_undistort_keypoints.argtypes = [vp, vp, vp, i32, vp, vp, i32]
     L.orbgpu_compute_image_bounds.argtypes = [vp, vp, vp, i32, i32, i32, C.POINTER(GridGeom)]
     L.orbgpu_set_undistortion.argtypes = [vp, vp, vp, i32]

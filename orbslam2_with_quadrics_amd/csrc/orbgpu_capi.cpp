@@ -8,6 +8,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -90,6 +92,9 @@ struct orbgpu_ctx {
     OgUndistort und{};
     DevBuf<orbgpu_kp_dev> kps_un;
     DevBuf<float> und_pts;
+    // ComputeBoW scratch: per-descriptor word / weight / node
+    DevBuf<int> bow_word, bow_nid;
+    DevBuf<double> bow_wt;
     // stereo scratch (Frame::ComputeStereoMatches)
     DevBuf<int> st_row_start, st_row_items, st_sad, st_nm;
     DevBuf<float> st_out;
@@ -535,6 +540,9 @@ void orbgpu_destroy(orbgpu_ctx* c)
     release(c->mlist_n);
     release(c->mcands);
     release(c->kps_un);
+    release(c->bow_word);
+    release(c->bow_nid);
+    release(c->bow_wt);
     release(c->und_pts);
     release(c->st_row_start);
     release(c->st_row_items);
@@ -928,6 +936,231 @@ int orbgpu_compute_stereo_from_rgbd(orbgpu_ctx* c, const void* depth, int is_u16
         if (uright) HIP_TRY(c, hipMemcpy(uright, ur, (size_t)cnt * 4, hipMemcpyDeviceToHost));
         if (depth_out) HIP_TRY(c, hipMemcpy(depth_out, de, (size_t)cnt * 4, hipMemcpyDeviceToHost));
     }
+    return ORBGPU_OK;
+}
+
+// ---- Frame::ComputeBoW: DBoW2 vocabulary + transform (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h) ------
+struct orbgpu_vocabulary {
+    int device = 0;
+    int k = 0, L = 0, scoring = 0, weighting = 0, n = 0, nwords = 0;
+    DevBuf<uint8_t> desc;
+    DevBuf<int> child_start, child_cnt, children, word_id;
+    DevBuf<double> weight;
+};
+
+static OgVocDev voc_dev(const orbgpu_vocabulary* v)
+{
+    return OgVocDev{v->n, v->L, v->scoring, v->weighting, v->desc.p, v->child_start.p, v->child_cnt.p,
+                    v->children.p, v->word_id.p, v->weight.p};
+}
+
+static void voc_release(orbgpu_vocabulary* v)
+{
+    release(v->desc);
+    release(v->child_start);
+    release(v->child_cnt);
+    release(v->children);
+    release(v->word_id);
+    release(v->weight);
+}
+
+// nn entries describe nodes 1..nn (node 0 = root) in file order: m_nodes[pid].children.push_back(nid) and
+// leaves numbered as words in file order (TemplatedVocabulary::loadFromTextFile, :1368-1418)
+static orbgpu_vocabulary* voc_build(orbgpu_ctx* c, int k, int L, int scoring, int weighting, int nn,
+                                    const int* parent, const uint8_t* is_leaf, const uint8_t* desc,
+                                    const double* weight)
+{
+    if (!c || nn < 0 || (nn && (!parent || !is_leaf || !desc || !weight))) return nullptr;
+    if (k < 0 || k > 20 || L < 1 || L > 10 || scoring < 0 || scoring > 5 || weighting < 0 || weighting > 3) {
+        c->err = "vocabulary: header out of range (loadFromTextFile limits)";
+        return nullptr;
+    }
+    const int n = nn + 1;
+    std::vector<int> cs(n + 1, 0), cc(n, 0), ch(n, 0), wid(n, -1), fill(n, 0);
+    std::vector<double> w(n, 0.0);
+    std::vector<uint8_t> d(32 * (size_t)n, 0);
+    int nwords = 0;
+    for (int i = 0; i < nn; i++) {
+        const int p = parent[i];
+        if (p < 0 || p > i) {  // a parent must precede its child (file order)
+            c->err = "vocabulary: node " + std::to_string(i + 1) + " has an invalid parent";
+            return nullptr;
+        }
+        cc[p]++;
+        std::memcpy(&d[32 * (size_t)(i + 1)], desc + 32 * (size_t)i, 32);
+        w[i + 1] = weight[i];
+        wid[i + 1] = is_leaf[i] ? nwords++ : -1;
+    }
+    for (int i = 0; i < n; i++) {
+        if (cc[i] > 64) {
+            c->err = "vocabulary: more than 64 children per node";
+            return nullptr;
+        }
+        cs[i + 1] = cs[i] + cc[i];
+    }
+    for (int i = 0; i < nn; i++) ch[cs[parent[i]] + fill[parent[i]]++] = i + 1;
+    orbgpu_vocabulary* v = new orbgpu_vocabulary();
+    v->device = c->device;
+    v->k = k;
+    v->L = L;
+    v->scoring = scoring;
+    v->weighting = weighting;
+    v->n = n;
+    v->nwords = nwords;
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = ensure(v->desc, d.size());
+    if (e == hipSuccess) e = ensure(v->child_start, (size_t)n);
+    if (e == hipSuccess) e = ensure(v->child_cnt, (size_t)n);
+    if (e == hipSuccess) e = ensure(v->children, (size_t)n);
+    if (e == hipSuccess) e = ensure(v->word_id, (size_t)n);
+    if (e == hipSuccess) e = ensure(v->weight, (size_t)n);
+    if (e == hipSuccess) e = hipMemcpy(v->desc.p, d.data(), d.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(v->child_start.p, cs.data(), sizeof(int) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(v->child_cnt.p, cc.data(), sizeof(int) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(v->children.p, ch.data(), sizeof(int) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(v->word_id.p, wid.data(), sizeof(int) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(v->weight.p, w.data(), sizeof(double) * n, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        c->err = std::string("vocabulary upload: ") + hipGetErrorString(e);
+        voc_release(v);
+        delete v;
+        return nullptr;
+    }
+    return v;
+}
+
+orbgpu_vocabulary* orbgpu_vocabulary_create(orbgpu_ctx* c, int k, int L, int scoring, int weighting, int nn,
+                                            const int* parent, const uint8_t* is_leaf, const uint8_t* desc,
+                                            const double* weight)
+{
+    return voc_build(c, k, L, scoring, weighting, nn, parent, is_leaf, desc, weight);
+}
+
+orbgpu_vocabulary* orbgpu_vocabulary_load_text(orbgpu_ctx* c, const char* path)
+{
+    if (!c || !path) return nullptr;
+    std::ifstream f(path);
+    if (!f) {
+        c->err = std::string("vocabulary: cannot open ") + path;
+        return nullptr;
+    }
+    std::string line;
+    std::getline(f, line);
+    std::stringstream hs(line);
+    int k = -1, L = -1, sc = -1, wt = -1;
+    hs >> k >> L >> sc >> wt;
+    std::vector<int> par;
+    std::vector<uint8_t> leaf, desc;
+    std::vector<double> w;
+    while (std::getline(f, line)) {
+        std::stringstream ss(line);
+        int pid, il;
+        if (!(ss >> pid >> il)) continue;  // blank line (the reference would parse it as a node)
+        uint8_t d[32];
+        for (int i = 0; i < 32; i++) {
+            int x = 0;
+            ss >> x;
+            d[i] = (uint8_t)x;
+        }
+        double ww = 0;
+        ss >> ww;
+        par.push_back(pid);
+        leaf.push_back(il > 0);
+        desc.insert(desc.end(), d, d + 32);
+        w.push_back(ww);
+    }
+    return voc_build(c, k, L, sc, wt, (int)par.size(), par.data(), leaf.data(), desc.data(), w.data());
+}
+
+void orbgpu_vocabulary_destroy(orbgpu_vocabulary* v)
+{
+    if (!v) return;
+    (void)hipSetDevice(v->device);
+    voc_release(v);
+    delete v;
+}
+
+int orbgpu_vocabulary_info(const orbgpu_vocabulary* v, int* k, int* L, int* nodes, int* words)
+{
+    if (!v) return ORBGPU_ERR_ARG;
+    if (k) *k = v->k;
+    if (L) *L = v->L;
+    if (nodes) *nodes = v->n;
+    if (words) *words = v->nwords;
+    return ORBGPU_OK;
+}
+
+int orbgpu_compute_bow_batch(orbgpu_ctx* c, const orbgpu_vocabulary* v, int levelsup, int32_t* d_words,
+                             double* d_values, int32_t* d_nwords, int32_t* d_nodes, int32_t* d_node_off,
+                             int32_t* d_feats, int32_t* d_nnodes)
+{
+    if (!c || !v || !c->last_B || !d_words || !d_values || !d_nwords || !d_nodes || !d_node_off || !d_feats ||
+        !d_nnodes)
+        return ORBGPU_ERR_ARG;
+    if (v->device != c->device) return ORBGPU_ERR_ARG;
+    const int fc = c->plan.frame_cap, B = c->last_B;
+    if (fc > OG_BOW_MAXN) {
+        c->err = "ComputeBoW: more keypoints per frame than the LDS sort holds";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, ensure(c->bow_word, (size_t)B * fc));
+    HIP_TRY(c, ensure(c->bow_nid, (size_t)B * fc));
+    HIP_TRY(c, ensure(c->bow_wt, (size_t)B * fc));
+    timer_mark(c, "bow_in");
+    og_launch_bow(c->stream, voc_dev(v), c->desc.p, c->counts.p, 0, fc, levelsup, c->bow_word.p, c->bow_wt.p,
+                  c->bow_nid.p, d_words, d_values, d_nwords, d_nodes, d_node_off, d_feats, d_nnodes, B);
+    timer_mark(c, "bow");
+    HIP_TRY(c, hipGetLastError());
+    return ORBGPU_OK;
+}
+
+int orbgpu_compute_bow(orbgpu_ctx* c, const orbgpu_vocabulary* v, const uint8_t* desc, int n, int levelsup,
+                       int32_t* words, double* values, int* nwords, int32_t* nodes, int32_t* node_off,
+                       int32_t* feats, int* nnodes)
+{
+    if (!c || !v || n < 0 || (n && !desc) || !words || !values || !nwords || !nodes || !node_off || !feats ||
+        !nnodes)
+        return ORBGPU_ERR_ARG;
+    if (v->device != c->device) return ORBGPU_ERR_ARG;
+    if (n > OG_BOW_MAXN) {
+        c->err = "ComputeBoW: more descriptors than the LDS sort holds";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
+    *nwords = 0;
+    *nnodes = 0;
+    node_off[0] = 0;
+    if (n == 0 || v->n <= 1) return ORBGPU_OK;  // empty(): v.clear(), fv.clear()
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t nn = (size_t)n;
+    HIP_TRY(c, ensure(c->mscratch, kCarvePad + nn * (32 + 4 + 8 + 4 + 4 + 8 + 4 + 4 + 4) + 64));
+    uint8_t* cur = c->mscratch.p;
+    uint8_t* dd = scratch_carve(cur, nn * 32);
+    int* wrd = (int*)scratch_carve(cur, nn * 4);
+    double* wt = (double*)scratch_carve(cur, nn * 8);
+    int* nid = (int*)scratch_carve(cur, nn * 4);
+    int* ow = (int*)scratch_carve(cur, nn * 4);
+    double* ov = (double*)scratch_carve(cur, nn * 8);
+    int* ond = (int*)scratch_carve(cur, nn * 4);
+    int* onoff = (int*)scratch_carve(cur, (nn + 1) * 4);
+    int* oft = (int*)scratch_carve(cur, nn * 4);
+    int* cnt = (int*)scratch_carve(cur, 16);
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(dd, desc, nn * 32, hipMemcpyHostToDevice, s));
+    og_launch_bow(s, voc_dev(v), dd, nullptr, n, n, levelsup, wrd, wt, nid, ow, ov, cnt, ond, onoff, oft, cnt + 1, 1);
+    HIP_TRY(c, hipGetLastError());
+    int hc[2] = {0, 0};
+    HIP_TRY(c, hipMemcpyAsync(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    *nwords = hc[0];
+    *nnodes = hc[1];
+    HIP_TRY(c, hipMemcpy(words, ow, (size_t)hc[0] * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(values, ov, (size_t)hc[0] * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(nodes, ond, (size_t)hc[1] * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(node_off, onoff, ((size_t)hc[1] + 1) * 4, hipMemcpyDeviceToHost));
+    int m = 0;
+    HIP_TRY(c, hipMemcpy(&m, onoff + hc[1], 4, hipMemcpyDeviceToHost));
+    if (m > 0) HIP_TRY(c, hipMemcpy(feats, oft, (size_t)m * 4, hipMemcpyDeviceToHost));
     return ORBGPU_OK;
 }
 

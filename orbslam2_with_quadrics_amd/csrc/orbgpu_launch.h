@@ -168,3 +168,20 @@ void og_launch_undistort_points(hipStream_t s, const float* xy, float* out, int 
 void og_launch_rgbd(hipStream_t s, const orbgpu_kp_dev* kps, const orbgpu_kp_dev* kps_un, const int* counts,
                     int n_fixed, int frame_cap, const uint8_t* depth, int is_u16, float factor, long long pitch,
                     long long fstride, float mbf, float* uright, float* dout, int B);
+
+// DBoW2 transform (orb_bow.hip): device vocabulary, children in CSR (insertion order of loadFromTextFile)
+struct OgVocDev {
+    int n, L, scoring, weighting;
+    const uint8_t* desc;      // n x 32
+    const int* child_start;   // n
+    const int* child_cnt;     // n
+    const int* children;      // n
+    const int* word_id;       // n (-1 for inner nodes)
+    const double* weight;     // n
+};
+#define OG_BOW_MAXN 8192  // features per frame the LDS sort of og_bow_reduce_kernel holds
+// counts == nullptr: one frame of n_fixed descriptors; word/wt/nid scratch and outputs at stride frame_cap
+// (node_off: frame_cap + 1)
+void og_launch_bow(hipStream_t s, const OgVocDev& V, const uint8_t* desc, const int* counts, int n_fixed,
+                   int frame_cap, int levelsup, int* word, double* wt, int* nid, int* words, double* values,
+                   int* nwords, int* nodes, int* node_off, int* feats, int* nnodes, int B);

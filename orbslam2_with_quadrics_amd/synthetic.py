@@ -203,3 +203,49 @@ def depth_u16(seed: int, height: int, width: int, p_hole: float = 0.08) -> np.nd
     raw = np.clip(np.rint(d * 5000.0), 0, 65535).astype(np.uint16)
     raw[rng.random((height, width)) < p_hole] = 0
     return raw
+
+
+def vocabulary(seed: int, k: int = 10, L: int = 6, p_short: float = 0.02, p_stop: float = 0.01,
+               scoring: int = 0, weighting: int = 0) -> dict:
+    """A DBoW2 vocabulary of ORBvoc.txt's shape (k=10, L=6, L1_NORM, TF_IDF by default) with random node
+    descriptors, in the node order of DBoW2's depth-first HKmeansStep (children of a node are contiguous,
+    created before the recursion into them).  A few nodes stop early (leaves above level L, as clusters with
+    <= 1 training feature do) and a few words are stopped (weight 0).  The real vocabulary is a 40 MB
+    download absent offline; the transform's semantics do not depend on its contents."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    parent, leaf, depth = [], [], []
+
+    def grow(pid, level):  # iterative DFS with the same order as the recursion
+        stack = [(pid, level)]
+        while stack:
+            p, lv = stack.pop()
+            first = len(parent) + 1
+            for _ in range(k):
+                parent.append(p)
+                depth.append(lv)
+                leaf.append(True)
+            ids = list(range(first, first + k))
+            kids = []
+            if lv < L:
+                for nid in ids:
+                    if rng.random() >= p_short:
+                        leaf[nid - 1] = False
+                        kids.append((nid, lv + 1))
+            stack.extend(reversed(kids))
+
+    grow(0, 1)
+    n = len(parent)
+    is_leaf = np.array(leaf, np.uint8)
+    weight = np.where(is_leaf == 1, rng.uniform(0.5, 9.0, n), 0.0)
+    weight[(is_leaf == 1) & (rng.random(n) < p_stop)] = 0.0
+    return dict(k=k, L=L, scoring=scoring, weighting=weighting, parent=np.array(parent, np.int32), is_leaf=is_leaf,
+                desc=rng.integers(0, 256, size=(n, 32), dtype=np.uint8), weight=weight)
+
+
+def write_vocabulary_text(voc: dict, path: str):
+    """DBoW2 text format (TemplatedVocabulary::saveToTextFile / ORBvoc.txt): header 'k L scoring weighting',
+    then per node 'parent isLeaf d0 .. d31 weight'."""
+    with open(path, "w") as fp:
+        fp.write(f"{voc['k']} {voc['L']} {voc['scoring']} {voc['weighting']}\n")
+        for p, lf, d, w in zip(voc["parent"], voc["is_leaf"], voc["desc"], voc["weight"]):
+            fp.write(f"{int(p)} {int(lf)} " + " ".join(str(int(x)) for x in d) + f" {float(w)!r}\n")

@@ -697,3 +697,59 @@ def search_by_projection_kf(F, cur, kf, th, orbdist, check_ori, owner=None):
                 owner[k] = -1
                 nm -= 1
     return nm, owner
+
+
+# ---------------------------------------------------------------------------------------------
+# DBoW2 TemplatedVocabulary::transform (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1127-1256)
+# ---------------------------------------------------------------------------------------------
+def bow_transform(voc, desc, levelsup=4):
+    n_nodes = len(voc["parent"]) + 1
+    children = [[] for _ in range(n_nodes)]
+    word_of = [-1] * n_nodes
+    nw = 0
+    for i, p in enumerate(voc["parent"]):
+        children[int(p)].append(i + 1)
+        if voc["is_leaf"][i]:
+            word_of[i + 1] = nw
+            nw += 1
+    bow, fv = {}, {}
+    tf = voc["weighting"] in (0, 1)
+    for fi, f in enumerate(desc):
+        nid_level = voc["L"] - levelsup
+        nid, node, level = 0, 0, 0
+        while True:
+            level += 1
+            kids = children[node]
+            node = kids[0]
+            best = popcount_dist(f, voc["desc"][node - 1])
+            for c in kids[1:]:
+                d = popcount_dist(f, voc["desc"][c - 1])
+                if d < best:
+                    best, node = d, c
+            if level == nid_level:
+                nid = node
+            if not children[node]:
+                break
+        w = float(voc["weight"][node - 1])
+        if w > 0:
+            wid = word_of[node]
+            if wid in bow:
+                if tf:
+                    bow[wid] += w
+            else:
+                bow[wid] = w
+            fv.setdefault(nid, []).append(fi)
+    items = sorted(bow.items())
+    must = voc["scoring"] != 5
+    if tf and items and not must:
+        items = [(k_, v / float(len(items))) for k_, v in items]
+    if must:
+        if voc["scoring"] == 1:
+            norm = math.sqrt(sum(v * v for _, v in items))
+        else:
+            norm = 0.0
+            for _, v in items:
+                norm += abs(v)
+        if norm > 0.0:
+            items = [(k_, v / norm) for k_, v in items]
+    return items, sorted(fv.items())

@@ -308,3 +308,24 @@ def test_stereo_from_rgbd_restatement(oracle):
         else:
             assert de[i] == -1 and ur[i] == -1
     assert (de > 0).sum() > len(k) // 2 and (de == -1).sum() > 0
+
+
+@pytest.mark.parametrize("k,L,scoring,weighting", [(10, 3, 0, 0), (6, 4, 1, 1), (9, 3, 5, 0), (8, 3, 0, 3)])
+def test_bow_transform_python_restatement(oracle, tmp_path, k, L, scoring, weighting):
+    """oo_bow_transform (ComputeBoW = DBoW2 transform, levelsup 4 -> here L-levelsup >= 0) vs refpy, from
+    arrays and through the text loader (loadFromTextFile format)."""
+    from orbslam2_with_quadrics_amd import synthetic
+
+    voc = synthetic.vocabulary(k * 100 + L, k, L, p_short=0.1, p_stop=0.05, scoring=scoring, weighting=weighting)
+    ex = oracle.OracleExtractor(500, 1.2, 8, 20, 7)
+    _, desc = ex(synthetic.frame(5, 240, 320))
+    levelsup = L - 2
+    want_bow, want_fv = refpy.bow_transform(voc, desc, levelsup)
+    path = str(tmp_path / "voc.txt")
+    synthetic.write_vocabulary_text(voc, path)
+    for ov in (oracle.OracleVocabulary(voc), oracle.OracleVocabulary(path=path)):
+        (w, v), (nodes, off, feats) = ov.transform(desc, levelsup)
+        assert [(int(a), float(b)) for a, b in zip(w, v)] == want_bow
+        got_fv = [(int(nodes[i]), feats[off[i]:off[i + 1]].tolist()) for i in range(len(nodes))]
+        assert got_fv == want_fv
+    assert len(want_bow) > 10
