@@ -147,59 +147,32 @@ def cpu_baseline(rows, cols, nfeat, seconds):
 
 
 # ------------------------------------------------------------------------------------------------
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128, help="frames per step per GPU")
-    ap.add_argument("--streams", type=int, default=2, help="concurrent extractor contexts (HIP streams) per GPU")
-    ap.add_argument("--rows", type=int, default=1080)
-    ap.add_argument("--cols", type=int, default=1920)
-    ap.add_argument("--nfeatures", type=int, default=2000)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
-    args = ap.parse_args()
-
-    world, rank, local = dist_env()
-    import torch  # noqa: F401  (imported before liborbgpu.so: one HIP runtime in the process)
-
-    from orbslam2_with_quadrics_amd import ORBextractor, _lib, synthetic
-
-    dist = dist_init(world, "nccl")
-    dev = local
-    torch.cuda.set_device(dev)
-    L = _lib.lib()
-    rows, cols, B, NF = args.rows, args.cols, args.batch, args.nfeatures
-
-    # ---- synthetic data, generated on the host once and staged into HBM (outside the timed region)
-    t = time.time()
-    scene = synthetic.make_scene(synthetic.SEED_BASE + 1000 + rank, rows, cols)
-    f1 = synthetic.render(scene, rows, cols, 0, 0, noise_seed=rank * 100000 + 1)
+# workloads: each sets up its contexts and device buffers and returns the timed step
+# ------------------------------------------------------------------------------------------------
+def _frames(synthetic, rows, cols, B, rank, seed_off=1000):
+    scene = synthetic.make_scene(synthetic.SEED_BASE + seed_off + rank, rows, cols)
     nuniq = min(B, 32)
     uniq = [synthetic.render(scene, rows, cols, int(3 + 5 * (i % 8)), int(2 + 3 * (i // 8)),
                              noise_seed=rank * 100000 + 10 + i) for i in range(nuniq)]
-    frames = np.stack([uniq[i % nuniq] for i in range(B)])
-    log(f"rank {rank}: generated {B} frames ({nuniq} distinct) in {time.time() - t:.1f}s")
+    f1 = synthetic.render(scene, rows, cols, 0, 0, noise_seed=rank * 100000 + 1)
+    return f1, np.stack([uniq[i % nuniq] for i in range(B)])
 
-    S = args.streams
-    if B % S:
-        raise SystemExit(f"--batch {B} must be a multiple of --streams {S}")
+
+def setup_mono_init(args, env):
+    """config 3: extract the initial frame and B frames, SearchForInitialization of each against it."""
+    L, C_, _lib, ORBextractor, synthetic = env["L"], C, env["_lib"], env["ORBextractor"], env["synthetic"]
+    rows, cols, B, NF, S, dev = args.rows, args.cols, args.batch, args.nfeatures, args.streams, env["dev"]
     Bs = B // S
+    f1, frames = _frames(synthetic, rows, cols, B, env["rank"])
     ex_ref = ORBextractor(NF, 1.2, 8, 20, 7, device=dev)
-    # S extractor contexts = S HIP streams, each extracting and matching B/S frames: the latency-bound
-    # stages of one stream (octree, describe, ordered matcher pass) overlap another stream's FAST/pyramid
     exs = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev) for _ in range(S)]
-    ex = exs[0]
     d_f1 = ex_ref.device_alloc(f1.nbytes)
-    d_frames = ex.device_alloc(frames.nbytes)
+    d_frames = exs[0].device_alloc(frames.nbytes)
     ex_ref.h2d(d_f1, f1)
-    ex.h2d(d_frames, frames)
+    exs[0].h2d(d_frames, frames)
     fbytes = rows * cols
     grid = _lib.GridGeom()
-    L.orbgpu_grid_geom_for_image(cols, rows, C.byref(grid))
-    # plan + output capacities (one untimed extraction)
+    L.orbgpu_grid_geom_for_image(cols, rows, C_.byref(grid))
     ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
     for s_, e in enumerate(exs):
         e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
@@ -209,29 +182,236 @@ def main():
     d_prev = [e.device_alloc(Bs * cap * 2 * 4) for e in exs]
     d_m12 = [e.device_alloc(Bs * cap * 4) for e in exs]
     d_nm = [e.device_alloc(Bs * 4) for e in exs]
-    counts_t = torch.zeros(B, dtype=torch.int32, device=f"cuda:{dev}")
 
     def step():
         ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
         for s_, e in enumerate(exs):
             e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
         for s_, e in enumerate(exs):
-            _lib.check(e.ctx, L.orbgpu_prev_matched_from_frame(ex_ref.ctx, 0, e.ctx, C.c_void_p(d_prev[s_])),
+            _lib.check(e.ctx, L.orbgpu_prev_matched_from_frame(ex_ref.ctx, 0, e.ctx, C_.c_void_p(d_prev[s_])),
                        "prev")
             _lib.check(e.ctx, L.orbgpu_search_for_initialization_batch(ex_ref.ctx, 0, e.ctx, grid, 0.9, 1, 100,
-                                                                         C.c_void_p(d_prev[s_]),
-                                                                         C.c_void_p(d_m12[s_]),
-                                                                         C.c_void_p(d_nm[s_])), "search_init")
-            if dist is not None:
-                _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C.c_void_p(counts_t.data_ptr() + 4 * s_ * Bs),
-                                                            C.c_void_p(outs[s_][2]), Bs * 4), "d2d")
+                                                                         C_.c_void_p(d_prev[s_]),
+                                                                         C_.c_void_p(d_m12[s_]),
+                                                                         C_.c_void_p(d_nm[s_])), "search_init")
+
+    def post():
+        counts = np.zeros(Bs, np.int32)
+        nm = np.zeros(Bs, np.int32)
+        kp_all, nm_all = 0, 0
+        for s_, e in enumerate(exs):
+            e.d2h(counts, outs[s_][2])
+            e.d2h(nm, d_nm[s_])
+            kp_all += int(counts.sum())
+            nm_all += int(nm.sum())
+        return {"mean_keypoints_per_frame": round(kp_all / B, 1),
+                "mean_init_matches_per_frame": round(nm_all / B, 1)}, kp_all / S
+
+    def free():
+        for s_, e in enumerate(exs):
+            for p in (d_prev[s_], d_m12[s_], d_nm[s_]):
+                e.device_free(p)
+        exs[0].device_free(d_frames)
+        ex_ref.device_free(d_f1)
+
+    return dict(metric=METRIC, exs=exs, step=step, post=post, free=free, Bs=Bs, frames_per_step=B,
+                counts=[o[2] for o in outs],
+                workload=f"config 3: {cols}x{rows} mono, {NF} features, ORB extract + SearchForInitialization "
+                         f"(window 100, ratio 0.9, checkOri) of every frame against an initial frame",
+                cpu=lambda: cpu_baseline(rows, cols, NF, args.cpu_seconds))
+
+
+def setup_extract(args, env):
+    """config 2 (640x480, 1000 features by default): ORB extraction only."""
+    _lib, ORBextractor, synthetic = env["_lib"], env["ORBextractor"], env["synthetic"]
+    rows, cols, B, NF, S, dev = args.rows, args.cols, args.batch, args.nfeatures, args.streams, env["dev"]
+    Bs = B // S
+    _, frames = _frames(synthetic, rows, cols, B, env["rank"], 2000)
+    exs = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev) for _ in range(S)]
+    d_frames = exs[0].device_alloc(frames.nbytes)
+    exs[0].h2d(d_frames, frames)
+    fbytes = rows * cols
+    for s_, e in enumerate(exs):
+        e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
+        e.synchronize()
+    outs = [e.batch_outputs() for e in exs]
+
+    def step():
+        for s_, e in enumerate(exs):
+            e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
+
+    def post():
+        counts = np.zeros(Bs, np.int32)
+        kp_all = 0
+        for s_, e in enumerate(exs):
+            e.d2h(counts, outs[s_][2])
+            kp_all += int(counts.sum())
+        return {"mean_keypoints_per_frame": round(kp_all / B, 1)}, kp_all / S
+
+    return dict(metric=f"frames/sec ORB extract @{cols}×{rows}, {NF} feat", exs=exs, step=step, post=post,
+                free=lambda: exs[0].device_free(d_frames), Bs=Bs, frames_per_step=B, counts=[o[2] for o in outs],
+                workload=f"config 2: {cols}x{rows}, {NF} features, ORB extraction (ORBextractor::operator())",
+                cpu=lambda: cpu_baseline_extract(rows, cols, NF, args.cpu_seconds))
+
+
+def setup_stereo(args, env):
+    """config 4 (KITTI 1241x376, 2000 features): left + right extraction and Frame::ComputeStereoMatches."""
+    L, _lib, ORBextractor, synthetic = env["L"], env["_lib"], env["ORBextractor"], env["synthetic"]
+    rows, cols, B, NF, S, dev = args.rows, args.cols, args.batch, args.nfeatures, args.streams, env["dev"]
+    Bs = B // S
+    nuniq = min(B, 16)
+    pairs = [synthetic.stereo_pair(3000 + env["rank"] * 100 + i, rows, cols) for i in range(nuniq)]
+    left = np.stack([pairs[i % nuniq][0] for i in range(B)])
+    right = np.stack([pairs[i % nuniq][1] for i in range(B)])
+    exL = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev) for _ in range(S)]
+    exR = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev) for _ in range(S)]
+    dL = exL[0].device_alloc(left.nbytes)
+    dR = exL[0].device_alloc(right.nbytes)
+    exL[0].h2d(dL, left)
+    exL[0].h2d(dR, right)
+    fbytes = rows * cols
+    for s_ in range(S):
+        exL[s_].extract_batch_device(dL + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
+        exR[s_].extract_batch_device(dR + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
+        exL[s_].synchronize()
+        exR[s_].synchronize()
+    outs = [e.batch_outputs() for e in exL]
+    cap = outs[0][3]
+    d_out = [e.device_alloc(Bs * cap * 8 + Bs * 4) for e in exL]
+    mbf, mb = 386.1448, 386.1448 / 718.856  # Examples/Stereo/KITTI00-02.yaml
+
+    def step():
+        for s_ in range(S):
+            exL[s_].extract_batch_device(dL + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
+            exR[s_].extract_batch_device(dR + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
+        for s_ in range(S):
+            o = d_out[s_]
+            _lib.check(exL[s_].ctx, L.orbgpu_compute_stereo_matches_batch(
+                exL[s_].ctx, exR[s_].ctx, mbf, mb, C.c_void_p(o), C.c_void_p(o + Bs * cap * 4),
+                C.c_void_p(o + Bs * cap * 8)), "stereo")
+
+    def post():
+        counts = np.zeros(Bs, np.int32)
+        nm = np.zeros(Bs, np.int32)
+        kp_all, nm_all = 0, 0
+        for s_ in range(S):
+            exL[s_].d2h(counts, outs[s_][2])
+            exL[s_].d2h(nm, d_out[s_] + Bs * cap * 8)
+            kp_all += int(counts.sum())
+            nm_all += int(nm.sum())
+        return {"mean_left_keypoints_per_frame": round(kp_all / B, 1),
+                "mean_stereo_matches_per_frame": round(nm_all / B, 1)}, kp_all / S
+
+    def free():
+        for s_ in range(S):
+            exL[s_].device_free(d_out[s_])
+        exL[0].device_free(dL)
+        exL[0].device_free(dR)
+
+    return dict(metric=f"stereo frames/sec ORB extract L+R + ComputeStereoMatches @{cols}×{rows}, {NF} feat",
+                exs=exL + exR, step=step, post=post, free=free, Bs=Bs, frames_per_step=B,
+                counts=[o[2] for o in outs],
+                workload=f"config 4: {cols}x{rows} rectified stereo pairs, {NF} features per image, "
+                         f"left + right ORB extraction and Frame::ComputeStereoMatches (bf 386.1448)",
+                cpu=lambda: cpu_baseline_stereo(rows, cols, NF, args.cpu_seconds))
+
+
+WORKLOADS = {"mono_init": setup_mono_init, "extract": setup_extract, "stereo": setup_stereo}
+DEFAULT_SHAPE = {"mono_init": (1080, 1920, 2000), "extract": (480, 640, 1000), "stereo": (376, 1241, 2000)}
+
+
+def cpu_baseline_extract(rows, cols, nfeat, seconds):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py as O
+    from orbslam2_with_quadrics_amd import synthetic
+
+    O.build()
+    ex = O.OracleExtractor(nfeat)
+    scene = synthetic.make_scene(synthetic.SEED_BASE + 998, rows, cols)
+    spent, frames = 0.0, 0
+    while spent < seconds or frames < 2:
+        f = synthetic.render(scene, rows, cols, frames % 9, frames % 5, noise_seed=100 + frames)
+        ts = time.perf_counter()
+        ex(f)
+        spent += time.perf_counter() - ts
+        frames += 1
+    return {"value": round(frames / spent, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{frames} frames of {cols}x{rows}, {nfeat} features: oracle extraction on one host thread"}
+
+
+def cpu_baseline_stereo(rows, cols, nfeat, seconds):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py as O
+    from orbslam2_with_quadrics_amd import synthetic
+
+    O.build()
+    exL, exR = O.OracleExtractor(nfeat), O.OracleExtractor(nfeat)
+    spent, frames = 0.0, 0
+    while spent < seconds or frames < 2:
+        l, r, _ = synthetic.stereo_pair(900 + frames % 4, rows, cols)
+        ts = time.perf_counter()
+        kL, dL = exL(l)
+        kR, dR = exR(r)
+        O.stereo_matches(exL, exR, kL, dL, kR, dR, 386.1448, 386.1448 / 718.856)
+        spent += time.perf_counter() - ts
+        frames += 1
+    return {"value": round(frames / spent, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{frames} stereo pairs of {cols}x{rows}, {nfeat} features: oracle L+R extraction + "
+                      f"ComputeStereoMatches on one host thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=128, help="frames (pairs) per step per GPU")
+    ap.add_argument("--streams", type=int, default=2, help="concurrent extractor contexts (HIP streams) per GPU")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="mono_init",
+                    help="mono_init = BASELINE.json's config 3 (the headline metric); extract = config 2; "
+                         "stereo = config 4")
+    ap.add_argument("--rows", type=int, default=None)
+    ap.add_argument("--cols", type=int, default=None)
+    ap.add_argument("--nfeatures", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    args = ap.parse_args()
+    r0, c0, n0 = DEFAULT_SHAPE[args.workload]
+    args.rows = args.rows or r0
+    args.cols = args.cols or c0
+    args.nfeatures = args.nfeatures or n0
+    if args.batch % args.streams:
+        raise SystemExit(f"--batch {args.batch} must be a multiple of --streams {args.streams}")
+
+    world, rank, local = dist_env()
+    import torch  # noqa: F401  (imported before liborbgpu.so: one HIP runtime in the process)
+
+    from orbslam2_with_quadrics_amd import ORBextractor, _lib, synthetic
+
+    dist = dist_init(world, "nccl")
+    dev = local
+    torch.cuda.set_device(dev)
+    env = dict(L=_lib.lib(), _lib=_lib, ORBextractor=ORBextractor, synthetic=synthetic, dev=dev, rank=rank)
+    t = time.time()
+    W = WORKLOADS[args.workload](args, env)
+    log(f"rank {rank}: {args.workload} set up in {time.time() - t:.1f}s")
+    exs, Bs, S, B = W["exs"], W["Bs"], args.streams, W["frames_per_step"]
+    counts_t = torch.zeros(B, dtype=torch.int32, device=f"cuda:{dev}")
+
+    def step():
+        W["step"]()
+        if dist is not None:  # north_star: all-gather of the per-frame keypoint counts over RCCL
+            for s_, dc in enumerate(W["counts"]):
+                _lib.check(exs[s_].ctx, _lib.lib().orbgpu_memcpy_d2d_async(
+                    exs[s_].ctx, C.c_void_p(counts_t.data_ptr() + 4 * s_ * Bs), C.c_void_p(dc), Bs * 4), "d2d")
         for e in exs:
             e.synchronize()
         if dist is not None:
             allgather_counts(dist, counts_t, world)
 
     stage_acc = {}
-    union_acc = {}  # stage -> total time with >= 1 launch of it running (union over the S streams)
+    union_acc = {}  # stage -> total time with >= 1 launch of it running (union over the concurrent contexts)
 
     def collect():
         for e in exs:
@@ -268,23 +448,15 @@ def main():
     for e in exs:
         e.set_stage_timing(False)
 
-    # ---- per-stage averages and the dominant kernel's roofline
-    # per-launch quantities: one launch processes one stream's Bs frames (stage times are per launch)
-    cand_total = sum(L.orbgpu_batch_candidate_total(e.ctx) for e in exs) / S
-    counts = np.zeros(Bs, np.int32)
-    nm = np.zeros(Bs, np.int32)
-    kp_all, nm_all = 0, 0
-    for s_, e in enumerate(exs):
-        e.d2h(counts, outs[s_][2])
-        e.d2h(nm, d_nm[s_])
-        kp_all += int(counts.sum())
-        nm_all += int(nm.sum())
-    kp_total = kp_all / S
-    P = level_pixels(cols, rows, ex.GetInverseScaleFactors())
+    # ---- per-stage averages and the dominant kernel's roofline (per-launch quantities: one launch processes
+    # one context's Bs frames)
+    cand_total = sum(_lib.lib().orbgpu_batch_candidate_total(e.ctx) for e in exs) / len(exs)
+    extra, kp_total = W["post"]()
+    P = level_pixels(args.cols, args.rows, exs[0].GetInverseScaleFactors())
     stages = {k: v[0] / max(v[1], 1) for k, v in stage_acc.items()}
-    kernels = {k: v for k, v in stages.items() if k not in ("pyramid", "match_init")}
+    kernels = {k: v for k, v in stages.items() if k in ("fast", "octree", "describe", "grid", "search_init")}
     dom = max(kernels, key=kernels.get)
-    # effective launch duration: time the GPU has >= 1 launch of the kernel running, per launch.  With S
+    # effective launch duration: time the GPU has >= 1 launch of the kernel running, per launch.  With
     # concurrent streams a launch's own event span also covers the co-running launches; the union does
     # not (and equals the plain average when launches do not overlap, e.g. under the profiler).
     launches = stage_acc[dom][1]
@@ -293,7 +465,7 @@ def main():
     dom_bytes = stage_bytes(dom, Bs, P, cand_total, kp_total)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
-    if os.path.exists(args.pmc_json):
+    if args.workload == "mono_init" and os.path.exists(args.pmc_json):
         try:
             pmc = json.load(open(args.pmc_json))
             traffic = pmc.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
@@ -305,7 +477,7 @@ def main():
     total_frames = world * B * args.steps
     value = total_frames / dt
     out = {
-        "metric": METRIC,
+        "metric": W["metric"],
         "value": round(value, 2),
         "unit": "frames/s",
         "n_gpus": world,
@@ -317,18 +489,16 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {
-            "workload": f"config 3: {cols}x{rows} mono, {NF} features, ORB extract + SearchForInitialization "
-                        f"(window 100, ratio 0.9, checkOri) of every frame against an initial frame",
+        "config": dict({
+            "workload": W["workload"],
             "frames_per_step_per_gpu": B,
             "streams_per_gpu": S,
             "frames_per_launch": Bs,
-            "resolution": f"{cols}x{rows}",
-            "nfeatures": NF,
-            "parallelism": f"frame-sharded x{world} GPUs, {S} streams per GPU (RCCL all-gather of keypoint counts only)",
-            "mean_keypoints_per_frame": round(kp_all / B, 1),
-            "mean_init_matches_per_frame": round(nm_all / B, 1),
-        },
+            "resolution": f"{args.cols}x{args.rows}",
+            "nfeatures": args.nfeatures,
+            "parallelism": f"frame-sharded x{world} GPUs, {S} streams per GPU (RCCL all-gather of keypoint "
+                           f"counts only)",
+        }, **extra),
         "roofline": {
             "bound": "hbm",
             "kernel": dom,
@@ -347,14 +517,10 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("timing the CPU baseline (oracle, 1 thread)")
-        out["cpu_baseline"] = cpu_baseline(rows, cols, NF, args.cpu_seconds)
+        out["cpu_baseline"] = W["cpu"]()
     elif rank == 0:
         out["cpu_baseline"] = None
-    for s_, e in enumerate(exs):
-        for p in (d_prev[s_], d_m12[s_], d_nm[s_]):
-            e.device_free(p)
-    ex.device_free(d_frames)
-    ex_ref.device_free(d_f1)
+    W["free"]()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -838,7 +838,7 @@ __device__ __forceinline__ int og_reflect101(int i, int n)
 
 #define DK_WAVES 4
 #define RAW_W 43
-#define RAW_S 44
+#define RAW_S 52  // 43 + 3 misalignment bytes, dword multiple; 13 dwords: conflict-free lane-per-row reads
 #define BL_W 37
 
 __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, const uint8_t* __restrict__ img0,
@@ -873,7 +873,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     uint8_t* R = raw[w];
     uint16_t* Hb = hb[w];
     uint8_t* Bl = bl[w];
-    int cx = 0, cy = 0, resp = 0, lw = 1, lh = 1;
+    int cx = 0, cy = 0, resp = 0, lw = 1, lh = 1, mis = 0;
     if (active) {
         const OgLevel& L = P.lv[l];
         const long long o = (long long)f * P.kcap_total + L.koff + li;
@@ -892,17 +892,32 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             img = pyr + (long long)f * P.pyr_per_frame + L.pyr_off;
             pitch = L.pitch;
         }
-        for (int idx = lane; idx < RAW_W * RAW_W; idx += 64) {
-            const int r = idx / RAW_W, c = idx - (idx / RAW_W) * RAW_W;
-            const int yy = og_reflect101(cy - 21 + r, lh), xx = og_reflect101(cx - 21 + c, lw);
-            R[r * RAW_S + c] = img[(long long)yy * pitch + xx];
+        if (cx >= 21 && cy >= 21 && cx + 21 < lw && cy + 21 < lh && (pitch & 3) == 0) {
+            // interior (almost every keypoint): 43 rows x <= 12 aligned dwords, the window origin `mis` bytes
+            // into every LDS row
+            const uint8_t* src0 = img + (long long)(cy - 21) * pitch + (cx - 21);
+            mis = (int)((uintptr_t)src0 & 3);
+            const uint32_t* base = (const uint32_t*)(src0 - mis);
+            const long long pw = pitch >> 2;
+            const int nd = (RAW_W + mis + 3) >> 2;
+            for (int idx = lane; idx < RAW_W * 12; idx += 64) {
+                const int r = idx / 12, q = idx - r * 12;
+                if (q < nd) *(uint32_t*)&R[r * RAW_S + 4 * q] = base[r * pw + q];
+            }
+        } else {  // within 21 px of the border: BORDER_REFLECT_101 per pixel
+            for (int idx = lane; idx < RAW_W * RAW_W; idx += 64) {
+                const int r = idx / RAW_W, c = idx - (idx / RAW_W) * RAW_W;
+                const int yy = og_reflect101(cy - 21 + r, lh), xx = og_reflect101(cx - 21 + c, lw);
+                R[r * RAW_S + c] = img[(long long)yy * pitch + xx];
+            }
         }
     }
     __syncthreads();
+    const uint8_t* Rb = R + mis;  // Rb[r * RAW_S + c] = window pixel (r, c)
     // ---- IC_Angle on the unblurred level (:77-104); integer moments are order-independent
     int m01 = 0, m10 = 0;
     if (active) {
-        const uint8_t* ctr = R + 21 * RAW_S + 21;
+        const uint8_t* ctr = Rb + 21 * RAW_S + 21;
         if (lane < 31) m10 += (lane - 15) * ctr[lane - 15];
         for (int v = 1; v <= OG_HALF_PATCH; v++) {
             const int d = P.umax[v];
@@ -922,25 +937,30 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     const float angle = og_fast_atan2((float)m01, (float)m10);
     // ---- 7x7 Gaussian (sigma 2, BORDER_REFLECT_101) of the 37x37 window the tests can reach
     const int gk[7] = {18, 34, 49, 55, 49, 34, 18};
-    if (active) {
-        for (int idx = lane; idx < RAW_W * BL_W; idx += 64) {
-            const int r = idx / BL_W, c = idx - (idx / BL_W) * BL_W;
-            const uint8_t* s = R + r * RAW_S + c;
-            int acc = 0;
+    // horizontal pass: one lane per window row, a 7-tap sliding window along it (43 rows x 37 outputs)
+    if (active && lane < RAW_W) {
+        const uint8_t* s = Rb + lane * RAW_S;
+        int w0 = s[0], w1 = s[1], w2 = s[2], w3 = s[3], w4 = s[4], w5 = s[5];
 #pragma unroll
-            for (int t = 0; t < 7; t++) acc += gk[t] * s[t];
-            Hb[idx] = (uint16_t)acc;
+        for (int c = 0; c < BL_W; c++) {
+            const int w6 = s[c + 6];
+            Hb[lane * BL_W + c] = (uint16_t)(gk[0] * w0 + gk[1] * w1 + gk[2] * w2 + gk[3] * w3 + gk[4] * w4 +
+                                             gk[5] * w5 + gk[6] * w6);
+            w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
         }
     }
     __syncthreads();
-    if (active) {
-        for (int idx = lane; idx < BL_W * BL_W; idx += 64) {
-            const int r = idx / BL_W, c = idx - (idx / BL_W) * BL_W;
-            int acc = 0;
+    // vertical pass: one lane per output column, sliding down the 37 output rows
+    if (active && lane < BL_W) {
+        const uint16_t* h = Hb + lane;
+        int w0 = h[0], w1 = h[BL_W], w2 = h[2 * BL_W], w3 = h[3 * BL_W], w4 = h[4 * BL_W], w5 = h[5 * BL_W];
 #pragma unroll
-            for (int t = 0; t < 7; t++) acc += gk[t] * (int)Hb[(r + t) * BL_W + c];
-            int v = (acc + (1 << 15)) >> 16;
-            Bl[idx] = (uint8_t)(v > 255 ? 255 : v);
+        for (int r = 0; r < BL_W; r++) {
+            const int w6 = h[(r + 6) * BL_W];
+            const int acc = gk[0] * w0 + gk[1] * w1 + gk[2] * w2 + gk[3] * w3 + gk[4] * w4 + gk[5] * w5 + gk[6] * w6;
+            const int v = (acc + (1 << 15)) >> 16;
+            Bl[r * BL_W + lane] = (uint8_t)(v > 255 ? 255 : v);
+            w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
         }
     }
     __syncthreads();

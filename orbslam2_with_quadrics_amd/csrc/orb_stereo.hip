@@ -22,77 +22,63 @@ typedef unsigned long long u64;
 #define ST_TH_LOW 50
 #define ST_MAXROWS 8192
 
-__global__ __launch_bounds__(256) void og_stereo_rows_kernel(OgStereoDev S)
+// vRowIndices (src/Frame.cc:476-493): right keypoint iR is pushed to every row of its band
+// [floor(y - 2 sf), ceil(y + 2 sf)] in index order.  Band ends live in LDS; row counts come from LDS atomics and
+// a block scan; then each row is filled by one thread that walks the keypoints in index order (LDS broadcast
+// reads), so every row list is in push_back order without sorting.
+#define ST_NT 1024
+#define ST_MAXR 8192      // right keypoints held in LDS
+__global__ __launch_bounds__(ST_NT) void og_stereo_rows_kernel(OgStereoDev S)
 {
     __shared__ int cnt[ST_MAXROWS + 1];
-    __shared__ int wsum[8];
-    const int b = blockIdx.x, tid = threadIdx.x;
-    const int Nr = S.R.counts[b];
+    __shared__ short lo_[ST_MAXR], hi_[ST_MAXR];
+    __shared__ int wsum[ST_NT / 64];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int Nr = min(S.R.counts[b], ST_MAXR);
     const orbgpu_kp_dev* KR = S.R.kps + (long long)b * S.R.frame_cap;
     int* RS = S.row_start + (long long)b * (S.nRows + 1);
     int* RI = S.row_items + (long long)b * S.row_cap;
-    for (int y = tid; y <= S.nRows; y += 256) cnt[y] = 0;
+    for (int y = tid; y <= S.nRows; y += ST_NT) cnt[y] = 0;
     __syncthreads();
-    for (int iR = tid; iR < Nr; iR += 256) {
+    for (int iR = tid; iR < Nr; iR += ST_NT) {
         const float kpY = KR[iR].y;
         const float r = 2.0f * S.sf[KR[iR].octave];
-        const int maxr = (int)ceilf(kpY + r), minr = (int)floorf(kpY - r);
-        for (int yi = max(minr, 0); yi <= min(maxr, S.nRows - 1); yi++) atomicAdd(&cnt[yi], 1);
+        const int lo = max((int)floorf(kpY - r), 0), hi = min((int)ceilf(kpY + r), S.nRows - 1);
+        lo_[iR] = (short)lo;
+        hi_[iR] = (short)hi;
+        for (int yi = lo; yi <= hi; yi++) atomicAdd(&cnt[yi], 1);
     }
     __syncthreads();
-    // exclusive scan of cnt[0..nRows) (serial chunks per thread + one scan of chunk sums)
-    const int per = (S.nRows + 255) / 256;
-    const int lo = tid * per, hi = min(lo + per, S.nRows);
-    int sum = 0;
-    for (int y = lo; y < hi; y++) sum += cnt[y];
-    const int lane = tid & 63, w = tid >> 6;
-    int x = sum;
+    // exclusive scan of cnt[0..nRows) in chunks of ST_NT
+    int carry = 0;
+    for (int y0 = 0; y0 < S.nRows; y0 += ST_NT) {
+        const int y = y0 + tid;
+        const int v = y < S.nRows ? cnt[y] : 0;
+        int x = v;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(x, o);
-        if (lane >= o) x += t;
-    }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    int before = 0;
-    for (int q = 0; q < w; q++) before += wsum[q];
-    int run = before + x - sum;
-    __syncthreads();
-    for (int y = lo; y < hi; y++) {
-        const int c = cnt[y];
-        RS[y] = run;
-        cnt[y] = run;  // cursor
-        run += c;
-    }
-    if (tid == 255) {
-        int tot = 0;
-        for (int q = 0; q < 4; q++) tot += wsum[q];
-        RS[S.nRows] = tot;
-    }
-    __syncthreads();
-    for (int iR = tid; iR < Nr; iR += 256) {
-        const float kpY = KR[iR].y;
-        const float r = 2.0f * S.sf[KR[iR].octave];
-        const int maxr = (int)ceilf(kpY + r), minr = (int)floorf(kpY - r);
-        for (int yi = max(minr, 0); yi <= min(maxr, S.nRows - 1); yi++) {
-            const int pos = atomicAdd(&cnt[yi], 1);
-            if (pos < S.row_cap) RI[pos] = iR;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(x, o);
+            if (lane >= o) x += t;
         }
+        if (lane == 63) wsum[wv] = x;
+        __syncthreads();
+        int before = carry, tot = 0;
+        for (int q = 0; q < ST_NT / 64; q++) {
+            if (q < wv) before += wsum[q];
+            tot += wsum[q];
+        }
+        if (y < S.nRows) RS[y] = before + x - v;
+        __syncthreads();
+        carry += tot;
     }
+    if (tid == 0) RS[S.nRows] = carry;
     __syncthreads();
     __threadfence_block();
-    // push_back order: ascending iR inside each row
-    for (int y = tid; y < S.nRows; y += 256) {
-        const int b0 = RS[y], e = min(RS[y + 1], S.row_cap);
-        for (int p = b0 + 1; p < e; p++) {
-            const int v = RI[p];
-            int q = p - 1;
-            while (q >= b0 && RI[q] > v) {
-                RI[q + 1] = RI[q];
-                q--;
-            }
-            RI[q + 1] = v;
-        }
+    for (int y = tid; y < S.nRows; y += ST_NT) {
+        int pos = RS[y];
+        const int end = min(pos + cnt[y], S.row_cap);
+        for (int iR = 0; iR < Nr && pos < end; iR++)
+            if (lo_[iR] <= y && y <= hi_[iR]) RI[pos++] = iR;
     }
 }
 
@@ -320,7 +306,7 @@ __global__ __launch_bounds__(256) void og_stereo_filter_kernel(OgStereoDev S)
 
 void og_launch_stereo(hipStream_t s, const OgStereoDev& S, int B)
 {
-    hipLaunchKernelGGL(og_stereo_rows_kernel, dim3(B), dim3(256), 0, s, S);
+    hipLaunchKernelGGL(og_stereo_rows_kernel, dim3(B), dim3(ST_NT), 0, s, S);
     hipLaunchKernelGGL(og_stereo_match_kernel, dim3((S.L.frame_cap + 3) / 4, B), dim3(256), 0, s, S);
     hipLaunchKernelGGL(og_stereo_filter_kernel, dim3(B), dim3(256), 0, s, S);
 }

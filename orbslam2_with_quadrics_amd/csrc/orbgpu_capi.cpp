@@ -1177,6 +1177,10 @@ static int stereo_launch(orbgpu_ctx* L, orbgpu_ctx* R, float mbf, float mb, floa
         L->err = "stereo: baseline must be positive";
         return ORBGPU_ERR_ARG;
     }
+    if (R->plan.frame_cap > 8192) {  // og_stereo_rows_kernel keeps the right keypoints' bands in LDS
+        L->err = "stereo: more than 8192 right keypoints per frame";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
     const int B = L->last_B;
     const OgPlan& P = L->plan;
     HIP_TRY(L, hipSetDevice(L->device));
