@@ -307,9 +307,25 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             if (r < rh && q < nd) *(uint32_t*)&roi[r * FB_RS + 4 * q] = buf[k];
         }
     } else {
-        for (int r = wv; r < rh; r += FB_NT / 64) {
-            const uint8_t* src = row0 + (long long)r * pitch;
-            for (int c = lane; c < rw; c += 64) roi[r * FB_RS + c] = src[c];
+        // rows with their own misalignment (odd pitch, e.g. a contiguous 1241-px image): every dword from two
+        // aligned loads funnel-shifted by the row's offset.  Reads stay inside the row: an ROI starts >= 16 px
+        // from the left edge and ends >= 13 px before the right one (the over-read is < 8 bytes).
+        const int nd = (rw + 3) >> 2;
+        uint32_t buf[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const int r = (tid >> 5) + 16 * k, q = tid & 31;
+            buf[k] = 0u;
+            if (r < rh && q < nd) {
+                const uint8_t* p = row0 + (long long)r * pitch + 4 * q;
+                const uint32_t* a = (const uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
+                buf[k] = __builtin_amdgcn_alignbyte(a[1], a[0], (unsigned)((uintptr_t)p & 3));
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const int r = (tid >> 5) + 16 * k, q = tid & 31;
+            if (r < rh && q < nd) *(uint32_t*)&roi[r * FB_RS + 4 * q] = buf[k];
         }
     }
     for (int idx = tid * 4; idx < dh * FB_MW; idx += FB_NT * 4) *(uint32_t*)&Ms[idx] = 0u;
@@ -873,7 +889,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     uint8_t* R = raw[w];
     uint16_t* Hb = hb[w];
     uint8_t* Bl = bl[w];
-    int cx = 0, cy = 0, resp = 0, lw = 1, lh = 1, mis = 0;
+    int cx = 0, cy = 0, resp = 0, lw = 1, lh = 1;
     if (active) {
         const OgLevel& L = P.lv[l];
         const long long o = (long long)f * P.kcap_total + L.koff + li;
@@ -892,17 +908,18 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             img = pyr + (long long)f * P.pyr_per_frame + L.pyr_off;
             pitch = L.pitch;
         }
-        if (cx >= 21 && cy >= 21 && cx + 21 < lw && cy + 21 < lh && (pitch & 3) == 0) {
-            // interior (almost every keypoint): 43 rows x <= 12 aligned dwords, the window origin `mis` bytes
-            // into every LDS row
+        if (cx >= 21 && cy >= 21 && cx + 28 < lw && cy + 21 < lh) {
+            // interior (almost every keypoint): 43 rows x 11 dwords.  Each dword comes from two aligned loads
+            // funnel-shifted by the row's own misalignment (any pitch, e.g. a contiguous 1241-px KITTI image);
+            // the farthest byte read is x = cx + 26, inside the row (level starts are 256-B aligned, so the
+            // rounded-down first load never precedes the image)
             const uint8_t* src0 = img + (long long)(cy - 21) * pitch + (cx - 21);
-            mis = (int)((uintptr_t)src0 & 3);
-            const uint32_t* base = (const uint32_t*)(src0 - mis);
-            const long long pw = pitch >> 2;
-            const int nd = (RAW_W + mis + 3) >> 2;
-            for (int idx = lane; idx < RAW_W * 12; idx += 64) {
-                const int r = idx / 12, q = idx - r * 12;
-                if (q < nd) *(uint32_t*)&R[r * RAW_S + 4 * q] = base[r * pw + q];
+            for (int idx = lane; idx < RAW_W * 11; idx += 64) {
+                const int r = idx / 11, q = idx - r * 11;
+                const uint8_t* p = src0 + (long long)r * pitch + 4 * q;
+                const uint32_t* a = (const uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
+                const unsigned sh = (unsigned)((uintptr_t)p & 3);
+                *(uint32_t*)&R[r * RAW_S + 4 * q] = __builtin_amdgcn_alignbyte(a[1], a[0], sh);
             }
         } else {  // within 21 px of the border: BORDER_REFLECT_101 per pixel
             for (int idx = lane; idx < RAW_W * RAW_W; idx += 64) {
@@ -913,7 +930,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         }
     }
     __syncthreads();
-    const uint8_t* Rb = R + mis;  // Rb[r * RAW_S + c] = window pixel (r, c)
+    const uint8_t* Rb = R;  // Rb[r * RAW_S + c] = window pixel (r, c)
     // ---- IC_Angle on the unblurred level (:77-104); integer moments are order-independent
     int m01 = 0, m10 = 0;
     if (active) {
