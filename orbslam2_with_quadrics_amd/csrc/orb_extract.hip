@@ -35,14 +35,17 @@ __device__ __forceinline__ unsigned og_xcd_remap(unsigned orig, unsigned nwg)
 // k1: pyramid level l from level l-1 (src/ORBextractor.cc:1120)
 // ------------------------------------------------------------------------------------------------
 #define RZ_NT 256
-#define RZ_ROWS 8                      // output rows per workgroup
-#define RZ_COLS (RZ_NT * 4)            // output columns per workgroup (4 per thread)
-#define RZ_SROWS 16                    // >= source rows an 8-row tile can touch (scale <= ~1.6)
-#define RZ_SCOLS 1664                  // >= source bytes of a 1024-column tile at scale 1.6 + slack
+#define RZ_TW 256                      // output columns per workgroup (64 lanes x 4)
+#define RZ_TH 16                       // output rows per workgroup (4 waves x 4 rows)
+#define RZ_SROWS 28                    // >= source rows a 16-row tile touches (15 * 1.6 + 2, scale <= 1.6)
+#define RZ_SC 448                      // LDS row stride: >= 255 * 1.6 + 2 source bytes + 15 alignment slack
 
-// One workgroup = 8 output rows x 1024 output columns of one frame.  The source rows/columns the tile
-// touches are staged in LDS with coalesced dword loads; each output pixel then costs 4 LDS byte reads.
-// The arithmetic is the scalar fixed-point form of cv::resize INTER_LINEAR.
+// One workgroup = 16 output rows x 256 output columns of one frame (balanced tiles: a 1111-px level is 5
+// tiles, not 1024 + 87).  The source rows/columns the tile touches are staged in LDS with 16-byte loads
+// from 16-byte aligned addresses, all issued before the first LDS store; each source row keeps its own
+// misalignment (mis[r]), so any pitch and any frame stride take the same path.  Each output pixel costs
+// 4 LDS byte reads; the arithmetic is the scalar fixed-point form of cv::resize INTER_LINEAR (DESIGN.md
+// §3.1).  The aligned 16-byte blocks read never leave the 16-byte block holding a pixel of the row.
 __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restrict__ src, long long src_pitch,
                                                           long long src_fstride, uint8_t* __restrict__ dst,
                                                           long long dst_pitch, long long dst_fstride, int sw,
@@ -50,48 +53,51 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
                                                           const int4* __restrict__ ytab, int xmax,
                                                           int* __restrict__ status)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t S[RZ_SROWS * RZ_SCOLS];
+    __shared__ __attribute__((aligned(16))) uint8_t S[RZ_SROWS * RZ_SC];
+    __shared__ int mis[RZ_SROWS];
     const int f = blockIdx.z, tid = threadIdx.x;
-    const int dy0 = blockIdx.y * RZ_ROWS, dx0 = blockIdx.x * RZ_COLS;
-    const int ny = min(RZ_ROWS, dh - dy0), nx = min(RZ_COLS, dw - dx0);
+    const int dy0 = blockIdx.y * RZ_TH, dx0 = blockIdx.x * RZ_TW;
+    const int ny = min(RZ_TH, dh - dy0), nx = min(RZ_TW, dw - dx0);
     const int sy0 = ytab[dy0].x, sy1 = ytab[dy0 + ny - 1].y;   // clipped rows, monotone in dy
     const int sx0 = xtab[dx0].x;
     const int sx1 = min(xtab[dx0 + nx - 1].x + 1, sw - 1);
     const uint8_t* base = src + (long long)f * src_fstride;
-    const int nrows = sy1 - sy0 + 1;
-    const bool al = ((src_pitch & 3) == 0) && ((((uintptr_t)base) & 3) == 0);
-    const int cx0 = al ? (sx0 & ~3) : sx0;                      // LDS column 0 <-> source column cx0
-    const int ncols = sx1 - cx0 + 1;
-    if (nrows > RZ_SROWS || ncols > RZ_SCOLS) {                 // unreachable: scaleFactor <= 1.6 on the host
+    const int nrows = sy1 - sy0 + 1, ncols = sx1 - sx0 + 1;
+    const int nch = (ncols + 15 + 15) >> 4;                      // 16-byte chunks per row incl. misalignment
+    if (nrows > RZ_SROWS || nch * 16 > RZ_SC) {                 // unreachable: scaleFactor <= 1.6 on the host
         if (tid == 0) atomicOr(status, 8);
         return;
     }
-    if (al) {
-        const int nd = (ncols + 3) >> 2;
-        const int fd = min(nd, (sw - cx0) >> 2);                 // dwords lying wholly inside the row
-        for (int idx = tid; idx < nrows * nd; idx += RZ_NT) {
-            const int r = idx / nd, q = idx - (idx / nd) * nd;
-            const uint8_t* sp = base + (long long)(sy0 + r) * src_pitch + cx0 + 4 * q;
-            if (q < fd) {
-                *(uint32_t*)&S[r * RZ_SCOLS + 4 * q] = *(const uint32_t*)sp;
-            } else {
-                for (int b = 0; b < 4 && 4 * q + b < ncols; b++) S[r * RZ_SCOLS + 4 * q + b] = sp[b];
+    {
+        uint4 buf[4];
+        const int q = tid & 31;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int r = (tid >> 5) + 8 * k;
+            buf[k] = make_uint4(0u, 0u, 0u, 0u);
+            if (r < nrows && q < nch) {
+                const uintptr_t a = (uintptr_t)(base + (long long)(sy0 + r) * src_pitch + sx0);
+                const uintptr_t a16 = a & ~(uintptr_t)15;
+                if (a16 + 16 * q <= a + (uintptr_t)(ncols - 1)) buf[k] = *(const uint4*)(a16 + 16 * q);
+                if (q == 0) mis[r] = (int)(a - a16);
             }
         }
-    } else {
-        for (int idx = tid; idx < nrows * ncols; idx += RZ_NT) {
-            const int r = idx / ncols, c = idx - (idx / ncols) * ncols;
-            S[r * RZ_SCOLS + c] = base[(long long)(sy0 + r) * src_pitch + cx0 + c];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int r = (tid >> 5) + 8 * k;
+            if (r < nrows && q < nch) *(uint4*)&S[r * RZ_SC + 16 * q] = buf[k];
         }
     }
     __syncthreads();
+    const int c = tid & 63, rg = tid >> 6;
+    const int dxt = dx0 + 4 * c;
+    if (dxt >= dw) return;
     int sx[4], a0[4], a1[4];
-    const int dxt = dx0 + 4 * tid;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int dx = min(dxt + k, dw - 1);
         const int4 xt = xtab[dx];
-        sx[k] = xt.x - cx0;
+        sx[k] = xt.x - sx0;
         if (dx < xmax) {
             a0[k] = xt.y;
             a1[k] = xt.z;
@@ -100,13 +106,16 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
             a1[k] = 0;
         }
     }
-    if (dxt >= dw) return;
     const int n = min(4, dw - dxt);
     uint8_t* D = dst + (long long)f * dst_fstride + dxt;
-    for (int r = 0; r < ny; r++) {
+#pragma unroll
+    for (int rr = 0; rr < 4; rr++) {
+        const int r = 4 * rg + rr;
+        if (r >= ny) break;
         const int4 yt = ytab[dy0 + r];
-        const uint8_t* R0 = S + (yt.x - sy0) * RZ_SCOLS;
-        const uint8_t* R1 = S + (yt.y - sy0) * RZ_SCOLS;
+        const int r0 = yt.x - sy0, r1 = yt.y - sy0;
+        const uint8_t* R0 = S + r0 * RZ_SC + mis[r0];
+        const uint8_t* R1 = S + r1 * RZ_SC + mis[r1];
         uint32_t packed = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -1116,7 +1125,7 @@ void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, lo
                       long long dst_pitch, long long dst_fstride, int sw, int sh, int dw, int dh, const int4* xtab,
                       const int4* ytab, int xmax, int* status, int B)
 {
-    dim3 grid((dw + RZ_COLS - 1) / RZ_COLS, (dh + RZ_ROWS - 1) / RZ_ROWS, B);
+    dim3 grid((dw + RZ_TW - 1) / RZ_TW, (dh + RZ_TH - 1) / RZ_TH, B);
     hipLaunchKernelGGL(og_resize_kernel, grid, dim3(RZ_NT), 0, s, src, src_pitch, src_fstride, dst, dst_pitch,
                        dst_fstride, sw, sh, dw, dh, xtab, ytab, xmax, status);
 }

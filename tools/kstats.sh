@@ -15,3 +15,4 @@ f = glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True)[0]
 for r in csv.DictReader(open(f)):
     print(f"{float(r['AverageNs'])/1e3:10.1f} us  x{r['Calls']:>4}  {r['Name'][:90]}")
 PY
+python3 "$ROOT/tools/ktrace_groups.py" "$OUT" ${KGROUPS:-resize}
