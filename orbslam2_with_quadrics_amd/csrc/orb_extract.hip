@@ -139,32 +139,36 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
 // k2: FAST cells (src/ORBextractor.cc:789-829 + cv::FAST TYPE_9_16 with nonmax suppression)
 // ------------------------------------------------------------------------------------------------
 // M(p) = max over the 16 contiguous 9-arcs and both polarities of min |I(p) - I(arc)|; the pixel is a
-// FAST corner at threshold t iff M > t and then cornerScore<16> == M - 1.
-__device__ __forceinline__ int og_fast_M(const uint8_t* p, int st)
+// FAST corner at threshold t iff M > t and then cornerScore<16> == M - 1.  Computed on the
+// circle values themselves: max_k min_arc(v - c) = v - min_k max_arc(c) and -min_k max_arc(v - c) =
+// max_k min_arc(c) - v, so M = max(v - A, B - v, 0) with A = min_k max_arc c, B = max_k min_arc c.  Each
+// 9-arc [k, k+8] is max3/min3(pairs-of-pairs at k and k+4, c[k+8]): 112 integer ops, exact.
+template <int SX, typename E>
+__device__ __forceinline__ int og_fast_M(const E* p, int st)
 {
     const int v = p[0];
-    int d[16];
-    d[0] = v - p[3 * st];
-    d[1] = v - p[1 + 3 * st];
-    d[2] = v - p[2 + 2 * st];
-    d[3] = v - p[3 + 1 * st];
-    d[4] = v - p[3];
-    d[5] = v - p[3 - 1 * st];
-    d[6] = v - p[2 - 2 * st];
-    d[7] = v - p[1 - 3 * st];
-    d[8] = v - p[-3 * st];
-    d[9] = v - p[-1 - 3 * st];
-    d[10] = v - p[-2 - 2 * st];
-    d[11] = v - p[-3 - 1 * st];
-    d[12] = v - p[-3];
-    d[13] = v - p[-3 + 1 * st];
-    d[14] = v - p[-2 + 2 * st];
-    d[15] = v - p[-1 + 3 * st];
+    int c[16];
+    c[0] = p[3 * st];
+    c[1] = p[1 * SX + 3 * st];
+    c[2] = p[2 * SX + 2 * st];
+    c[3] = p[3 * SX + 1 * st];
+    c[4] = p[3 * SX];
+    c[5] = p[3 * SX - 1 * st];
+    c[6] = p[2 * SX - 2 * st];
+    c[7] = p[1 * SX - 3 * st];
+    c[8] = p[-3 * st];
+    c[9] = p[-1 * SX - 3 * st];
+    c[10] = p[-2 * SX - 2 * st];
+    c[11] = p[-3 * SX - 1 * st];
+    c[12] = p[-3 * SX];
+    c[13] = p[-3 * SX + 1 * st];
+    c[14] = p[-2 * SX + 2 * st];
+    c[15] = p[-1 * SX + 3 * st];
     int mn2[16], mx2[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        mn2[k] = min(d[k], d[(k + 1) & 15]);
-        mx2[k] = max(d[k], d[(k + 1) & 15]);
+        mn2[k] = min(c[k], c[(k + 1) & 15]);
+        mx2[k] = max(c[k], c[(k + 1) & 15]);
     }
     int mn4[16], mx4[16];
 #pragma unroll
@@ -172,16 +176,13 @@ __device__ __forceinline__ int og_fast_M(const uint8_t* p, int st)
         mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
         mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
     }
-    int apos = -1024, bneg = 1024;
+    int A = 255, B = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        const int mn8 = min(mn4[k], mn4[(k + 4) & 15]);
-        const int mx8 = max(mx4[k], mx4[(k + 4) & 15]);
-        apos = max(apos, min(mn8, d[(k + 8) & 15]));
-        bneg = min(bneg, max(mx8, d[(k + 8) & 15]));
+        A = min(A, max(max(mx4[k], mx4[(k + 4) & 15]), c[(k + 8) & 15]));
+        B = max(B, min(min(mn4[k], mn4[(k + 4) & 15]), c[(k + 8) & 15]));
     }
-    const int M = max(apos, -bneg);
-    return M > 0 ? M : 0;
+    return max(max(v - A, B - v), 0);
 }
 
 
@@ -220,6 +221,43 @@ __device__ __forceinline__ bool og_fast_quick(const uint8_t* p, int t)
     return (md < v - t) | (mb > v + t);
 }
 
+// The same quick test for two pixels at once: each dword of the pair-interleaved ROI holds (pixel x, pixel
+// x + H) as two u16, so one LDS read gives a circle sample of both pixels and v_pk_min/max_u16 test both.
+// Returns a dword whose low (high) half is nonzero iff the first (second) pixel survives.
+typedef unsigned short og_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ og_u16x2 og_as_u16x2(uint32_t x) { return __builtin_bit_cast(og_u16x2, x); }
+__device__ __forceinline__ uint32_t og_fast_quick2(const uint32_t* p, int st, og_u16x2 tt)
+{
+    og_u16x2 c[16];
+    c[0] = og_as_u16x2(p[3 * st]);
+    c[1] = og_as_u16x2(p[1 + 3 * st]);
+    c[2] = og_as_u16x2(p[2 + 2 * st]);
+    c[3] = og_as_u16x2(p[3 + 1 * st]);
+    c[4] = og_as_u16x2(p[3]);
+    c[5] = og_as_u16x2(p[3 - 1 * st]);
+    c[6] = og_as_u16x2(p[2 - 2 * st]);
+    c[7] = og_as_u16x2(p[1 - 3 * st]);
+    c[8] = og_as_u16x2(p[-3 * st]);
+    c[9] = og_as_u16x2(p[-1 - 3 * st]);
+    c[10] = og_as_u16x2(p[-2 - 2 * st]);
+    c[11] = og_as_u16x2(p[-3 - 1 * st]);
+    c[12] = og_as_u16x2(p[-3]);
+    c[13] = og_as_u16x2(p[-3 + 1 * st]);
+    c[14] = og_as_u16x2(p[-2 + 2 * st]);
+    c[15] = og_as_u16x2(p[-1 + 3 * st]);
+    const og_u16x2 v = og_as_u16x2(p[0]);
+    og_u16x2 md = __builtin_elementwise_min(c[0], c[8]), mb = __builtin_elementwise_max(c[0], c[8]);
+#pragma unroll
+    for (int k = 1; k < 8; k++) {
+        md = __builtin_elementwise_max(md, __builtin_elementwise_min(c[k], c[k + 8]));
+        mb = __builtin_elementwise_min(mb, __builtin_elementwise_max(c[k], c[k + 8]));
+    }
+    // dark: md < v - t (saturated: v < t leaves no darker value), bright: mb > v + t (<= 510, no overflow)
+    const og_u16x2 dark = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, tt), md);
+    const og_u16x2 bright = __builtin_elementwise_sub_sat(mb, v + tt);
+    return __builtin_bit_cast(uint32_t, dark) | __builtin_bit_cast(uint32_t, bright);
+}
+
 #ifndef OG_EXP_FAST_STOP
 #define OG_EXP_FAST_STOP 0
 #endif
@@ -233,33 +271,19 @@ __device__ __forceinline__ bool og_fast_quick(const uint8_t* p, int t)
 // global reservation per block, 15 % less halo than per-cell ROIs.
 // ------------------------------------------------------------------------------------------------
 #define FB_NT 512
-#define FB_RS 92                 // ROI row stride in LDS (>= 86 columns + 3 misalignment, dword multiple)
+#define FB_NW (FB_NT / 64)
+#define FB_S2 52                 // pair-ROI row stride in dwords (>= 40 + 6 + 3 misalignment, 4-dword multiple)
 #define FB_ROWS 86               // ROI rows (detection <= 80 + 6)
 #define FB_MW 80                 // detection width/height capacity of a block (2 x 40 or 1 x 64)
-#define FB_DW ((FB_RS / 4) < 32 ? (FB_RS / 4) : 32)
+#define FB_MSW (FB_MW + 3)       // score map stride: a zero gap column before, between and after the cells
+#define FB_MSZ ((FB_MSW * FB_MSW + 3) & ~3)
+#define FB_SEG (((FB_MW * FB_MW / 2 + FB_NT - 1) / FB_NT) * 128)  // pixels one wave tests: its pair slots x 2
 
-__device__ __forceinline__ int og_fast_M_blk(const uint8_t* p) { return og_fast_M(p, FB_RS); }
-
-// cell-local 3x3 NMS at two thresholds, neighbours outside the pixel's cell count as 0
-__device__ __forceinline__ void og_nms_keep2_blk(const uint8_t* Ms, int i, int j, int dw, int dh, int wC, int hC,
-                                                 int ta, int tb, bool& ka, bool& kb)
+// score-map index of detection pixel (i, j): one zero row/column separates the block's cells and surrounds
+// them, so a pixel's 8 neighbours outside its cell (or outside the detection area) read 0 without checks
+__device__ __forceinline__ int og_ms_idx(int i, int j, int wC, int hC)
 {
-    const int m = Ms[i * FB_MW + j];
-    const int ci = i >= hC, cj = j >= wC;
-    int na = 0, nb = 0;
-#pragma unroll
-    for (int di = -1; di <= 1; di++)
-#pragma unroll
-        for (int dj = -1; dj <= 1; dj++) {
-            if (di == 0 && dj == 0) continue;
-            const int ii = i + di, jj = j + dj;
-            const bool in = ii >= 0 && ii < dh && jj >= 0 && jj < dw && (ii >= hC) == ci && (jj >= wC) == cj;
-            const int mn = in ? (int)Ms[ii * FB_MW + jj] : 0;
-            na = max(na, mn > ta ? mn - 1 : 0);
-            nb = max(nb, mn > tb ? mn - 1 : 0);
-        }
-    ka = m > ta && m - 1 > na;
-    kb = m > tb && m - 1 > nb;
+    return (i + 1 + (i >= hC)) * FB_MSW + (j + 1 + (j >= wC));
 }
 
 __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_fast_blocks_kernel(OgPlan P, const OgCell* __restrict__ blocks,
@@ -268,11 +292,10 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                                                                u64* __restrict__ cand, int* __restrict__ cand_count,
                                                                int* __restrict__ status)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t roi[FB_ROWS * FB_RS + 16];
-    __shared__ __attribute__((aligned(16))) uint8_t Ms[FB_MW * FB_MW];
-    __shared__ uint16_t lst[FB_MW * FB_MW];
-    __shared__ int sh_n[4];        // 0: survivors, 1: total kept, 2: emission base, 3: cursor
-    __shared__ int cnt1[4], cnt2[4];
+    __shared__ __attribute__((aligned(16))) uint32_t roi2[FB_ROWS * FB_S2];
+    __shared__ __attribute__((aligned(16))) uint8_t Ms[FB_MSZ];
+    __shared__ uint16_t lst[FB_NW * FB_SEG];   // wave w's survivors at [w * FB_SEG, w * FB_SEG + count_w)
+    __shared__ __attribute__((aligned(16))) int wk[FB_NW][8];  // per wave: kept at t1 per cell [0..3], at t2 [4..7]
     const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int f = (int)(lin / gridDim.x);
     const OgCell cd = blocks[lin % gridDim.x];
@@ -292,141 +315,187 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const int dw = rw - 6, dh = rh - 6;
     const int wC = L.wCell, hC = L.hCell;
     if (dw <= 0 || dh <= 0) return;
-    if (tid < 4) {
-        sh_n[tid] = 0;
-        cnt1[tid] = 0;
-        cnt2[tid] = 0;
-    }
-    // ---- ROI -> LDS (dword loads of 4-byte aligned rows, all issued before the LDS stores)
+    // ---- ROI -> LDS as column pairs: roi2 dword (r, x) = ROI pixel (r, x) | ROI pixel (r, x + H) << 16, with
+    // H = the detection half-width rounded up to 4 (so both halves load from 4-byte aligned addresses).  The
+    // dwords are read from global memory first (all loads issued before the LDS stores), then split with
+    // v_perm into four pair dwords and stored as one 16-byte write.
+    const int H = (((dw + 1) >> 1) + 3) & ~3;
     const uint8_t* row0 = img + (long long)cd.y0 * pitch + cd.x0;
-    const int mis = (int)((uintptr_t)row0 & 3);
     const bool aligned_rows = ((pitch & 3) == 0);
-    uint8_t* T = roi + (aligned_rows ? mis : 0);  // T[r*FB_RS + c] = ROI pixel (r, c)
-    if (aligned_rows) {
-        const int nd = (rw + mis + 3) >> 2;
-        uint32_t buf[6];
+    const int mis = aligned_rows ? (int)((uintptr_t)row0 & 3) : 0;
+    const uint32_t* T2 = roi2 + mis;                 // T2[r*FB_S2 + x] = pair (x, x + H) of ROI row r
+    {
+        const int nq = (H + 6 + mis + 3) >> 2;       // dword groups per row
+        uint32_t blo[3], bhi[3];
+        const int q = tid & 15;
 #pragma unroll
-        for (int k = 0; k < 6; k++) {
-            const int r = (tid >> 5) + 16 * k, q = tid & 31;
-            buf[k] = (r < rh && q < nd) ? ((const uint32_t*)(row0 + (long long)r * pitch - mis))[q] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 6; k++) {
-            const int r = (tid >> 5) + 16 * k, q = tid & 31;
-            if (r < rh && q < nd) *(uint32_t*)&roi[r * FB_RS + 4 * q] = buf[k];
-        }
-    } else {
-        // rows with their own misalignment (odd pitch, e.g. a contiguous 1241-px image): every dword from two
-        // aligned loads funnel-shifted by the row's offset.  Reads stay inside the row: an ROI starts >= 16 px
-        // from the left edge and ends >= 13 px before the right one (the over-read is < 8 bytes).
-        const int nd = (rw + 3) >> 2;
-        uint32_t buf[6];
-#pragma unroll
-        for (int k = 0; k < 6; k++) {
-            const int r = (tid >> 5) + 16 * k, q = tid & 31;
-            buf[k] = 0u;
-            if (r < rh && q < nd) {
-                const uint8_t* p = row0 + (long long)r * pitch + 4 * q;
-                const uint32_t* a = (const uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
-                buf[k] = __builtin_amdgcn_alignbyte(a[1], a[0], (unsigned)((uintptr_t)p & 3));
+        for (int k = 0; k < 3; k++) {
+            const int r = (tid >> 4) + 32 * k;
+            blo[k] = 0u;
+            bhi[k] = 0u;
+            if (r < rh && q < nq) {
+                const uint8_t* rp = row0 + (long long)r * pitch - mis;
+                const int x = 4 * q - mis;          // ROI column of the dword's first byte
+                if (aligned_rows) {
+                    if (x < rw) blo[k] = *(const uint32_t*)(rp + 4 * q);
+                    if (x + H < rw) bhi[k] = *(const uint32_t*)(rp + 4 * q + H);
+                } else {
+                    // odd pitch: two aligned loads funnel-shifted by the row's offset.  Reads stay inside the
+                    // row: an ROI starts >= 16 px from the left edge, ends >= 13 px before the right one.
+                    if (x < rw) {
+                        const uint8_t* pp = rp + 4 * q;
+                        const uint32_t* a = (const uint32_t*)((uintptr_t)pp & ~(uintptr_t)3);
+                        blo[k] = __builtin_amdgcn_alignbyte(a[1], a[0], (unsigned)((uintptr_t)pp & 3));
+                    }
+                    if (x + H < rw) {
+                        const uint8_t* pp = rp + 4 * q + H;
+                        const uint32_t* a = (const uint32_t*)((uintptr_t)pp & ~(uintptr_t)3);
+                        bhi[k] = __builtin_amdgcn_alignbyte(a[1], a[0], (unsigned)((uintptr_t)pp & 3));
+                    }
+                }
             }
         }
 #pragma unroll
-        for (int k = 0; k < 6; k++) {
-            const int r = (tid >> 5) + 16 * k, q = tid & 31;
-            if (r < rh && q < nd) *(uint32_t*)&roi[r * FB_RS + 4 * q] = buf[k];
+        for (int k = 0; k < 3; k++) {
+            const int r = (tid >> 4) + 32 * k;
+            if (r < rh && q < nq) {
+                uint4 o;
+                o.x = __builtin_amdgcn_perm(bhi[k], blo[k], 0x0c040c00u);
+                o.y = __builtin_amdgcn_perm(bhi[k], blo[k], 0x0c050c01u);
+                o.z = __builtin_amdgcn_perm(bhi[k], blo[k], 0x0c060c02u);
+                o.w = __builtin_amdgcn_perm(bhi[k], blo[k], 0x0c070c03u);
+                *(uint4*)&roi2[r * FB_S2 + 4 * q] = o;
+            }
         }
     }
-    for (int idx = tid * 4; idx < dh * FB_MW; idx += FB_NT * 4) *(uint32_t*)&Ms[idx] = 0u;
+    for (int idx = tid * 4; idx < FB_MSZ; idx += FB_NT * 4) *(uint32_t*)&Ms[idx] = 0u;
     __syncthreads();
 #if OG_EXP_FAST_STOP == 1  // timing experiments only (tools/fast_variants.py): results are wrong
-    if (roi[tid] == 255 && roi[tid + 1] == 254) cand_count[0] = 1;
+    if (roi2[tid] == 255u && roi2[tid + 1] == 254u) cand_count[0] = 1;
     return;
 #endif
     const int t1 = min(max(P.iniTh, 0), 255), t2 = min(max(P.minTh, 0), 255);
     const int tq = min(t1, t2);
-    // ---- stage 1: quick test on every detection pixel (one row per wave, lanes over columns)
-    for (int i = wv; i < dh; i += FB_NT / 64) {
-        for (int j0 = 0; j0 < dw; j0 += 64) {
-            const int j = j0 + lane;
-            const bool sv = j < dw && og_fast_quick<FB_RS>(&T[(i + 3) * FB_RS + (j + 3)], tq);
-            const u64 mask = __ballot(sv);
-            if (mask) {
-                int base = 0;
-                if (lane == 0) base = atomicAdd(&sh_n[0], __popcll(mask));
-                base = __shfl(base, 0);
-                if (sv) lst[base + __popcll(mask & ((1ull << lane) - 1ull))] = (uint16_t)(i * FB_MW + j);
-            }
-        }
+    const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
+    const u64 lt_mask = (1ull << lane) - 1ull;
+    uint16_t* seg = lst + wv * FB_SEG;
+    // ---- stage 1: quick test on every detection pixel, two per lane: pair slot p -> row i, column c (pixels
+    // (i, c) and (i, c + H)); wave w takes slots [64w, 64w + 64) + 512k and appends its survivors to its own
+    // segment (wave-uniform count, no atomics)
+    const int npair = dh * H;
+    const unsigned invH = (1u << 20) / (unsigned)H + 1u;  // exact p / H for p < 3200, H <= 40
+    int ns = 0;
+    for (int p0 = wv * 64; p0 < npair; p0 += FB_NT) {
+        const int pp = p0 + lane;
+        const int i = (int)(__umul24((unsigned)pp, invH) >> 20), c = pp - (int)__umul24((unsigned)i, (unsigned)H);
+        uint32_t r = 0u;
+        if (pp < npair) r = og_fast_quick2(&T2[(i + 3) * FB_S2 + (c + 3)], FB_S2, tt);
+        const bool s0 = (r & 0xffffu) != 0u && c < dw;
+        const bool s1 = (r >> 16) != 0u && c + H < dw;
+        const u64 m0 = __ballot(s0);
+        const u64 m1 = __ballot(s1);
+        const int n0 = __popcll(m0);
+        if (s0) seg[ns + __popcll(m0 & lt_mask)] = (uint16_t)((i << 7) | c);
+        if (s1) seg[ns + n0 + __popcll(m1 & lt_mask)] = (uint16_t)((i << 7) | (c + H));
+        ns += n0 + __popcll(m1);
     }
-    __syncthreads();
-    const int nsurv = sh_n[0];
 #if OG_EXP_FAST_STOP == 2
-    if (nsurv == 12345) cand_count[0] = 1;
+    if (ns == 12345) cand_count[0] = 1;
     return;
 #endif
-    if (nsurv == 0) return;
-    // ---- stage 2: exact M for every survivor (eager: ~92 % of 2x2 blocks hold a cell that falls back to
-    // minThFAST, so a lazy second pass costs more than it saves)
-    for (int e = tid; e < nsurv; e += FB_NT) {
-        const int pix = lst[e] & 0x1fff;
-        const int i = pix / FB_MW, j = pix % FB_MW;
-        Ms[pix] = (uint8_t)og_fast_M_blk(&T[(i + 3) * FB_RS + (j + 3)]);
+    // ---- stage 2: exact M for every survivor of the wave (eager: ~92 % of 2x2 blocks hold a cell that falls
+    // back to minThFAST, so a lazy second pass costs more than it saves).  Single pixels are u16 reads of
+    // the pair layout (element step 2 per column).
+    const uint16_t* T16 = (const uint16_t*)T2;
+    for (int e = lane; e < ns; e += 64) {
+        const int ent = seg[e];
+        const int i = ent >> 7, j = ent & 127;
+        const int hi = j >= H;
+        const int x = j - (hi ? H : 0);
+        Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)og_fast_M<2>(&T16[2 * ((i + 3) * FB_S2 + (x + 3)) + hi], 2 * FB_S2);
     }
     __syncthreads();
-    // ---- stage 3: same-cell NMS at both thresholds; keep bits in the entry (13: t1, 14: t2), counts per cell
-    for (int e = tid; e < nsurv; e += FB_NT) {
-        const int pix = lst[e] & 0x1fff;
-        const int i = pix / FB_MW, j = pix % FB_MW;
-        bool k1, k2;
-        og_nms_keep2_blk(Ms, i, j, dw, dh, wC, hC, t1, t2, k1, k2);
-        lst[e] = (uint16_t)(pix | (k1 ? 0x2000 : 0) | (k2 ? 0x4000 : 0));
-        const int cell = (i >= hC) * 2 + (j >= wC);
-        if (k1) atomicAdd(&cnt1[cell], 1);
-        if (k2) atomicAdd(&cnt2[cell], 1);
+    // ---- stage 3: same-cell 3x3 NMS at both thresholds.  cv::FAST keeps a corner (score M-1) iff its score
+    // beats every neighbour's score, where non-corners score 0: with the gap layout and M <= t for every
+    // non-corner, that is  M > max(t, 1)  and  M > max over the 8 neighbours of M.
+    const int tA = max(t1, 1), tB = max(t2, 1);
+    int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
+    for (int e0 = 0; e0 < ns; e0 += 64) {
+        const int e = e0 + lane;
+        bool k1 = false, k2 = false;
+        int cell = 0;
+        if (e < ns) {
+            const int ent = seg[e];
+            const int i = ent >> 7, j = ent & 127;
+            const uint8_t* q = &Ms[og_ms_idx(i, j, wC, hC) - FB_MSW - 1];
+            const int m = q[FB_MSW + 1];
+            const int nb = max(max(max(q[0], q[1]), max(q[2], q[FB_MSW])),
+                               max(max(q[FB_MSW + 2], q[2 * FB_MSW]), max(q[2 * FB_MSW + 1], q[2 * FB_MSW + 2])));
+            k1 = m > tA && m > nb;
+            k2 = m > tB && m > nb;
+            cell = (i >= hC) * 2 + (j >= wC);
+            seg[e] = (uint16_t)(ent | (k1 ? 0x4000 : 0) | (k2 ? 0x8000 : 0));
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            c1[c] += __popcll(__ballot(k1 && cell == c));
+            c2[c] += __popcll(__ballot(k2 && cell == c));
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            wk[wv][c] = c1[c];
+            wk[wv][4 + c] = c2[c];
+        }
     }
     __syncthreads();
     // per cell: iniThFAST unless the cell is empty at it (src/ORBextractor.cc:809-816)
-    int cnt = 0;
+    int tot1[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int w = 0; w < FB_NW; w++) {
+        const int4 a = *(const int4*)&wk[w][0];
+        tot1[0] += a.x;
+        tot1[1] += a.y;
+        tot1[2] += a.z;
+        tot1[3] += a.w;
+    }
     unsigned useT2 = 0;
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-        const int a = cnt1[c];
-        cnt += a ? a : cnt2[c];
-        useT2 |= (a ? 0u : 1u) << c;
-    }
-    if (cnt == 0) return;
+    for (int c = 0; c < 4; c++) useT2 |= (tot1[c] ? 0u : 1u) << c;
+    int kept = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) kept += ((useT2 >> c) & 1u) ? wk[wv][4 + c] : wk[wv][c];
 #if OG_EXP_FAST_STOP == 3
-    if (cnt == 12345) cand_count[0] = 1;
+    if (kept == 12345) cand_count[0] = 1;
     return;
 #endif
-    if (tid == 0) {
-        const int base = atomicAdd(&cand_count[f * P.nlevels + l], cnt);
-        sh_n[2] = base;
-        if (base + cnt > L.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
+    if (kept == 0) return;
+    // ---- stage 4: each wave reserves its own slots (the octree orders candidates by position, not slot)
+    int base = 0;
+    if (lane == 0) {
+        base = atomicAdd(&cand_count[f * P.nlevels + l], kept);
+        if (base + kept > L.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
     }
-    __syncthreads();
-    const int base = sh_n[2];
-    if (base + cnt > L.cand_cap) return;
+    base = __shfl(base, 0);
+    if (base + kept > L.cand_cap) return;
     u64* out = cand + (long long)f * P.cand_per_frame + L.cand_off + base;
     const int ox = cd.x0 - L.minB + 3, oy = cd.y0 - L.minB + 3;
-    for (int e = tid; e - tid < nsurv; e += FB_NT) {
-        int ent = 0;
-        if (e < nsurv) ent = lst[e];
-        const int pix = ent & 0x1fff;
-        const int i = pix / FB_MW, j = pix % FB_MW;
-        const int cell = (i >= hC) * 2 + (j >= wC);
-        const bool keep = e < nsurv && ((ent & (((useT2 >> cell) & 1u) ? 0x4000 : 0x2000)) != 0);
-        const u64 mask = __ballot(keep);
-        if (mask) {
-            int wb = 0;
-            if (lane == 0) wb = atomicAdd(&sh_n[3], __popcll(mask));
-            wb = __shfl(wb, 0);
-            if (keep) {
-                const int pos = wb + __popcll(mask & ((1ull << lane) - 1ull));
-                out[pos] = og_pack_cand(ox + j, oy + i, Ms[pix] - 1);
-            }
+    int run = 0;
+    for (int e0 = 0; e0 < ns; e0 += 64) {
+        const int e = e0 + lane;
+        bool keep = false;
+        int i = 0, j = 0;
+        if (e < ns) {
+            const int ent = seg[e];
+            i = (ent >> 7) & 127;
+            j = ent & 127;
+            const int cell = (i >= hC) * 2 + (j >= wC);
+            keep = (ent & (((useT2 >> cell) & 1u) ? 0x8000 : 0x4000)) != 0;
         }
+        const u64 mask = __ballot(keep);
+        if (keep) out[run + __popcll(mask & lt_mask)] = og_pack_cand(ox + j, oy + i, Ms[og_ms_idx(i, j, wC, hC)] - 1);
+        run += __popcll(mask);
     }
 }
 
