@@ -277,7 +277,6 @@ __device__ __forceinline__ uint32_t og_fast_quick2(const uint32_t* p, int st, og
 #define FB_MW 80                 // detection width/height capacity of a block (2 x 40 or 1 x 64)
 #define FB_MSW (FB_MW + 3)       // score map stride: a zero gap column before, between and after the cells
 #define FB_MSZ ((FB_MSW * FB_MSW + 3) & ~3)
-#define FB_SEG (((FB_MW * FB_MW / 2 + FB_NT - 1) / FB_NT) * 128)  // pixels one wave tests: its pair slots x 2
 
 // score-map index of detection pixel (i, j): one zero row/column separates the block's cells and surrounds
 // them, so a pixel's 8 neighbours outside its cell (or outside the detection area) read 0 without checks
@@ -294,8 +293,10 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 {
     __shared__ __attribute__((aligned(16))) uint32_t roi2[FB_ROWS * FB_S2];
     __shared__ __attribute__((aligned(16))) uint8_t Ms[FB_MSZ];
-    __shared__ uint16_t lst[FB_NW * FB_SEG];   // wave w's survivors at [w * FB_SEG, w * FB_SEG + count_w)
+    __shared__ uint16_t lst[FB_MW * FB_MW];    // quick-test survivors, (i << 7) | j + keep bits 14 (t1), 15 (t2)
+    __shared__ int sh_ns;
     __shared__ __attribute__((aligned(16))) int wk[FB_NW][8];  // per wave: kept at t1 per cell [0..3], at t2 [4..7]
+    __shared__ int sh_base;
     const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int f = (int)(lin / gridDim.x);
     const OgCell cd = blocks[lin % gridDim.x];
@@ -369,6 +370,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
     }
     for (int idx = tid * 4; idx < FB_MSZ; idx += FB_NT * 4) *(uint32_t*)&Ms[idx] = 0u;
+    if (tid == 0) sh_ns = 0;
     __syncthreads();
 #if OG_EXP_FAST_STOP == 1  // timing experiments only (tools/fast_variants.py): results are wrong
     if (roi2[tid] == 255u && roi2[tid + 1] == 254u) cand_count[0] = 1;
@@ -378,13 +380,11 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const int tq = min(t1, t2);
     const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
     const u64 lt_mask = (1ull << lane) - 1ull;
-    uint16_t* seg = lst + wv * FB_SEG;
     // ---- stage 1: quick test on every detection pixel, two per lane: pair slot p -> row i, column c (pixels
-    // (i, c) and (i, c + H)); wave w takes slots [64w, 64w + 64) + 512k and appends its survivors to its own
-    // segment (wave-uniform count, no atomics)
+    // (i, c) and (i, c + H)); wave w takes slots [64w, 64w + 64) + 512k; one LDS reservation per wave
+    // iteration appends its survivors to the block's flat list (stages 2-4 then spread the list evenly)
     const int npair = dh * H;
     const unsigned invH = (1u << 20) / (unsigned)H + 1u;  // exact p / H for p < 3200, H <= 40
-    int ns = 0;
     for (int p0 = wv * 64; p0 < npair; p0 += FB_NT) {
         const int pp = p0 + lane;
         const int i = (int)(__umul24((unsigned)pp, invH) >> 20), c = pp - (int)__umul24((unsigned)i, (unsigned)H);
@@ -394,11 +394,17 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const bool s1 = (r >> 16) != 0u && c + H < dw;
         const u64 m0 = __ballot(s0);
         const u64 m1 = __ballot(s1);
-        const int n0 = __popcll(m0);
-        if (s0) seg[ns + __popcll(m0 & lt_mask)] = (uint16_t)((i << 7) | c);
-        if (s1) seg[ns + n0 + __popcll(m1 & lt_mask)] = (uint16_t)((i << 7) | (c + H));
-        ns += n0 + __popcll(m1);
+        const int n0 = __popcll(m0), n = n0 + __popcll(m1);
+        if (n) {
+            int b = 0;
+            if (lane == 0) b = atomicAdd(&sh_ns, n);
+            b = __builtin_amdgcn_readfirstlane(b);
+            if (s0) lst[b + __popcll(m0 & lt_mask)] = (uint16_t)((i << 7) | c);
+            if (s1) lst[b + n0 + __popcll(m1 & lt_mask)] = (uint16_t)((i << 7) | (c + H));
+        }
     }
+    __syncthreads();
+    const int ns = sh_ns;
 #if OG_EXP_FAST_STOP == 2
     if (ns == 12345) cand_count[0] = 1;
     return;
@@ -407,8 +413,8 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     // back to minThFAST, so a lazy second pass costs more than it saves).  Single pixels are u16 reads of
     // the pair layout (element step 2 per column).
     const uint16_t* T16 = (const uint16_t*)T2;
-    for (int e = lane; e < ns; e += 64) {
-        const int ent = seg[e];
+    for (int e = tid; e < ns; e += FB_NT) {
+        const int ent = lst[e];
         const int i = ent >> 7, j = ent & 127;
         const int hi = j >= H;
         const int x = j - (hi ? H : 0);
@@ -420,12 +426,12 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     // non-corner, that is  M > max(t, 1)  and  M > max over the 8 neighbours of M.
     const int tA = max(t1, 1), tB = max(t2, 1);
     int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
-    for (int e0 = 0; e0 < ns; e0 += 64) {
+    for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {  // same entry -> wave assignment as stage 4
         const int e = e0 + lane;
         bool k1 = false, k2 = false;
         int cell = 0;
         if (e < ns) {
-            const int ent = seg[e];
+            const int ent = lst[e];
             const int i = ent >> 7, j = ent & 127;
             const uint8_t* q = &Ms[og_ms_idx(i, j, wC, hC) - FB_MSW - 1];
             const int m = q[FB_MSW + 1];
@@ -434,7 +440,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             k1 = m > tA && m > nb;
             k2 = m > tB && m > nb;
             cell = (i >= hC) * 2 + (j >= wC);
-            seg[e] = (uint16_t)(ent | (k1 ? 0x4000 : 0) | (k2 ? 0x8000 : 0));
+            lst[e] = (uint16_t)(ent | (k1 ? 0x4000 : 0) | (k2 ? 0x8000 : 0));
         }
 #pragma unroll
         for (int c = 0; c < 4; c++) {
@@ -463,31 +469,41 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     unsigned useT2 = 0;
 #pragma unroll
     for (int c = 0; c < 4; c++) useT2 |= (tot1[c] ? 0u : 1u) << c;
-    int kept = 0;
+    // kept per wave (selected threshold per cell), this wave's offset and the block total
+    int kept = 0, before = 0, total = 0;
 #pragma unroll
-    for (int c = 0; c < 4; c++) kept += ((useT2 >> c) & 1u) ? wk[wv][4 + c] : wk[wv][c];
+    for (int w = 0; w < FB_NW; w++) {
+        int kw = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) kw += ((useT2 >> c) & 1u) ? wk[w][4 + c] : wk[w][c];
+        before += w < wv ? kw : 0;
+        kept = w == wv ? kw : kept;
+        total += kw;
+    }
 #if OG_EXP_FAST_STOP == 3
-    if (kept == 12345) cand_count[0] = 1;
+    if (total == 12345) cand_count[0] = 1;
     return;
 #endif
-    if (kept == 0) return;
-    // ---- stage 4: each wave reserves its own slots (the octree orders candidates by position, not slot)
-    int base = 0;
-    if (lane == 0) {
-        base = atomicAdd(&cand_count[f * P.nlevels + l], kept);
-        if (base + kept > L.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
+    if (total == 0) return;  // block-uniform
+    // ---- stage 4: one reservation per block (sh_base); each wave writes its kept entries at its offset (the
+    // octree orders candidates by position, not slot)
+    if (tid == 0) {
+        const int b = atomicAdd(&cand_count[f * P.nlevels + l], total);
+        if (b + total > L.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
+        sh_base = b;
     }
-    base = __shfl(base, 0);
-    if (base + kept > L.cand_cap) return;
+    __syncthreads();
+    const int base = sh_base + before;
+    if (sh_base + total > L.cand_cap || kept == 0) return;
     u64* out = cand + (long long)f * P.cand_per_frame + L.cand_off + base;
     const int ox = cd.x0 - L.minB + 3, oy = cd.y0 - L.minB + 3;
     int run = 0;
-    for (int e0 = 0; e0 < ns; e0 += 64) {
+    for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
         const int e = e0 + lane;
         bool keep = false;
         int i = 0, j = 0;
         if (e < ns) {
-            const int ent = seg[e];
+            const int ent = lst[e];
             i = (ent >> 7) & 127;
             j = ent & 127;
             const int cell = (i >= hC) * 2 + (j >= wC);
