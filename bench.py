@@ -28,6 +28,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "frames/sec ORB extract+match @1920×1080, 2000 feat; 1/2/4/8 MI355X"
+VALU_CLK_HZ = 2.4e9
+VALU_SIMDS = 1024
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -465,14 +467,26 @@ def main():
     dom_bytes = stage_bytes(dom, Bs, P, cand_total, kp_total)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
+    valu = None
     if args.workload == "mono_init" and os.path.exists(args.pmc_json):
         try:
             pmc = json.load(open(args.pmc_json))
-            traffic = pmc.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
-            if traffic is not None and pmc.get("batch", Bs) != Bs:  # per-frame linear in the batch
-                traffic = int(traffic * Bs / pmc["batch"])
+            pk = pmc.get("kernels", {}).get(dom, {})
+            scale = Bs / pmc["batch"] if pmc.get("batch", Bs) != Bs else 1.0  # per-frame linear in the batch
+            traffic = pk.get("hbm_bytes_per_launch")
+            if traffic is not None:
+                traffic = int(traffic * scale)
+            if pk.get("SQ_INSTS_VALU"):
+                # VALU issue utilisation: a wave64 VALU instruction occupies a SIMD-32 for 2 cycles
+                # (MI355X_MICROARCH.md, wave scheduling); 256 CUs x 4 SIMDs at 2.4 GHz
+                insts = pk["SQ_INSTS_VALU"] * scale
+                valu = {"insts_per_launch": int(insts),
+                        "issue_frac": round(insts * 2 / (dom_ms * 1e-3 * VALU_CLK_HZ * VALU_SIMDS), 4),
+                        "note": "PMC SQ_INSTS_VALU (profiles/pmc_latest.json) x 2 cycles / (avg_launch_ms x "
+                                "2.4 GHz x 1024 SIMDs)"}
         except Exception:
             traffic = None
+            valu = None
 
     total_frames = world * B * args.steps
     value = total_frames / dt
@@ -511,6 +525,7 @@ def main():
             "avg_launch_ms": round(dom_ms, 4),
             "avg_launch_span_ms": round(dom_ms_span, 4),
             "launch_time": "union of the kernel's HIP-event intervals over the concurrent streams / launches",
+            "valu": valu,
         },
         "stages_ms_per_launch": {k: round(v, 4) for k, v in stages.items()},
         "stages_busy_ms_per_step": {k: round(v / args.steps, 4) for k, v in union_acc.items()},
