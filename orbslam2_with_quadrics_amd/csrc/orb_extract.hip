@@ -585,7 +585,9 @@ __device__ __forceinline__ unsigned og_cand_order(int x, int y, const OgLevel& L
     return (unsigned)(((ci * L.nCols + cj) * L.hCell + ly) * L.wCell + lx);
 }
 
+#ifndef OCT_U
 #define OCT_U 4  // candidates per thread per pass with all loads hoisted (latency batching)
+#endif
 
 #ifndef OG_OCT_PROFILE
 #define OG_OCT_PROFILE 0
@@ -624,10 +626,14 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     __shared__ int wsum[32];
     __shared__ int sv[16];
 
-    const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    // level-major dispatch order, level 0 first: the finest level has the most candidates (and rounds), so
+    // its workgroups start in the first wave of residency instead of being interleaved with the short ones
+    const int nb = (int)gridDim.x / P.nlevels;  // frames in the launch
+    const int l = (int)blockIdx.x / nb, f = (int)blockIdx.x % nb, tid = threadIdx.x;
     const OgLevel& L = P.lv[l];
     const int C = min(cand_count[f * P.nlevels + l], L.cand_cap);
     const u64* K = cand + (long long)f * P.cand_per_frame + L.cand_off;
+    const uint32_t* K32 = (const uint32_t*)K;  // [2k] = x | y << 16, [2k+1] = response
     uint16_t* NO = node_of + (long long)f * P.cand_per_frame + L.cand_off;
     const int N = L.N;
     const int nIni = L.nIni;
@@ -688,12 +694,12 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     __syncthreads();
     // remap keys to root positions and count the children of the first pass's splits (cnt > 1)
     for (int base = tid; base < C; base += OCT_NT * OCT_U) {
-        u64 kv[OCT_U];
+        uint32_t kv[OCT_U];
         int no[OCT_U];
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) {
             const int k = base + u * OCT_NT;
-            kv[u] = k < C ? K[k] : 0ull;
+            kv[u] = k < C ? K32[2 * k] : 0u;
             no[u] = k < C ? NO[k] : 0;
         }
 #pragma unroll
@@ -703,8 +709,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 const int n = aux[no[u]];
                 NO[k] = (uint16_t)n;
                 const OctNode& nd = nodes[0][n];
-                if (nd.cnt > 1)
-                    atomicAdd(&childCnt[4 * n + og_quadrant((int)(kv[u] & 0xffff), (int)((kv[u] >> 16) & 0xffff), nd)], 1);
+                if (nd.cnt > 1) atomicAdd(&childCnt[4 * n + og_quadrant((int)(kv[u] & 0xffff), (int)(kv[u] >> 16), nd)], 1);
             }
         }
     }
@@ -844,12 +849,12 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         // ---- one pass over the keys: move to the new list position, and either count the children of
         // the next round's split candidates or (last round) keep the best key per node (:744-760)
         for (int base = tid; base < C; base += OCT_NT * OCT_U) {
-            u64 kv[OCT_U];
+            uint32_t kv[OCT_U];
             int no[OCT_U];
 #pragma unroll
             for (int u = 0; u < OCT_U; u++) {
                 const int k = base + u * OCT_NT;
-                kv[u] = k < C ? K[k] : 0ull;
+                kv[u] = k < C ? K32[2 * k] : 0u;
                 no[u] = k < C ? NO[k] : 0;
             }
 #pragma unroll
@@ -857,14 +862,14 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 const int k = base + u * OCT_NT;
                 if (k < C) {
                     const int n = no[u];
-                    const int x = (int)(kv[u] & 0xffff), y = (int)((kv[u] >> 16) & 0xffff);
+                    const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
                     const int r = splitRank[n];
                     int n2;
                     if (r >= 0 && r < A) n2 = childPos[4 * n + og_quadrant(x, y, cn[n])];
                     else n2 = newPos[n];
                     NO[k] = (uint16_t)n2;
                     if (done) {
-                        const int resp = (int)((kv[u] >> 32) & 0xff);
+                        const int resp = (int)(K32[2 * k + 1] & 0xff);
                         atomicMax(&best[n2], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
                     } else {
                         const OctNode& nd = nn[n2];
@@ -1225,7 +1230,7 @@ void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const u
 void og_launch_octree(hipStream_t s, const OgPlan& P, const u64* cand, const int* cand_count, uint16_t* node_of,
                       uint32_t* oct_xy, uint8_t* oct_resp, int* oct_count, int* status, int B)
 {
-    hipLaunchKernelGGL(og_octree_kernel, dim3(P.nlevels, B), dim3(OCT_NT), 0, s, P, cand, cand_count, node_of, oct_xy,
+    hipLaunchKernelGGL(og_octree_kernel, dim3(P.nlevels * B), dim3(OCT_NT), 0, s, P, cand, cand_count, node_of, oct_xy,
                        oct_resp, oct_count, status);
 }
 
