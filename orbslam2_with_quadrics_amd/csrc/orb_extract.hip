@@ -955,6 +955,8 @@ __device__ __forceinline__ int og_reflect101(int i, int n)
 #define RAW_W 43
 #define RAW_S 52  // 43 + 3 misalignment bytes, dword multiple; 13 dwords: conflict-free lane-per-row reads
 #define BL_W 37
+#define HP_ROWS 22  // row pairs of the horizontal pass (43 rows -> 22 pairs)
+#define HP_S 40     // pair-row stride in dwords (10 groups of 4 columns)
 
 __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, const uint8_t* __restrict__ img0,
                                                                     long long pitch0, long long fstride0,
@@ -966,8 +968,8 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
                                                                     uint8_t* __restrict__ desc,
                                                                     int* __restrict__ counts)
 {
-    __shared__ uint8_t raw[DK_WAVES][RAW_W * RAW_S];
-    __shared__ uint16_t hb[DK_WAVES][RAW_W * BL_W];
+    __shared__ __attribute__((aligned(16))) uint8_t raw[DK_WAVES][RAW_W * RAW_S];
+    __shared__ __attribute__((aligned(16))) uint32_t hp[DK_WAVES][HP_ROWS * HP_S];
     __shared__ uint8_t bl[DK_WAVES][BL_W * BL_W + 3];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
@@ -986,7 +988,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     if (g == 0 && lane == 0) counts[f] = total;
     const bool active = l >= 0;
     uint8_t* R = raw[w];
-    uint16_t* Hb = hb[w];
+    uint32_t* Hp = hp[w];
     uint8_t* Bl = bl[w];
     int cx = 0, cy = 0, resp = 0, lw = 1, lh = 1;
     if (active) {
@@ -1012,13 +1014,28 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             // funnel-shifted by the row's own misalignment (any pitch, e.g. a contiguous 1241-px KITTI image);
             // the farthest byte read is x = cx + 26, inside the row (level starts are 256-B aligned, so the
             // rounded-down first load never precedes the image)
+            // All 2 x 8 loads of a lane are issued before the first use (one memory round trip, not eight).
             const uint8_t* src0 = img + (long long)(cy - 21) * pitch + (cx - 21);
-            for (int idx = lane; idx < RAW_W * 11; idx += 64) {
+            constexpr int NIT = (RAW_W * 11 + 63) / 64;
+            uint32_t lo[NIT], hi[NIT];
+            unsigned sh[NIT];
+#pragma unroll
+            for (int k = 0; k < NIT; k++) {
+                const int idx = min(lane + 64 * k, RAW_W * 11 - 1);
                 const int r = idx / 11, q = idx - r * 11;
                 const uint8_t* p = src0 + (long long)r * pitch + 4 * q;
                 const uint32_t* a = (const uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
-                const unsigned sh = (unsigned)((uintptr_t)p & 3);
-                *(uint32_t*)&R[r * RAW_S + 4 * q] = __builtin_amdgcn_alignbyte(a[1], a[0], sh);
+                sh[k] = (unsigned)((uintptr_t)p & 3);
+                lo[k] = a[0];
+                hi[k] = a[1];
+            }
+#pragma unroll
+            for (int k = 0; k < NIT; k++) {
+                const int idx = lane + 64 * k;
+                if (idx < RAW_W * 11) {
+                    const int r = idx / 11, q = idx - r * 11;
+                    *(uint32_t*)&R[r * RAW_S + 4 * q] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+                }
             }
         } else {  // within 21 px of the border: BORDER_REFLECT_101 per pixel
             for (int idx = lane; idx < RAW_W * RAW_W; idx += 64) {
@@ -1051,32 +1068,64 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         }
     }
     const float angle = og_fast_atan2((float)m01, (float)m10);
-    // ---- 7x7 Gaussian (sigma 2, BORDER_REFLECT_101) of the 37x37 window the tests can reach
-    const int gk[7] = {18, 34, 49, 55, 49, 34, 18};
-    // horizontal pass: one lane per window row, a 7-tap sliding window along it (43 rows x 37 outputs)
-    if (active && lane < RAW_W) {
-        const uint8_t* s = Rb + lane * RAW_S;
-        int w0 = s[0], w1 = s[1], w2 = s[2], w3 = s[3], w4 = s[4], w5 = s[5];
+    // ---- 7x7 Gaussian (sigma 2, BORDER_REFLECT_101) of the 37x37 window the tests can reach.  Integer
+    // weights gk[i]*gk[j] summed exactly and rounded once ((acc + 2^15) >> 16), so any factoring is exact:
+    // horizontal pass with v_dot4_u32_u8 (taps 0-3 and 4-6 of a byte window), vertical pass with
+    // v_dot2_u32_u16 over row pairs of the horizontal sums (<= 257 * 255 = 65535, exact in u16).
+    // horizontal: item = (row pair rp, 4-column group g): rows 2rp, 2rp+1, outputs 4g..4g+3, stored as
+    // (row 2rp, row 2rp+1) u16 pairs Hp[rp][col]
+    if (active) {
+        const uint32_t glo = 18u | (34u << 8) | (49u << 16) | (55u << 24), ghi = 49u | (34u << 8) | (18u << 16);
+        for (int it = lane; it < HP_ROWS * 10; it += 64) {
+            const int rp = it / 10, g = it - rp * 10;
+            uint32_t hv[2][4];
 #pragma unroll
-        for (int c = 0; c < BL_W; c++) {
-            const int w6 = s[c + 6];
-            Hb[lane * BL_W + c] = (uint16_t)(gk[0] * w0 + gk[1] * w1 + gk[2] * w2 + gk[3] * w3 + gk[4] * w4 +
-                                             gk[5] * w5 + gk[6] * w6);
-            w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
+            for (int h = 0; h < 2; h++) {
+                const int r = min(2 * rp + h, RAW_W - 1);  // row 43 (pair 21, high half) is never read
+                const uint32_t* rr = (const uint32_t*)(Rb + r * RAW_S) + g;
+                const uint32_t d0 = rr[0], d1 = rr[1], d2 = rr[2];
+                hv[h][0] = __builtin_amdgcn_udot4(d1 & 0x00ffffffu, ghi, __builtin_amdgcn_udot4(d0, glo, 0u, false), false);
+#pragma unroll
+                for (int k = 1; k < 4; k++) {
+                    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, k), w1 = __builtin_amdgcn_alignbyte(d2, d1, k);
+                    hv[h][k] = __builtin_amdgcn_udot4(w1 & 0x00ffffffu, ghi, __builtin_amdgcn_udot4(w0, glo, 0u, false), false);
+                }
+            }
+            uint4 o;
+            o.x = hv[0][0] | (hv[1][0] << 16);
+            o.y = hv[0][1] | (hv[1][1] << 16);
+            o.z = hv[0][2] | (hv[1][2] << 16);
+            o.w = hv[0][3] | (hv[1][3] << 16);
+            *(uint4*)&Hp[rp * HP_S + 4 * g] = o;
         }
     }
     __syncthreads();
-    // vertical pass: one lane per output column, sliding down the 37 output rows
-    if (active && lane < BL_W) {
-        const uint16_t* h = Hb + lane;
-        int w0 = h[0], w1 = h[BL_W], w2 = h[2 * BL_W], w3 = h[3 * BL_W], w4 = h[4 * BL_W], w5 = h[5 * BL_W];
+    // vertical: item = (column c, 4 output rows 4m..4m+3) from row pairs 2m..2m+4; even rows take taps
+    // (g0,g1)(g2,g3)(g4,g5)(g6,0), odd rows (0,g0)(g1,g2)(g3,g4)(g5,g6)
+    if (active) {
+        typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+        const u16x2v e0 = {18, 34}, e1 = {49, 55}, e2 = {49, 34}, e3 = {18, 0};
+        const u16x2v o0 = {0, 18}, o1 = {34, 49}, o2 = {55, 49}, o3 = {34, 18};
+        for (int it = lane; it < BL_W * 10; it += 64) {
+            const int m = it / BL_W, c = it - m * BL_W;
+            u16x2v pr[5];
 #pragma unroll
-        for (int r = 0; r < BL_W; r++) {
-            const int w6 = h[(r + 6) * BL_W];
-            const int acc = gk[0] * w0 + gk[1] * w1 + gk[2] * w2 + gk[3] * w3 + gk[4] * w4 + gk[5] * w5 + gk[6] * w6;
-            const int v = (acc + (1 << 15)) >> 16;
-            Bl[r * BL_W + lane] = (uint8_t)(v > 255 ? 255 : v);
-            w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
+            for (int k = 0; k < 5; k++) pr[k] = __builtin_bit_cast(u16x2v, Hp[min(2 * m + k, HP_ROWS - 1) * HP_S + c]);
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int r0 = 4 * m + 2 * h;  // rows r0 (even) and r0 + 1 (odd) from pairs 2m+h ..
+                const u16x2v* q = pr + h;
+                uint32_t ae = __builtin_amdgcn_udot2(q[0], e0, 0u, false);
+                ae = __builtin_amdgcn_udot2(q[1], e1, ae, false);
+                ae = __builtin_amdgcn_udot2(q[2], e2, ae, false);
+                ae = __builtin_amdgcn_udot2(q[3], e3, ae, false);
+                uint32_t ao = __builtin_amdgcn_udot2(q[0], o0, 0u, false);
+                ao = __builtin_amdgcn_udot2(q[1], o1, ao, false);
+                ao = __builtin_amdgcn_udot2(q[2], o2, ao, false);
+                ao = __builtin_amdgcn_udot2(q[3], o3, ao, false);
+                if (r0 < BL_W) Bl[r0 * BL_W + c] = (uint8_t)min((ae + (1u << 15)) >> 16, 255u);
+                if (r0 + 1 < BL_W) Bl[(r0 + 1) * BL_W + c] = (uint8_t)min((ao + (1u << 15)) >> 16, 255u);
+            }
         }
     }
     __syncthreads();
