@@ -39,6 +39,7 @@ __device__ __forceinline__ unsigned og_xcd_remap(unsigned orig, unsigned nwg)
 #define RZ_TH 16                       // output rows per workgroup (4 waves x 4 rows)
 #define RZ_SROWS 28                    // >= source rows a 16-row tile touches (15 * 1.6 + 2, scale <= 1.6)
 #define RZ_SC 448                      // LDS row stride: >= 255 * 1.6 + 2 source bytes + 15 alignment slack
+typedef unsigned short og_rz_u16x2 __attribute__((ext_vector_type(2)));
 
 // One workgroup = 16 output rows x 256 output columns of one frame (balanced tiles: a 1111-px level is 5
 // tiles, not 1024 + 87).  The source rows/columns the tile touches are staged in LDS with 16-byte loads
@@ -108,6 +109,51 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
     }
     const int n = min(4, dw - dxt);
     uint8_t* D = dst + (long long)f * dst_fstride + dxt;
+    auto store = [&](int r, uint32_t packed) {
+        uint8_t* Dr = D + (long long)(dy0 + r) * dst_pitch;
+        if (n == 4 && ((((uintptr_t)Dr) & 3) == 0)) {
+            *(uint32_t*)Dr = packed;
+        } else {
+            for (int k = 0; k < n; k++) Dr[k] = (uint8_t)(packed >> (8 * k));
+        }
+    };
+    if ((src_pitch & 15) == 0) {
+        // every staged row has the same misalignment: the (S[sx], S[sx+1]) pair of column k is one v_perm of
+        // the two LDS dwords around it (selector fixed per thread), the horizontal pass one v_dot2_u32_u16
+        const int m0 = mis[0];
+        int dwk[4];
+        uint32_t sel[4];
+        og_rz_u16x2 wt[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int bp = m0 + sx[k];
+            const unsigned o = (unsigned)(bp & 3);
+            dwk[k] = bp >> 2;
+            sel[k] = o | 0x0c00u | ((o + 1u) << 16) | 0x0c000000u;
+            wt[k] = og_rz_u16x2{(unsigned short)a0[k], (unsigned short)a1[k]};  // a1 = 0 at the right border
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; rr++) {
+            const int r = 4 * rg + rr;
+            if (r >= ny) break;
+            const int4 yt = ytab[dy0 + r];
+            const uint32_t* R0 = (const uint32_t*)(S + (yt.x - sy0) * RZ_SC);
+            const uint32_t* R1 = (const uint32_t*)(S + (yt.y - sy0) * RZ_SC);
+            uint32_t packed = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t p0 = __builtin_amdgcn_perm(R0[dwk[k] + 1], R0[dwk[k]], sel[k]);
+                const uint32_t p1 = __builtin_amdgcn_perm(R1[dwk[k] + 1], R1[dwk[k]], sel[k]);
+                const uint32_t d0 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[k], 0u, false);
+                const uint32_t d1 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[k], 0u, false);
+                // all terms >= 0 and < 2^32: yt.z, yt.w <= 2048, d <= 255 * 2049
+                const uint32_t v = (__umul24((unsigned)yt.z, d0) + __umul24((unsigned)yt.w, d1) + (1u << 21)) >> 22;
+                packed |= min(v, 255u) << (8 * k);
+            }
+            store(r, packed);
+        }
+        return;
+    }
 #pragma unroll
     for (int rr = 0; rr < 4; rr++) {
         const int r = 4 * rg + rr;
@@ -126,12 +172,7 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
             v = v < 0 ? 0 : (v > 255 ? 255 : v);
             packed |= (uint32_t)v << (8 * k);
         }
-        uint8_t* Dr = D + (long long)(dy0 + r) * dst_pitch;
-        if (n == 4 && ((((uintptr_t)Dr) & 3) == 0)) {
-            *(uint32_t*)Dr = packed;
-        } else {
-            for (int k = 0; k < n; k++) Dr[k] = (uint8_t)(packed >> (8 * k));
-        }
+        store(r, packed);
     }
 }
 
