@@ -626,6 +626,26 @@ __device__ __forceinline__ unsigned og_cand_order(int x, int y, const OgLevel& L
     return (unsigned)(((ci * L.nCols + cj) * L.hCell + ly) * L.wCell + lx);
 }
 
+// atomicAdd(&ctr[addr], 1) for every active lane, one LDS atomic per DISTINCT address of the wave: the
+// wave's keys are consecutive FAST outputs (one block's corners), so they fall into few nodes and plain
+// atomics would serialise on the same counters.  Wave-uniform control flow; exact counts.
+__device__ __forceinline__ void og_wave_count(int* ctr, int addr, bool act)
+{
+    u64 rem = __ballot(act);
+    const int lane = threadIdx.x & 63;
+    // the two most common addresses of the wave are counted by one atomic each; lanes with any other
+    // address (a wave spread over many nodes) fall back to plain atomics
+#pragma unroll
+    for (int it = 0; it < 2 && rem; it++) {
+        const int ld = __builtin_ctzll(rem);
+        const int a = __builtin_amdgcn_readlane(addr, ld);
+        const u64 m = __ballot(act && addr == a) & rem;
+        if (lane == ld) atomicAdd(&ctr[a], (int)__popcll(m));
+        rem &= ~m;
+    }
+    if ((rem >> lane) & 1ull) atomicAdd(&ctr[addr], 1);
+}
+
 #ifndef OCT_U
 #define OCT_U 4  // candidates per thread per pass with all loads hoisted (latency batching)
 #endif
@@ -695,12 +715,13 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) {
             const int k = base + u * OCT_NT;
+            int r = 0;
             if (k < C) {
-                int r = (int)((float)(int)(kv[u] & 0xffff) / L.hX);
+                r = (int)((float)(int)(kv[u] & 0xffff) / L.hX);
                 r = min(r, nIni - 1);
                 NO[k] = (uint16_t)r;
-                atomicAdd(&childCnt[r], 1);
             }
+            og_wave_count(childCnt, r, k < C);
         }
     }
     __syncthreads();
@@ -746,12 +767,16 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) {
             const int k = base + u * OCT_NT;
+            int a = 0;
+            bool cnt = false;
             if (k < C) {
                 const int n = aux[no[u]];
                 NO[k] = (uint16_t)n;
                 const OctNode& nd = nodes[0][n];
-                if (nd.cnt > 1) atomicAdd(&childCnt[4 * n + og_quadrant((int)(kv[u] & 0xffff), (int)(kv[u] >> 16), nd)], 1);
+                cnt = nd.cnt > 1;
+                a = 4 * n + og_quadrant((int)(kv[u] & 0xffff), (int)(kv[u] >> 16), nd);
             }
+            og_wave_count(childCnt, a, cnt);
         }
     }
     __syncthreads();
@@ -901,6 +926,8 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 #pragma unroll
             for (int u = 0; u < OCT_U; u++) {
                 const int k = base + u * OCT_NT;
+                int a = 0;
+                bool cnt = false;
                 if (k < C) {
                     const int n = no[u];
                     const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
@@ -914,9 +941,11 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                         atomicMax(&best[n2], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
                     } else {
                         const OctNode& nd = nn[n2];
-                        if (nd.cnt > 1 && (nextMode == 0 || nf[n2])) atomicAdd(&NCC[4 * n2 + og_quadrant(x, y, nd)], 1);
+                        cnt = nd.cnt > 1 && (nextMode == 0 || nf[n2]);
+                        a = 4 * n2 + og_quadrant(x, y, nd);
                     }
                 }
+                if (!done) og_wave_count(NCC, a, cnt);  // `done` is workgroup-uniform
             }
         }
         __syncthreads();
