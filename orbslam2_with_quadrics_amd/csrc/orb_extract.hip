@@ -426,22 +426,43 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     // iteration appends its survivors to the block's flat list (stages 2-4 then spread the list evenly)
     const int npair = dh * H;
     const unsigned invH = (1u << 20) / (unsigned)H + 1u;  // exact p / H for p < 3200, H <= 40
-    for (int p0 = wv * 64; p0 < npair; p0 += FB_NT) {
-        const int pp = p0 + lane;
-        const int i = (int)(__umul24((unsigned)pp, invH) >> 20), c = pp - (int)__umul24((unsigned)i, (unsigned)H);
-        uint32_t r = 0u;
-        if (pp < npair) r = og_fast_quick2(&T2[(i + 3) * FB_S2 + (c + 3)], FB_S2, tt);
-        const bool s0 = (r & 0xffffu) != 0u && c < dw;
-        const bool s1 = (r >> 16) != 0u && c + H < dw;
-        const u64 m0 = __ballot(s0);
-        const u64 m1 = __ballot(s1);
-        const int n0 = __popcll(m0), n = n0 + __popcll(m1);
+    // two pair slots per lane per iteration (slots p and p + 512): twice the LDS reads in flight and one
+    // reservation for the four survivor ballots
+    for (int p0 = wv * 64; p0 < npair; p0 += 2 * FB_NT) {
+        int ii[2], cc[2];
+        uint32_t r[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int pp = p0 + h * FB_NT + lane;
+            ii[h] = (int)(__umul24((unsigned)pp, invH) >> 20);
+            cc[h] = pp - (int)__umul24((unsigned)ii[h], (unsigned)H);
+            r[h] = 0u;
+            if (pp < npair) r[h] = og_fast_quick2(&T2[(ii[h] + 3) * FB_S2 + (cc[h] + 3)], FB_S2, tt);
+        }
+        bool sv[4];
+        u64 m[4];
+        int nn[4];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            sv[2 * h] = (r[h] & 0xffffu) != 0u && cc[h] < dw;
+            sv[2 * h + 1] = (r[h] >> 16) != 0u && cc[h] + H < dw;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            m[q] = __ballot(sv[q]);
+            nn[q] = __popcll(m[q]);
+        }
+        const int n = nn[0] + nn[1] + nn[2] + nn[3];
         if (n) {
             int b = 0;
             if (lane == 0) b = atomicAdd(&sh_ns, n);
             b = __builtin_amdgcn_readfirstlane(b);
-            if (s0) lst[b + __popcll(m0 & lt_mask)] = (uint16_t)((i << 7) | c);
-            if (s1) lst[b + n0 + __popcll(m1 & lt_mask)] = (uint16_t)((i << 7) | (c + H));
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int h = q >> 1;
+                if (sv[q]) lst[b + __popcll(m[q] & lt_mask)] = (uint16_t)((ii[h] << 7) | (cc[h] + ((q & 1) ? H : 0)));
+                b += nn[q];
+            }
         }
     }
     __syncthreads();
