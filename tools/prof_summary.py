@@ -24,10 +24,12 @@ def main():
         k = short(r["Kernel_Name"])
         gx, gy, gz = int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]), int(r["Grid_Size_Z"])
         wx, wy, wz = int(r["Workgroup_Size_X"]), int(r["Workgroup_Size_Y"]), int(r["Workgroup_Size_Z"])
-        # frames per launch: z for the pyramid kernel, x for the matcher, y for the others
+        # frames per launch: z for the pyramid kernel, x/8 for the octree, x for the matchers, y for the others
         if k.startswith("og_resize"):
             batch = gz // max(wz, 1)
-        elif k.startswith(("og_search_init", "og_grid")):
+        elif k.startswith("og_octree"):  # level-major 1-D grid: 8 levels x B frames
+            batch = gx // max(wx, 1) // 8
+        elif k.startswith(("og_search_init", "og_grid", "og_init_resolve")):
             batch = gx // max(wx, 1)
         else:
             batch = gy // max(wy, 1)
