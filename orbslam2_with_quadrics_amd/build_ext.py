@@ -64,5 +64,39 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
     return target
 
 
+# ---- C++ host layer (ORB_SLAM2::ORBextractor / Frame / ORBmatcher / ORBVocabulary over the C ABI) ----
+ROOT = os.path.dirname(HERE)
+HOST_SRC = os.path.join(HERE, "host")
+HOST_SOURCES = ["ORBextractor.cc", "Frame.cc", "ORBmatcher.cc", "ORBVocabulary.cc"]
+HOST_LIB = os.path.join(HERE, "liborbslam2_gpu.so")
+HOST_DRIVER = os.path.join(ROOT, "tests", "cpp", "host_parity")
+# -ffp-contract=off: the host layer's own float arithmetic (mOw = -Rcw^T tcw) follows OpenCV's baseline
+# build, which has no FMA
+HOST_FLAGS = ["-O2", "-std=c++14", "-fPIC", "-ffp-contract=off", "-Wall", "-Wextra", "-Wno-unused-parameter",
+              "-I", os.path.join(ROOT, "include")]
+
+
+def build_host(verbose: bool = False) -> str:
+    """Build liborbslam2_gpu.so (links liborbgpu.so, found next to it through $ORIGIN) and the parity driver
+    tests/cpp/host_parity.  g++ only: the host layer holds no device code."""
+    cxx = shutil.which("g++") or "g++"
+    cmd = [cxx, *HOST_FLAGS, "-shared", "-o", HOST_LIB + ".tmp",
+           *[os.path.join(HOST_SRC, f) for f in HOST_SOURCES],
+           "-L", HERE, "-l:liborbgpu.so", "-Wl,-rpath,$ORIGIN", "-pthread"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(HOST_LIB + ".tmp", HOST_LIB)
+    cmd = [cxx, *HOST_FLAGS, "-o", HOST_DRIVER + ".tmp", os.path.join(ROOT, "tests", "cpp", "host_parity.cc"),
+           "-L", HERE, "-l:liborbslam2_gpu.so", "-l:liborbgpu.so",
+           "-Wl,-rpath,$ORIGIN/../../orbslam2_with_quadrics_amd", "-pthread"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(HOST_DRIVER + ".tmp", HOST_DRIVER)
+    return HOST_LIB
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_host(verbose=True))
