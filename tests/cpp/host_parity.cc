@@ -5,7 +5,8 @@
 //
 //   host_parity probe                      -> constructs an ORBextractor; exit 3 with the GpuError text
 //                                             when no device is visible (no CPU fallback)
-//   host_parity <mode> <case_dir>          -> mode in {mono_init, stereo, rgbd, projection, frustum, bow}
+//   host_parity <mode> <case_dir>          -> mode in {mono_init, stereo, rgbd, projection, frustum, bow,
+//                                             last_frame, keyframe}
 //
 // params.txt in the case dir: whitespace-separated `key value` pairs (rows cols nfeatures fx fy cx cy bf
 // ndist d0..d4 th nnratio ...).
@@ -330,6 +331,124 @@ int mode_bow()
     write_vec("fv_feats.bin", feats);
     return 0;
 }
+// two mono frames (last, current) with poses; LastFrame map points from lf_* files; optional current-frame
+// mvuRight and pre-existing claims (claim.u8: 1 = claimed by a foreign point, claim_obs.i32: its Observations())
+struct TwoFrames {
+    std::unique_ptr<ORBextractor> ex;
+    std::unique_ptr<Frame> last, cur;
+    std::vector<uint8_t> b1, b2;
+    std::vector<std::unique_ptr<MapPoint>> own;
+};
+
+void load_two_frames(TwoFrames& t, const Setup& s)
+{
+    t.ex.reset(new ORBextractor(s.nf, 1.2f, 8, 20, 7));
+    t.ex->SetPyramidDownload(false);
+    ImageU8 i1 = load_image("img_last.u8", t.b1, s.rows, s.cols), i2 = load_image("img_cur.u8", t.b2, s.rows, s.cols);
+    t.last.reset(new Frame(i1, 0.0, t.ex.get(), nullptr, s.K, s.dist, s.bf, 40.f));
+    t.cur.reset(new Frame(i2, 0.033, t.ex.get(), nullptr, s.K, s.dist, s.bf, 40.f));
+    Pose P;
+    const auto Tl = read_arr<float>("pose_last.f32");
+    std::memcpy(P.T, Tl.data(), sizeof(P.T));
+    t.last->SetPose(P);
+    const auto Tc = read_arr<float>("pose_cur.f32");
+    std::memcpy(P.T, Tc.data(), sizeof(P.T));
+    t.cur->SetPose(P);
+    const auto ow = t.cur->GetCameraCenter();
+    write_arr("ow_cur.bin", ow.data(), 3);
+    const auto owl = t.last->GetCameraCenter();
+    write_arr("ow_last.bin", owl.data(), 3);
+    write_frame("last", *t.last);
+    write_frame("cur", *t.cur);
+    std::ifstream ur(gDir + "/uright.f32", std::ios::binary);
+    if (ur) t.cur->mvuRight = read_arr<float>("uright.f32");
+    const auto claim = read_arr<uint8_t>("claim.u8");
+    const auto claimObs = read_arr<int32_t>("claim_obs.i32");
+    for (int i = 0; i < t.cur->N && i < (int)claim.size(); ++i)
+        if (claim[i]) {
+            t.own.emplace_back(new MapPoint());
+            t.own.back()->SetObservations(claimObs[i]);
+            t.cur->mvpMapPoints[i] = t.own.back().get();
+        }
+}
+
+// current-frame ownership as indices: -1 NULL, j for the j-th candidate point, `foreign` for a pre-claim
+void write_owner(const Frame& F, const std::vector<MapPoint*>& cands, int foreign)
+{
+    std::map<MapPoint*, int> index;
+    for (size_t j = 0; j < cands.size(); ++j)
+        if (cands[j]) index[cands[j]] = (int)j;
+    std::vector<int32_t> owner(F.N, -1);
+    for (int i = 0; i < F.N; ++i) {
+        MapPoint* p = F.mvpMapPoints[i];
+        if (!p) continue;
+        auto it = index.find(p);
+        owner[i] = it == index.end() ? foreign : it->second;
+    }
+    write_vec("owner.bin", owner);
+}
+
+int mode_last_frame()
+{
+    Setup s = setup();
+    TwoFrames t;
+    load_two_frames(t, s);
+    Frame& L = *t.last;
+    const auto hasMp = read_arr<uint8_t>("lf_has_mp.bin");
+    const auto outl = read_arr<uint8_t>("lf_outlier.bin");
+    const auto pos = read_arr<float>("lf_pos.bin");
+    const auto nobs = read_arr<int32_t>("lf_n_obs.bin");
+    const auto desc = read_arr<uint8_t>("lf_desc.bin");
+    if ((int)hasMp.size() != L.N) throw std::runtime_error("lf arrays do not match LastFrame.N");
+    for (int i = 0; i < L.N; ++i) {
+        L.mvbOutlier[i] = outl[i] != 0;
+        if (!hasMp[i]) continue;
+        t.own.emplace_back(new MapPoint());
+        MapPoint* p = t.own.back().get();
+        p->SetWorldPos(&pos[3 * i]);
+        p->SetObservations(nobs[i]);
+        p->SetDescriptor(&desc[32 * i]);
+        L.mvpMapPoints[i] = p;
+    }
+    ORBmatcher matcher(0.9f, s.get("check_ori", 1) != 0);
+    const int nm = matcher.SearchByProjection(*t.cur, L, (float)s.get("th", 7.0), s.get("mono", 1) != 0);
+    write_owner(*t.cur, L.mvpMapPoints, L.N);
+    write_arr("nmatches.bin", &nm, 1);
+    return 0;
+}
+
+int mode_keyframe()
+{
+    Setup s = setup();
+    TwoFrames t;
+    load_two_frames(t, s);
+    const auto valid = read_arr<uint8_t>("kf_valid.bin");  // 0 = NULL, 1 = valid, 2 = bad, 3 = already found
+    const auto pos = read_arr<float>("kf_pos.bin");
+    const auto mx = read_arr<float>("kf_max.bin");
+    const auto mn = read_arr<float>("kf_min.bin");
+    const auto desc = read_arr<uint8_t>("kf_desc.bin");
+    std::vector<MapPoint*> mps(valid.size(), nullptr);
+    std::set<MapPoint*> already;
+    for (size_t i = 0; i < valid.size(); ++i) {
+        if (valid[i] == 0) continue;
+        t.own.emplace_back(new MapPoint());
+        MapPoint* p = t.own.back().get();
+        p->SetWorldPos(&pos[3 * i]);
+        p->SetDistances(mn[i], mx[i]);
+        p->SetDescriptor(&desc[32 * i]);
+        p->SetObservations(2);
+        if (valid[i] == 2) p->SetBadFlag();
+        if (valid[i] == 3) already.insert(p);
+        mps[i] = p;
+    }
+    KeyFrame kf(t.last->mvKeysUn, mps);
+    ORBmatcher matcher(0.9f, s.get("check_ori", 1) != 0);
+    const int nm = matcher.SearchByProjection(*t.cur, &kf, already, (float)s.get("th", 10.0),
+                                              (int)s.get("orbdist", 100));
+    write_owner(*t.cur, mps, (int)mps.size());
+    write_arr("nmatches.bin", &nm, 1);
+    return 0;
+}
 }  // namespace
 
 int main(int argc, char** argv)
@@ -353,6 +472,8 @@ int main(int argc, char** argv)
         if (mode == "projection") return mode_projection();
         if (mode == "frustum") return mode_frustum();
         if (mode == "bow") return mode_bow();
+        if (mode == "last_frame") return mode_last_frame();
+        if (mode == "keyframe") return mode_keyframe();
         std::cerr << "unknown mode " << mode << "\n";
         return 2;
     } catch (const GpuError& e) {

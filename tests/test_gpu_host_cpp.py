@@ -212,3 +212,90 @@ def test_host_compute_bow(gpu, oracle, tmp_path):
     assert np.array_equal(_load(tmp_path, "fv_nodes.bin", np.int32), wn)
     assert np.array_equal(_load(tmp_path, "fv_off.bin", np.int32), wo)
     assert np.array_equal(_load(tmp_path, "fv_feats.bin", np.int32), wf)
+
+
+def _two_frame_case(tmp_path, seed, rows, cols, tz=0.0):
+    f1, f2 = synthetic.frame_pair(150 + seed, rows, cols, (5, 2))
+    f1.tofile(tmp_path / "img_last.u8")
+    f2.tofile(tmp_path / "img_cur.u8")
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = 0.73 * cols, 0.73 * cols, cols / 2 - 0.37, rows / 2 + 0.21, 0.54 * 0.73 * cols
+    R0 = synthetic.rotation(*rng.uniform(-0.05, 0.05, 3))
+    t0 = rng.uniform(-0.3, 0.3, 3)
+    dR = synthetic.rotation(*rng.uniform(-0.01, 0.01, 3))
+    cams = []
+    for name, R, t in (("last", R0, t0), ("cur", dR @ R0, dR @ t0 + np.array([-0.02, -0.01, tz]))):
+        T = np.eye(4, dtype=np.float32)
+        T[:3, :3], T[:3, 3] = R, t
+        T.tofile(tmp_path / f"pose_{name}.f32")
+        cams.append(synthetic.camera(cols, rows, R, t, fx, fy, cx, cy, bf))
+    return f1, f2, cams, _params(rows, cols, 1000, dict(fx=fx, fy=fy, cx=cx, cy=cy), bf=bf)
+
+
+def _with_cpp_centres(tmp_path, cams):
+    out = []
+    for name, cam in zip(("last", "cur"), cams):
+        out.append(dict(cam, Ow=_load(tmp_path, f"ow_{name}.bin", np.float32)))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,mono,tz,th,ori", [(0, True, 0.0, 7.0, True), (1, False, 0.8, 7.0, True),
+                                                 (2, False, -0.8, 15.0, False)])
+def test_host_search_by_projection_last_frame(gpu, oracle, tmp_path, seed, mono, tz, th, ori):
+    rows, cols = 480, 640
+    f1, f2, cams, params = _two_frame_case(tmp_path, seed, rows, cols, tz)
+    oe = oracle.OracleExtractor(1000)
+    k1, d1 = oe(f1)
+    k2, d2 = oe(f2)
+    sf = oe.tables()["scale"]
+    lf = synthetic.last_frame_points(seed, k1, d1, cams[0])
+    for key in ("has_mp", "outlier", "pos", "n_obs", "desc"):
+        np.ascontiguousarray(lf[key]).tofile(tmp_path / f"lf_{key}.bin")
+    rng = np.random.default_rng(seed + 9)
+    uright = None
+    if not mono:
+        uright = np.where(rng.random(len(k2)) < 0.5, k2["x"] - rng.uniform(1, 40, len(k2)), -1).astype(np.float32)
+        uright.tofile(tmp_path / "uright.f32")
+    claim = np.zeros(len(k2), np.uint8)
+    claim[::17] = 1
+    claim_obs = np.zeros(len(k2), np.int32)
+    claim_obs[::34] = 1
+    claim.tofile(tmp_path / "claim.u8")
+    claim_obs.tofile(tmp_path / "claim_obs.i32")
+    _run("last_frame", tmp_path, dict(params, th=th, mono=int(mono), check_ori=int(ori)))
+    assert _load(tmp_path, "cur_kps.bin", KP_DTYPE).tobytes() == k2.tobytes()
+    last, cur = _with_cpp_centres(tmp_path, cams)
+    owner0 = np.where(claim == 1, len(k1), -1).astype(np.int32)
+    wn, wown, _ = oracle.search_by_projection_last(oracle.OracleFrame(k2, d2, cols, rows, sf, uright), cur, last, lf,
+                                                   th, mono, ori, owner0, claim_obs)
+    assert int(_load(tmp_path, "nmatches.bin", np.int32)[0]) == wn and wn > 20
+    assert np.array_equal(_load(tmp_path, "owner.bin", np.int32), wown)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,th,orbdist", [(0, 10.0, 100), (1, 3.0, 64)])
+def test_host_search_by_projection_keyframe(gpu, oracle, tmp_path, seed, th, orbdist):
+    rows, cols = 480, 640
+    f1, f2, cams, params = _two_frame_case(tmp_path, seed, rows, cols)
+    oe = oracle.OracleExtractor(1000)
+    k1, d1 = oe(f1)
+    k2, d2 = oe(f2)
+    sf = oe.tables()["scale"]
+    kf = synthetic.keyframe_points(seed, k1, d1, cams[0])
+    # invalid entries: no map point, a bad point, or a point in sAlreadyFound
+    code = np.where(kf["valid"] == 1, 1, np.random.default_rng(seed).choice([0, 2, 3], len(k1))).astype(np.uint8)
+    code.tofile(tmp_path / "kf_valid.bin")
+    for key, name in (("pos", "pos"), ("max_dist", "max"), ("min_dist", "min"), ("desc", "desc")):
+        np.ascontiguousarray(kf[key]).tofile(tmp_path / f"kf_{name}.bin")
+    claim = np.zeros(len(k2), np.uint8)
+    claim[::13] = 1
+    claim.tofile(tmp_path / "claim.u8")
+    np.zeros(len(k2), np.int32).tofile(tmp_path / "claim_obs.i32")
+    _run("keyframe", tmp_path, dict(params, th=th, orbdist=orbdist, check_ori=1))
+    _, cur = _with_cpp_centres(tmp_path, cams)
+    owner0 = np.where(claim == 1, len(k1), -1).astype(np.int32)
+    wn, wown = oracle.search_by_projection_kf(oracle.OracleFrame(k2, d2, cols, rows, sf), cur, kf, th, orbdist, True,
+                                              owner0)
+    assert int(_load(tmp_path, "nmatches.bin", np.int32)[0]) == wn and wn > 10
+    assert np.array_equal(_load(tmp_path, "owner.bin", np.int32), wown)
