@@ -98,7 +98,7 @@ __device__ __forceinline__ int og_wave_sum(int v)
 //     best/second reduction and the steal/rot-hist bookkeeping remain sequential.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void og_init_cand_kernel(OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G,
-                                                           int windowSize, const float* __restrict__ prev_xy,
+                                                           int windowSize, int dkeep, const float* __restrict__ prev_xy,
                                                            int prev_stride, uint32_t* __restrict__ lists,
                                                            int list_cap, int* __restrict__ list_n)
 {
@@ -167,8 +167,9 @@ __global__ __launch_bounds__(256) void og_init_cand_kernel(OgFrameDev F1, int re
                     if (fabsf(distx) < r && fabsf(disty) < r) {
                         uint4 ea, eb;
                         og_load_desc(D2 + (long long)i2 * 32, ea, eb);
-                        entry = ((uint32_t)og_hamming(da, db, ea, eb) << 16) | (uint32_t)i2;
-                        valid = true;
+                        const int dist = og_hamming(da, db, ea, eb);
+                        entry = ((uint32_t)dist << 16) | (uint32_t)i2;
+                        valid = dist <= dkeep;  // og_init_keep_bound: farther candidates cannot change the result
                     }
                 }
             }
@@ -442,13 +443,27 @@ size_t og_init_resolve_lds(int cap1, int cap2, int ecap)
     return (b + 15) & ~(size_t)15;
 }
 
+// Largest candidate distance that can still change SearchForInitialization's outcome.  A candidate at d > TH_LOW
+// is never the accepted best, and if TH_LOW < (float)d * nnratio then every acceptable best b <= TH_LOW passes
+// the ratio test against it (b < (float)d * nnratio), so as a second-best it never causes a rejection; the
+// same holds for every larger d (the float product is monotonic).  Dropping such candidates therefore leaves
+// the best candidate, the accept/reject decision and every vMatchedDistance update of the reference loop
+// (src/ORBmatcher.cc:430-462) unchanged, while the lists shrink to the near matches.
+int og_init_keep_bound(float nnratio)
+{
+    if (!(nnratio > 0.0f)) return 255;
+    for (int d = TH_LOW + 1; d <= 256; d++)
+        if ((float)TH_LOW < (float)d * nnratio) return d - 1;
+    return 256;
+}
+
 void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G, float nnratio,
                            int checkOri, int windowSize, float* prev_xy, int prev_stride, int* matches12,
                            int match_stride, int* nmatches, uint32_t* lists, int list_cap, int* list_n, int* status,
                            int B)
 {
     hipLaunchKernelGGL(og_init_cand_kernel, dim3((F1.frame_cap + 3) / 4, B), dim3(256), 0, s, F1, ref, F2, G,
-                       windowSize, prev_xy, prev_stride, lists, list_cap, list_n);
+                       windowSize, og_init_keep_bound(nnratio), prev_xy, prev_stride, lists, list_cap, list_n);
     static bool lds_attr = false;  // allow more than the default dynamic LDS per workgroup (benign race)
     if (!lds_attr) {
         (void)hipFuncSetAttribute((const void*)og_init_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -456,7 +471,9 @@ void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2,
         lds_attr = true;
     }
     const size_t fixed = og_init_resolve_lds(F1.frame_cap, F2.frame_cap, 0);
-    const int ecap = (int)std::min<size_t>(16384, (OG_INIT_LDS_MAX - fixed) / 4);
+    // staging for the (pruned, short) lists: a few KB keep several workgroups per CU; one list (<= list_cap)
+    // must always fit, longer query ranges are staged in chunks
+    const int ecap = (int)std::min<size_t>(std::max(list_cap, 2048), (OG_INIT_LDS_MAX - fixed) / 4);
     const size_t shm = og_init_resolve_lds(F1.frame_cap, F2.frame_cap, ecap);
     hipLaunchKernelGGL(og_init_resolve_kernel, dim3(B), dim3(INIT_NT), shm, s, F1, ref, F2, nnratio, checkOri,
                        prev_xy, prev_stride, lists, list_cap, list_n, matches12, match_stride, nmatches, status,

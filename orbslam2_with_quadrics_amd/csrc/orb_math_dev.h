@@ -35,42 +35,41 @@ __device__ __forceinline__ float og_fast_atan2(float y, float x)
 // glibc 2.35 x86_64 sincosf (FMA ifunc variant) for |y| < 120; the reference's
 // `(float)cos(angle), (float)sin(angle)` (src/ORBextractor.cc:113) is one sincosf call under
 // GCC -O3 -march=native.  Same double-precision operation sequence as the host libm machine code.
-__constant__ const double og_sincosf_tab[2][14] = {
-    {1.0, -1.0, -1.0, 1.0, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 0x1.0p+0,
-     -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7,
-     -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16},
-    {1.0, -1.0, -1.0, 1.0, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -0x1.0p+0,
-     0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7,
-     0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16},
-};
-
+// The constants of the two coefficient tables of that code; the second table negates entries 6, 7, 9, 11 and
+// 13 (and the quadrant sign is +1, -1, -1, +1 for n & 3).  Selected, not indexed, so the function makes no
+// memory access (a describe wave keeps the next keypoint's window loads in flight across it).
 __device__ __forceinline__ void og_sincosf(float y, float* sinp, float* cosp)
 {
+    const double C4 = 0x1.45f306dc9c883p+23, C5 = 0x1.921fb54442d18p+0;
+    const double C7 = -0x1.ffffffd0c621cp-2, C8 = -0x1.555545995a603p-3, C9 = 0x1.55553e1068f19p-5;
+    const double C10 = 0x1.1107605230bc4p-7, C11 = -0x1.6c087e89a359dp-10, C12 = -0x1.994eb3774cf24p-13;
+    const double C13 = 0x1.99343027bf8c3p-16;
     const uint32_t t = (__float_as_uint(y) >> 20) & 0x7ff;
-    const double* T;
+    bool flip = false;  // second table
     double xs, x2;
     int n = 0;
     if (t < 0x3f4) {
         if (t < 0x398) { *sinp = y; *cosp = 1.0f; return; }
-        T = og_sincosf_tab[0];
         xs = (double)y;
         x2 = __dmul_rn(xs, xs);
     } else {
         const double x = (double)y;
-        const double* T0 = og_sincosf_tab[0];
-        n = (((int32_t)__dmul_rn(x, T0[4])) + 0x800000) >> 24;
-        const double r = __fma_rn(-(double)n, T0[5], x);
-        T = og_sincosf_tab[(n & 2) ? 1 : 0];
-        xs = __dmul_rn(r, T0[n & 3]);
+        n = (((int32_t)__dmul_rn(x, C4)) + 0x800000) >> 24;
+        const double r = __fma_rn(-(double)n, C5, x);
+        flip = (n & 2) != 0;
+        const double sg = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
+        xs = __dmul_rn(r, sg);
         x2 = __dmul_rn(r, r);
     }
+    const double T6 = flip ? -1.0 : 1.0, T7 = flip ? -C7 : C7, T9 = flip ? -C9 : C9;
+    const double T11 = flip ? -C11 : C11, T13 = flip ? -C13 : C13;
     const double x3 = __dmul_rn(x2, xs), x4 = __dmul_rn(x2, x2);
     const double x5 = __dmul_rn(x2, x3), x6 = __dmul_rn(x2, x4);
-    const double s1v = __fma_rn(x2, T[12], T[10]);
-    const double c2v = __fma_rn(x2, T[13], T[11]);
-    const double c1v = __fma_rn(x2, T[7], T[6]);
-    const double s = __fma_rn(x3, T[8], xs);
-    const double c = __fma_rn(x4, T[9], c1v);
+    const double s1v = __fma_rn(x2, C12, C10);
+    const double c2v = __fma_rn(x2, T13, T11);
+    const double c1v = __fma_rn(x2, T7, T6);
+    const double s = __fma_rn(x3, C8, xs);
+    const double c = __fma_rn(x4, T9, c1v);
     const float so = (float)__fma_rn(s1v, x5, s);
     const float co = (float)__fma_rn(c2v, x6, c);
     if (n & 1) { *sinp = co; *cosp = so; }

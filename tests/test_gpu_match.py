@@ -172,3 +172,47 @@ def test_batch_search_for_initialization(gpu, oracle):
         exr.device_free(p)
     for p in (d_prev, d_m, d_n):
         exb.device_free(p)
+
+
+@pytest.mark.parametrize("ratio", [0.6, 0.75, 0.9, 1.0, 1.5])
+def test_search_for_initialization_distance_bound(gpu, oracle, ratio):
+    """Crafted candidates at Hamming distances around the pruning bound of og_init_keep_bound (d > 50 with
+    50 < d * ratio): best 40-52, seconds 50-90, plus shared candidates that steal from each other."""
+    rng = np.random.default_rng(int(ratio * 100))
+    rows, cols, n1 = 480, 640, 300
+    k1 = np.zeros(n1, gpu.KP_DTYPE)
+    k1["x"] = rng.uniform(30, cols - 30, n1).astype(np.float32)
+    k1["y"] = rng.uniform(30, rows - 30, n1).astype(np.float32)
+    k1["angle"] = rng.uniform(0, 360, n1).astype(np.float32)
+    k1["size"], k1["octave"], k1["class_id"] = 31.0, 0, -1
+    d1 = rng.integers(0, 256, (n1, 32), dtype=np.uint8)
+
+    def at_distance(d, n):
+        bits = np.unpackbits(d, bitorder="little")
+        flip = rng.choice(256, n, replace=False)
+        bits[flip] ^= 1
+        return np.packbits(bits, bitorder="little")
+
+    k2l, d2l = [], []
+    for i in range(n1):
+        for dist in (int(rng.integers(40, 53)), int(rng.integers(50, 91)), int(rng.integers(50, 91))):
+            kp = np.zeros(1, gpu.KP_DTYPE)
+            kp["x"] = k1["x"][i] + rng.uniform(-3, 3)
+            kp["y"] = k1["y"][i] + rng.uniform(-3, 3)
+            kp["angle"] = (k1["angle"][i] + rng.choice([0.0, 0.0, 0.0, 90.0])) % 360
+            kp["size"], kp["octave"], kp["class_id"] = 31.0, 0, -1
+            k2l.append(kp)
+            d2l.append(at_distance(d1[i], dist))
+    k2 = np.concatenate(k2l)
+    d2 = np.stack(d2l)
+    sf = np.float32(1.2) ** np.arange(8, dtype=np.float32)
+    ex = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+    pg = prev.copy()
+    n, m12 = gpu.ORBmatcher(ratio, True, context=ex).SearchForInitialization(
+        gpu.Frame(k1, d1, cols, rows, sf), gpu.Frame(k2, d2, cols, rows, sf), pg, 12)
+    no, mo, po = oracle.search_for_initialization(oracle.OracleFrame(k1, d1, cols, rows, sf),
+                                                  oracle.OracleFrame(k2, d2, cols, rows, sf), prev, ratio, True, 12)
+    assert n == no and n > 10
+    assert np.array_equal(m12, mo)
+    assert np.array_equal(pg, po)
