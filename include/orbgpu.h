@@ -159,6 +159,17 @@ int orbgpu_search_by_projection(orbgpu_ctx* ctx, const orbgpu_frame_view* F,
                                 const orbgpu_mappoints_view* mp, float nnratio, float th,
                                 int32_t* owner, int32_t* owner_obs, int* nmatches);
 
+/* Device-resident batch form of SearchByProjection(Frame&, vpMapPoints, th) (src/ORBmatcher.cc:45-137), as
+ * Tracking::SearchLocalPoints runs it for every camera of a rig (src/Tracking.cc:1184-1191): frame b of ctx's
+ * last batch against its own map-point snapshot, whose point j is element b*mp_stride + j of every array of
+ * *d_mp (device pointers; d_mp->m points per frame, desc rows 32 B).  d_uright: B x frame_cap mvuRight
+ * (device) or NULL for monocular frames.  d_owner / d_owner_obs: B x frame_cap ints (in/out, device; owner =
+ * map-point index j, -1 == NULL, indices >= d_mp->m = claims made before the call), d_nmatches: B ints.
+ * Enqueued on the context stream (one int is read back to size the candidate lists). */
+int orbgpu_search_by_projection_batch(orbgpu_ctx* ctx, const orbgpu_mappoints_view* d_mp, int mp_stride,
+                                      float nnratio, float th, const float* d_uright, int32_t* d_owner,
+                                      int32_t* d_owner_obs, int* d_nmatches);
+
 /* ---- Frame post-processing: UndistortKeyPoints / ComputeImageBounds ---------------------------- */
 
 /* Replaces void Frame::UndistortKeyPoints() -- src/Frame.cc:404-434: mvKeysUn from mvKeys through

@@ -21,7 +21,7 @@ EXPORTS = [
     "orbgpu_max_keypoints", "orbgpu_get_level", "orbgpu_extract_batch_device", "orbgpu_batch_outputs",
     "orbgpu_batch_download", "orbgpu_grid_geom_for_image", "orbgpu_descriptor_distance",
     "orbgpu_search_for_initialization", "orbgpu_search_for_initialization_batch",
-    "orbgpu_search_by_projection", "orbgpu_stream", "orbgpu_synchronize", "orbgpu_set_stage_timing",
+    "orbgpu_search_by_projection", "orbgpu_search_by_projection_batch", "orbgpu_stream", "orbgpu_synchronize", "orbgpu_set_stage_timing",
     "orbgpu_stage_times", "orbgpu_last_error", "orbgpu_debug_candidates", "orbgpu_debug_octree",
     "orbgpu_device_alloc", "orbgpu_device_free", "orbgpu_memcpy_h2d", "orbgpu_memcpy_d2h",
     "orbgpu_memset_d", "orbgpu_prev_matched_from_frame", "orbgpu_memcpy_d2d_async",
@@ -108,6 +108,7 @@ def _declare(L):
     L.orbgpu_search_for_initialization_batch.argtypes = [vp, i32, vp, GridGeom, f32, i32, i32, vp, vp, vp]
     L.orbgpu_search_by_projection.argtypes = [vp, C.POINTER(FrameView), C.POINTER(MapPointsView), f32,
                                               f32, vp, vp, C.POINTER(i32)]
+    L.orbgpu_search_by_projection_batch.argtypes = [vp, C.POINTER(MapPointsView), i32, f32, f32, vp, vp, vp, vp]
     L.orbgpu_stream.restype = vp
     L.orbgpu_stream.argtypes = [vp]
     L.orbgpu_synchronize.argtypes = [vp]

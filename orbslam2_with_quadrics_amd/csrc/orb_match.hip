@@ -5,10 +5,10 @@
 //       vnMatches21 state couples them, :444, :463-470); the candidates of one query are scored in
 //       parallel (XOR + popcount over 8 u32) and reduced to (best, second) with a lexicographic
 //       (distance, candidate position) wave min -- exactly the reference's strict-< update order.
-//   og_proj_count/fill/resolve : ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th)
-//       (src/ORBmatcher.cc:45-137).  Candidate lists + distances are built in parallel (one thread per
-//       map point); the order-dependent claim resolution (:87-89, :123) is a single ordered pass over
-//       the precomputed lists.
+//   og_projb_count/scan/fill/resolve : ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th)
+//       (src/ORBmatcher.cc:45-137) for B frames.  Candidate lists + distances are built in parallel (one
+//       thread per map point); the order-dependent claims (:87-89, :123) are resolved by a parallel
+//       fixed-point iteration of the triangular claim system (og_projb_resolve_kernel).
 #include <hip/hip_runtime.h>
 #include <limits.h>
 
@@ -513,7 +513,7 @@ struct OgProjCand {
 // filters (levels, window, stereo check); claims are dynamic and applied in the ordered pass.
 template <bool FILL>
 __device__ int og_proj_enum(const OgFrameDev& F, const OgGridGeom& G, const float* sf, const OgMapPointsDev& mp,
-                            int m, float th, OgProjCand* out)
+                            int m, float th, OgProjCand* out, int dkeep = 256)
 {
     if (!mp.track_in_view[m] || mp.is_bad[m]) return 0;
     const int lvl = mp.level[m];
@@ -551,20 +551,13 @@ __device__ int og_proj_enum(const OgFrameDev& F, const OgGridGeom& G, const floa
                     c.idx = idx;
                     c.dist = (short)og_hamming(da, db, ea, eb);
                     c.octave = (short)kp.octave;
+                    if (c.dist > dkeep) continue;  // og_proj_keep_bound
                     out[n] = c;
                 }
                 n++;
             }
         }
     return n;
-}
-
-__global__ __launch_bounds__(256) void og_proj_count_kernel(OgFrameDev F, OgGridGeom G, const float* sf,
-                                                            OgMapPointsDev mp, float th, int* cnt)
-{
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= mp.m) return;
-    cnt[m] = og_proj_enum<false>(F, G, sf, mp, m, th, nullptr);
 }
 
 __global__ __launch_bounds__(1024) void og_scan_kernel(const int* cnt, int n, int* off)
@@ -603,68 +596,264 @@ __global__ __launch_bounds__(1024) void og_scan_kernel(const int* cnt, int n, in
     if (threadIdx.x == 0) off[n] = carry;
 }
 
-__global__ __launch_bounds__(256) void og_proj_fill_kernel(OgFrameDev F, OgGridGeom G, const float* sf,
-                                                           OgMapPointsDev mp, float th, const int* off,
-                                                           OgProjCand* cands)
+// ---- batched SearchByProjection(F, vpMapPoints, th): frame b of a batch against its own map-point snapshot ----
+// Largest candidate distance that can change the outcome: a candidate at d > TH_HIGH is never the accepted
+// best, and if TH_HIGH <= nnratio * (float)d then no acceptable best b <= TH_HIGH satisfies b > nnratio * d, so as
+// a second-best it never triggers the ratio rejection (src/ORBmatcher.cc:115-121); the same holds for every
+// larger d.  Dropping those candidates leaves every point's decision and bestIdx unchanged.
+int og_proj_keep_bound(float nnratio)
 {
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= mp.m) return;
-    og_proj_enum<true>(F, G, sf, mp, m, th, cands + off[m]);
+    if (!(nnratio > 0.0f)) return 256;
+    for (int d = TH_HIGH + 1; d <= 256; d++)
+        if ((float)TH_HIGH <= nnratio * (float)d) return d - 1;
+    return 256;
 }
 
-// ordered claim resolution: a single lane replays the reference loop over the precomputed lists
-__global__ __launch_bounds__(64) void og_proj_resolve_kernel(OgMapPointsDev mp, const int* off,
-                                                             const OgProjCand* cands, float nnratio, int n,
-                                                             int* owner, int* owner_obs, int* nmatches)
+__device__ __forceinline__ OgFrameDev og_frame_of(const OgFrameDev& F, int b)
 {
-    if (threadIdx.x != 0) return;
-    int nm = 0;
-    for (int m = 0; m < mp.m; m++) {
-        const int b = off[m], e = off[m + 1];
-        if (b == e) continue;
-        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
-        for (int c = b; c < e; c++) {
-            const OgProjCand cc = cands[c];
-            if (owner[cc.idx] >= 0 && owner_obs[cc.idx]) continue;  // :87-89
-            const int dist = cc.dist;
-            if (dist < bestDist) {
-                bestDist2 = bestDist;
-                bestDist = dist;
-                bestLevel2 = bestLevel;
-                bestLevel = cc.octave;
-                bestIdx = cc.idx;
-            } else if (dist < bestDist2) {
-                bestLevel2 = cc.octave;
-                bestDist2 = dist;
-            }
+    OgFrameDev f = F;
+    f.kps += (long long)b * F.frame_cap;
+    f.desc += (long long)b * F.frame_cap * 32;
+    f.counts += b;
+    f.cell_start += (long long)b * (OG_GRID_CELLS + 1);
+    f.cell_items += (long long)b * F.frame_cap;
+    if (F.uright) f.uright += (long long)b * F.frame_cap;
+    return f;
+}
+
+__device__ __forceinline__ OgMapPointsDev og_mp_of(const OgMapPointsDev& mp, int b, int stride)
+{
+    const long long o = (long long)b * stride;
+    OgMapPointsDev q = mp;
+    q.track_in_view += o;
+    q.is_bad += o;
+    q.level += o;
+    q.view_cos += o;
+    q.proj_x += o;
+    q.proj_y += o;
+    q.proj_xr += o;
+    q.n_obs += o;
+    q.desc += o * 32;
+    return q;
+}
+
+// candidates per (frame, point) before the distance bound (an upper bound for the fill pass)
+__global__ __launch_bounds__(256) void og_projb_count_kernel(OgFrameDev F, OgGridGeom G, const float* sf,
+                                                             OgMapPointsDev mp, int stride, float th, int* cnt)
+{
+    const int b = blockIdx.y, m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= mp.m) return;
+    cnt[(long long)b * stride + m] = og_proj_enum<false>(og_frame_of(F, b), G, sf, og_mp_of(mp, b, stride), m, th,
+                                                         nullptr);
+}
+
+// per-frame exclusive scan of the counts (one workgroup per frame); tot[b] = the frame's total
+__global__ __launch_bounds__(1024) void og_projb_scan_kernel(const int* cnt, int stride, int n, int* off, int* tot)
+{
+    __shared__ int wsum[16];
+    __shared__ int carry;
+    const int b = blockIdx.x;
+    const int* C = cnt + (long long)b * stride;
+    int* O = off + (long long)b * stride;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < n; base += 1024) {
+        const int i = base + threadIdx.x;
+        const int v = i < n ? C[i] : 0;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        int x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
         }
-        if (bestDist <= TH_HIGH) {
-            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
-            owner[bestIdx] = m;
-            owner_obs[bestIdx] = mp.n_obs[m] > 0;
-            nm++;
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        int before = carry;
+        for (int q = 0; q < w; q++) before += wsum[q];
+        if (i < n) O[i] = before + x - v;
+        int t = 0;
+        for (int q = 0; q < 16; q++) t += wsum[q];
+        __syncthreads();
+        if (threadIdx.x == 0) carry += t;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tot[b] = carry;
+}
+
+// frame bases of the candidate buffer (exclusive scan over B frame totals, one workgroup); base[B] = total
+__global__ __launch_bounds__(1024) void og_projb_base_kernel(const int* tot, int B, long long* base)
+{
+    __shared__ long long carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int b0 = 0; b0 < B; b0 += 1024) {
+        if (threadIdx.x == 0) {
+            long long c = carry;
+            for (int b = b0; b < min(B, b0 + 1024); b++) {
+                base[b] = c;
+                c += tot[b];
+            }
+            carry = c;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) base[B] = carry;
+}
+
+__global__ __launch_bounds__(256) void og_projb_fill_kernel(OgFrameDev F, OgGridGeom G, const float* sf,
+                                                            OgMapPointsDev mp, int stride, float th, int dkeep,
+                                                            const int* off, const long long* base, OgProjCand* cands,
+                                                            int* kept)
+{
+    const int b = blockIdx.y, m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= mp.m) return;
+    const long long o = (long long)b * stride + m;
+    kept[o] = og_proj_enum<true>(og_frame_of(F, b), G, sf, og_mp_of(mp, b, stride), m, th, cands + base[b] + off[o],
+                                 dkeep);
+}
+
+// The reference's ordered loop over map points (src/ORBmatcher.cc:53-129) couples points only through the
+// claims: point m skips keypoint i while it is held by a map point with Observations() > 0 (:87-89).  In the
+// sequential run such a holder is the FIRST accepted claimant with observations (later points cannot take the
+// keypoint from it), so with  FO[i] = -1 for a keypoint held before the call by a point with observations, else
+// the smallest accepted point with observations whose best is i  the decision of point m is a function of
+// { i : FO[i] < m } alone.  That system is triangular (m depends on points < m only): iterating "decide every
+// point from FO; rebuild FO from the decisions" (Jacobi) reaches its unique fixed point -- the sequential
+// result -- after at most (longest dependency chain + 1) rounds, and a round that leaves FO unchanged is that
+// fixed point.  One workgroup per frame; every point's decision within a round is independent.
+// Final ownership: keypoint i belongs to the LAST accepted claimant (assignment order), else keeps its holder.
+#define PJ_NT 1024
+__global__ __launch_bounds__(PJ_NT) void og_projb_resolve_kernel(OgMapPointsDev mp, int stride, const int* off,
+                                                                 const long long* base, const int* kept,
+                                                                 const OgProjCand* cands, const int* counts,
+                                                                 int frame_cap, float nnratio, int* owner,
+                                                                 int* owner_obs, int* nmatches, int* res, int* status)
+{
+    extern __shared__ int pj_lds[];
+    int* FO = pj_lds;               // [frame_cap] current round
+    int* NF = pj_lds + frame_cap;   // [frame_cap] next round / final owner
+    __shared__ int sh_changed, sh_nm;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int n = counts[b];
+    const OgMapPointsDev q = og_mp_of(mp, b, stride);
+    const int* OFF = off + (long long)b * stride;
+    const int* KEPT = kept + (long long)b * stride;
+    const OgProjCand* CB = cands + base[b];
+    int* OWN = owner + (long long)b * frame_cap;
+    int* OBS = owner_obs + (long long)b * frame_cap;
+    int* RES = res + (long long)b * stride;
+    for (int i = tid; i < n; i += PJ_NT) {
+        const int pre = (OWN[i] >= 0 && OBS[i]) ? -1 : INT_MAX;
+        FO[i] = INT_MAX;  // round 0: no claims yet (pre-claims enter through NF below)
+        NF[i] = pre;
+    }
+    if (tid == 0) sh_changed = 1;
+    __syncthreads();
+    // round 0 starts from the pre-call claims only
+    for (int i = tid; i < n; i += PJ_NT) FO[i] = NF[i];
+    __syncthreads();
+    int rounds = 0;
+    for (;;) {
+        for (int m = tid; m < q.m; m += PJ_NT) {
+            const int nc = KEPT[m];
+            const OgProjCand* L = CB + OFF[m];
+            int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+            for (int c = 0; c < nc; c++) {
+                const OgProjCand cc = L[c];
+                if (FO[cc.idx] < m) continue;  // :87-89
+                const int dist = cc.dist;
+                if (dist < bestDist) {
+                    bestDist2 = bestDist;
+                    bestDist = dist;
+                    bestLevel2 = bestLevel;
+                    bestLevel = cc.octave;
+                    bestIdx = cc.idx;
+                } else if (dist < bestDist2) {
+                    bestLevel2 = cc.octave;
+                    bestDist2 = dist;
+                }
+            }
+            int r = -1;
+            if (bestDist <= TH_HIGH && !(bestLevel == bestLevel2 && bestDist > nnratio * bestDist2)) r = bestIdx;
+            RES[m] = r;
+            if (r >= 0 && q.n_obs[m] > 0) atomicMin(&NF[r], m);
+        }
+        __syncthreads();
+        int ch = 0;
+        for (int i = tid; i < n; i += PJ_NT) {
+            const int v = NF[i];
+            ch |= v != FO[i];
+            FO[i] = v;
+            NF[i] = (OWN[i] >= 0 && OBS[i]) ? -1 : INT_MAX;
+        }
+        if (tid == 0) sh_changed = 0;
+        __syncthreads();
+        if (ch) sh_changed = 1;
+        __syncthreads();
+        const bool again = sh_changed != 0;
+        __syncthreads();
+        if (!again) break;
+        if (++rounds > q.m + 1) {  // cannot happen (triangular system); reported, never silent
+            if (tid == 0) atomicOr(status, 32);
+            break;
         }
     }
-    *nmatches = nm;
+    // final ownership and the count of assignments
+    for (int i = tid; i < n; i += PJ_NT) NF[i] = -1;
+    if (tid == 0) sh_nm = 0;
+    __syncthreads();
+    int cnt = 0;
+    for (int m = tid; m < q.m; m += PJ_NT) {
+        const int r = RES[m];
+        if (r >= 0) {
+            atomicMax(&NF[r], m);
+            cnt++;
+        }
+    }
+    cnt = og_wave_sum(cnt);
+    if ((tid & 63) == 0) atomicAdd(&sh_nm, cnt);
+    __syncthreads();
+    for (int i = tid; i < n; i += PJ_NT) {
+        const int o = NF[i];
+        if (o >= 0) {
+            OWN[i] = o;
+            OBS[i] = q.n_obs[o] > 0;
+        }
+    }
+    if (tid == 0) nmatches[b] = sh_nm;
 }
 
-void og_launch_proj_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, float th,
-                          int* cnt, int* off)
+void og_launch_projb_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, int stride,
+                           float th, int B, int* cnt, int* off, int* tot, long long* base)
 {
-    const int blocks = (mp.m + 255) / 256;
-    if (blocks > 0) hipLaunchKernelGGL(og_proj_count_kernel, dim3(blocks), dim3(256), 0, s, F, G, sf, mp, th, cnt);
-    hipLaunchKernelGGL(og_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, mp.m, off);
+    if (mp.m > 0 && B > 0) {
+        hipLaunchKernelGGL(og_projb_count_kernel, dim3((mp.m + 255) / 256, B), dim3(256), 0, s, F, G, sf, mp, stride,
+                           th, cnt);
+        hipLaunchKernelGGL(og_projb_scan_kernel, dim3(B), dim3(1024), 0, s, cnt, stride, mp.m, off, tot);
+    } else if (B > 0) {
+        (void)hipMemsetAsync(tot, 0, sizeof(int) * (size_t)B, s);
+    }
+    hipLaunchKernelGGL(og_projb_base_kernel, dim3(1), dim3(1024), 0, s, tot, B, base);
 }
 
-void og_launch_proj_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp,
-                            float nnratio, float th, const int* off, OgProjCand* cands, int* owner, int* owner_obs,
-                            int* nmatches)
+void og_launch_projb_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, int stride,
+                             float nnratio, float th, int B, const int* off, const long long* base, OgProjCand* cands,
+                             int* kept, int* res, int* owner, int* owner_obs, int* nmatches, int* status)
 {
-    const int blocks = (mp.m + 255) / 256;
-    if (blocks > 0)
-        hipLaunchKernelGGL(og_proj_fill_kernel, dim3(blocks), dim3(256), 0, s, F, G, sf, mp, th, off, cands);
-    hipLaunchKernelGGL(og_proj_resolve_kernel, dim3(1), dim3(64), 0, s, mp, off, cands, nnratio, 0, owner, owner_obs,
-                       nmatches);
+    if (B <= 0) return;
+    if (mp.m > 0)
+        hipLaunchKernelGGL(og_projb_fill_kernel, dim3((mp.m + 255) / 256, B), dim3(256), 0, s, F, G, sf, mp, stride, th,
+                           og_proj_keep_bound(nnratio), off, base, cands, kept);
+    static bool lds_attr = false;
+    const size_t shm = 2 * sizeof(int) * (size_t)F.frame_cap;
+    if (!lds_attr) {
+        (void)hipFuncSetAttribute((const void*)og_projb_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  OG_INIT_LDS_MAX);
+        lds_attr = true;
+    }
+    hipLaunchKernelGGL(og_projb_resolve_kernel, dim3(B), dim3(PJ_NT), shm, s, mp, stride, off, base, kept, cands,
+                       F.counts, F.frame_cap, nnratio, owner, owner_obs, nmatches, res, status);
 }
 
 size_t og_proj_cand_size() { return sizeof(OgProjCand); }

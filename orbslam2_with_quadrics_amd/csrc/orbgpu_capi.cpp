@@ -86,6 +86,9 @@ struct orbgpu_ctx {
     DevBuf<uint32_t> mlists;  // SearchForInitialization candidate lists {dist:16|i2:16}
     DevBuf<int> mlist_n;
     DevBuf<uint8_t> mcands;   // projection-matcher candidate lists (grown on demand, kept)
+    DevBuf<int> pj_int;       // projection matcher: counts, offsets, kept counts, decisions, frame totals
+    DevBuf<long long> pj_base;
+    DevBuf<float> sf_dev;     // mvScaleFactors on the device
     // Frame::UndistortKeyPoints on the device (set by orbgpu_set_undistortion): batches then also hold
     // mvKeysUn, and the grid and the matchers use it with the undistorted image bounds
     bool undist = false;
@@ -539,6 +542,9 @@ void orbgpu_destroy(orbgpu_ctx* c)
     release(c->mlists);
     release(c->mlist_n);
     release(c->mcands);
+    release(c->pj_int);
+    release(c->pj_base);
+    release(c->sf_dev);
     release(c->kps_un);
     release(c->bow_word);
     release(c->bow_nid);
@@ -1268,18 +1274,45 @@ int orbgpu_compute_stereo_matches(orbgpu_ctx* left, orbgpu_ctx* right, float mbf
     return ORBGPU_OK;
 }
 
+// The candidate lists of the batched projection matcher: count + per-frame scan, one int read back to size the
+// list buffer exactly, then fill + the fixed-point resolve (og_projb_*, orb_match.hip).
+static int run_projection(orbgpu_ctx* c, hipStream_t s, const OgFrameDev& fd, const OgGridGeom& G, const float* sfd,
+                          const OgMapPointsDev& mpd, int stride, int B, float nnratio, float th, int* own, int* obs,
+                          int* nm)
+{
+    const size_t pts = (size_t)B * (size_t)std::max(stride, 1);
+    HIP_TRY(c, ensure(c->pj_int, 4 * pts + (size_t)B));
+    HIP_TRY(c, ensure(c->pj_base, (size_t)B + 1));
+    int* cnt = c->pj_int.p;
+    int* off = cnt + pts;
+    int* kept = off + pts;
+    int* res = kept + pts;
+    int* tot = res + pts;
+    og_launch_projb_count(s, fd, G, sfd, mpd, stride, th, B, cnt, off, tot, c->pj_base.p);
+    long long total = 0;
+    HIP_TRY(c, hipMemcpyAsync(&total, c->pj_base.p + B, sizeof(total), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    HIP_TRY(c, ensure(c->mcands, (size_t)std::max<long long>(total, 1) * og_proj_cand_size()));
+    og_launch_projb_resolve(s, fd, G, sfd, mpd, stride, nnratio, th, B, off, c->pj_base.p, (OgProjCand*)c->mcands.p,
+                            kept, res, own, obs, nm, c->status.p);
+    HIP_TRY(c, hipGetLastError());
+    return ORBGPU_OK;
+}
+
 int orbgpu_search_by_projection(orbgpu_ctx* c, const orbgpu_frame_view* F, const orbgpu_mappoints_view* mp,
                                 float nnratio, float th, int32_t* owner, int32_t* owner_obs, int* nmatches)
 {
     if (!c || !F || !mp || !nmatches || F->n < 0 || mp->m < 0) return ORBGPU_ERR_ARG;
     if (F->n && (!owner || !owner_obs)) return ORBGPU_ERR_ARG;
     if (!F->scale_factors || F->nlevels < 1) return ORBGPU_ERR_ARG;
+    if ((size_t)2 * sizeof(int) * (size_t)std::max(F->n, 1) > OG_INIT_LDS_MAX) {
+        c->err = "SearchByProjection: more keypoints than the LDS-resident claim table holds";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
     HIP_TRY(c, hipSetDevice(c->device));
     const int n = std::max(F->n, 1), m = std::max(mp->m, 1);
-    // generous bound for the candidate lists: every map point may see every keypoint of its levels;
-    // the count pass gives the exact total, so size the list region after it
     const size_t fixed = kCarvePad + (size_t)n * (28 + 32 + 4 + 4 + 4 + 4) + (OG_GRID_CELLS + 1) * 4 +
-                         (size_t)m * (1 + 1 + 4 + 4 + 4 + 4 + 4 + 4 + 32 + 4 + 4 + 4) + 64 + F->nlevels * 4;
+                         (size_t)m * (1 + 1 + 4 + 4 + 4 + 4 + 4 + 4 + 32) + 64 + F->nlevels * 4;
     HIP_TRY(c, ensure(c->mscratch, fixed));
     uint8_t* cur = c->mscratch.p;
     orbgpu_kp_dev* k = (orbgpu_kp_dev*)scratch_carve(cur, (size_t)n * 28);
@@ -1300,8 +1333,6 @@ int orbgpu_search_by_projection(orbgpu_ctx* c, const orbgpu_frame_view* F, const
     float* pxr = (float*)scratch_carve(cur, (size_t)m * 4);
     int* nobs = (int*)scratch_carve(cur, (size_t)m * 4);
     uint8_t* md = scratch_carve(cur, (size_t)m * 32);
-    int* cnt = (int*)scratch_carve(cur, (size_t)m * 4);
-    int* off = (int*)scratch_carve(cur, (size_t)(m + 1) * 4);
     int* nm = (int*)scratch_carve(cur, 16);
     hipStream_t s = c->stream;
     if (F->n) {
@@ -1329,14 +1360,8 @@ int orbgpu_search_by_projection(orbgpu_ctx* c, const orbgpu_frame_view* F, const
     og_launch_grid(s, k, cnts, n, G, cs, ci, 1);
     OgFrameDev fd{k, d, cnts, cs, ci, F->uright ? ur : nullptr, n};
     OgMapPointsDev mpd{mp->m, tiv, bad, lvl, vc, px, py, pxr, nobs, md};
-    // exact candidate-list size from a count pass, then the list buffer
-    og_launch_proj_count(s, fd, G, sfd, mpd, th, cnt, off);
-    int total = 0;
-    HIP_TRY(c, hipMemcpyAsync(&total, off + mp->m, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipStreamSynchronize(s));
-    HIP_TRY(c, ensure(c->mcands, (size_t)std::max(total, 1) * og_proj_cand_size()));
-    og_launch_proj_resolve(s, fd, G, sfd, mpd, nnratio, th, off, (OgProjCand*)c->mcands.p, own, obs, nm);
-    HIP_TRY(c, hipGetLastError());
+    int r = run_projection(c, s, fd, G, sfd, mpd, m, 1, nnratio, th, own, obs, nm);
+    if (r) return r;
     int hnm = 0;
     HIP_TRY(c, hipMemcpyAsync(&hnm, nm, sizeof(int), hipMemcpyDeviceToHost, s));
     if (F->n) {
@@ -1344,8 +1369,39 @@ int orbgpu_search_by_projection(orbgpu_ctx* c, const orbgpu_frame_view* F, const
         HIP_TRY(c, hipMemcpyAsync(owner_obs, obs, (size_t)F->n * 4, hipMemcpyDeviceToHost, s));
     }
     HIP_TRY(c, hipStreamSynchronize(s));
+    r = check_status(c);
+    if (r) return r;
     *nmatches = hnm;
     return ORBGPU_OK;
+}
+
+int orbgpu_search_by_projection_batch(orbgpu_ctx* c, const orbgpu_mappoints_view* d_mp, int mp_stride, float nnratio,
+                                      float th, const float* d_uright, int32_t* d_owner, int32_t* d_owner_obs,
+                                      int* d_nmatches)
+{
+    if (!c || !c->last_B || !d_mp || d_mp->m < 0 || mp_stride < d_mp->m || !d_owner || !d_owner_obs || !d_nmatches)
+        return ORBGPU_ERR_ARG;
+    if (d_mp->m && (!d_mp->track_in_view || !d_mp->is_bad || !d_mp->level || !d_mp->view_cos || !d_mp->proj_x ||
+                    !d_mp->proj_y || !d_mp->proj_xr || !d_mp->n_obs || !d_mp->desc))
+        return ORBGPU_ERR_ARG;
+    if ((size_t)2 * sizeof(int) * (size_t)c->plan.frame_cap > OG_INIT_LDS_MAX) {
+        c->err = "SearchByProjection: frame capacity exceeds the LDS-resident claim table";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    if (c->sf_dev.n < (size_t)c->nlevels) {
+        HIP_TRY(c, ensure(c->sf_dev, (size_t)c->nlevels));
+        HIP_TRY(c, hipMemcpyAsync(c->sf_dev.p, c->sf.data(), sizeof(float) * c->nlevels, hipMemcpyHostToDevice, s));
+    }
+    timer_mark(c, "match_proj");
+    OgFrameDev fd{kps_match(c), c->desc.p, c->counts.p, c->cell_start.p, c->cell_items.p, d_uright, c->plan.frame_cap};
+    OgMapPointsDev mpd{d_mp->m,      d_mp->track_in_view, d_mp->is_bad, d_mp->level, d_mp->view_cos, d_mp->proj_x,
+                       d_mp->proj_y, d_mp->proj_xr,       d_mp->n_obs,  d_mp->desc};
+    int r = run_projection(c, s, fd, c->grid_geom, c->sf_dev.p, mpd, mp_stride, c->last_B, nnratio, th, d_owner,
+                           d_owner_obs, d_nmatches);
+    timer_mark(c, "search_proj");
+    return r;
 }
 
 static OgCameraDev camera_dev(const orbgpu_camera* cam, float minX, float maxX, float minY, float maxY)

@@ -69,11 +69,15 @@ struct OgMapPointsDev {
 
 struct OgProjCand;
 size_t og_proj_cand_size();
-void og_launch_proj_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, float th,
-                          int* cnt, int* off);
-void og_launch_proj_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp,
-                            float nnratio, float th, const int* off, OgProjCand* cands, int* owner, int* owner_obs,
-                            int* nmatches);
+// batched form (B frames, map point j of frame b at b*stride + j of every mp array; mp.m points per frame):
+// count + per-frame scan + frame bases (base[B] = the candidate total, read by the host to size `cands`), then
+// fill + the parallel fixed-point resolve (one workgroup per frame; LDS 2 * frame_cap ints)
+int og_proj_keep_bound(float nnratio);
+void og_launch_projb_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, int stride,
+                           float th, int B, int* cnt, int* off, int* tot, long long* base);
+void og_launch_projb_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, int stride,
+                             float nnratio, float th, int B, const int* off, const long long* base, OgProjCand* cands,
+                             int* kept, int* res, int* owner, int* owner_obs, int* nmatches, int* status);
 
 // stereo (orb_stereo.hip): Frame::ComputeStereoMatches over frame pairs b of two extractor batches
 struct OgStereoDev {

@@ -216,3 +216,89 @@ def test_search_for_initialization_distance_bound(gpu, oracle, ratio):
     assert n == no and n > 10
     assert np.array_equal(m12, mo)
     assert np.array_equal(pg, po)
+
+
+def _mp_conflicts(rng, k, d, M):
+    """Map points that fight over the same keypoints: each source keypoint is projected by several points with
+    near-identical descriptors, mixed n_obs 0/2 (claims that do / do not block later points)."""
+    src = np.repeat(rng.integers(0, len(k), M // 6), 6)[:M]
+    mp = _mappoints(rng, k, d, len(src))
+    mp["level"] = k["octave"][src].astype(np.int32)
+    mp["proj_x"] = (k["x"][src] + rng.normal(0, 0.5, len(src))).astype(np.float32)
+    mp["proj_y"] = (k["y"][src] + rng.normal(0, 0.5, len(src))).astype(np.float32)
+    mp["desc"] = d[src] ^ np.packbits(rng.random((len(src), 256)) < 0.02, axis=1)
+    mp["n_obs"] = np.where(rng.random(len(src)) < 0.4, 0, 2).astype(np.int32)
+    return mp
+
+
+@pytest.mark.parametrize("rows,cols,nf,M,conflicts", [(480, 640, 1000, 1500, False), (480, 640, 1000, 1800, True),
+                                                      (1080, 1920, 4000, 5000, False)])
+def test_search_by_projection_batch_vs_oracle(gpu, oracle, rows, cols, nf, M, conflicts):
+    """orbgpu_search_by_projection_batch: B frames of a device batch, each against its own map-point snapshot
+    (config 5 shape in the last case), with claims made before the call; per-frame owners and counts bit-exact."""
+    import ctypes as C
+
+    from orbslam2_with_quadrics_amd import _lib
+
+    B = 3
+    ex = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
+    imgs = np.stack([synthetic.frame(200 + b, rows, cols) for b in range(B)])
+    dimg = ex.device_alloc(imgs.nbytes)
+    bufs = [dimg]
+    try:
+        ex.h2d(dimg, imgs)
+        ex.extract_batch_device(dimg, B, cols, rows, cols, rows * cols)
+        _, _, _, cap = ex.batch_outputs()
+        sf = ex.GetScaleFactors()
+        rng = np.random.default_rng(M)
+        frames, mps, owner0, obs0 = [], [], np.full((B, cap), -1, np.int32), np.zeros((B, cap), np.int32)
+        for b in range(B):
+            k, d = ex.batch_download(b)
+            frames.append((k, d))
+            mp = _mp_conflicts(rng, k, d, M) if conflicts else _mappoints(rng, k, d, M)
+            mp["n_obs"][::7] = 0
+            mp["track_in_view"][::11] = 0
+            mp["is_bad"][::13] = 1
+            mps.append(mp)
+            owner0[b, :len(k)][::19] = M  # claims made before the call
+            obs0[b, :len(k)][::38] = 1
+        stride = M + 5
+        dev = {}
+        for key in ("track_in_view", "is_bad", "level", "view_cos", "proj_x", "proj_y", "proj_xr", "n_obs", "desc"):
+            a0 = mps[0][key]
+            arr = np.zeros((B, stride) + a0.shape[1:], a0.dtype)
+            for b in range(B):
+                arr[b, :M] = mps[b][key]
+            p = ex.device_alloc(arr.nbytes)
+            bufs.append(p)
+            ex.h2d(p, arr)
+            dev[key] = p
+        d_own, d_obs, d_nm = (ex.device_alloc(B * cap * 4), ex.device_alloc(B * cap * 4), ex.device_alloc(B * 4))
+        bufs += [d_own, d_obs, d_nm]
+        ex.h2d(d_own, owner0)
+        ex.h2d(d_obs, obs0)
+        mv = _lib.MapPointsView(M, *[dev[k] for k in ("track_in_view", "is_bad", "level", "view_cos", "proj_x",
+                                                        "proj_y", "proj_xr", "n_obs", "desc")])
+        for th in (1.0, 3.0):
+            ex.h2d(d_own, owner0)
+            ex.h2d(d_obs, obs0)
+            _lib.check(ex.ctx, _lib.lib().orbgpu_search_by_projection_batch(ex.ctx, C.byref(mv), stride, 0.8, th, None,
+                                                                             C.c_void_p(d_own), C.c_void_p(d_obs),
+                                                                             C.c_void_p(d_nm)), "sbp_batch")
+            own = np.zeros((B, cap), np.int32)
+            obs = np.zeros((B, cap), np.int32)
+            nm = np.zeros(B, np.int32)
+            ex.d2h(own, d_own)
+            ex.d2h(obs, d_obs)
+            ex.d2h(nm, d_nm)
+            for b in range(B):
+                k, d = frames[b]
+                n = len(k)
+                wn, wown, wobs = oracle.search_by_projection(oracle.OracleFrame(k, d, cols, rows, sf), mps[b], 0.8, th,
+                                                             owner0[b, :n], obs0[b, :n])
+                assert nm[b] == wn and wn > 50, (b, th)
+                assert np.array_equal(own[b, :n], wown), (b, th)
+                assert np.array_equal(obs[b, :n], wobs), (b, th)
+    finally:
+        for p in bufs:
+            ex.device_free(p)
