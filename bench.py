@@ -85,7 +85,7 @@ def level_pixels(cols, rows, inv_scale):
     return [int(np.rint(np.float32(cols) * s)) * int(np.rint(np.float32(rows) * s)) for s in inv_scale]
 
 
-def stage_bytes(stage, B, P, cand_total, kp_total):
+def stage_bytes(stage, B, P, cand_total, kp_total, mappoints=0):
     """Algorithmic HBM bytes of one launch of `stage` for a batch of B frames."""
     if stage == "pyramid":  # read levels 0..L-2, write levels 1..L-1
         return B * (sum(P[:-1]) + sum(P[1:]))
@@ -99,6 +99,8 @@ def stage_bytes(stage, B, P, cand_total, kp_total):
         return kp_total * (28 + 4) + B * 3073 * 4
     if stage == "search_init":  # F2 keypoints + descriptors + grid, F1 once
         return kp_total * 60 + B * 3073 * 4
+    if stage == "search_proj":  # map-point snapshot (58 B per point) + keypoints + descriptors + grid
+        return B * mappoints * 58 + kp_total * 60 + B * 3073 * 4
     return 0
 
 
@@ -318,8 +320,129 @@ def setup_stereo(args, env):
                 cpu=lambda: cpu_baseline_stereo(rows, cols, NF, args.cpu_seconds))
 
 
-WORKLOADS = {"mono_init": setup_mono_init, "extract": setup_extract, "stereo": setup_stereo}
-DEFAULT_SHAPE = {"mono_init": (1080, 1920, 2000), "extract": (480, 640, 1000), "stereo": (376, 1241, 2000)}
+MP_KEYS = ("track_in_view", "is_bad", "level", "view_cos", "proj_x", "proj_y", "proj_xr", "n_obs", "desc")
+
+
+def tracking_mappoints(k, d, M, seed):
+    """M local-map points sampled from the camera's own extraction -- descriptor bits
+    flipped with p = 0.05, projection = keypoint + N(0, 1 px), level = octave, viewCos ~ U(0.9, 1), in view,
+    2 observations, no right projection (th = 1)."""
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, len(k), M)
+    return dict(track_in_view=np.ones(M, np.uint8), is_bad=np.zeros(M, np.uint8),
+                level=k["octave"][src].astype(np.int32), view_cos=rng.uniform(0.9, 1.0, M).astype(np.float32),
+                proj_x=(k["x"][src] + rng.normal(0, 1, M)).astype(np.float32),
+                proj_y=(k["y"][src] + rng.normal(0, 1, M)).astype(np.float32),
+                proj_xr=np.full(M, -1, np.float32), n_obs=np.full(M, 2, np.int32),
+                desc=d[src] ^ np.packbits(rng.random((M, 256)) < 0.05, axis=1))
+
+
+def cpu_baseline_tracking(rows, cols, nfeat, M, seconds):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py as O
+    from orbslam2_with_quadrics_amd import synthetic
+
+    O.build()
+    ex = O.OracleExtractor(nfeat)
+    sf = ex.tables()["scale"]
+    scene = synthetic.make_scene(synthetic.SEED_BASE + 997, rows, cols)
+    spent, frames = 0.0, 0
+    while spent < seconds or frames < 2:
+        f = synthetic.render(scene, rows, cols, frames % 9, frames % 5, noise_seed=300 + frames)
+        k0, d0 = ex(f)
+        mp = tracking_mappoints(k0, d0, M, frames)
+        ts = time.perf_counter()
+        k, d = ex(f)
+        O.search_by_projection(O.OracleFrame(k, d, cols, rows, sf), mp, 0.8, 1.0)
+        spent += time.perf_counter() - ts
+        frames += 1
+    return {"value": round(frames / spent, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{frames} frames of {cols}x{rows}, {nfeat} features: oracle extraction + SearchByProjection "
+                      f"vs {M} map points (th 1) on one host thread"}
+
+
+def setup_tracking(args, env):
+    """config 5 (8-camera 1920x1080 rig, 4000 features): per camera frame, ORB extraction and
+    SearchByProjection(F, local map points, th=1) (Tracking::SearchLocalPoints, src/Tracking.cc:1184-1191) against
+    --mappoints points; one camera per frame slot, cameras sharded over GPUs."""
+    L, _lib, ORBextractor, synthetic = env["L"], env["_lib"], env["ORBextractor"], env["synthetic"]
+    rows, cols, B, NF, S, dev = args.rows, args.cols, args.batch, args.nfeatures, args.streams, env["dev"]
+    M = args.mappoints
+    Bs = B // S
+    _, frames = _frames(synthetic, rows, cols, B, env["rank"], 5000)
+    exs = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev) for _ in range(S)]
+    d_frames = exs[0].device_alloc(frames.nbytes)
+    exs[0].h2d(d_frames, frames)
+    fbytes = rows * cols
+    for s_, e in enumerate(exs):
+        e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
+        e.synchronize()
+    outs = [e.batch_outputs() for e in exs]
+    cap = outs[0][3]
+    # each camera's local map from its own extraction (host, once)
+    per = {}
+    mps_dev, own_dev = [], []
+    for s_, e in enumerate(exs):
+        arrs = {key: [] for key in MP_KEYS}
+        for b in range(Bs):
+            fid = s_ * Bs + b
+            key = fid % min(B, 32)  # frames repeat with period min(B, 32) (_frames)
+            if key not in per:
+                k, d = e.batch_download(b)
+                per[key] = tracking_mappoints(k, d, M, 7000 + key + 1000 * env["rank"])
+            for kk in MP_KEYS:
+                arrs[kk].append(per[key][kk])
+        dp = {}
+        for kk in MP_KEYS:
+            a = np.ascontiguousarray(np.stack(arrs[kk]))
+            dp[kk] = e.device_alloc(a.nbytes)
+            e.h2d(dp[kk], a)
+        mps_dev.append(dp)
+        d_none = e.device_alloc(Bs * cap * 4)  # mvpMapPoints all NULL at SearchLocalPoints time
+        e.h2d(d_none, np.full(Bs * cap, -1, np.int32))
+        own_dev.append((d_none, e.device_alloc(Bs * cap * 4), e.device_alloc(Bs * cap * 4), e.device_alloc(Bs * 4)))
+    views = [_lib.MapPointsView(M, *[mps_dev[s_][kk] for kk in MP_KEYS]) for s_ in range(S)]
+
+    def step():
+        for s_, e in enumerate(exs):
+            e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
+            d_none, d_own, d_obs, _ = own_dev[s_]
+            _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C.c_void_p(d_own), C.c_void_p(d_none), Bs * cap * 4), "d2d")
+            _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C.c_void_p(d_obs), C.c_void_p(d_none), Bs * cap * 4), "d2d")
+        for s_, e in enumerate(exs):
+            _, d_own, d_obs, d_nm = own_dev[s_]
+            _lib.check(e.ctx, L.orbgpu_search_by_projection_batch(e.ctx, C.byref(views[s_]), M, 0.8, 1.0, None,
+                                                                   C.c_void_p(d_own), C.c_void_p(d_obs),
+                                                                   C.c_void_p(d_nm)), "search_proj")
+
+    def post():
+        counts = np.zeros(Bs, np.int32)
+        nm = np.zeros(Bs, np.int32)
+        kp_all, nm_all = 0, 0
+        for s_, e in enumerate(exs):
+            e.d2h(counts, outs[s_][2])
+            e.d2h(nm, own_dev[s_][3])
+            kp_all += int(counts.sum())
+            nm_all += int(nm.sum())
+        return {"mean_keypoints_per_frame": round(kp_all / B, 1), "map_points_per_frame": M,
+                "mean_projection_matches_per_frame": round(nm_all / B, 1)}, kp_all / S
+
+    def free():
+        for s_, e in enumerate(exs):
+            for p in list(mps_dev[s_].values()) + list(own_dev[s_]):
+                e.device_free(p)
+        exs[0].device_free(d_frames)
+
+    return dict(metric=f"frames/sec ORB extract + SearchByProjection vs {M} map points @{cols}×{rows}, {NF} feat",
+                exs=exs, step=step, post=post, free=free, Bs=Bs, frames_per_step=B, counts=[o[2] for o in outs],
+                workload=f"config 5: {cols}x{rows} camera frames, {NF} features, ORB extraction + SearchByProjection "
+                         f"(th 1, ratio 0.8) against {M} local-map points per camera",
+                cpu=lambda: cpu_baseline_tracking(rows, cols, NF, M, args.cpu_seconds))
+
+
+WORKLOADS = {"mono_init": setup_mono_init, "extract": setup_extract, "stereo": setup_stereo, "tracking": setup_tracking}
+DEFAULT_SHAPE = {"mono_init": (1080, 1920, 2000), "extract": (480, 640, 1000), "stereo": (376, 1241, 2000),
+                 "tracking": (1080, 1920, 4000)}
 
 
 def cpu_baseline_extract(rows, cols, nfeat, seconds):
@@ -371,7 +494,8 @@ def main():
     ap.add_argument("--streams", type=int, default=2, help="concurrent extractor contexts (HIP streams) per GPU")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="mono_init",
                     help="mono_init = BASELINE.json's config 3 (the headline metric); extract = config 2; "
-                         "stereo = config 4")
+                         "stereo = config 4; tracking = config 5")
+    ap.add_argument("--mappoints", type=int, default=5000, help="local-map points per camera (tracking)")
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--cols", type=int, default=None)
     ap.add_argument("--nfeatures", type=int, default=None)
@@ -456,7 +580,8 @@ def main():
     extra, kp_total = W["post"]()
     P = level_pixels(args.cols, args.rows, exs[0].GetInverseScaleFactors())
     stages = {k: v[0] / max(v[1], 1) for k, v in stage_acc.items()}
-    kernels = {k: v for k, v in stages.items() if k in ("fast", "octree", "describe", "grid", "search_init")}
+    kernels = {k: v for k, v in stages.items()
+               if k in ("fast", "octree", "describe", "grid", "search_init", "search_proj")}
     dom = max(kernels, key=kernels.get)
     # effective launch duration: time the GPU has >= 1 launch of the kernel running, per launch.  With
     # concurrent streams a launch's own event span also covers the co-running launches; the union does
@@ -464,7 +589,7 @@ def main():
     launches = stage_acc[dom][1]
     dom_ms = union_acc[dom] / max(launches, 1)
     dom_ms_span = kernels[dom]
-    dom_bytes = stage_bytes(dom, Bs, P, cand_total, kp_total)
+    dom_bytes = stage_bytes(dom, Bs, P, cand_total, kp_total, args.mappoints)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
     valu = None
