@@ -163,10 +163,16 @@ def _frames(synthetic, rows, cols, B, rank, seed_off=1000):
 
 
 def setup_mono_init(args, env):
-    """config 3: extract the initial frame and B frames, SearchForInitialization of each against it."""
+    """config 3: extract the initial frame and B frames, SearchForInitialization of each against it.  The B frames
+    are split over S contexts (streams) and, per context, K sequential launches (--chunks; one launch is fastest,
+    profiles/sweeps/r01_stagger_chunks.txt)."""
     L, C_, _lib, ORBextractor, synthetic = env["L"], C, env["_lib"], env["ORBextractor"], env["synthetic"]
     rows, cols, B, NF, S, dev = args.rows, args.cols, args.batch, args.nfeatures, args.streams, env["dev"]
+    K = args.chunks
     Bs = B // S
+    if Bs % K:
+        raise SystemExit(f"--batch/--streams = {Bs} frames per stream must be a multiple of --chunks {K}")
+    Bc = Bs // K
     f1, frames = _frames(synthetic, rows, cols, B, env["rank"])
     ex_ref = ORBextractor(NF, 1.2, 8, 20, 7, device=dev)
     exs = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev) for _ in range(S)]
@@ -179,47 +185,51 @@ def setup_mono_init(args, env):
     L.orbgpu_grid_geom_for_image(cols, rows, C_.byref(grid))
     ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
     for s_, e in enumerate(exs):
-        e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
+        e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bc, cols, rows, cols, fbytes)
         e.synchronize()
     outs = [e.batch_outputs() for e in exs]
     cap = outs[0][3]
-    d_prev = [e.device_alloc(Bs * cap * 2 * 4) for e in exs]
-    d_m12 = [e.device_alloc(Bs * cap * 4) for e in exs]
-    d_nm = [e.device_alloc(Bs * 4) for e in exs]
+    d_prev = [e.device_alloc(Bc * cap * 2 * 4) for e in exs]
+    d_m12 = [e.device_alloc(Bc * cap * 4) for e in exs]
+    d_nm = [e.device_alloc(Bc * 4) for e in exs]
+    d_cnt = [e.device_alloc(Bs * 4) for e in exs]  # per-frame keypoint counts of all K chunks (all-gathered)
 
     def step():
         ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
-        for s_, e in enumerate(exs):
-            e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
-        for s_, e in enumerate(exs):
-            _lib.check(e.ctx, L.orbgpu_prev_matched_from_frame(ex_ref.ctx, 0, e.ctx, C_.c_void_p(d_prev[s_])),
-                       "prev")
-            _lib.check(e.ctx, L.orbgpu_search_for_initialization_batch(ex_ref.ctx, 0, e.ctx, grid, 0.9, 1, 100,
-                                                                         C_.c_void_p(d_prev[s_]),
-                                                                         C_.c_void_p(d_m12[s_]),
-                                                                         C_.c_void_p(d_nm[s_])), "search_init")
+        for r in range(K):
+            for s_, e in enumerate(exs):
+                e.extract_batch_device(d_frames + (s_ * Bs + r * Bc) * fbytes, Bc, cols, rows, cols, fbytes)
+                _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C_.c_void_p(d_cnt[s_] + 4 * r * Bc),
+                                                            C_.c_void_p(outs[s_][2]), Bc * 4), "d2d")
+                _lib.check(e.ctx, L.orbgpu_prev_matched_from_frame(ex_ref.ctx, 0, e.ctx, C_.c_void_p(d_prev[s_])),
+                           "prev")
+                _lib.check(e.ctx, L.orbgpu_search_for_initialization_batch(ex_ref.ctx, 0, e.ctx, grid, 0.9, 1, 100,
+                                                                             C_.c_void_p(d_prev[s_]),
+                                                                             C_.c_void_p(d_m12[s_]),
+                                                                             C_.c_void_p(d_nm[s_])), "search_init")
 
-    def post():
-        counts = np.zeros(Bs, np.int32)
-        nm = np.zeros(Bs, np.int32)
+    def post():  # the last chunk of every context
+        counts = np.zeros(Bc, np.int32)
+        nm = np.zeros(Bc, np.int32)
         kp_all, nm_all = 0, 0
         for s_, e in enumerate(exs):
             e.d2h(counts, outs[s_][2])
             e.d2h(nm, d_nm[s_])
             kp_all += int(counts.sum())
             nm_all += int(nm.sum())
-        return {"mean_keypoints_per_frame": round(kp_all / B, 1),
-                "mean_init_matches_per_frame": round(nm_all / B, 1)}, kp_all / S
+        return {"mean_keypoints_per_frame": round(kp_all / (Bc * S), 1),
+                "mean_init_matches_per_frame": round(nm_all / (Bc * S), 1),
+                "chunks_per_stream": K}, kp_all / S
 
     def free():
         for s_, e in enumerate(exs):
-            for p in (d_prev[s_], d_m12[s_], d_nm[s_]):
+            for p in (d_prev[s_], d_m12[s_], d_nm[s_], d_cnt[s_]):
                 e.device_free(p)
         exs[0].device_free(d_frames)
         ex_ref.device_free(d_f1)
 
-    return dict(metric=METRIC, exs=exs, step=step, post=post, free=free, Bs=Bs, frames_per_step=B,
-                counts=[o[2] for o in outs],
+    return dict(metric=METRIC, exs=exs, step=step, post=post, free=free, Bs=Bc, per_stream=Bs, frames_per_step=B,
+                counts=d_cnt,
                 workload=f"config 3: {cols}x{rows} mono, {NF} features, ORB extract + SearchForInitialization "
                          f"(window 100, ratio 0.9, checkOri) of every frame against an initial frame",
                 cpu=lambda: cpu_baseline(rows, cols, NF, args.cpu_seconds))
@@ -490,12 +500,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128, help="frames (pairs) per step per GPU")
+    ap.add_argument("--batch", type=int, default=512, help="frames (pairs) per step per GPU")
     ap.add_argument("--streams", type=int, default=2, help="concurrent extractor contexts (HIP streams) per GPU")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="mono_init",
                     help="mono_init = BASELINE.json's config 3 (the headline metric); extract = config 2; "
                          "stereo = config 4; tracking = config 5")
     ap.add_argument("--mappoints", type=int, default=5000, help="local-map points per camera (tracking)")
+    ap.add_argument("--chunks", type=int, default=1, help="sequential launches per stream per step (mono_init)")
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--cols", type=int, default=None)
     ap.add_argument("--nfeatures", type=int, default=None)
@@ -523,6 +534,7 @@ def main():
     W = WORKLOADS[args.workload](args, env)
     log(f"rank {rank}: {args.workload} set up in {time.time() - t:.1f}s")
     exs, Bs, S, B = W["exs"], W["Bs"], args.streams, W["frames_per_step"]
+    Bps = W.get("per_stream", Bs)  # frames per stream per step (Bs = frames per launch)
     counts_t = torch.zeros(B, dtype=torch.int32, device=f"cuda:{dev}")
 
     def step():
@@ -530,7 +542,7 @@ def main():
         if dist is not None:  # north_star: all-gather of the per-frame keypoint counts over RCCL
             for s_, dc in enumerate(W["counts"]):
                 _lib.check(exs[s_].ctx, _lib.lib().orbgpu_memcpy_d2d_async(
-                    exs[s_].ctx, C.c_void_p(counts_t.data_ptr() + 4 * s_ * Bs), C.c_void_p(dc), Bs * 4), "d2d")
+                    exs[s_].ctx, C.c_void_p(counts_t.data_ptr() + 4 * s_ * Bps), C.c_void_p(dc), Bps * 4), "d2d")
         for e in exs:
             e.synchronize()
         if dist is not None:

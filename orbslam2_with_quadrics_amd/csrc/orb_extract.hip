@@ -180,94 +180,61 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
 // k2: FAST cells (src/ORBextractor.cc:789-829 + cv::FAST TYPE_9_16 with nonmax suppression)
 // ------------------------------------------------------------------------------------------------
 // M(p) = max over the 16 contiguous 9-arcs and both polarities of min |I(p) - I(arc)|; the pixel is a
-// FAST corner at threshold t iff M > t and then cornerScore<16> == M - 1.  Computed on the
-// circle values themselves: max_k min_arc(v - c) = v - min_k max_arc(c) and -min_k max_arc(v - c) =
-// max_k min_arc(c) - v, so M = max(v - A, B - v, 0) with A = min_k max_arc c, B = max_k min_arc c.  Each
-// 9-arc [k, k+8] is max3/min3(pairs-of-pairs at k and k+4, c[k+8]): 112 integer ops, exact.
+// FAST corner at threshold t iff M > t and then cornerScore<16> == M - 1.  Per polarity on the
+// circle values themselves: the dark score is v - A with A = min_k max_arc c, the bright one B - v with
+// B = max_k min_arc c.  og_fast_M1 computes ONE polarity: with fm = 0xff the values are complemented
+// (255 - x == x ^ 0xff), which turns the bright score into the dark form.  A survivor of the quick test at tq
+// that fails one polarity's quick test has that polarity's score <= tq, and scores <= tq never decide anything
+// (a kept corner needs M > max(t, 1) >= tq and then beats every neighbour <= tq), so the passing polarity's
+// score stands for M; the rare survivors passing both take the max of the two.  Each 9-arc [k, k+8] is the
+// max3 of the 3-arcs at k, k+3, k+6: ~40 integer ops per polarity, exact.
 template <int SX, typename E>
-__device__ __forceinline__ int og_fast_M(const E* p, int st)
+__device__ __forceinline__ int og_fast_M1(const E* p, int st, int fm)
 {
-    const int v = p[0];
+    const int v = p[0] ^ fm;
     int c[16];
-    c[0] = p[3 * st];
-    c[1] = p[1 * SX + 3 * st];
-    c[2] = p[2 * SX + 2 * st];
-    c[3] = p[3 * SX + 1 * st];
-    c[4] = p[3 * SX];
-    c[5] = p[3 * SX - 1 * st];
-    c[6] = p[2 * SX - 2 * st];
-    c[7] = p[1 * SX - 3 * st];
-    c[8] = p[-3 * st];
-    c[9] = p[-1 * SX - 3 * st];
-    c[10] = p[-2 * SX - 2 * st];
-    c[11] = p[-3 * SX - 1 * st];
-    c[12] = p[-3 * SX];
-    c[13] = p[-3 * SX + 1 * st];
-    c[14] = p[-2 * SX + 2 * st];
-    c[15] = p[-1 * SX + 3 * st];
-    int mn2[16], mx2[16];
+    c[0] = p[3 * st] ^ fm;
+    c[1] = p[1 * SX + 3 * st] ^ fm;
+    c[2] = p[2 * SX + 2 * st] ^ fm;
+    c[3] = p[3 * SX + 1 * st] ^ fm;
+    c[4] = p[3 * SX] ^ fm;
+    c[5] = p[3 * SX - 1 * st] ^ fm;
+    c[6] = p[2 * SX - 2 * st] ^ fm;
+    c[7] = p[1 * SX - 3 * st] ^ fm;
+    c[8] = p[-3 * st] ^ fm;
+    c[9] = p[-1 * SX - 3 * st] ^ fm;
+    c[10] = p[-2 * SX - 2 * st] ^ fm;
+    c[11] = p[-3 * SX - 1 * st] ^ fm;
+    c[12] = p[-3 * SX] ^ fm;
+    c[13] = p[-3 * SX + 1 * st] ^ fm;
+    c[14] = p[-2 * SX + 2 * st] ^ fm;
+    c[15] = p[-1 * SX + 3 * st] ^ fm;
+    int mx3[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        mn2[k] = min(c[k], c[(k + 1) & 15]);
-        mx2[k] = max(c[k], c[(k + 1) & 15]);
-    }
-    int mn4[16], mx4[16];
+    for (int k = 0; k < 16; k++) mx3[k] = max(max(c[k], c[(k + 1) & 15]), c[(k + 2) & 15]);
+    int mx9[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
-    }
-    int A = 255, B = 0;
+    for (int k = 0; k < 16; k++) mx9[k] = max(max(mx3[k], mx3[(k + 3) & 15]), mx3[(k + 6) & 15]);
+    int a[6];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        A = min(A, max(max(mx4[k], mx4[(k + 4) & 15]), c[(k + 8) & 15]));
-        B = max(B, min(min(mn4[k], mn4[(k + 4) & 15]), c[(k + 8) & 15]));
-    }
-    return max(max(v - A, B - v), 0);
+    for (int k = 0; k < 5; k++) a[k] = min(min(mx9[3 * k], mx9[3 * k + 1]), mx9[3 * k + 2]);
+    a[5] = mx9[15];
+    const int A = min(min(min(a[0], a[1]), a[2]), min(min(a[3], a[4]), a[5]));
+    return max(v - A, 0);
 }
 
 
 // OpenCV FAST_t quick rejection (src: cv::FAST, pairs {k, k+8}): a pixel can only be a corner at
 // threshold t if for every opposite pair one pixel is darker than v-t (resp. brighter than v+t).
 // Necessary condition => every pixel that fails it has M <= t.  Restated threshold-free:
-//   dark(t)   <=>  max_k min(c_k, c_k+8) < v - t,   bright(t) <=> min_k max(c_k, c_k+8) > v + t,
-// (16 byte loads, 8 min + 8 max reductions, 2 compares).
-template <int RS>
-__device__ __forceinline__ bool og_fast_quick(const uint8_t* p, int t)
-{
-    const int v = p[0];
-    int c[16];
-    c[0] = p[3 * RS];
-    c[1] = p[1 + 3 * RS];
-    c[2] = p[2 + 2 * RS];
-    c[3] = p[3 + 1 * RS];
-    c[4] = p[3];
-    c[5] = p[3 - 1 * RS];
-    c[6] = p[2 - 2 * RS];
-    c[7] = p[1 - 3 * RS];
-    c[8] = p[-3 * RS];
-    c[9] = p[-1 - 3 * RS];
-    c[10] = p[-2 - 2 * RS];
-    c[11] = p[-3 - 1 * RS];
-    c[12] = p[-3];
-    c[13] = p[-3 + 1 * RS];
-    c[14] = p[-2 + 2 * RS];
-    c[15] = p[-1 + 3 * RS];
-    int md = 0, mb = 255;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        md = max(md, min(c[k], c[k + 8]));
-        mb = min(mb, max(c[k], c[k + 8]));
-    }
-    return (md < v - t) | (mb > v + t);
-}
-
+//   dark(t)   <=>  max_k min(c_k, c_k+8) < v - t,   bright(t) <=> min_k max(c_k, c_k+8) > v + t.
 // The same quick test for two pixels at once: each dword of the pair-interleaved ROI holds (pixel x, pixel
 // x + H) as two u16, so one LDS read gives a circle sample of both pixels and v_pk_min/max_u16 test both.
-// Returns a dword whose low (high) half is nonzero iff the first (second) pixel survives.
+// Returns {dark, bright} dwords whose low (high) half is nonzero iff the first (second) pixel passes that
+// polarity's test.
 typedef unsigned short og_u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ og_u16x2 og_as_u16x2(uint32_t x) { return __builtin_bit_cast(og_u16x2, x); }
-__device__ __forceinline__ uint32_t og_fast_quick2(const uint32_t* p, int st, og_u16x2 tt)
+__device__ __forceinline__ uint2 og_fast_quick2(const uint32_t* p, int st, og_u16x2 tt)
 {
     og_u16x2 c[16];
     c[0] = og_as_u16x2(p[3 * st]);
@@ -296,7 +263,7 @@ __device__ __forceinline__ uint32_t og_fast_quick2(const uint32_t* p, int st, og
     // dark: md < v - t (saturated: v < t leaves no darker value), bright: mb > v + t (<= 510, no overflow)
     const og_u16x2 dark = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, tt), md);
     const og_u16x2 bright = __builtin_elementwise_sub_sat(mb, v + tt);
-    return __builtin_bit_cast(uint32_t, dark) | __builtin_bit_cast(uint32_t, bright);
+    return make_uint2(__builtin_bit_cast(uint32_t, dark), __builtin_bit_cast(uint32_t, bright));
 }
 
 #ifndef OG_EXP_FAST_STOP
@@ -334,7 +301,8 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 {
     __shared__ __attribute__((aligned(16))) uint32_t roi2[FB_ROWS * FB_S2];
     __shared__ __attribute__((aligned(16))) uint8_t Ms[FB_MSZ];
-    __shared__ uint16_t lst[FB_MW * FB_MW];    // quick-test survivors, (i << 7) | j + keep bits 14 (t1), 15 (t2)
+    __shared__ uint16_t lst[FB_MW * FB_MW];    // survivors (i << 7) | j; bits 14/15: dark/bright passes (stages 1-2),
+                                               // then kept at t1/t2 (stages 3-4)
     __shared__ int sh_ns;
     __shared__ __attribute__((aligned(16))) int wk[FB_NW][8];  // per wave: kept at t1 per cell [0..3], at t2 [4..7]
     __shared__ int sh_base;
@@ -430,22 +398,25 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     // reservation for the four survivor ballots
     for (int p0 = wv * 64; p0 < npair; p0 += 2 * FB_NT) {
         int ii[2], cc[2];
-        uint32_t r[2];
+        uint2 r[2];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const int pp = p0 + h * FB_NT + lane;
             ii[h] = (int)(__umul24((unsigned)pp, invH) >> 20);
             cc[h] = pp - (int)__umul24((unsigned)ii[h], (unsigned)H);
-            r[h] = 0u;
+            r[h] = make_uint2(0u, 0u);
             if (pp < npair) r[h] = og_fast_quick2(&T2[(ii[h] + 3) * FB_S2 + (cc[h] + 3)], FB_S2, tt);
         }
         bool sv[4];
+        int pol[4];
         u64 m[4];
         int nn[4];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-            sv[2 * h] = (r[h] & 0xffffu) != 0u && cc[h] < dw;
-            sv[2 * h + 1] = (r[h] >> 16) != 0u && cc[h] + H < dw;
+            pol[2 * h] = ((r[h].x & 0xffffu) ? 0x4000 : 0) | ((r[h].y & 0xffffu) ? 0x8000 : 0);
+            pol[2 * h + 1] = ((r[h].x >> 16) ? 0x4000 : 0) | ((r[h].y >> 16) ? 0x8000 : 0);
+            sv[2 * h] = pol[2 * h] != 0 && cc[h] < dw;
+            sv[2 * h + 1] = pol[2 * h + 1] != 0 && cc[h] + H < dw;
         }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -460,7 +431,8 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int h = q >> 1;
-                if (sv[q]) lst[b + __popcll(m[q] & lt_mask)] = (uint16_t)((ii[h] << 7) | (cc[h] + ((q & 1) ? H : 0)));
+                if (sv[q])
+                    lst[b + __popcll(m[q] & lt_mask)] = (uint16_t)(pol[q] | (ii[h] << 7) | (cc[h] + ((q & 1) ? H : 0)));
                 b += nn[q];
             }
         }
@@ -477,10 +449,14 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const uint16_t* T16 = (const uint16_t*)T2;
     for (int e = tid; e < ns; e += FB_NT) {
         const int ent = lst[e];
-        const int i = ent >> 7, j = ent & 127;
+        const int i = (ent >> 7) & 127, j = ent & 127;
         const int hi = j >= H;
         const int x = j - (hi ? H : 0);
-        Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)og_fast_M<2>(&T16[2 * ((i + 3) * FB_S2 + (x + 3)) + hi], 2 * FB_S2);
+        const uint16_t* pc = &T16[2 * ((i + 3) * FB_S2 + (x + 3)) + hi];
+        const bool dark = (ent & 0x4000) != 0, bright = (ent & 0x8000) != 0;
+        int M = og_fast_M1<2>(pc, 2 * FB_S2, dark ? 0 : 0xff);
+        if (dark && bright) M = max(M, og_fast_M1<2>(pc, 2 * FB_S2, 0xff));  // rare: both polarities pass
+        Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)M;
     }
     __syncthreads();
     // ---- stage 3: same-cell 3x3 NMS at both thresholds.  cv::FAST keeps a corner (score M-1) iff its score
@@ -493,7 +469,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         bool k1 = false, k2 = false;
         int cell = 0;
         if (e < ns) {
-            const int ent = lst[e];
+            const int ent = lst[e] & 0x3fff;
             const int i = ent >> 7, j = ent & 127;
             const uint8_t* q = &Ms[og_ms_idx(i, j, wC, hC) - FB_MSW - 1];
             const int m = q[FB_MSW + 1];

@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 ROOT=$(pwd)
 timeout -k 10 600 bash tools/pmc_profile.sh "$OUT/pmc"
-python3 tools/pmc_summary.py "$OUT/pmc" --json "$OUT/pmc_latest.json" --md "$OUT/pmc_summary.md" --batch 64
+python3 tools/pmc_summary.py "$OUT/pmc" --json "$OUT/pmc_latest.json" --md "$OUT/pmc_summary.md" --batch 256
 cp "$OUT/pmc_latest.json" profiles/pmc_latest.json
 timeout -k 10 600 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 cat "$OUT/bench.json"
