@@ -1018,7 +1018,9 @@ __device__ __forceinline__ int og_reflect101(int i, int n)
     return i;
 }
 
+#ifndef DK_WAVES
 #define DK_WAVES 4
+#endif
 #define RAW_W 43
 #define RAW_S 52  // 43 + 3 misalignment bytes, dword multiple; 13 dwords: conflict-free lane-per-row reads
 #define BL_W 37
@@ -1037,7 +1039,6 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 {
     __shared__ __attribute__((aligned(16))) uint8_t raw[DK_WAVES][RAW_W * RAW_S];
     __shared__ __attribute__((aligned(16))) uint32_t hp[DK_WAVES][HP_ROWS * HP_S];
-    __shared__ uint8_t bl[DK_WAVES][BL_W * BL_W + 3];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int f = (int)(lin / gridDim.x);
@@ -1056,7 +1057,9 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     const bool active = l >= 0;
     uint8_t* R = raw[w];
     uint32_t* Hp = hp[w];
-    uint8_t* Bl = bl[w];
+    // the blurred window reuses the raw window's bytes: the raw window's last readers (IC angle, horizontal
+    // pass) are done before the vertical pass writes Bl; 5.8 KB of LDS per wave keeps ~27 waves per CU resident
+    uint8_t* Bl = raw[w];
     int cx = 0, cy = 0, resp = 0, lw = 1, lh = 1;
     if (active) {
         const OgLevel& L = P.lv[l];
