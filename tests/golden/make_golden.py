@@ -6,6 +6,9 @@ extract_golden.json : the oracle's ORB extraction of seeded synthetic frames (ha
                       This pins the oracle against regressions; it is NOT a reference-binary output
                       (the reference cannot be built here -- DESIGN.md §4).
 match_golden.json   : oracle SearchForInitialization on a seeded 1080p pair (match vector hash).
+tracking_golden.json: oracle SearchByProjection(F, 5000 map points, th 1) on a config-5 frame (1920x1080, 4000
+                      features; SURVEY.md §8(d) map-point recipe) -- owner vector hash -- and oracle
+                      Frame::ComputeStereoMatches on a KITTI-shape pair (mvuRight / mvDepth hashes).
 """
 import ctypes as C
 import hashlib
@@ -76,9 +79,51 @@ def match_cases():
               open(os.path.join(OUT, "match_golden.json"), "w"), indent=1)
 
 
+def config5_mappoints(k, d, M, seed):
+    """points from the camera's own extraction (bits flipped with p = 0.05, projection
+    = keypoint + N(0, 1 px), level = octave, viewCos ~ U(0.9, 1), in view, 2 observations)."""
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, len(k), M)
+    return dict(track_in_view=np.ones(M, np.uint8), is_bad=np.zeros(M, np.uint8),
+                level=k["octave"][src].astype(np.int32), view_cos=rng.uniform(0.9, 1.0, M).astype(np.float32),
+                proj_x=(k["x"][src] + rng.normal(0, 1, M)).astype(np.float32),
+                proj_y=(k["y"][src] + rng.normal(0, 1, M)).astype(np.float32),
+                proj_xr=np.full(M, -1, np.float32), n_obs=np.full(M, 2, np.int32),
+                desc=d[src] ^ np.packbits(rng.random((M, 256)) < 0.05, axis=1))
+
+
+def tracking_cases():
+    proj = []
+    for fid, M, th in [(11, 5000, 1.0), (12, 5000, 3.0)]:
+        img = synthetic.frame(fid, 1080, 1920)
+        ex = O.OracleExtractor(4000)
+        k, d = ex(img)
+        mp = config5_mappoints(k, d, M, fid)
+        n, own, obs = O.search_by_projection(O.OracleFrame(k, d, 1920, 1080, ex.tables()["scale"]), mp, 0.8, th)
+        proj.append(dict(frame_id=fid, rows=1080, cols=1920, nfeatures=4000, mappoints=M, th=th, mp_seed=fid,
+                         nmatches=int(n), owner_sha256=hashlib.sha256(own.astype(np.int32).tobytes()).hexdigest(),
+                         owner_obs_sha256=hashlib.sha256(obs.astype(np.int32).tobytes()).hexdigest()))
+    stereo = []
+    for pid in (2, 3):
+        left, right, _ = synthetic.stereo_pair(pid, 376, 1241)
+        exL, exR = O.OracleExtractor(2000), O.OracleExtractor(2000)
+        kl, dl = exL(left)
+        kr, dr = exR(right)
+        mb = float(np.float32(386.1448) / np.float32(718.856))
+        n, ur, de = O.stereo_matches(exL, exR, kl, dl, kr, dr, 386.1448, mb)
+        stereo.append(dict(pair_id=pid, rows=376, cols=1241, nfeatures=2000, mbf=386.1448, mb=mb, nmatches=int(n),
+                           uright_sha256=hashlib.sha256(ur.tobytes()).hexdigest(),
+                           depth_sha256=hashlib.sha256(de.tobytes()).hexdigest()))
+    json.dump({"generator": "oracle SearchByProjection / ComputeStereoMatches via tests/golden/make_golden.py",
+               "projection": proj, "stereo": stereo},
+              open(os.path.join(OUT, "tracking_golden.json"), "w"), indent=1)
+
+
 if __name__ == "__main__":
     O.build()
-    sincos_vectors()
-    extract_cases()
-    match_cases()
+    if "--only-tracking" not in sys.argv:
+        sincos_vectors()
+        extract_cases()
+        match_cases()
+    tracking_cases()
     print("golden fixtures written to", OUT)

@@ -3,6 +3,7 @@ ABI) against the CPU oracle -- match indices, counts and updated state must be i
 import hashlib
 import json
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -302,3 +303,70 @@ def test_search_by_projection_batch_vs_oracle(gpu, oracle, rows, cols, nf, M, co
     finally:
         for p in bufs:
             ex.device_free(p)
+
+
+def test_golden_tracking_projection_and_stereo(gpu):
+    """The GPU path against the committed oracle goldens (tests/golden/tracking_golden.json): config-5
+    SearchByProjection through the host C ABI and through the batched device form, and KITTI-shape stereo."""
+    import ctypes as C
+
+    from orbslam2_with_quadrics_amd import _lib
+
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_golden
+
+    g = json.load(open(os.path.join(ROOT, "tests/golden/tracking_golden.json")))
+    for case in g["projection"]:
+        rows, cols = case["rows"], case["cols"]
+        ex = gpu.ORBextractor(case["nfeatures"], 1.2, 8, 20, 7)
+        img = synthetic.frame(case["frame_id"], rows, cols)
+        k, d = ex(img)
+        mp = make_golden.config5_mappoints(k, d, case["mappoints"], case["mp_seed"])
+        n, own, obs = gpu.ORBmatcher(0.8, context=ex).SearchByProjection(gpu.Frame(k, d, cols, rows,
+                                                                                   ex.GetScaleFactors()),
+                                                                         mp, case["th"])
+        assert n == case["nmatches"]
+        assert hashlib.sha256(own.astype(np.int32).tobytes()).hexdigest() == case["owner_sha256"]
+        assert hashlib.sha256(obs.astype(np.int32).tobytes()).hexdigest() == case["owner_obs_sha256"]
+        # batched device form, one frame
+        d_img = ex.device_alloc(img.nbytes)
+        bufs = [d_img]
+        try:
+            ex.h2d(d_img, img)
+            ex.extract_batch_device(d_img, 1, cols, rows, cols, img.nbytes)
+            _, _, _, cap = ex.batch_outputs()
+            dev = {}
+            for key in ("track_in_view", "is_bad", "level", "view_cos", "proj_x", "proj_y", "proj_xr", "n_obs", "desc"):
+                a = np.ascontiguousarray(mp[key])
+                dev[key] = ex.device_alloc(a.nbytes)
+                bufs.append(dev[key])
+                ex.h2d(dev[key], a)
+            d_own, d_obs, d_nm = ex.device_alloc(cap * 4), ex.device_alloc(cap * 4), ex.device_alloc(4)
+            bufs += [d_own, d_obs, d_nm]
+            ex.h2d(d_own, np.full(cap, -1, np.int32))
+            ex.h2d(d_obs, np.zeros(cap, np.int32))
+            M = case["mappoints"]
+            mv = _lib.MapPointsView(M, *[dev[kk] for kk in ("track_in_view", "is_bad", "level", "view_cos", "proj_x",
+                                                              "proj_y", "proj_xr", "n_obs", "desc")])
+            _lib.check(ex.ctx, _lib.lib().orbgpu_search_by_projection_batch(ex.ctx, C.byref(mv), M, 0.8, case["th"],
+                                                                             None, C.c_void_p(d_own),
+                                                                             C.c_void_p(d_obs), C.c_void_p(d_nm)),
+                       "sbp_batch")
+            bown = np.zeros(cap, np.int32)
+            nm = np.zeros(1, np.int32)
+            ex.d2h(bown, d_own)
+            ex.d2h(nm, d_nm)
+            assert nm[0] == case["nmatches"]
+            assert hashlib.sha256(bown[:len(k)].tobytes()).hexdigest() == case["owner_sha256"]
+        finally:
+            for p in bufs:
+                ex.device_free(p)
+    for case in g["stereo"]:
+        left, right, _ = synthetic.stereo_pair(case["pair_id"], case["rows"], case["cols"])
+        exL, exR = gpu.ORBextractor(case["nfeatures"], 1.2, 8, 20, 7), gpu.ORBextractor(case["nfeatures"], 1.2, 8, 20, 7)
+        exL(left)
+        exR(right)
+        ur, de, n = gpu.ComputeStereoMatches(exL, exR, case["mbf"], case["mb"])
+        assert n == case["nmatches"]
+        assert hashlib.sha256(ur.tobytes()).hexdigest() == case["uright_sha256"]
+        assert hashlib.sha256(de.tobytes()).hexdigest() == case["depth_sha256"]

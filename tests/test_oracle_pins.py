@@ -6,6 +6,7 @@ import math
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -173,3 +174,33 @@ def test_oracle_golden_extraction(oracle):
         head = np.array(case["head"], np.float64)
         assert np.array_equal(np.stack([k["x"], k["y"], k["angle"], k["response"]], 1)[:len(head)]
                               .astype(np.float64), head)
+
+
+def test_oracle_golden_tracking_and_stereo(oracle):
+    """Regression pin of the oracle's SearchByProjection (config 5: 1080p, 4000 features, 5000 map points) and
+    ComputeStereoMatches (KITTI shape) on the committed tracking_golden.json."""
+    from orbslam2_with_quadrics_amd import synthetic
+
+    sys.path.insert(0, GOLDEN)
+    import make_golden
+
+    g = json.load(open(os.path.join(GOLDEN, "tracking_golden.json")))
+    for case in g["projection"]:
+        img = synthetic.frame(case["frame_id"], case["rows"], case["cols"])
+        ex = oracle.OracleExtractor(case["nfeatures"])
+        k, d = ex(img)
+        mp = make_golden.config5_mappoints(k, d, case["mappoints"], case["mp_seed"])
+        n, own, obs = oracle.search_by_projection(oracle.OracleFrame(k, d, case["cols"], case["rows"],
+                                                                     ex.tables()["scale"]), mp, 0.8, case["th"])
+        assert n == case["nmatches"]
+        assert hashlib.sha256(own.astype(np.int32).tobytes()).hexdigest() == case["owner_sha256"]
+        assert hashlib.sha256(obs.astype(np.int32).tobytes()).hexdigest() == case["owner_obs_sha256"]
+    for case in g["stereo"]:
+        left, right, _ = synthetic.stereo_pair(case["pair_id"], case["rows"], case["cols"])
+        exL, exR = oracle.OracleExtractor(case["nfeatures"]), oracle.OracleExtractor(case["nfeatures"])
+        kl, dl = exL(left)
+        kr, dr = exR(right)
+        n, ur, de = oracle.stereo_matches(exL, exR, kl, dl, kr, dr, case["mbf"], case["mb"])
+        assert n == case["nmatches"]
+        assert hashlib.sha256(ur.tobytes()).hexdigest() == case["uright_sha256"]
+        assert hashlib.sha256(de.tobytes()).hexdigest() == case["depth_sha256"]
