@@ -193,12 +193,24 @@ def setup_mono_init(args, env):
     d_m12 = [e.device_alloc(Bc * cap * 4) for e in exs]
     d_nm = [e.device_alloc(Bc * 4) for e in exs]
     d_cnt = [e.device_alloc(Bs * 4) for e in exs]  # per-frame keypoint counts of all K chunks (all-gathered)
+    host = None
+    if args.host_io:  # frames from pinned host memory, keypoints + descriptors back to pinned host memory
+        import torch
+
+        host = dict(frames=torch.from_numpy(frames).pin_memory(),
+                    kps=[torch.empty(Bc * cap * 28, dtype=torch.uint8).pin_memory() for _ in exs],
+                    desc=[torch.empty(Bc * cap * 32, dtype=torch.uint8).pin_memory() for _ in exs])
 
     def step():
         ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
         for r in range(K):
             for s_, e in enumerate(exs):
-                e.extract_batch_device(d_frames + (s_ * Bs + r * Bc) * fbytes, Bc, cols, rows, cols, fbytes)
+                off = (s_ * Bs + r * Bc) * fbytes
+                if host is not None:
+                    _lib.check(e.ctx, L.orbgpu_memcpy_h2d_async(e.ctx, C_.c_void_p(d_frames + off),
+                                                                C_.c_void_p(host["frames"].data_ptr() + off),
+                                                                Bc * fbytes), "h2d")
+                e.extract_batch_device(d_frames + off, Bc, cols, rows, cols, fbytes)
                 _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C_.c_void_p(d_cnt[s_] + 4 * r * Bc),
                                                             C_.c_void_p(outs[s_][2]), Bc * 4), "d2d")
                 _lib.check(e.ctx, L.orbgpu_prev_matched_from_frame(ex_ref.ctx, 0, e.ctx, C_.c_void_p(d_prev[s_])),
@@ -207,6 +219,11 @@ def setup_mono_init(args, env):
                                                                              C_.c_void_p(d_prev[s_]),
                                                                              C_.c_void_p(d_m12[s_]),
                                                                              C_.c_void_p(d_nm[s_])), "search_init")
+                if host is not None:  # mvKeys + mDescriptors of the chunk back to the host
+                    _lib.check(e.ctx, L.orbgpu_memcpy_d2h_async(e.ctx, C_.c_void_p(host["kps"][s_].data_ptr()),
+                                                                C_.c_void_p(outs[s_][0]), Bc * cap * 28), "d2h")
+                    _lib.check(e.ctx, L.orbgpu_memcpy_d2h_async(e.ctx, C_.c_void_p(host["desc"][s_].data_ptr()),
+                                                                C_.c_void_p(outs[s_][1]), Bc * cap * 32), "d2h")
 
     def post():  # the last chunk of every context
         counts = np.zeros(Bc, np.int32)
@@ -228,7 +245,8 @@ def setup_mono_init(args, env):
         exs[0].device_free(d_frames)
         ex_ref.device_free(d_f1)
 
-    return dict(metric=METRIC, exs=exs, step=step, post=post, free=free, Bs=Bc, per_stream=Bs, frames_per_step=B,
+    metric = METRIC if host is None else METRIC + " (PCIe-inclusive: frames H2D, keypoints + descriptors D2H)"
+    return dict(metric=metric, exs=exs, step=step, post=post, free=free, Bs=Bc, per_stream=Bs, frames_per_step=B,
                 counts=d_cnt,
                 workload=f"config 3: {cols}x{rows} mono, {NF} features, ORB extract + SearchForInitialization "
                          f"(window 100, ratio 0.9, checkOri) of every frame against an initial frame",
@@ -507,6 +525,9 @@ def main():
                          "stereo = config 4; tracking = config 5")
     ap.add_argument("--mappoints", type=int, default=5000, help="local-map points per camera (tracking)")
     ap.add_argument("--chunks", type=int, default=1, help="sequential launches per stream per step (mono_init)")
+    ap.add_argument("--host-io", action="store_true",
+                    help="mono_init: frames come from pinned host memory and keypoints/descriptors go back to it "
+                         "inside the timed step (the PCIe-inclusive rate; not the headline value)")
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--cols", type=int, default=None)
     ap.add_argument("--nfeatures", type=int, default=None)

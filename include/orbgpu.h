@@ -371,6 +371,9 @@ int orbgpu_device_free(orbgpu_ctx* ctx, void* p);
 int orbgpu_memcpy_h2d(orbgpu_ctx* ctx, void* dst, const void* src, size_t bytes);
 int orbgpu_memcpy_d2h(orbgpu_ctx* ctx, void* dst, const void* src, size_t bytes);
 int orbgpu_memset_d(orbgpu_ctx* ctx, void* dst, int value, size_t bytes);
+/* Asynchronous copies on the context stream (host memory should be pinned for the H2D/D2H forms to overlap). */
+int orbgpu_memcpy_h2d_async(orbgpu_ctx* ctx, void* dst, const void* src, size_t bytes);
+int orbgpu_memcpy_d2h_async(orbgpu_ctx* ctx, void* dst, const void* src, size_t bytes);
 /* Asynchronous device-to-device copy on the context stream. */
 int orbgpu_memcpy_d2d_async(orbgpu_ctx* ctx, void* dst, const void* src, size_t bytes);
 /* Total FAST candidates of the last batch (all frames, all levels); synchronises.  < 0 on error. */

@@ -31,7 +31,7 @@ EXPORTS = [
     "orbgpu_batch_outputs_undistorted", "orbgpu_search_by_projection_keyframe",
     "orbgpu_compute_stereo_from_rgbd", "orbgpu_compute_stereo_from_rgbd_batch",
     "orbgpu_vocabulary_load_text", "orbgpu_vocabulary_create", "orbgpu_vocabulary_destroy", "orbgpu_vocabulary_info",
-    "orbgpu_compute_bow", "orbgpu_compute_bow_batch",
+    "orbgpu_compute_bow", "orbgpu_compute_bow_batch", "orbgpu_memcpy_h2d_async", "orbgpu_memcpy_d2h_async",
 ]
 
 OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
@@ -109,6 +109,8 @@ def _declare(L):
     L.orbgpu_search_by_projection.argtypes = [vp, C.POINTER(FrameView), C.POINTER(MapPointsView), f32,
                                               f32, vp, vp, C.POINTER(i32)]
     L.orbgpu_search_by_projection_batch.argtypes = [vp, C.POINTER(MapPointsView), i32, f32, f32, vp, vp, vp, vp]
+    L.orbgpu_memcpy_h2d_async.argtypes = [vp, vp, vp, sz]
+    L.orbgpu_memcpy_d2h_async.argtypes = [vp, vp, vp, sz]
     L.orbgpu_stream.restype = vp
     L.orbgpu_stream.argtypes = [vp]
     L.orbgpu_synchronize.argtypes = [vp]

@@ -1771,6 +1771,18 @@ int orbgpu_memcpy_d2h(orbgpu_ctx* c, void* dst, const void* src, size_t bytes)
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return ORBGPU_OK;
 }
+int orbgpu_memcpy_h2d_async(orbgpu_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return ORBGPU_OK;
+}
+int orbgpu_memcpy_d2h_async(orbgpu_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    return ORBGPU_OK;
+}
 int orbgpu_memcpy_d2d_async(orbgpu_ctx* c, void* dst, const void* src, size_t bytes)
 {
     if (!c) return ORBGPU_ERR_ARG;
