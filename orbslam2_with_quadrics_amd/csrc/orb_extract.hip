@@ -177,6 +177,130 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
 }
 
 // ------------------------------------------------------------------------------------------------
+// k1': two chained pyramid levels per launch (A = level l from S = level l-1, then B = level l+1 from A).
+// One workgroup = one 16 x 256 tile of B.  The A rows/columns the tile reads are computed into LDS from the
+// staged S region (never re-read from HBM); the A pixels the tile OWNS are also stored.  Ownership of A
+// follows B's tiles through the source index of their first row/column (ytabB[y].x, xtabB[x].x, monotone):
+// tile [y0, y1) x [x0, x1) owns A rows [ytabB[y0].x, ytabB[y1].x) and columns [xtabB[x0].x, xtabB[x1].x),
+// the last tile of a row/column up to the level edge -- a partition of A, so every A pixel is stored once.
+// The arithmetic is og_resize_kernel's (cv::resize INTER_LINEAR, scalar fixed-point form).
+// ------------------------------------------------------------------------------------------------
+
+// 4 horizontally adjacent outputs of one row from two LDS source rows: sx = byte offsets in the rows, weights
+// (a0, a1) per column (a1 = 0 at the right border), vertical weights (yz, yw)
+__device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t* R1, const int* sx,
+                                               const og_rz_u16x2* wt, unsigned yz, unsigned yw)
+{
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t p0 = (uint32_t)R0[sx[k]] | ((uint32_t)R0[sx[k] + 1] << 16);
+        const uint32_t p1 = (uint32_t)R1[sx[k]] | ((uint32_t)R1[sx[k] + 1] << 16);
+        const uint32_t d0 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[k], 0u, false);
+        const uint32_t d1 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[k], 0u, false);
+        const uint32_t v = (__umul24(yz, d0) + __umul24(yw, d1) + (1u << 21)) >> 22;
+        packed |= min(v, 255u) << (8 * k);
+    }
+    return packed;
+}
+
+__device__ __forceinline__ void og_rz_weights(const int4* xtab, int xmax, int dx, int base, int* sx, og_rz_u16x2* wt,
+                                              int k)
+{
+    const int4 xt = xtab[dx];
+    sx[k] = xt.x - base;
+    wt[k] = dx < xmax ? og_rz_u16x2{(unsigned short)xt.y, (unsigned short)xt.z} : og_rz_u16x2{2048, 0};
+}
+
+__device__ __forceinline__ void og_rz_store4(uint8_t* Dr, uint32_t packed, int n)
+{
+    if (n == 4 && ((((uintptr_t)Dr) & 3) == 0)) {
+        *(uint32_t*)Dr = packed;
+    } else {
+        for (int k = 0; k < n; k++) Dr[k] = (uint8_t)(packed >> (8 * k));
+    }
+}
+
+__global__ __launch_bounds__(RZ_NT) void og_resize2_kernel(const uint8_t* __restrict__ src, long long src_pitch,
+                                                           long long src_fstride, uint8_t* __restrict__ dstA,
+                                                           long long pitchA, uint8_t* __restrict__ dstB,
+                                                           long long pitchB, long long dst_fstride, OgRz2Geom g,
+                                                           int* __restrict__ status)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t rz2_lds[];
+    uint8_t* S = rz2_lds;                          // [SR][SC] staged source rows (own misalignment each)
+    uint8_t* A = S + g.SR * g.SC;                  // [AR][AC] level-A region, column ac0 at byte 0
+    int* mis = (int*)(A + g.AR * g.AC);            // [SR]
+    const int f = blockIdx.z, tid = threadIdx.x;
+    const int by0 = blockIdx.y * RZ_TH, bx0 = blockIdx.x * RZ_TW;
+    const int nyB = min(RZ_TH, g.bh - by0), nxB = min(RZ_TW, g.bw - bx0);
+    // A region: what B's tile reads, plus the A pixels it owns
+    const int ar0 = g.ytabB[by0].x;
+    const int own_r1 = by0 + nyB == g.bh ? g.ah : g.ytabB[by0 + nyB].x;
+    const int ar1 = max(g.ytabB[by0 + nyB - 1].y, own_r1 - 1);
+    const int ac0 = g.xtabB[bx0].x;
+    const int own_c1 = bx0 + nxB == g.bw ? g.aw : g.xtabB[bx0 + nxB].x;
+    const int ac1 = max(min(g.xtabB[bx0 + nxB - 1].x + 1, g.aw - 1), own_c1 - 1);
+    // S region the A region reads
+    const int sr0 = g.ytabA[ar0].x, sr1 = g.ytabA[ar1].y;
+    const int sc0 = g.xtabA[ac0].x, sc1 = min(g.xtabA[ac1].x + 1, g.sw - 1);
+    const int nrS = sr1 - sr0 + 1, ncS = sc1 - sc0 + 1, nrA = ar1 - ar0 + 1, ncA = ac1 - ac0 + 1;
+    const int nch = (ncS + 15 + 15) >> 4;
+    if (nrS > g.SR || nch * 16 > g.SC - 16 || nrA > g.AR || ((ncA + 3) & ~3) > g.AC - 16) {  // host maxima
+        if (tid == 0) atomicOr(status, 8);
+        return;
+    }
+    const uint8_t* base = src + (long long)f * src_fstride;
+    for (int it = tid; it < nrS * nch; it += RZ_NT) {
+        const int r = it / nch, q = it - r * nch;
+        const uintptr_t a = (uintptr_t)(base + (long long)(sr0 + r) * src_pitch + sc0);
+        const uintptr_t a16 = a & ~(uintptr_t)15;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (a16 + 16 * q <= a + (uintptr_t)(ncS - 1)) v = *(const uint4*)(a16 + 16 * q);
+        *(uint4*)&S[r * g.SC + 16 * q] = v;
+        if (q == 0) mis[r] = (int)(a - a16);
+    }
+    __syncthreads();
+    // ---- level A region -> LDS (and the owned part -> HBM)
+    uint8_t* DA = dstA + (long long)f * dst_fstride;
+    const int nqA = (ncA + 3) >> 2;
+    for (int it = tid; it < nrA * nqA; it += RZ_NT) {
+        const int rr = it / nqA, q = it - rr * nqA;
+        const int r = ar0 + rr, c = ac0 + 4 * q;
+        int sx[4];
+        og_rz_u16x2 wt[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) og_rz_weights(g.xtabA, g.xmaxA, min(c + k, ac1), sc0, sx, wt, k);
+        const int4 yt = g.ytabA[r];
+        const int r0 = yt.x - sr0, r1 = yt.y - sr0;
+        const uint32_t packed = og_rz_quad(S + r0 * g.SC + mis[r0], S + r1 * g.SC + mis[r1], sx, wt, (unsigned)yt.z,
+                                           (unsigned)yt.w);
+        *(uint32_t*)&A[rr * g.AC + 4 * q] = packed;
+        if (r < own_r1 && c < own_c1) og_rz_store4(DA + (long long)r * pitchA + c, packed, min(4, own_c1 - c));
+    }
+    __syncthreads();
+    // ---- level B tile from the A region
+    const int cth = tid & 63, rg = tid >> 6;
+    const int dxt = bx0 + 4 * cth;
+    if (dxt >= g.bw) return;
+    int sx[4];
+    og_rz_u16x2 wt[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) og_rz_weights(g.xtabB, g.xmaxB, min(dxt + k, g.bw - 1), ac0, sx, wt, k);
+    const int n = min(4, g.bw - dxt);
+    uint8_t* DB = dstB + (long long)f * dst_fstride + dxt;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int r = 4 * rg + q;
+        if (r >= nyB) break;
+        const int4 yt = g.ytabB[by0 + r];
+        const uint32_t packed = og_rz_quad(A + (yt.x - ar0) * g.AC, A + (yt.y - ar0) * g.AC, sx, wt, (unsigned)yt.z,
+                                           (unsigned)yt.w);
+        og_rz_store4(DB + (long long)(by0 + r) * pitchB, packed, n);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // k2: FAST cells (src/ORBextractor.cc:789-829 + cv::FAST TYPE_9_16 with nonmax suppression)
 // ------------------------------------------------------------------------------------------------
 // M(p) = max over the 16 contiguous 9-arcs and both polarities of min |I(p) - I(arc)|; the pixel is a
@@ -1337,6 +1461,22 @@ void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, lo
     dim3 grid((dw + RZ_TW - 1) / RZ_TW, (dh + RZ_TH - 1) / RZ_TH, B);
     hipLaunchKernelGGL(og_resize_kernel, grid, dim3(RZ_NT), 0, s, src, src_pitch, src_fstride, dst, dst_pitch,
                        dst_fstride, sw, sh, dw, dh, xtab, ytab, xmax, status);
+}
+
+void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dstA,
+                       long long pitchA, uint8_t* dstB, long long pitchB, long long dst_fstride, const OgRz2Geom& g,
+                       int* status, int B)
+{
+    const size_t shm = (size_t)g.SR * g.SC + (size_t)g.AR * g.AC + 4 * (size_t)g.SR;
+    static bool lds_attr = false;
+    if (!lds_attr) {
+        (void)hipFuncSetAttribute((const void*)og_resize2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  64 * 1024);
+        lds_attr = true;
+    }
+    dim3 grid((g.bw + RZ_TW - 1) / RZ_TW, (g.bh + RZ_TH - 1) / RZ_TH, B);
+    hipLaunchKernelGGL(og_resize2_kernel, grid, dim3(RZ_NT), shm, s, src, src_pitch, src_fstride, dstA, pitchA, dstB,
+                       pitchB, dst_fstride, g, status);
 }
 
 void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,

@@ -321,6 +321,42 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
         pw = L.w;
         ph = L.h;
     }
+    // fused resize launches (levels l, l+1 for odd l): the largest S / A regions over the tiles of l+1, replaying
+    // og_resize2_kernel's region arithmetic on the host tables
+    for (int l = 1; l + 1 < P.nlevels; l += 2) {
+        OgLevel& A = P.lv[l];
+        const OgLevel& Bv = P.lv[l + 1];
+        const OgLevel& S = P.lv[l - 1];
+        const int4* xA = tabs.data() + A.xtab_off;
+        const int4* yA = tabs.data() + A.ytab_off;
+        const int4* xB = tabs.data() + Bv.xtab_off;
+        const int4* yB = tabs.data() + Bv.ytab_off;
+        int SR = 0, SC = 0, AR = 0, AC = 0;
+        for (int by0 = 0; by0 < Bv.h; by0 += 16)
+            for (int bx0 = 0; bx0 < Bv.w; bx0 += 256) {
+                const int nyB = std::min(16, Bv.h - by0), nxB = std::min(256, Bv.w - bx0);
+                const int ar0 = yB[by0].x;
+                const int own_r1 = by0 + nyB == Bv.h ? A.h : yB[by0 + nyB].x;
+                const int ar1 = std::max(yB[by0 + nyB - 1].y, own_r1 - 1);
+                const int ac0 = xB[bx0].x;
+                const int own_c1 = bx0 + nxB == Bv.w ? A.w : xB[bx0 + nxB].x;
+                const int ac1 = std::max(std::min(xB[bx0 + nxB - 1].x + 1, A.w - 1), own_c1 - 1);
+                const int sr0 = yA[ar0].x, sr1 = yA[ar1].y;
+                const int sc0 = xA[ac0].x, sc1 = std::min(xA[ac1].x + 1, S.w - 1);
+                SR = std::max(SR, sr1 - sr0 + 1);
+                SC = std::max(SC, ((sc1 - sc0 + 1 + 15 + 15) >> 4) * 16 + 16);
+                AR = std::max(AR, ar1 - ar0 + 1);
+                AC = std::max(AC, ((ac1 - ac0 + 1 + 3) & ~3) + 16);
+            }
+        A.fz_SR = SR;
+        A.fz_SC = SC;
+        A.fz_AR = AR;
+        A.fz_AC = AC;
+        if ((size_t)SR * SC + (size_t)AR * AC + 4 * (size_t)SR > 64 * 1024) {
+            c->err = "fused resize region exceeds the LDS budget";
+            return ORBGPU_ERR_UNSUPPORTED;
+        }
+    }
     P.total_cells = (int)cells.size();
     P.kcap_total = koff;
     P.frame_cap = koff;
@@ -395,14 +431,25 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
     HIP_TRY(c, hipMemsetAsync(c->cand_count.p, 0, sizeof(int) * (size_t)B * P.nlevels, s));
     HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(int) * 4, s));
     // k1: chained pyramid, src/ORBextractor.cc:1107-1132
-    for (int l = 1; l < P.nlevels; l++) {
+    // levels (1,2), (3,4), (5,6) in one launch each (og_resize2_kernel), a last odd level alone
+    for (int l = 1; l < P.nlevels;) {
         const OgLevel& L = P.lv[l];
         const OgLevel& Lp = P.lv[l - 1];
         const uint8_t* src = l == 1 ? d_imgs : c->pyr.p + Lp.pyr_off;
         const long long sp = l == 1 ? pitch : Lp.pitch;
         const long long sfs = l == 1 ? fstride : P.pyr_per_frame;
-        og_launch_resize(s, src, sp, sfs, c->pyr.p + L.pyr_off, L.pitch, P.pyr_per_frame, Lp.w, Lp.h, L.w, L.h,
-                         c->tabs.p + L.xtab_off, c->tabs.p + L.ytab_off, L.xmax, c->status.p, B);
+        if (l + 1 < P.nlevels) {
+            const OgLevel& Ln = P.lv[l + 1];
+            OgRz2Geom g{Lp.w, Lp.h, L.w, L.h, Ln.w, Ln.h, c->tabs.p + L.xtab_off, c->tabs.p + L.ytab_off, L.xmax,
+                        c->tabs.p + Ln.xtab_off, c->tabs.p + Ln.ytab_off, Ln.xmax, L.fz_SR, L.fz_SC, L.fz_AR, L.fz_AC};
+            og_launch_resize2(s, src, sp, sfs, c->pyr.p + L.pyr_off, L.pitch, c->pyr.p + Ln.pyr_off, Ln.pitch,
+                              P.pyr_per_frame, g, c->status.p, B);
+            l += 2;
+        } else {
+            og_launch_resize(s, src, sp, sfs, c->pyr.p + L.pyr_off, L.pitch, P.pyr_per_frame, Lp.w, Lp.h, L.w, L.h,
+                             c->tabs.p + L.xtab_off, c->tabs.p + L.ytab_off, L.xmax, c->status.p, B);
+            l += 1;
+        }
     }
     timer_mark(c, "pyramid");
     og_launch_fast(s, P, c->cells.p, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p, c->status.p, B);

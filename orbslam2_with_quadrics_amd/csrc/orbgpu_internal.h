@@ -40,6 +40,8 @@ struct OgLevel {
     int cand_cap;
     // resize tables (levels >= 1), src/ORBextractor.cc:1120 -> cv::resize INTER_LINEAR
     int xtab_off, ytab_off, xmax;
+    // level l fused with level l+1 in one launch (og_resize2_kernel): LDS capacities over all tiles of l+1
+    int fz_SR, fz_SC, fz_AR, fz_AC;
     float scale;           // mvScaleFactor[l]
     int patch_size;        // (int)(PATCH_SIZE * mvScaleFactor[l])
 };

@@ -16,6 +16,20 @@ struct OgGridGeom {
 
 hipError_t og_upload_pattern(int device);
 
+// two chained levels per launch (og_resize2_kernel): A = level l from S = level l-1, B = level l+1 from A
+struct OgRz2Geom {
+    int sw, sh, aw, ah, bw, bh;
+    const int4* xtabA;
+    const int4* ytabA;
+    int xmaxA;
+    const int4* xtabB;
+    const int4* ytabB;
+    int xmaxB;
+    int SR, SC, AR, AC;  // LDS capacities: staged S rows x row stride, A rows x row stride (host-computed maxima)
+};
+void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dstA,
+                       long long pitchA, uint8_t* dstB, long long pitchB, long long dst_fstride, const OgRz2Geom& g,
+                       int* status, int B);
 void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,
                       long long dst_pitch, long long dst_fstride, int sw, int sh, int dw, int dh, const int4* xtab,
                       const int4* ytab, int xmax, int* status, int B);
