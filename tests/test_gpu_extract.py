@@ -160,3 +160,47 @@ def test_two_contexts_interleaved(gpu, oracle):
     oe = oracle.OracleExtractor(2000)
     assert_same(*out["L"], *oe(L))
     assert_same(*out["R"], *oe(R))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_parameters_vs_oracle(gpu, oracle, seed):
+    """Randomised extractor parameters and image shapes (scale factor up to the 1.6 the fused pyramid's LDS is
+    sized for, 1-8 levels, thresholds, odd widths and pitches): keypoints, descriptors and the whole pyramid
+    bit-exact.  Configurations the reference itself cannot run (a level narrower than one FAST cell, or zero
+    initial octree nodes) and levels of more than 1016 features must be rejected with ORBGPU_ERR_UNSUPPORTED."""
+    rng = np.random.default_rng(1000 + seed)
+    rows, cols = int(rng.integers(120, 1100)), int(rng.integers(160, 1300))
+    scale = float(np.float32(rng.uniform(1.05, 1.6)))
+    nlevels = int(rng.integers(1, 9))
+    # level 0 takes nf * (1 - 1/s) / (1 - s^-L) features (src/ORBextractor.cc:435-446): stay within 1000 of them
+    f = 1.0 / scale
+    share0 = (1 - f) / (1 - f ** nlevels) if nlevels > 1 else 1.0
+    nf = int(rng.integers(100, max(101, int(1000 / share0))))
+    ini = int(rng.integers(8, 40))
+    mn = int(rng.integers(3, ini))
+    img = synthetic.frame(300 + seed, rows, cols)
+    if seed % 3 == 0:  # a wider pitch than the width (a view into a larger image)
+        big = np.zeros((rows, cols + 13), np.uint8)
+        big[:, :cols] = img
+        img = big[:, :cols]
+    try:
+        ex = gpu.ORBextractor(nf, scale, nlevels, ini, mn)
+        k, d = ex(img)
+    except RuntimeError as e:
+        # the reference's own impossibilities, or more than 1016 features on one level (the LDS octree's list
+        # capacity, DESIGN.md §8): reported, never silently wrong
+        assert "FAST cell" in str(e) or "initial octree" in str(e) or "octree capacity" in str(e), str(e)
+        return
+    oe = oracle.OracleExtractor(nf, scale, nlevels, ini, mn)
+    ko, do = oe(np.ascontiguousarray(img))
+    assert_same(k, d, ko, do)
+    for lvl in range(nlevels):
+        assert np.array_equal(ex.level(lvl), oe.level(lvl)), (lvl, rows, cols, scale, nlevels)
+
+
+def test_level_capacity_is_reported(gpu):
+    """More than 1016 features on one level exceeds the LDS octree list: ORBGPU_ERR_UNSUPPORTED with a message,
+    never a silently different keypoint set."""
+    ex = gpu.ORBextractor(5000, 1.2, 8, 20, 7)  # level 0 budget 1085
+    with pytest.raises(RuntimeError, match="octree capacity"):
+        ex(synthetic.frame(3, 480, 640))
