@@ -56,6 +56,7 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
 {
     __shared__ __attribute__((aligned(16))) uint8_t S[RZ_SROWS * RZ_SC];
     __shared__ int mis[RZ_SROWS];
+    __shared__ int4 YT[RZ_TH];  // ytab rows of the tile (read once, not once per row by every thread)
     const int f = blockIdx.z, tid = threadIdx.x;
     const int dy0 = blockIdx.y * RZ_TH, dx0 = blockIdx.x * RZ_TW;
     const int ny = min(RZ_TH, dh - dy0), nx = min(RZ_TW, dw - dx0);
@@ -70,6 +71,7 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
         return;
     }
     {
+        if (tid < ny) YT[tid] = ytab[dy0 + tid];
         uint4 buf[4];
         const int q = tid & 31;
 #pragma unroll
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
         for (int rr = 0; rr < 4; rr++) {
             const int r = 4 * rg + rr;
             if (r >= ny) break;
-            const int4 yt = ytab[dy0 + r];
+            const int4 yt = YT[r];
             const uint32_t* R0 = (const uint32_t*)(S + (yt.x - sy0) * RZ_SC);
             const uint32_t* R1 = (const uint32_t*)(S + (yt.y - sy0) * RZ_SC);
             uint32_t packed = 0;
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
     for (int rr = 0; rr < 4; rr++) {
         const int r = 4 * rg + rr;
         if (r >= ny) break;
-        const int4 yt = ytab[dy0 + r];
+        const int4 yt = YT[r];
         const int r0 = yt.x - sy0, r1 = yt.y - sy0;
         const uint8_t* R0 = S + r0 * RZ_SC + mis[r0];
         const uint8_t* R1 = S + r1 * RZ_SC + mis[r1];
@@ -212,6 +214,10 @@ __device__ __forceinline__ void og_rz_weights(const int4* xtab, int xmax, int dx
     wt[k] = dx < xmax ? og_rz_u16x2{(unsigned short)xt.y, (unsigned short)xt.z} : og_rz_u16x2{2048, 0};
 }
 
+#ifndef RZ2_U
+#define RZ2_U 3
+#endif
+
 __device__ __forceinline__ void og_rz_store4(uint8_t* Dr, uint32_t packed, int n)
 {
     if (n == 4 && ((((uintptr_t)Dr) & 3) == 0)) {
@@ -228,73 +234,104 @@ __global__ __launch_bounds__(RZ_NT) void og_resize2_kernel(const uint8_t* __rest
                                                            int* __restrict__ status)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t rz2_lds[];
-    uint8_t* S = rz2_lds;                          // [SR][SC] staged source rows (own misalignment each)
+    // LDS layout (og_rz2_lds_bytes): the tile's rows of both y tables, then S, A and the row misalignments
+    int4* YA = (int4*)rz2_lds;                     // [AR]  ytabA[ar0 + i]
+    int4* YB = YA + g.AR;                          // [16]  ytabB[by0 + i]
+    uint8_t* S = (uint8_t*)(YB + RZ_TH);           // [SR][SC] staged source rows (own misalignment each)
     uint8_t* A = S + g.SR * g.SC;                  // [AR][AC] level-A region, column ac0 at byte 0
     int* mis = (int*)(A + g.AR * g.AC);            // [SR]
     const int f = blockIdx.z, tid = threadIdx.x;
     const int by0 = blockIdx.y * RZ_TH, bx0 = blockIdx.x * RZ_TW;
-    const int nyB = min(RZ_TH, g.bh - by0), nxB = min(RZ_TW, g.bw - bx0);
-    // A region: what B's tile reads, plus the A pixels it owns
-    const int ar0 = g.ytabB[by0].x;
-    const int own_r1 = by0 + nyB == g.bh ? g.ah : g.ytabB[by0 + nyB].x;
-    const int ar1 = max(g.ytabB[by0 + nyB - 1].y, own_r1 - 1);
-    const int ac0 = g.xtabB[bx0].x;
-    const int own_c1 = bx0 + nxB == g.bw ? g.aw : g.xtabB[bx0 + nxB].x;
-    const int ac1 = max(min(g.xtabB[bx0 + nxB - 1].x + 1, g.aw - 1), own_c1 - 1);
-    // S region the A region reads
-    const int sr0 = g.ytabA[ar0].x, sr1 = g.ytabA[ar1].y;
-    const int sc0 = g.xtabA[ac0].x, sc1 = min(g.xtabA[ac1].x + 1, g.sw - 1);
+    const int nyB = min(RZ_TH, g.bh - by0);
+    // A region (what B's tile reads, plus the A pixels it owns) and the S region it reads: replayed on the host
+    // from the tables (orbgpu_capi.cpp), one load instead of a chain of dependent table lookups
+    const int4* T = g.tiles + 3 * (blockIdx.y * gridDim.x + blockIdx.x);
+    const int4 t0 = T[0], t1 = T[1], t2 = T[2];
+    const int ar0 = t0.x, ar1 = t0.y, own_r1 = t0.z, ac0 = t0.w;
+    const int ac1 = t1.x, own_c1 = t1.y, sr0 = t1.z, sr1 = t1.w;
+    const int sc0 = t2.x, sc1 = t2.y;
     const int nrS = sr1 - sr0 + 1, ncS = sc1 - sc0 + 1, nrA = ar1 - ar0 + 1, ncA = ac1 - ac0 + 1;
     const int nch = (ncS + 15 + 15) >> 4;
-    if (nrS > g.SR || nch * 16 > g.SC - 16 || nrA > g.AR || ((ncA + 3) & ~3) > g.AC - 16) {  // host maxima
+    if (nrS > g.SR || nch * 16 > g.SC - 16 || nrA > g.AR || ((ncA + 3) & ~3) > g.AC - 16 || nrA > RZ_NT ||
+        ncA > 4 * RZ_NT) {  // host maxima; one thread per A row / column quad
         if (tid == 0) atomicOr(status, 8);
         return;
     }
+    // the A pass's x weights, loaded before the staging so that they are in flight with it.  A pass: thread =
+    // one fixed column quad (qa) x every G-th row of the region; B pass: column quad cth, 4 rows.
+    const int nqA = (ncA + 3) >> 2;                // <= RZ_NT (checked above)
+    const int G = RZ_NT / nqA;
+    const int qa = tid % nqA, rga = tid / nqA;
+    const int cA = ac0 + 4 * qa;
+    int sxA[4], sxB[4];
+    og_rz_u16x2 wtA[4], wtB[4];
+    const int cth = tid & 63, rg = tid >> 6;
+    const int dxt = bx0 + 4 * cth;
+#pragma unroll
+    for (int k = 0; k < 4; k++) og_rz_weights(g.xtabA, g.xmaxA, min(cA + k, ac1), sc0, sxA, wtA, k);
     const uint8_t* base = src + (long long)f * src_fstride;
-    for (int it = tid; it < nrS * nch; it += RZ_NT) {
-        const int r = it / nch, q = it - r * nch;
-        const uintptr_t a = (uintptr_t)(base + (long long)(sr0 + r) * src_pitch + sc0);
-        const uintptr_t a16 = a & ~(uintptr_t)15;
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (a16 + 16 * q <= a + (uintptr_t)(ncS - 1)) v = *(const uint4*)(a16 + 16 * q);
-        *(uint4*)&S[r * g.SC + 16 * q] = v;
-        if (q == 0) mis[r] = (int)(a - a16);
+    // RZ2_U chunks per thread per round, all loads issued before the first LDS store; the y-table rows of the
+    // tile ride along (each pass below reads its vertical weights from LDS, not from a global load per row)
+    const int nIt = nrS * nch;
+    const int4 ya = tid < nrA ? g.ytabA[ar0 + tid] : make_int4(0, 0, 0, 0);
+    const int4 yb = tid < nyB ? g.ytabB[by0 + tid] : make_int4(0, 0, 0, 0);
+    for (int it0 = tid; it0 < nIt; it0 += RZ_NT * RZ2_U) {
+        uint4 v[RZ2_U];
+#pragma unroll
+        for (int u = 0; u < RZ2_U; u++) {
+            const int it = it0 + u * RZ_NT;
+            v[u] = make_uint4(0u, 0u, 0u, 0u);
+            if (it < nIt) {
+                const int r = it / nch, q = it - r * nch;
+                const uintptr_t a = (uintptr_t)(base + (long long)(sr0 + r) * src_pitch + sc0);
+                const uintptr_t a16 = a & ~(uintptr_t)15;
+                if (a16 + 16 * q <= a + (uintptr_t)(ncS - 1)) v[u] = *(const uint4*)(a16 + 16 * q);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < RZ2_U; u++) {
+            const int it = it0 + u * RZ_NT;
+            if (it < nIt) {
+                const int r = it / nch, q = it - r * nch;
+                *(uint4*)&S[r * g.SC + 16 * q] = v[u];
+                if (q == 0) {
+                    const uintptr_t a = (uintptr_t)(base + (long long)(sr0 + r) * src_pitch + sc0);
+                    mis[r] = (int)(a & 15);
+                }
+            }
+        }
     }
+    if (tid < nrA) YA[tid] = ya;
+    if (tid < nyB) YB[tid] = yb;
     __syncthreads();
     // ---- level A region -> LDS (and the owned part -> HBM)
     uint8_t* DA = dstA + (long long)f * dst_fstride;
-    const int nqA = (ncA + 3) >> 2;
-    for (int it = tid; it < nrA * nqA; it += RZ_NT) {
-        const int rr = it / nqA, q = it - rr * nqA;
-        const int r = ar0 + rr, c = ac0 + 4 * q;
-        int sx[4];
-        og_rz_u16x2 wt[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) og_rz_weights(g.xtabA, g.xmaxA, min(c + k, ac1), sc0, sx, wt, k);
-        const int4 yt = g.ytabA[r];
-        const int r0 = yt.x - sr0, r1 = yt.y - sr0;
-        const uint32_t packed = og_rz_quad(S + r0 * g.SC + mis[r0], S + r1 * g.SC + mis[r1], sx, wt, (unsigned)yt.z,
-                                           (unsigned)yt.w);
-        *(uint32_t*)&A[rr * g.AC + 4 * q] = packed;
-        if (r < own_r1 && c < own_c1) og_rz_store4(DA + (long long)r * pitchA + c, packed, min(4, own_c1 - c));
+    if (rga < G) {
+        const bool own_c = cA < own_c1;
+        const int nown = min(4, own_c1 - cA);
+        for (int rr = rga; rr < nrA; rr += G) {
+            const int4 yt = YA[rr];
+            const int r = ar0 + rr;
+            const int r0 = yt.x - sr0, r1 = yt.y - sr0;
+            const uint32_t packed = og_rz_quad(S + r0 * g.SC + mis[r0], S + r1 * g.SC + mis[r1], sxA, wtA,
+                                               (unsigned)yt.z, (unsigned)yt.w);
+            *(uint32_t*)&A[rr * g.AC + 4 * qa] = packed;
+            if (r < own_r1 && own_c) og_rz_store4(DA + (long long)r * pitchA + cA, packed, nown);
+        }
     }
     __syncthreads();
     // ---- level B tile from the A region
-    const int cth = tid & 63, rg = tid >> 6;
-    const int dxt = bx0 + 4 * cth;
     if (dxt >= g.bw) return;
-    int sx[4];
-    og_rz_u16x2 wt[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) og_rz_weights(g.xtabB, g.xmaxB, min(dxt + k, g.bw - 1), ac0, sx, wt, k);
+    for (int k = 0; k < 4; k++) og_rz_weights(g.xtabB, g.xmaxB, min(dxt + k, g.bw - 1), ac0, sxB, wtB, k);
     const int n = min(4, g.bw - dxt);
     uint8_t* DB = dstB + (long long)f * dst_fstride + dxt;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int r = 4 * rg + q;
         if (r >= nyB) break;
-        const int4 yt = g.ytabB[by0 + r];
-        const uint32_t packed = og_rz_quad(A + (yt.x - ar0) * g.AC, A + (yt.y - ar0) * g.AC, sx, wt, (unsigned)yt.z,
+        const int4 yt = YB[r];
+        const uint32_t packed = og_rz_quad(A + (yt.x - ar0) * g.AC, A + (yt.y - ar0) * g.AC, sxB, wtB, (unsigned)yt.z,
                                            (unsigned)yt.w);
         og_rz_store4(DB + (long long)(by0 + r) * pitchB, packed, n);
     }
@@ -393,6 +430,7 @@ __device__ __forceinline__ uint2 og_fast_quick2(const uint32_t* p, int st, og_u1
 #ifndef OG_EXP_FAST_STOP
 #define OG_EXP_FAST_STOP 0
 #endif
+
 
 // ------------------------------------------------------------------------------------------------
 // k2': FAST over blocks of up to 2x2 cells.  The cells' detection areas tile a level without overlap
@@ -1151,6 +1189,25 @@ __device__ __forceinline__ int og_reflect101(int i, int n)
 #define HP_ROWS 22  // row pairs of the horizontal pass (43 rows -> 22 pairs)
 #define HP_S 40     // pair-row stride in dwords (10 groups of 4 columns)
 
+#ifndef OG_DK_BLOCKSYNC
+#define OG_DK_BLOCKSYNC 0
+#endif
+// The describe kernel's waves share no LDS: each wave owns its raw/blurred windows.  A wave only has to see
+// its own LDS writes before it reads them back, so it synchronises with itself (LDS counter drained, no
+// reordering across the point) instead of with the other waves of the workgroup; a wave that finished its
+// loads does not wait for a neighbour's global loads.
+__device__ __forceinline__ void og_dk_sync()
+{
+#if OG_DK_BLOCKSYNC
+    __syncthreads();
+#else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores have landed
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+}
+
 __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, const uint8_t* __restrict__ img0,
                                                                     long long pitch0, long long fstride0,
                                                                     const uint8_t* __restrict__ pyr,
@@ -1239,7 +1296,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             }
         }
     }
-    __syncthreads();
+    og_dk_sync();
     const uint8_t* Rb = R;  // Rb[r * RAW_S + c] = window pixel (r, c)
     // ---- IC_Angle on the unblurred level (:77-104); integer moments are order-independent
     int m01 = 0, m10 = 0;
@@ -1293,7 +1350,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             *(uint4*)&Hp[rp * HP_S + 4 * g] = o;
         }
     }
-    __syncthreads();
+    og_dk_sync();
     // vertical: item = (column c, 4 output rows 4m..4m+3) from row pairs 2m..2m+4; even rows take taps
     // (g0,g1)(g2,g3)(g4,g5)(g6,0), odd rows (0,g0)(g1,g2)(g3,g4)(g5,g6)
     if (active) {
@@ -1322,7 +1379,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             }
         }
     }
-    __syncthreads();
+    og_dk_sync();
     if (!active) return;
     // ---- rBRIEF (:108-147)
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
@@ -1467,7 +1524,7 @@ void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, l
                        long long pitchA, uint8_t* dstB, long long pitchB, long long dst_fstride, const OgRz2Geom& g,
                        int* status, int B)
 {
-    const size_t shm = (size_t)g.SR * g.SC + (size_t)g.AR * g.AC + 4 * (size_t)g.SR;
+    const size_t shm = og_rz2_lds_bytes(g.SR, g.SC, g.AR, g.AC);
     static bool lds_attr = false;
     if (!lds_attr) {
         (void)hipFuncSetAttribute((const void*)og_resize2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

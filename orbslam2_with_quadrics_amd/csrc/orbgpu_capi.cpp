@@ -332,6 +332,7 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
         const int4* xB = tabs.data() + Bv.xtab_off;
         const int4* yB = tabs.data() + Bv.ytab_off;
         int SR = 0, SC = 0, AR = 0, AC = 0;
+        std::vector<int4> tt;  // per tile of B: the region bounds og_resize2_kernel reads (3 int4, row-major tiles)
         for (int by0 = 0; by0 < Bv.h; by0 += 16)
             for (int bx0 = 0; bx0 < Bv.w; bx0 += 256) {
                 const int nyB = std::min(16, Bv.h - by0), nxB = std::min(256, Bv.w - bx0);
@@ -347,12 +348,17 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
                 SC = std::max(SC, ((sc1 - sc0 + 1 + 15 + 15) >> 4) * 16 + 16);
                 AR = std::max(AR, ar1 - ar0 + 1);
                 AC = std::max(AC, ((ac1 - ac0 + 1 + 3) & ~3) + 16);
+                tt.push_back(make_int4(ar0, ar1, own_r1, ac0));
+                tt.push_back(make_int4(ac1, own_c1, sr0, sr1));
+                tt.push_back(make_int4(sc0, sc1, 0, 0));
             }
+        A.fz_tile_off = (int)tabs.size();  // xA.. are not used past this point: the append may reallocate
+        tabs.insert(tabs.end(), tt.begin(), tt.end());
         A.fz_SR = SR;
         A.fz_SC = SC;
         A.fz_AR = AR;
         A.fz_AC = AC;
-        if ((size_t)SR * SC + (size_t)AR * AC + 4 * (size_t)SR > 64 * 1024) {
+        if (og_rz2_lds_bytes(SR, SC, AR, AC) > 64 * 1024) {
             c->err = "fused resize region exceeds the LDS budget";
             return ORBGPU_ERR_UNSUPPORTED;
         }
@@ -441,7 +447,8 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
         if (l + 1 < P.nlevels) {
             const OgLevel& Ln = P.lv[l + 1];
             OgRz2Geom g{Lp.w, Lp.h, L.w, L.h, Ln.w, Ln.h, c->tabs.p + L.xtab_off, c->tabs.p + L.ytab_off, L.xmax,
-                        c->tabs.p + Ln.xtab_off, c->tabs.p + Ln.ytab_off, Ln.xmax, L.fz_SR, L.fz_SC, L.fz_AR, L.fz_AC};
+                        c->tabs.p + Ln.xtab_off, c->tabs.p + Ln.ytab_off, Ln.xmax, L.fz_SR, L.fz_SC, L.fz_AR, L.fz_AC,
+                        c->tabs.p + L.fz_tile_off};
             og_launch_resize2(s, src, sp, sfs, c->pyr.p + L.pyr_off, L.pitch, c->pyr.p + Ln.pyr_off, Ln.pitch,
                               P.pyr_per_frame, g, c->status.p, B);
             l += 2;

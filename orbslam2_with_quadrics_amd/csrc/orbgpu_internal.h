@@ -42,6 +42,7 @@ struct OgLevel {
     int xtab_off, ytab_off, xmax;
     // level l fused with level l+1 in one launch (og_resize2_kernel): LDS capacities over all tiles of l+1
     int fz_SR, fz_SC, fz_AR, fz_AC;
+    int fz_tile_off;       // per-tile region bounds of that launch (3 int4 per tile of l+1, in the resize tables)
     float scale;           // mvScaleFactor[l]
     int patch_size;        // (int)(PATCH_SIZE * mvScaleFactor[l])
 };

@@ -26,7 +26,13 @@ struct OgRz2Geom {
     const int4* ytabB;
     int xmaxB;
     int SR, SC, AR, AC;  // LDS capacities: staged S rows x row stride, A rows x row stride (host-computed maxima)
+    const int4* tiles;   // per tile (row-major over B's 16 x 256 tiles): {ar0, ar1, own_r1, ac0}, {ac1, own_c1, sr0, sr1}, {sc0, sc1}
 };
+// dynamic LDS of og_resize2_kernel: y-table rows of the tile (AR + 16 int4), S, A, row misalignments
+static inline size_t og_rz2_lds_bytes(int SR, int SC, int AR, int AC)
+{
+    return 16 * ((size_t)AR + 16) + (size_t)SR * SC + (size_t)AR * AC + 4 * (size_t)SR;
+}
 void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dstA,
                        long long pitchA, uint8_t* dstB, long long pitchB, long long dst_fstride, const OgRz2Geom& g,
                        int* status, int B);
