@@ -227,7 +227,7 @@ __device__ __forceinline__ void og_rz_store4(uint8_t* Dr, uint32_t packed, int n
     }
 }
 
-__global__ __launch_bounds__(RZ_NT) void og_resize2_kernel(const uint8_t* __restrict__ src, long long src_pitch,
+__global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __restrict__ src, long long src_pitch,
                                                            long long src_fstride, uint8_t* __restrict__ dstA,
                                                            long long pitchA, uint8_t* __restrict__ dstB,
                                                            long long pitchB, long long dst_fstride, OgRz2Geom g,
@@ -236,13 +236,13 @@ __global__ __launch_bounds__(RZ_NT) void og_resize2_kernel(const uint8_t* __rest
     extern __shared__ __attribute__((aligned(16))) uint8_t rz2_lds[];
     // LDS layout (og_rz2_lds_bytes): the tile's rows of both y tables, then S, A and the row misalignments
     int4* YA = (int4*)rz2_lds;                     // [AR]  ytabA[ar0 + i]
-    int4* YB = YA + g.AR;                          // [16]  ytabB[by0 + i]
-    uint8_t* S = (uint8_t*)(YB + RZ_TH);           // [SR][SC] staged source rows (own misalignment each)
+    int4* YB = YA + g.AR;                          // [RZ2_TH]  ytabB[by0 + i]
+    uint8_t* S = (uint8_t*)(YB + RZ2_TH);           // [SR][SC] staged source rows (own misalignment each)
     uint8_t* A = S + g.SR * g.SC;                  // [AR][AC] level-A region, column ac0 at byte 0
     int* mis = (int*)(A + g.AR * g.AC);            // [SR]
     const int f = blockIdx.z, tid = threadIdx.x;
-    const int by0 = blockIdx.y * RZ_TH, bx0 = blockIdx.x * RZ_TW;
-    const int nyB = min(RZ_TH, g.bh - by0);
+    const int by0 = blockIdx.y * RZ2_TH, bx0 = blockIdx.x * RZ_TW;
+    const int nyB = min(RZ2_TH, g.bh - by0);
     // A region (what B's tile reads, plus the A pixels it owns) and the S region it reads: replayed on the host
     // from the tables (orbgpu_capi.cpp), one load instead of a chain of dependent table lookups
     const int4* T = g.tiles + 3 * (blockIdx.y * gridDim.x + blockIdx.x);
@@ -252,15 +252,15 @@ __global__ __launch_bounds__(RZ_NT) void og_resize2_kernel(const uint8_t* __rest
     const int sc0 = t2.x, sc1 = t2.y;
     const int nrS = sr1 - sr0 + 1, ncS = sc1 - sc0 + 1, nrA = ar1 - ar0 + 1, ncA = ac1 - ac0 + 1;
     const int nch = (ncS + 15 + 15) >> 4;
-    if (nrS > g.SR || nch * 16 > g.SC - 16 || nrA > g.AR || ((ncA + 3) & ~3) > g.AC - 16 || nrA > RZ_NT ||
-        ncA > 4 * RZ_NT) {  // host maxima; one thread per A row / column quad
+    if (nrS > g.SR || nch * 16 > g.SC - 16 || nrA > g.AR || ((ncA + 3) & ~3) > g.AC - 16 || nrA > RZ2_NT ||
+        ncA > 4 * RZ2_NT) {  // host maxima; one thread per A row / column quad
         if (tid == 0) atomicOr(status, 8);
         return;
     }
     // the A pass's x weights, loaded before the staging so that they are in flight with it.  A pass: thread =
     // one fixed column quad (qa) x every G-th row of the region; B pass: column quad cth, 4 rows.
-    const int nqA = (ncA + 3) >> 2;                // <= RZ_NT (checked above)
-    const int G = RZ_NT / nqA;
+    const int nqA = (ncA + 3) >> 2;                // <= RZ2_NT (checked above)
+    const int G = RZ2_NT / nqA;
     const int qa = tid % nqA, rga = tid / nqA;
     const int cA = ac0 + 4 * qa;
     int sxA[4], sxB[4];
@@ -275,11 +275,11 @@ __global__ __launch_bounds__(RZ_NT) void og_resize2_kernel(const uint8_t* __rest
     const int nIt = nrS * nch;
     const int4 ya = tid < nrA ? g.ytabA[ar0 + tid] : make_int4(0, 0, 0, 0);
     const int4 yb = tid < nyB ? g.ytabB[by0 + tid] : make_int4(0, 0, 0, 0);
-    for (int it0 = tid; it0 < nIt; it0 += RZ_NT * RZ2_U) {
+    for (int it0 = tid; it0 < nIt; it0 += RZ2_NT * RZ2_U) {
         uint4 v[RZ2_U];
 #pragma unroll
         for (int u = 0; u < RZ2_U; u++) {
-            const int it = it0 + u * RZ_NT;
+            const int it = it0 + u * RZ2_NT;
             v[u] = make_uint4(0u, 0u, 0u, 0u);
             if (it < nIt) {
                 const int r = it / nch, q = it - r * nch;
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(RZ_NT) void og_resize2_kernel(const uint8_t* __rest
         }
 #pragma unroll
         for (int u = 0; u < RZ2_U; u++) {
-            const int it = it0 + u * RZ_NT;
+            const int it = it0 + u * RZ2_NT;
             if (it < nIt) {
                 const int r = it / nch, q = it - r * nch;
                 *(uint4*)&S[r * g.SC + 16 * q] = v[u];
@@ -1189,6 +1189,25 @@ __device__ __forceinline__ int og_reflect101(int i, int n)
 #define HP_ROWS 22  // row pairs of the horizontal pass (43 rows -> 22 pairs)
 #define HP_S 40     // pair-row stride in dwords (10 groups of 4 columns)
 
+// IC_Angle's disk (src/ORBextractor.cc:77-104) as a flat list of the (u, v) points with v >= 1: each pair of
+// points (u, +-v) is one lane's item, so a wave covers the 359 pairs in 6 full iterations instead of 15 row
+// iterations with 2 * umax[v] + 1 of 64 lanes active.  umax depends only on HALF_PATCH_SIZE = 15 (:454-469); the
+// host checks that its table equals OG_UMAX (orbgpu_create).  Padding items are (0, 0): they add nothing.
+#define OG_DISK_ITEMS 384
+struct OgDisk {
+    short e[OG_DISK_ITEMS];  // (u & 0xff) | v << 8
+};
+constexpr OgDisk og_make_disk()
+{
+    OgDisk d{};
+    constexpr int umax[16] = {OG_UMAX};
+    int k = 0;
+    for (int v = 1; v <= 15; v++)
+        for (int u = -umax[v]; u <= umax[v]; u++) d.e[k++] = (short)((u & 0xff) | (v << 8));
+    return d;
+}
+__constant__ OgDisk og_disk = og_make_disk();
+
 #ifndef OG_DK_BLOCKSYNC
 #define OG_DK_BLOCKSYNC 0
 #endif
@@ -1303,14 +1322,15 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     if (active) {
         const uint8_t* ctr = Rb + 21 * RAW_S + 21;
         if (lane < 31) m10 += (lane - 15) * ctr[lane - 15];
-        for (int v = 1; v <= OG_HALF_PATCH; v++) {
-            const int d = P.umax[v];
-            const int u = lane - d;
-            if (u <= d) {
-                const int vp = ctr[u + v * RAW_S], vm = ctr[u - v * RAW_S];
-                m01 += v * (vp - vm);
-                m10 += u * (vp + vm);
-            }
+        short e[OG_DISK_ITEMS / 64];
+#pragma unroll
+        for (int it = 0; it < OG_DISK_ITEMS / 64; it++) e[it] = og_disk.e[lane + 64 * it];
+#pragma unroll
+        for (int it = 0; it < OG_DISK_ITEMS / 64; it++) {
+            const int u = (int)(signed char)(e[it] & 0xff), v = e[it] >> 8;
+            const int vp = ctr[u + v * RAW_S], vm = ctr[u - v * RAW_S];
+            m01 += v * (vp - vm);
+            m10 += u * (vp + vm);
         }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
@@ -1531,8 +1551,8 @@ void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, l
                                   64 * 1024);
         lds_attr = true;
     }
-    dim3 grid((g.bw + RZ_TW - 1) / RZ_TW, (g.bh + RZ_TH - 1) / RZ_TH, B);
-    hipLaunchKernelGGL(og_resize2_kernel, grid, dim3(RZ_NT), shm, s, src, src_pitch, src_fstride, dstA, pitchA, dstB,
+    dim3 grid((g.bw + RZ_TW - 1) / RZ_TW, (g.bh + RZ2_TH - 1) / RZ2_TH, B);
+    hipLaunchKernelGGL(og_resize2_kernel, grid, dim3(RZ2_NT), shm, s, src, src_pitch, src_fstride, dstA, pitchA, dstB,
                        pitchB, dst_fstride, g, status);
 }
 

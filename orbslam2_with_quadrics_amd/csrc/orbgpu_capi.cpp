@@ -333,9 +333,9 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
         const int4* yB = tabs.data() + Bv.ytab_off;
         int SR = 0, SC = 0, AR = 0, AC = 0;
         std::vector<int4> tt;  // per tile of B: the region bounds og_resize2_kernel reads (3 int4, row-major tiles)
-        for (int by0 = 0; by0 < Bv.h; by0 += 16)
+        for (int by0 = 0; by0 < Bv.h; by0 += RZ2_TH)
             for (int bx0 = 0; bx0 < Bv.w; bx0 += 256) {
-                const int nyB = std::min(16, Bv.h - by0), nxB = std::min(256, Bv.w - bx0);
+                const int nyB = std::min(RZ2_TH, Bv.h - by0), nxB = std::min(256, Bv.w - bx0);
                 const int ar0 = yB[by0].x;
                 const int own_r1 = by0 + nyB == Bv.h ? A.h : yB[by0 + nyB].x;
                 const int ar1 = std::max(yB[by0 + nyB - 1].y, own_r1 - 1);
@@ -567,6 +567,11 @@ orbgpu_ctx* orbgpu_create(int device, int nfeatures, float scaleFactor, int nlev
         while (c->umax[v0] == c->umax[v0 + 1]) ++v0;
         c->umax[v] = v0;
         ++v0;
+    }
+    static const int kUmax[16] = {OG_UMAX};
+    if (std::memcmp(c->umax, kUmax, sizeof(kUmax)) != 0) {  // cannot happen: umax depends on constants only
+        orbgpu_destroy(c);
+        return nullptr;
     }
     return c;
 }

@@ -12,6 +12,9 @@
 #pragma once
 #include <stdint.h>
 
+// umax of src/ORBextractor.cc:454-469 for HALF_PATCH_SIZE = 15 (the reference's constant); the describe
+// kernel's flattened IC_Angle disk is built from it at compile time
+#define OG_UMAX 15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3
 #define OG_MAXLEVELS 16
 #define OG_EDGE 19
 #define OG_PATCH 31

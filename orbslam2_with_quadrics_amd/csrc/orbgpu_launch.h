@@ -28,10 +28,16 @@ struct OgRz2Geom {
     int SR, SC, AR, AC;  // LDS capacities: staged S rows x row stride, A rows x row stride (host-computed maxima)
     const int4* tiles;   // per tile (row-major over B's 16 x 256 tiles): {ar0, ar1, own_r1, ac0}, {ac1, own_c1, sr0, sr1}, {sc0, sc1}
 };
-// dynamic LDS of og_resize2_kernel: y-table rows of the tile (AR + 16 int4), S, A, row misalignments
+// og_resize2_kernel tiles: RZ2_TH rows x 256 columns of the coarser level per workgroup of 16 * RZ2_TH threads
+// (4 output rows x 4 columns per thread in its last pass)
+#ifndef RZ2_TH
+#define RZ2_TH 16
+#endif
+#define RZ2_NT (16 * RZ2_TH)
+// dynamic LDS of og_resize2_kernel: y-table rows of the tile (AR + RZ2_TH int4), S, A, row misalignments
 static inline size_t og_rz2_lds_bytes(int SR, int SC, int AR, int AC)
 {
-    return 16 * ((size_t)AR + 16) + (size_t)SR * SC + (size_t)AR * AC + 4 * (size_t)SR;
+    return 16 * ((size_t)AR + RZ2_TH) + (size_t)SR * SC + (size_t)AR * AC + 4 * (size_t)SR;
 }
 void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dstA,
                        long long pitchA, uint8_t* dstB, long long pitchB, long long dst_fstride, const OgRz2Geom& g,
