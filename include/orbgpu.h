@@ -296,6 +296,31 @@ int orbgpu_compute_stereo_matches_batch(orbgpu_ctx* left, orbgpu_ctx* right, flo
  * product build. */
 int orbgpu_debug_octree_profile(orbgpu_ctx* ctx, unsigned long long* out, int n);
 
+/* ---- Colour input: Tracking::GrabImage* -------------------------------------------------------------- */
+
+/* cv::cvtColor codes accepted by the colour entry points (OpenCV's own values, so a caller passes what it
+ * passed to cvtColor): 3-channel BGR / RGB, 4-channel BGRA / RGBA, 8 bits per channel. */
+#define ORBGPU_COLOR_BGR2GRAY 6
+#define ORBGPU_COLOR_RGB2GRAY 7
+#define ORBGPU_COLOR_BGRA2GRAY 10
+#define ORBGPU_COLOR_RGBA2GRAY 11
+
+/* Replaces the cvtColor(mImGray, mImGray, CV_RGB2GRAY / CV_BGR2GRAY / CV_RGBA2GRAY / CV_BGRA2GRAY) of
+ * Tracking::GrabImageStereo / GrabImageRGBD / GrabImageMonocular (src/Tracking.cc:169-198, 209-225, 240-255),
+ * batched and device-resident: frame b at d_src + b*src_frame_stride (rows of cols*channels bytes at
+ * src_pitch) -> 8-bit gray at d_dst + b*dst_frame_stride (dst_pitch).  OpenCV's integer RGB2Gray<uchar>:
+ * Y = (B*1868 + G*9617 + R*4899 + 2^13) >> 14.  Runs on the context's stream. */
+int orbgpu_cvt_color_to_gray_batch(orbgpu_ctx* ctx, const uint8_t* d_src, int B, int cols, int rows,
+                                   size_t src_pitch, size_t src_frame_stride, int code, uint8_t* d_dst,
+                                   size_t dst_pitch, size_t dst_frame_stride);
+
+/* Tracking::GrabImage*'s colour conversion followed by Frame::ExtractORB -> ORBextractor::operator()
+ * (src/Tracking.cc:209-230, src/Frame.cc:247-253) for one host colour image: the image goes to HBM once, is
+ * converted there and extracted from the gray copy (which also backs orbgpu_get_level(0)).  Same outputs,
+ * capacity and empty-image rules as orbgpu_extract; step = bytes per source row. */
+int orbgpu_extract_color(orbgpu_ctx* ctx, const uint8_t* img, int cols, int rows, size_t step, int code,
+                         orbgpu_keypoint* kps, uint8_t* desc, int cap, int* n);
+
 /* ---- RGB-D ------------------------------------------------------------------------------------------ */
 
 /* Replaces void Frame::ComputeStereoFromRGBD(const cv::Mat& imDepth) -- src/Frame.cc:643-664, called from the

@@ -72,6 +72,7 @@ def lib():
         L.oo_search_by_projection_kf.argtypes = [vp, vp, vp, f32, i32, i32, vp]
         L.oo_stereo_from_rgbd.argtypes = [vp, vp, i32, vp, i32, f32, vp, vp]
         L.oo_depth_u16_to_f32.argtypes = [vp, i32, f32, vp]
+        L.oo_cvt_gray.argtypes = [vp, i32, i32, i32, i32, i32, vp, i32]
         L.oo_vocab_from_arrays.restype = vp
         L.oo_vocab_from_arrays.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp]
         L.oo_vocab_load_text.restype = vp
@@ -329,6 +330,21 @@ def depth_u16_to_f32(depth_u16, factor):
     src = np.ascontiguousarray(depth_u16, np.uint16)
     out = np.zeros(src.shape, np.float32)
     lib().oo_depth_u16_to_f32(_p(src), src.size, factor, _p(out))
+    return out
+
+
+# cv::cvtColor codes (OpenCV's values) -> (channels, index of blue)
+COLOR_CODES = {6: (3, 0), 7: (3, 2), 10: (4, 0), 11: (4, 2)}
+
+
+def cvt_gray(img, code):
+    """cvtColor(img, gray, code) for 8U BGR/RGB/BGRA/RGBA (Tracking::GrabImage*, src/Tracking.cc:169-255)."""
+    cn, bidx = COLOR_CODES[code]
+    src = np.ascontiguousarray(img, np.uint8)
+    assert src.ndim == 3 and src.shape[2] == cn
+    rows, cols = src.shape[:2]
+    out = np.zeros((rows, cols), np.uint8)
+    lib().oo_cvt_gray(_p(src), cols, rows, cols * cn, cn, bidx, _p(out), cols)
     return out
 
 

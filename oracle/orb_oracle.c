@@ -1424,3 +1424,18 @@ void oo_depth_u16_to_f32(const uint16_t* src, int n, float factor, float* dst)
 {
     for (int i = 0; i < n; i++) dst[i] = (float)src[i] * factor;
 }
+
+/* cv::cvtColor(img, gray, CV_{BGR,RGB,BGRA,RGBA}2GRAY) on 8U, as Tracking::GrabImage{Stereo,RGBD,Monocular}
+ * apply it before the Frame is built (src/Tracking.cc:169-198, 209-225, 240-255).  OpenCV 3.x RGB2Gray<uchar>
+ * (third-party, not vendored; restated): yuv_shift = 14, B2Y = 1868, G2Y = 9617, R2Y = 4899,
+ * Y = (B*B2Y + G*G2Y + R*R2Y + (1 << 13)) >> 14.  bidx = index of the blue channel (0 for BGR/BGRA, 2 for
+ * RGB/RGBA), cn = 3 or 4 (alpha ignored). */
+void oo_cvt_gray(const uint8_t* src, int cols, int rows, int step, int cn, int bidx, uint8_t* dst, int dstep)
+{
+    const int cb = bidx == 0 ? 1868 : 4899, cr = bidx == 0 ? 4899 : 1868;
+    for (int y = 0; y < rows; y++) {
+        const uint8_t* s = src + (size_t)y * step;
+        for (int x = 0; x < cols; x++, s += cn)
+            dst[(size_t)y * dstep + x] = (uint8_t)((s[0] * cb + s[1] * 9617 + s[2] * cr + (1 << 13)) >> 14);
+    }
+}

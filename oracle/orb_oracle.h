@@ -181,6 +181,8 @@ int oo_search_by_projection_kf(const oo_frame* F, const oo_camera* cur, const oo
 void oo_stereo_from_rgbd(const oo_keypoint* kps, const oo_keypoint* kps_un, int n, const float* depth, int step,
                          float mbf, float* uright, float* depth_out);
 void oo_depth_u16_to_f32(const uint16_t* src, int n, float factor, float* dst);
+/* cvtColor(..., CV_xxx2GRAY) 8U of Tracking::GrabImage* (src/Tracking.cc:169-255); bidx = blue channel */
+void oo_cvt_gray(const uint8_t* src, int cols, int rows, int step, int cn, int bidx, uint8_t* dst, int dstep);
 
 /* DBoW2 vocabulary + transform (oracle/oo_bow.c): Frame::ComputeBoW, src/Frame.cc:395-402 */
 typedef struct oo_vocab oo_vocab;

@@ -32,7 +32,12 @@ EXPORTS = [
     "orbgpu_compute_stereo_from_rgbd", "orbgpu_compute_stereo_from_rgbd_batch",
     "orbgpu_vocabulary_load_text", "orbgpu_vocabulary_create", "orbgpu_vocabulary_destroy", "orbgpu_vocabulary_info",
     "orbgpu_compute_bow", "orbgpu_compute_bow_batch", "orbgpu_memcpy_h2d_async", "orbgpu_memcpy_d2h_async",
+    "orbgpu_cvt_color_to_gray_batch", "orbgpu_extract_color",
 ]
+
+# cv::cvtColor codes of the colour entry points (include/orbgpu.h ORBGPU_COLOR_*, OpenCV's values)
+COLOR_BGR2GRAY, COLOR_RGB2GRAY, COLOR_BGRA2GRAY, COLOR_RGBA2GRAY = 6, 7, 10, 11
+COLOR_CHANNELS = {COLOR_BGR2GRAY: 3, COLOR_RGB2GRAY: 3, COLOR_BGRA2GRAY: 4, COLOR_RGBA2GRAY: 4}
 
 OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
 
@@ -96,6 +101,8 @@ def _declare(L):
               "orbgpu_get_features_per_level"):
         getattr(L, n).argtypes = [vp, vp]
     L.orbgpu_extract.argtypes = [vp, vp, i32, i32, sz, vp, vp, i32, C.POINTER(i32)]
+    L.orbgpu_extract_color.argtypes = [vp, vp, i32, i32, sz, i32, vp, vp, i32, C.POINTER(i32)]
+    L.orbgpu_cvt_color_to_gray_batch.argtypes = [vp, vp, i32, i32, i32, sz, sz, i32, vp, sz, sz]
     L.orbgpu_max_keypoints.argtypes = [vp]
     L.orbgpu_get_level.argtypes = [vp, i32, vp, sz, C.POINTER(i32), C.POINTER(i32)]
     L.orbgpu_extract_batch_device.argtypes = [vp, vp, i32, i32, i32, sz, sz]

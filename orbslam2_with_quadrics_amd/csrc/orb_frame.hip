@@ -99,3 +99,63 @@ void og_launch_rgbd(hipStream_t s, const orbgpu_kp_dev* kps, const orbgpu_kp_dev
         hipLaunchKernelGGL(og_rgbd_kernel, dim3(gx, B), dim3(256), 0, s, kps, kps_un, counts, n_fixed, frame_cap, depth,
                            is_u16, factor, pitch, fstride, mbf, uright, dout);
 }
+
+// ------------------------------------------------------------------------------------------------
+// cv::cvtColor(..., CV_RGB2GRAY / CV_BGR2GRAY / CV_RGBA2GRAY / CV_BGRA2GRAY) on 8U images, the conversion
+// Tracking::GrabImageMonocular / GrabImageRGBD / GrabImageStereo apply before building the Frame
+// (src/Tracking.cc:169-198, 209-225, 240-255).  OpenCV's integer RGB2Gray<uchar>: Y = (B*1868 + G*9617 + R*4899
+// + 2^13) >> 14 (yuv_shift 14; the coefficients sum to 2^14, so no saturation is needed).  `bidx` is the channel
+// index of blue (0: BGR/BGRA input, 2: RGB/RGBA input).  One thread = 4 output pixels: 3 or 4 dword loads when
+// the source quad is dword-aligned (any pitch otherwise takes the byte path), one dword store when the output is.
+// HBM-bound: (cn + 1) bytes per pixel.
+__global__ __launch_bounds__(256) void og_gray_kernel(const uint8_t* __restrict__ src, int cols, int rows, int cn,
+                                                      int bidx, long long spitch, long long sfstride,
+                                                      uint8_t* __restrict__ dst, long long dpitch, long long dfstride)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;  // pixel quad of the row
+    const int y = blockIdx.y, b = blockIdx.z;
+    const int x0 = 4 * q;
+    if (x0 >= cols) return;
+    const uint8_t* srow = src + (long long)b * sfstride + (long long)y * spitch + (long long)x0 * cn;
+    uint8_t* drow = dst + (long long)b * dfstride + (long long)y * dpitch + x0;
+    const int n = min(4, cols - x0);
+    const unsigned cb = bidx == 0 ? 1868u : 4899u, cr = bidx == 0 ? 4899u : 1868u;  // weight of channel 0 / 2
+    uint8_t px[16];
+    if (n == 4 && (((uintptr_t)srow) & 3) == 0) {
+        const uint32_t* s32 = (const uint32_t*)srow;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (k < cn) {
+                const uint32_t w = s32[k];
+                px[4 * k] = (uint8_t)w;
+                px[4 * k + 1] = (uint8_t)(w >> 8);
+                px[4 * k + 2] = (uint8_t)(w >> 16);
+                px[4 * k + 3] = (uint8_t)(w >> 24);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) px[k] = 0;
+        for (int k = 0; k < n * cn; k++) px[k] = srow[k];
+    }
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int o = k * cn;
+        const unsigned g = (px[o] * cb + px[o + 1] * 9617u + px[o + 2] * cr + (1u << 13)) >> 14;
+        packed |= g << (8 * k);
+    }
+    if (n == 4 && (((uintptr_t)drow) & 3) == 0) {
+        *(uint32_t*)drow = packed;
+    } else {
+        for (int k = 0; k < n; k++) drow[k] = (uint8_t)(packed >> (8 * k));
+    }
+}
+
+void og_launch_gray(hipStream_t s, const uint8_t* src, int cols, int rows, int cn, int bidx, long long spitch,
+                    long long sfstride, uint8_t* dst, long long dpitch, long long dfstride, int B)
+{
+    const int nq = (cols + 3) / 4;
+    hipLaunchKernelGGL(og_gray_kernel, dim3((nq + 255) / 256, rows, B), dim3(256), 0, s, src, cols, rows, cn, bidx,
+                       spitch, sfstride, dst, dpitch, dfstride);
+}

@@ -81,6 +81,7 @@ struct orbgpu_ctx {
     OgGridGeom grid_geom{};
     // single-frame host path
     DevBuf<uint8_t> in_img;
+    DevBuf<uint8_t> in_color;  // colour frame staged by orbgpu_extract_color
     // matcher scratch
     DevBuf<uint8_t> mscratch;
     DevBuf<uint32_t> mlists;  // SearchForInitialization candidate lists {dist:16|i2:16}
@@ -597,6 +598,7 @@ void orbgpu_destroy(orbgpu_ctx* c)
     release(c->cell_items);
     release(c->status);
     release(c->in_img);
+    release(c->in_color);
     release(c->mscratch);
     release(c->mlists);
     release(c->mlist_n);
@@ -708,6 +710,59 @@ int orbgpu_extract(orbgpu_ctx* c, const uint8_t* img, int cols, int rows, size_t
     HIP_TRY(c, hipMemcpy2DAsync(c->in_img.p, pitch, img, step, (size_t)cols, (size_t)rows, hipMemcpyHostToDevice,
                                 c->stream));
     int r = orbgpu_extract_batch_device(c, c->in_img.p, 1, cols, rows, pitch, pitch * (size_t)rows);
+    if (r) return r;
+    return orbgpu_batch_download(c, 0, kps, desc, cap, n);
+}
+
+static int og_color_code(int code, int* cn, int* bidx)
+{
+    switch (code) {
+    case ORBGPU_COLOR_BGR2GRAY: *cn = 3; *bidx = 0; return 1;
+    case ORBGPU_COLOR_RGB2GRAY: *cn = 3; *bidx = 2; return 1;
+    case ORBGPU_COLOR_BGRA2GRAY: *cn = 4; *bidx = 0; return 1;
+    case ORBGPU_COLOR_RGBA2GRAY: *cn = 4; *bidx = 2; return 1;
+    default: return 0;
+    }
+}
+
+int orbgpu_cvt_color_to_gray_batch(orbgpu_ctx* c, const uint8_t* d_src, int B, int cols, int rows, size_t src_pitch,
+                                   size_t src_frame_stride, int code, uint8_t* d_dst, size_t dst_pitch,
+                                   size_t dst_frame_stride)
+{
+    int cn = 0, bidx = 0;
+    if (!c || !d_src || !d_dst || B < 1 || cols <= 0 || rows <= 0 || !og_color_code(code, &cn, &bidx))
+        return ORBGPU_ERR_ARG;
+    if (src_pitch < (size_t)cols * cn || dst_pitch < (size_t)cols ||
+        (B > 1 && (src_frame_stride < src_pitch * rows || dst_frame_stride < dst_pitch * rows)))
+        return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    og_launch_gray(c->stream, d_src, cols, rows, cn, bidx, (long long)src_pitch, (long long)src_frame_stride, d_dst,
+                   (long long)dst_pitch, (long long)dst_frame_stride, B);
+    HIP_TRY(c, hipGetLastError());
+    return ORBGPU_OK;
+}
+
+int orbgpu_extract_color(orbgpu_ctx* c, const uint8_t* img, int cols, int rows, size_t step, int code,
+                         orbgpu_keypoint* kps, uint8_t* desc, int cap, int* n)
+{
+    int cn = 0, bidx = 0;
+    if (!c || !n || !og_color_code(code, &cn, &bidx)) return ORBGPU_ERR_ARG;
+    if (!img || cols <= 0 || rows <= 0) {  // _image.empty(): return without touching the outputs
+        *n = -1;
+        return ORBGPU_OK;
+    }
+    if (step < (size_t)cols * cn) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t cpitch = ((size_t)cols * cn + 63) & ~(size_t)63;
+    const size_t pitch = ((size_t)cols + 63) & ~(size_t)63;
+    HIP_TRY(c, ensure(c->in_color, cpitch * (size_t)rows));
+    HIP_TRY(c, ensure(c->in_img, pitch * (size_t)rows));
+    HIP_TRY(c, hipMemcpy2DAsync(c->in_color.p, cpitch, img, step, (size_t)cols * cn, (size_t)rows,
+                                hipMemcpyHostToDevice, c->stream));
+    int r = orbgpu_cvt_color_to_gray_batch(c, c->in_color.p, 1, cols, rows, cpitch, cpitch * (size_t)rows, code,
+                                           c->in_img.p, pitch, pitch * (size_t)rows);
+    if (r) return r;
+    r = orbgpu_extract_batch_device(c, c->in_img.p, 1, cols, rows, pitch, pitch * (size_t)rows);
     if (r) return r;
     return orbgpu_batch_download(c, 0, kps, desc, cap, n);
 }

@@ -195,6 +195,8 @@ void og_launch_undistort(hipStream_t s, const orbgpu_kp_dev* in, orbgpu_kp_dev* 
 void og_launch_undistort_points(hipStream_t s, const float* xy, float* out, int n, const OgUndistort& U);
 // Frame::ComputeStereoFromRGBD over B frames (counts == nullptr: one frame of n_fixed keypoints); depth rows
 // are `pitch` bytes apart, frames `fstride` bytes; is_u16: raw CV_16U scaled by `factor`, else CV_32F
+void og_launch_gray(hipStream_t s, const uint8_t* src, int cols, int rows, int cn, int bidx, long long spitch,
+                    long long sfstride, uint8_t* dst, long long dpitch, long long dfstride, int B);
 void og_launch_rgbd(hipStream_t s, const orbgpu_kp_dev* kps, const orbgpu_kp_dev* kps_un, const int* counts,
                     int n_fixed, int frame_cap, const uint8_t* depth, int is_u16, float factor, long long pitch,
                     long long fstride, float mbf, float* uright, float* dout, int B);

@@ -97,6 +97,39 @@ class ORBextractor:
             return kps[:n.value].copy(), desc[:n.value].copy()
         raise RuntimeError("orbgpu_extract: capacity negotiation failed")
 
+    # ---- Tracking::GrabImage* colour conversion + Frame::ExtractORB (src/Tracking.cc:169-255)
+    def extract_color(self, image: np.ndarray, code: int):
+        """cvtColor(image, gray, code) on the GPU followed by operator() on the gray image (code: one of
+        _lib.COLOR_*; image: rows x cols x 3 or 4, uint8).  Returns (keypoints, descriptors) as __call__."""
+        if image is None or image.size == 0:
+            return None, None
+        img = np.asarray(image)
+        cn = _lib.COLOR_CHANNELS.get(code)
+        if cn is None or img.dtype != np.uint8 or img.ndim != 3 or img.shape[2] != cn:
+            raise ValueError(f"extract_color: code {code} needs a rows x cols x {cn} uint8 image")
+        if img.strides[2] != 1 or img.strides[1] != cn:
+            img = np.ascontiguousarray(img)
+        cap = self._L.orbgpu_max_keypoints(self._ctx)
+        for _ in range(2):
+            kps = np.zeros(max(cap, 1), KP_DTYPE)
+            desc = np.zeros((max(cap, 1), 32), np.uint8)
+            n = C.c_int(0)
+            rc = self._L.orbgpu_extract_color(self._ctx, _p(img), img.shape[1], img.shape[0], img.strides[0], code,
+                                              _p(kps), _p(desc), cap, C.byref(n))
+            if rc == _lib.ERR_CAPACITY:
+                cap = n.value
+                continue
+            _lib.check(self._ctx, rc, "orbgpu_extract_color")
+            return kps[:n.value].copy(), desc[:n.value].copy()
+        raise RuntimeError("orbgpu_extract_color: capacity negotiation failed")
+
+    def cvt_color_to_gray_batch(self, d_src: int, B: int, cols: int, rows: int, src_pitch: int,
+                                src_frame_stride: int, code: int, d_dst: int, dst_pitch: int, dst_frame_stride: int):
+        """Device-resident batched cvtColor(..., code) on the context's stream (orbgpu_cvt_color_to_gray_batch)."""
+        _lib.check(self._ctx, self._L.orbgpu_cvt_color_to_gray_batch(
+            self._ctx, C.c_void_p(d_src), B, cols, rows, src_pitch, src_frame_stride, code, C.c_void_p(d_dst),
+            dst_pitch, dst_frame_stride), "orbgpu_cvt_color_to_gray_batch")
+
     # ---- mvImagePyramid (public member, include/ORBextractor.h:85)
     def level(self, level: int) -> np.ndarray:
         w, h = C.c_int(), C.c_int()

@@ -249,3 +249,38 @@ def write_vocabulary_text(voc: dict, path: str):
         fp.write(f"{voc['k']} {voc['L']} {voc['scoring']} {voc['weighting']}\n")
         for p, lf, d, w in zip(voc["parent"], voc["is_leaf"], voc["desc"], voc["weight"]):
             fp.write(f"{int(p)} {int(lf)} " + " ".join(str(int(x)) for x in d) + f" {float(w)!r}\n")
+
+
+def color_frame(frame_id: int, height: int, width: int, alpha: bool = False) -> np.ndarray:
+    """A colour (RGB or RGBA, uint8) rendering of frame `frame_id`: the gray frame with seeded per-pixel
+    channel offsets, so RGB -> gray and BGR -> gray give different images."""
+    g = frame(frame_id, height, width).astype(np.int16)
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + 31 * frame_id + 5))
+    off = rng.integers(-24, 25, size=(height, width, 3), dtype=np.int16)
+    rgb = np.clip(g[..., None] + off, 0, 255).astype(np.uint8)
+    if alpha:
+        rgb = np.concatenate([rgb, rng.integers(0, 256, size=(height, width, 1), dtype=np.uint8)], axis=2)
+    return np.ascontiguousarray(rgb)
+
+
+def write_tum_rgbd_sequence(root: str, n: int, height: int = 480, width: int = 640, t0: float = 1305031102.175304):
+    """A TUM RGB-D sequence directory (rgb/<t>.png colour, depth/<t>.png 16-bit, associations.txt in the
+    format of Examples/RGB-D/associations/*.txt) written with Pillow; returns the association path."""
+    import os
+
+    from PIL import Image
+
+    os.makedirs(os.path.join(root, "rgb"), exist_ok=True)
+    os.makedirs(os.path.join(root, "depth"), exist_ok=True)
+    lines = []
+    for i in range(n):
+        t = t0 + i / 30.0
+        td = t - 0.0149
+        name, dname = f"rgb/{t:.6f}.png", f"depth/{td:.6f}.png"
+        Image.fromarray(color_frame(i, height, width), "RGB").save(os.path.join(root, name))
+        Image.fromarray(depth_u16(SEED_BASE + i, height, width)).save(os.path.join(root, dname))
+        lines.append(f"{t:.6f} {name} {td:.6f} {dname}")
+    path = os.path.join(root, "associations.txt")
+    with open(path, "w") as fp:
+        fp.write("\n".join(lines) + "\n")
+    return path
