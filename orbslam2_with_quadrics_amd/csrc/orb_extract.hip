@@ -1448,6 +1448,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 // ------------------------------------------------------------------------------------------------
 // k5: Frame::AssignFeaturesToGrid (src/Frame.cc:230-245, PosInGrid :382-392)
 // ------------------------------------------------------------------------------------------------
+#define OG_GRID_LDS_ITEMS 8192
 __global__ __launch_bounds__(256) void og_grid_kernel(const orbgpu_kp_dev* __restrict__ kps,
                                                       const int* __restrict__ counts, int frame_cap,
                                                       OgGridGeom G, int* __restrict__ cell_start,
@@ -1455,6 +1456,9 @@ __global__ __launch_bounds__(256) void og_grid_kernel(const orbgpu_kp_dev* __res
 {
     __shared__ int cnt[OG_GRID_CELLS + 1];
     __shared__ int wsum[32];
+    __shared__ int starts[OG_GRID_CELLS + 1];
+    __shared__ int sitems[OG_GRID_LDS_ITEMS];
+    auto cnt_start = [&](int c) { return starts[c]; };
     const int f = blockIdx.x, tid = threadIdx.x;
     const int n = counts[f];
     const orbgpu_kp_dev* K = kps + (long long)f * frame_cap;
@@ -1478,8 +1482,8 @@ __global__ __launch_bounds__(256) void og_grid_kernel(const orbgpu_kp_dev* __res
     }
     int tot;
     const int ex = og_block_excl_scan(s, wsum, &tot);
-    for (int q = 0; q < per; q++) CS[tid * per + q] = ex + local[q];
-    if (tid == 0) CS[OG_GRID_CELLS] = tot;
+    for (int q = 0; q < per; q++) CS[tid * per + q] = starts[tid * per + q] = ex + local[q];
+    if (tid == 0) CS[OG_GRID_CELLS] = starts[OG_GRID_CELLS] = tot;
     __syncthreads();
     for (int q = 0; q < per; q++) cnt[tid * per + q] = ex + local[q];  // cursors
     __syncthreads();
@@ -1493,18 +1497,31 @@ __global__ __launch_bounds__(256) void og_grid_kernel(const orbgpu_kp_dev* __res
     }
     __syncthreads();
     __threadfence_block();
-    // restore ascending index order inside each cell (push_back order of the reference)
+    // restore ascending index order inside each cell (push_back order of the reference): an insertion sort per
+    // cell (a few items each), in LDS when the frame's items fit (every frame of up to OG_GRID_LDS_ITEMS
+    // keypoints), so the dependent compare-and-shift chain costs LDS latency rather than global round trips
+    const int nin = starts[OG_GRID_CELLS];
+    const bool in_lds = nin <= OG_GRID_LDS_ITEMS;
+    int* SI = in_lds ? sitems : CI;
+    if (in_lds) {
+        for (int p = tid; p < nin; p += 256) sitems[p] = CI[p];
+        __syncthreads();
+    }
     for (int c = tid; c < OG_GRID_CELLS; c += 256) {
-        const int b = CS[c], e = CS[c + 1];
+        const int b = cnt_start(c), e = cnt_start(c + 1);
         for (int p = b + 1; p < e; p++) {
-            const int v = CI[p];
+            const int v = SI[p];
             int q = p - 1;
-            while (q >= b && CI[q] > v) {
-                CI[q + 1] = CI[q];
+            while (q >= b && SI[q] > v) {
+                SI[q + 1] = SI[q];
                 q--;
             }
-            CI[q + 1] = v;
+            SI[q + 1] = v;
         }
+    }
+    if (in_lds) {
+        __syncthreads();
+        for (int p = tid; p < nin; p += 256) CI[p] = sitems[p];
     }
 }
 
