@@ -788,6 +788,9 @@ __device__ __forceinline__ unsigned og_cand_order(int x, int y, const OgLevel& L
 // atomicAdd(&ctr[addr], 1) for every active lane, one LDS atomic per DISTINCT address of the wave: the
 // wave's keys are consecutive FAST outputs (one block's corners), so they fall into few nodes and plain
 // atomics would serialise on the same counters.  Wave-uniform control flow; exact counts.
+#ifndef OCT_WC_IT
+#define OCT_WC_IT 2  // distinct counter addresses per wave aggregated by ballots before plain atomics
+#endif
 __device__ __forceinline__ void og_wave_count(int* ctr, int addr, bool act)
 {
     u64 rem = __ballot(act);
@@ -795,7 +798,7 @@ __device__ __forceinline__ void og_wave_count(int* ctr, int addr, bool act)
     // the two most common addresses of the wave are counted by one atomic each; lanes with any other
     // address (a wave spread over many nodes) fall back to plain atomics
 #pragma unroll
-    for (int it = 0; it < 2 && rem; it++) {
+    for (int it = 0; it < OCT_WC_IT && rem; it++) {
         const int ld = __builtin_ctzll(rem);
         const int a = __builtin_amdgcn_readlane(addr, ld);
         const u64 m = __ballot(act && addr == a) & rem;

@@ -1,7 +1,7 @@
 """Per-round timeline of the level-0 octree workgroup (test infrastructure).
 
 python tools/octree_profile.py --build     # here: variant library with OG_OCT_PROFILE=1
-python tools/octree_profile.py --run       # GPU box: one 64-frame 1080p batch, prints per-round cycles
+python tools/octree_profile.py --run [--batch B]  # GPU box: one B-frame (default 64) 1080p batch, per-round cycles
 """
 import os
 import sys
@@ -26,7 +26,8 @@ def run():
 
     from orbslam2_with_quadrics_amd import ORBextractor, _lib, synthetic
 
-    rows, cols, B = 1080, 1920, 64
+    rows, cols = 1080, 1920
+    B = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else 64
     frames = np.stack([synthetic.frame(i % 8, rows, cols) for i in range(B)])
     ex = ORBextractor(2000, 1.2, 8, 20, 7)
     d = ex.device_alloc(frames.nbytes)
