@@ -791,8 +791,30 @@ __device__ __forceinline__ unsigned og_cand_order(int x, int y, const OgLevel& L
 #ifndef OCT_WC_IT
 #define OCT_WC_IT 2  // distinct counter addresses per wave aggregated by ballots before plain atomics
 #endif
+#ifndef OCT_WC_RUNS
+#define OCT_WC_RUNS 1  // 0: ballot aggregation over the OCT_WC_IT most common addresses, then atomics
+#endif
 __device__ __forceinline__ void og_wave_count(int* ctr, int addr, bool act)
 {
+#if OCT_WC_RUNS
+    // runs of equal addresses among the active lanes (keys arrive in candidate order, so neighbours share
+    // nodes): the first lane of each run adds the run's length -- one atomic per run
+    {
+        const int lane = threadIdx.x & 63;
+        const int a = act ? addr : -1;
+        const int prev = __shfl_up(a, 1);
+        const bool head = act && (lane == 0 || prev != a);
+        const u64 heads = __ballot(head);
+        const u64 actm = __ballot(act);
+        if (head) {
+            const u64 after = lane == 63 ? 0ull : (heads >> (lane + 1)) << (lane + 1);
+            const int end = after ? __builtin_ctzll(after) : 64;  // next head (or past the wave)
+            const u64 span = (end == 64 ? ~0ull : ((1ull << end) - 1ull)) & ~((1ull << lane) - 1ull);
+            atomicAdd(&ctr[addr], (int)__popcll(actm & span));
+        }
+        return;
+    }
+#endif
     u64 rem = __ballot(act);
     const int lane = threadIdx.x & 63;
     // the two most common addresses of the wave are counted by one atomic each; lanes with any other
@@ -1451,7 +1473,24 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 // ------------------------------------------------------------------------------------------------
 // k5: Frame::AssignFeaturesToGrid (src/Frame.cc:230-245, PosInGrid :382-392)
 // ------------------------------------------------------------------------------------------------
+#ifndef OG_GRID_SORT_LDS
+#define OG_GRID_SORT_LDS 0  // the LDS form of the per-cell sort below (under test)
+#endif
 #define OG_GRID_LDS_ITEMS 8192
+// insertion sort of one cell's item indices [b, e) (a few items per cell)
+template <typename T>
+__device__ __forceinline__ void og_sort_cell(T* SI, int b, int e)
+{
+    for (int p = b + 1; p < e; p++) {
+        const int v = SI[p];
+        int q = p - 1;
+        while (q >= b && SI[q] > v) {
+            SI[q + 1] = SI[q];
+            q--;
+        }
+        SI[q + 1] = v;
+    }
+}
 __global__ __launch_bounds__(256) void og_grid_kernel(const orbgpu_kp_dev* __restrict__ kps,
                                                       const int* __restrict__ counts, int frame_cap,
                                                       OgGridGeom G, int* __restrict__ cell_start,
@@ -1460,8 +1499,9 @@ __global__ __launch_bounds__(256) void og_grid_kernel(const orbgpu_kp_dev* __res
     __shared__ int cnt[OG_GRID_CELLS + 1];
     __shared__ int wsum[32];
     __shared__ int starts[OG_GRID_CELLS + 1];
+#if OG_GRID_SORT_LDS
     __shared__ int sitems[OG_GRID_LDS_ITEMS];
-    auto cnt_start = [&](int c) { return starts[c]; };
+#endif
     const int f = blockIdx.x, tid = threadIdx.x;
     const int n = counts[f];
     const orbgpu_kp_dev* K = kps + (long long)f * frame_cap;
@@ -1503,29 +1543,20 @@ __global__ __launch_bounds__(256) void og_grid_kernel(const orbgpu_kp_dev* __res
     // restore ascending index order inside each cell (push_back order of the reference): an insertion sort per
     // cell (a few items each), in LDS when the frame's items fit (every frame of up to OG_GRID_LDS_ITEMS
     // keypoints), so the dependent compare-and-shift chain costs LDS latency rather than global round trips
+    // (two explicit copies of the sort: no generic pointer selecting LDS or global memory)
     const int nin = starts[OG_GRID_CELLS];
-    const bool in_lds = nin <= OG_GRID_LDS_ITEMS;
-    int* SI = in_lds ? sitems : CI;
-    if (in_lds) {
+#if OG_GRID_SORT_LDS
+    if (nin <= OG_GRID_LDS_ITEMS) {
         for (int p = tid; p < nin; p += 256) sitems[p] = CI[p];
         __syncthreads();
-    }
-    for (int c = tid; c < OG_GRID_CELLS; c += 256) {
-        const int b = cnt_start(c), e = cnt_start(c + 1);
-        for (int p = b + 1; p < e; p++) {
-            const int v = SI[p];
-            int q = p - 1;
-            while (q >= b && SI[q] > v) {
-                SI[q + 1] = SI[q];
-                q--;
-            }
-            SI[q + 1] = v;
-        }
-    }
-    if (in_lds) {
+        for (int c = tid; c < OG_GRID_CELLS; c += 256) og_sort_cell(sitems, starts[c], starts[c + 1]);
         __syncthreads();
         for (int p = tid; p < nin; p += 256) CI[p] = sitems[p];
+        return;
     }
+#endif
+    (void)nin;
+    for (int c = tid; c < OG_GRID_CELLS; c += 256) og_sort_cell(CI, starts[c], starts[c + 1]);
 }
 
 // ------------------------------------------------------------------------------------------------

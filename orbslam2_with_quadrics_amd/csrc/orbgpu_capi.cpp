@@ -413,8 +413,26 @@ static void timer_begin(orbgpu_ctx* c)
     c->timer.used = 0;
     c->timer.names.clear();
 }
+// ORBGPU_DEBUG_SYNC=1 (diagnostics only): synchronise after every stage and report the first stage whose
+// kernels failed, so a device fault names its kernel instead of surfacing at the next unrelated sync
+static bool debug_sync()
+{
+    static const int on = [] {
+        const char* e = std::getenv("ORBGPU_DEBUG_SYNC");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    return on != 0;
+}
+
 static void timer_mark(orbgpu_ctx* c, const char* name)
 {
+    if (debug_sync()) {
+        const hipError_t e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            std::fprintf(stderr, "orbgpu: stage '%s' failed: %s\n", name, hipGetErrorString(e));
+            std::fflush(stderr);
+        }
+    }
     StageTimer& t = c->timer;
     if (!t.on) return;
     if ((int)t.ev.size() <= t.used) {
