@@ -1474,7 +1474,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 // k5: Frame::AssignFeaturesToGrid (src/Frame.cc:230-245, PosInGrid :382-392)
 // ------------------------------------------------------------------------------------------------
 #ifndef OG_GRID_SORT_LDS
-#define OG_GRID_SORT_LDS 0  // the LDS form of the per-cell sort below (under test)
+#define OG_GRID_SORT_LDS 1  // 0: sort in global memory
 #endif
 #define OG_GRID_LDS_ITEMS 8192
 // insertion sort of one cell's item indices [b, e) (a few items per cell)
