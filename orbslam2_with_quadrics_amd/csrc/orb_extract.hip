@@ -886,33 +886,43 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 
     OCT_PROF(0, clock64());
     OCT_PROF(1, (unsigned long long)C);
-    // ---- roots (src/ORBextractor.cc:552-585)
-    for (int r = tid; r < nIni; r += OCT_NT) childCnt[r] = 0;
+    // ---- roots (src/ORBextractor.cc:552-585) and the children of the first pass's splits, in ONE key pass:
+    // each key's root r = x / hX and its quadrant in that root are counted together (childCnt[4r + q]); a root's
+    // size is the sum of its four quadrant counts.  NO[k] holds the root id until the first round's key pass,
+    // which maps it to the root's list position through aux[] (`noRoot`).
+    for (int q = tid; q < 4 * nIni; q += OCT_NT) childCnt[q] = 0;
     __syncthreads();
     for (int base = tid; base < C; base += OCT_NT * OCT_U) {
-        u64 kv[OCT_U];
+        uint32_t kv[OCT_U];
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) {
             const int k = base + u * OCT_NT;
-            kv[u] = k < C ? K[k] : 0ull;
+            kv[u] = k < C ? K32[2 * k] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) {
             const int k = base + u * OCT_NT;
-            int r = 0;
+            int a = 0;
             if (k < C) {
-                r = (int)((float)(int)(kv[u] & 0xffff) / L.hX);
-                r = min(r, nIni - 1);
+                const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
+                const int r = min((int)((float)x / L.hX), nIni - 1);
                 NO[k] = (uint16_t)r;
+                OctNode rn;
+                rn.x0 = (short)(int)(L.hX * (float)r);
+                rn.x1 = (short)(int)(L.hX * (float)(r + 1));
+                rn.y0 = 0;
+                rn.y1 = (short)H;
+                a = 4 * r + og_quadrant(x, y, rn);
             }
-            og_wave_count(childCnt, r, k < C);
+            og_wave_count(childCnt, a, k < C);
         }
     }
     __syncthreads();
     if (tid == 0) {
         int Ln = 0;
         for (int r = 0; r < nIni; r++) {
-            const int c = childCnt[r];
+            const int c0 = childCnt[4 * r], c1 = childCnt[4 * r + 1], c2 = childCnt[4 * r + 2], c3 = childCnt[4 * r + 3];
+            const int c = c0 + c1 + c2 + c3;
             if (c > 0) {
                 OctNode n;
                 n.x0 = (short)(int)(L.hX * (float)r);
@@ -923,11 +933,17 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 n.cid = r;
                 nodes[0][Ln] = n;
                 fresh[0][Ln] = 0;
+                // quadrant counts follow the root to its list position (Ln <= r: a forward in-place move)
+                childCnt[4 * Ln] = c0;
+                childCnt[4 * Ln + 1] = c1;
+                childCnt[4 * Ln + 2] = c2;
+                childCnt[4 * Ln + 3] = c3;
                 aux[r] = Ln++;
             } else {
                 aux[r] = -1;
             }
         }
+        for (int q = 4 * Ln; q < 4 * nIni; q++) childCnt[q] = 0;
         sv[0] = Ln;      // list length
         sv[1] = 0;       // mode of the coming round: 0 normal pass, 1 final phase
         sv[2] = nIni;    // next creation id
@@ -936,34 +952,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         sv[8] = 0;       // `best` filled by a key pass
     }
     __syncthreads();
-    for (int q = tid; q < 4 * OG_OCT_MAXL; q += OCT_NT) childCnt[q] = 0;
-    __syncthreads();
-    // remap keys to root positions and count the children of the first pass's splits (cnt > 1)
-    for (int base = tid; base < C; base += OCT_NT * OCT_U) {
-        uint32_t kv[OCT_U];
-        int no[OCT_U];
-#pragma unroll
-        for (int u = 0; u < OCT_U; u++) {
-            const int k = base + u * OCT_NT;
-            kv[u] = k < C ? K32[2 * k] : 0u;
-            no[u] = k < C ? NO[k] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < OCT_U; u++) {
-            const int k = base + u * OCT_NT;
-            int a = 0;
-            bool cnt = false;
-            if (k < C) {
-                const int n = aux[no[u]];
-                NO[k] = (uint16_t)n;
-                const OctNode& nd = nodes[0][n];
-                cnt = nd.cnt > 1;
-                a = 4 * n + og_quadrant((int)(kv[u] & 0xffff), (int)(kv[u] >> 16), nd);
-            }
-            og_wave_count(childCnt, a, cnt);
-        }
-    }
-    __syncthreads();
+    bool noRoot = true;  // NO[] holds root ids (workgroup-uniform)
 
     OCT_PROF(2, clock64());
     for (int round = 0; round < 4096; round++) {
@@ -1113,7 +1102,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 int a = 0;
                 bool cnt = false;
                 if (k < C) {
-                    const int n = no[u];
+                    const int n = noRoot ? aux[no[u]] : no[u];
                     const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
                     const int r = splitRank[n];
                     int n2;
@@ -1133,6 +1122,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             }
         }
         __syncthreads();
+        noRoot = false;
         if (tid == 0) {
             sv[0] = Lnew;
             sv[1] = nextMode;
@@ -1164,7 +1154,8 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 if (k < C) {
                     const int x = (int)(kv[u] & 0xffff), y = (int)((kv[u] >> 16) & 0xffff);
                     const int resp = (int)((kv[u] >> 32) & 0xff);
-                    atomicMax(&best[no[u]], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
+                    atomicMax(&best[noRoot ? aux[no[u]] : no[u]],
+                              ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
                 }
             }
         }
