@@ -866,7 +866,9 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     // children) before the key pass accumulates the next round's, with barriers in between; the last key
     // pass keeps the best key per node in the same storage.  ~74 KB of LDS in total: 2 workgroups per CU.
     __shared__ __attribute__((aligned(16))) int childCnt[4 * OG_OCT_MAXL];
-    __shared__ uint16_t childPos[4 * OG_OCT_MAXL];
+    __shared__ __attribute__((aligned(16))) uint16_t childPos[4 * OG_OCT_MAXL];
+    // final-phase planning only: the candidates' (size, creation id) keys, in the previous round's (dead) childPos
+    u64* skey = (u64*)childPos;
     u64* best = (u64*)childCnt;  // [OG_OCT_MAXL], final key pass only
     __shared__ int wsum[32];
     __shared__ int sv[16];
@@ -980,16 +982,19 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             // the back (src/ORBextractor.cc:684-685): order = descending (cnt, creation id)
             const bool flag = i < Ln && cf[i] && cn[i].cnt > 1;
             const int c = og_block_excl_scan(flag ? 1 : 0, wsum, &S);
-            if (flag) aux[c] = i;
+            u64 mk = 0;
+            if (flag) {
+                mk = ((u64)(uint32_t)cn[i].cnt << 32) | (u64)(uint32_t)cn[i].cid;  // (size, ptr) order, unique
+                skey[c] = mk;
+            }
             __syncthreads();
             if (i < Ln) splitRank[i] = -1;
             if (flag) {
-                const int mc = cn[i].cnt, mid = cn[i].cid;
+                // rank = number of candidates with a larger key: every lane reads the same key (broadcast), no
+                // dependent lookups, so the loop pipelines
                 int rank = 0;
-                for (int q = 0; q < S; q++) {
-                    const OctNode& o = cn[aux[q]];
-                    rank += (o.cnt > mc) || (o.cnt == mc && o.cid > mid);
-                }
+#pragma unroll 8
+                for (int q = 0; q < S; q++) rank += skey[q] > mk;
                 splitRank[i] = rank;
                 splitNode[rank] = i;
             }
