@@ -1035,6 +1035,8 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             const OctNode par = cn[sn];
             const int groupStart = T - (exNc + nc);
             const int cidBase = sv[2] + exNc;
+            // the key pass's remap record of node sn: its split point here, its children's positions below
+            newPos[sn] = (par.x0 + ((par.x1 - par.x0 + 1) >> 1)) | ((par.y0 + ((par.y1 - par.y0 + 1) >> 1)) << 16);
             int before = 0;  // non-empty children among q' < q (creation order n1..n4)
             for (int q = 0; q < 4; q++) {
                 const int c = CC[4 * sn + q];
@@ -1058,7 +1060,9 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const int kr = og_block_excl_scan(kept ? 1 : 0, wsum, &keptTot);
         if (kept) {
             const int pos = T + kr;
-            newPos[i] = pos;
+            // remap record of a kept node: split point (0, 0) selects quadrant 3, and all four entries are pos
+            newPos[i] = 0;
+            ((u64*)childPos)[i] = (u64)(uint16_t)pos * 0x0001000100010001ull;
             if (pos < OG_OCT_MAXL) {
                 nn[pos] = cn[i];
                 nf[pos] = 0;
@@ -1085,8 +1089,18 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             if (Lnew >= N || Lnew == Ln) done = 1;
         }
         for (int q = tid; q < 4 * Lnew; q += OCT_NT) NCC[q] = 0;
-        if (done)
+        if (done) {
             for (int q = tid; q < Lnew; q += OCT_NT) best[q] = 0ull;
+        } else {
+            // counting record of every node of the new list (splitRank is dead until the next round's plan):
+            // split point x | y << 15, bit 30 = the node is a split candidate of the next round
+            for (int q = tid; q < Lnew; q += OCT_NT) {
+                const OctNode& nd = nn[q];
+                const int countable = nd.cnt > 1 && (nextMode == 0 || nf[q]);
+                splitRank[q] = (nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1)) | ((nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1)) << 15) |
+                               (countable << 30);
+            }
+        }
         __syncthreads();
         OCT_PROF(10 + 4 * round, clock64());
         OCT_PROF(11 + 4 * round, (unsigned long long)S | ((unsigned long long)A << 32));
@@ -1109,18 +1123,19 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 if (k < C) {
                     const int n = noRoot ? aux[no[u]] : no[u];
                     const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
-                    const int r = splitRank[n];
-                    int n2;
-                    if (r >= 0 && r < A) n2 = childPos[4 * n + og_quadrant(x, y, cn[n])];
-                    else n2 = newPos[n];
+                    // remap record: the node's split point (newPos) and its four target positions (childPos)
+                    const int mm = newPos[n];
+                    const u64 tp = ((const u64*)childPos)[n];
+                    const int q = (x >= (mm & 0xffff) ? 1 : 0) | (y >= (mm >> 16) ? 2 : 0);  // og_quadrant
+                    const int n2 = (int)((tp >> (16 * q)) & 0xffffu);
                     NO[k] = (uint16_t)n2;
                     if (done) {
                         const int resp = (int)(K32[2 * k + 1] & 0xff);
                         atomicMax(&best[n2], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
                     } else {
-                        const OctNode& nd = nn[n2];
-                        cnt = nd.cnt > 1 && (nextMode == 0 || nf[n2]);
-                        a = 4 * n2 + og_quadrant(x, y, nd);
+                        const int rc = splitRank[n2];
+                        cnt = (rc >> 30) & 1;
+                        a = 4 * n2 + ((x >= (rc & 0x7fff) ? 1 : 0) | (y >= ((rc >> 15) & 0x7fff) ? 2 : 0));
                     }
                 }
                 if (!done) og_wave_count(NCC, a, cnt);  // `done` is workgroup-uniform

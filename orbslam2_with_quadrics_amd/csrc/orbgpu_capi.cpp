@@ -170,6 +170,10 @@ static int image_bounds(orbgpu_ctx* c, bool undist, const OgUndistort& U, int co
 static int build_plan(orbgpu_ctx* c, int W, int H)
 {
     if (c->planned && c->W == W && c->H == H) return ORBGPU_OK;
+    if (W >= 32768 || H >= 32768) {  // candidate keys and the octree's remap records pack coordinates in 15 bits
+        c->err = "image larger than 32767 pixels in a dimension";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
     OgPlan P{};
     P.nlevels = c->nlevels;
     P.iniTh = c->iniTh;
