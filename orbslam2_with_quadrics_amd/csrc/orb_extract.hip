@@ -427,6 +427,10 @@ __device__ __forceinline__ uint2 og_fast_quick2(const uint32_t* p, int st, og_u1
     return make_uint2(__builtin_bit_cast(uint32_t, dark), __builtin_bit_cast(uint32_t, bright));
 }
 
+#ifndef OG_FAST_SLOTS
+#define OG_FAST_SLOTS 2  // pair slots per lane per stage-1 iteration
+#endif
+
 #ifndef OG_EXP_FAST_STOP
 #define OG_EXP_FAST_STOP 0
 #endif
@@ -558,40 +562,41 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const unsigned invH = (1u << 20) / (unsigned)H + 1u;  // exact p / H for p < 3200, H <= 40
     // two pair slots per lane per iteration (slots p and p + 512): twice the LDS reads in flight and one
     // reservation for the four survivor ballots
-    for (int p0 = wv * 64; p0 < npair; p0 += 2 * FB_NT) {
-        int ii[2], cc[2];
-        uint2 r[2];
+    for (int p0 = wv * 64; p0 < npair; p0 += OG_FAST_SLOTS * FB_NT) {
+        int ii[OG_FAST_SLOTS], cc[OG_FAST_SLOTS];
+        uint2 r[OG_FAST_SLOTS];
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
+        for (int h = 0; h < OG_FAST_SLOTS; h++) {
             const int pp = p0 + h * FB_NT + lane;
             ii[h] = (int)(__umul24((unsigned)pp, invH) >> 20);
             cc[h] = pp - (int)__umul24((unsigned)ii[h], (unsigned)H);
             r[h] = make_uint2(0u, 0u);
             if (pp < npair) r[h] = og_fast_quick2(&T2[(ii[h] + 3) * FB_S2 + (cc[h] + 3)], FB_S2, tt);
         }
-        bool sv[4];
-        int pol[4];
-        u64 m[4];
-        int nn[4];
+        bool sv[2 * OG_FAST_SLOTS];
+        int pol[2 * OG_FAST_SLOTS];
+        u64 m[2 * OG_FAST_SLOTS];
+        int nn[2 * OG_FAST_SLOTS];
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
+        for (int h = 0; h < OG_FAST_SLOTS; h++) {
             pol[2 * h] = ((r[h].x & 0xffffu) ? 0x4000 : 0) | ((r[h].y & 0xffffu) ? 0x8000 : 0);
             pol[2 * h + 1] = ((r[h].x >> 16) ? 0x4000 : 0) | ((r[h].y >> 16) ? 0x8000 : 0);
             sv[2 * h] = pol[2 * h] != 0 && cc[h] < dw;
             sv[2 * h + 1] = pol[2 * h + 1] != 0 && cc[h] + H < dw;
         }
+        int n = 0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+        for (int q = 0; q < 2 * OG_FAST_SLOTS; q++) {
             m[q] = __ballot(sv[q]);
             nn[q] = __popcll(m[q]);
+            n += nn[q];
         }
-        const int n = nn[0] + nn[1] + nn[2] + nn[3];
         if (n) {
             int b = 0;
             if (lane == 0) b = atomicAdd(&sh_ns, n);
             b = __builtin_amdgcn_readfirstlane(b);
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
+            for (int q = 0; q < 2 * OG_FAST_SLOTS; q++) {
                 const int h = q >> 1;
                 if (sv[q])
                     lst[b + __popcll(m[q] & lt_mask)] = (uint16_t)(pol[q] | (ii[h] << 7) | (cc[h] + ((q & 1) ? H : 0)));
