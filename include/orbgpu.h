@@ -47,6 +47,39 @@ orbgpu_ctx* orbgpu_create(int device, int nfeatures, float scaleFactor, int nlev
 /* Replaces ORBextractor::~ORBextractor (include/ORBextractor.h:54). */
 void orbgpu_destroy(orbgpu_ctx* ctx);
 
+/* ---- OpenCV / compiler semantics switch -----------------------------------------
+ * The reference takes three pixel-level behaviours from outside its own source, and they differ between
+ * OpenCV versions/ISAs and compiler flags.  Each context reproduces one choice per behaviour:
+ *  - cv::resize INTER_LINEAR 8U vertical pass (src/ORBextractor.cc:1120):
+ *      default  OpenCV's VResizeLinear 8U specialisation ((b0*(D0>>4))>>16 + (b1*(D1>>4))>>16 + 2) >> 2
+ *               (OpenCV 2.4-4.x; its SSE2 mulhi body and its scalar tail compute the same form);
+ *      ORBGPU_SEM_RESIZE_FIXEDPT  the generic FixedPtCast form (b0*D0 + b1*D1 + 2^21) >> 22;
+ *  - GaussianBlur 7x7 sigma 2 on CV_8U (src/ORBextractor.cc:1086), ORBGPU_SEM_BLUR_*:
+ *      SSE2_257     OpenCV 3.0-3.4.1 on x86-64 without IPP: kernel [18,34,49,55,49,34,18], column sums
+ *                   rounded half-to-even (float SIMD) in columns x < 4*floor(w/4), half-up in the tail;
+ *      SCALAR_257   the same kernel rounded half-up everywhere (no SIMD);
+ *      BITEXACT_256 the bit-exact fixed-point GaussianBlur, kernel [18,34,49,54,49,34,18];
+ *      BITEXACT_ED  the bit-exact GaussianBlur with the error-diffused kernel [18,34,48,56,48,34,18];
+ *  - rBRIEF rotation (src/ORBextractor.cc:118-120): default fma(x, b, y*a) as GCC -O3 -march=native
+ *    contracts it on an FMA host (the reference's CMakeLists.txt:11 flags); ORBGPU_SEM_BRIEF_NOFMA rounds
+ *    both products.
+ * ORBGPU_SEM_DEFAULT (0) = OpenCV 3.x (< 3.4.2) on x86-64 without IPP, reference built with its own flags. */
+#define ORBGPU_SEM_DEFAULT 0x00
+#define ORBGPU_SEM_RESIZE_FIXEDPT 0x01
+#define ORBGPU_SEM_BLUR_SHIFT 2
+#define ORBGPU_SEM_BLUR_SSE2_257 (0 << ORBGPU_SEM_BLUR_SHIFT)
+#define ORBGPU_SEM_BLUR_SCALAR_257 (1 << ORBGPU_SEM_BLUR_SHIFT)
+#define ORBGPU_SEM_BLUR_BITEXACT_256 (2 << ORBGPU_SEM_BLUR_SHIFT)
+#define ORBGPU_SEM_BLUR_BITEXACT_ED (3 << ORBGPU_SEM_BLUR_SHIFT)
+#define ORBGPU_SEM_BLUR_MASK (7 << ORBGPU_SEM_BLUR_SHIFT)
+#define ORBGPU_SEM_BRIEF_NOFMA 0x20
+#define ORBGPU_SEM_ALL (ORBGPU_SEM_RESIZE_FIXEDPT | ORBGPU_SEM_BLUR_MASK | ORBGPU_SEM_BRIEF_NOFMA)
+/* the round-1 semantics of this build: generic resize form, 257-kernel rounded half-up, FMA rotation */
+#define ORBGPU_SEM_ROUND1 (ORBGPU_SEM_RESIZE_FIXEDPT | ORBGPU_SEM_BLUR_SCALAR_257)
+/* Select the semantics of later extractions on ctx.  ORBGPU_ERR_ARG for unknown bits or blur variants. */
+int orbgpu_set_semantics(orbgpu_ctx* ctx, int flags);
+int orbgpu_get_semantics(const orbgpu_ctx* ctx);
+
 /* Inline getters of include/ORBextractor.h:63-83.  Vector getters write nlevels floats. */
 int orbgpu_get_levels(const orbgpu_ctx* ctx);
 float orbgpu_get_scale_factor(const orbgpu_ctx* ctx);

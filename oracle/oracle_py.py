@@ -47,8 +47,10 @@ def lib():
         L.oo_level_candidates.argtypes = [vp, i32, vp, vp, i32]
         L.oo_distribute_octree.restype = i32
         L.oo_distribute_octree.argtypes = [vp, vp, i32, i32, i32, i32, i32, i32, vp, vp]
-        L.oo_resize_linear.argtypes = [vp, i32, i32, vp, i32, i32]
-        L.oo_gaussian7.argtypes = [vp, i32, i32, vp]
+        L.oo_resize_linear.argtypes = [vp, i32, i32, vp, i32, i32, i32]
+        L.oo_gaussian7.argtypes = [vp, i32, i32, vp, i32]
+        L.oo_set_semantics.restype = i32
+        L.oo_set_semantics.argtypes = [vp, i32]
         L.oo_fast_score.restype = i32
         L.oo_fast_score.argtypes = [vp, i32, i32, i32]
         L.oo_fastatan2.restype = f32
@@ -97,12 +99,15 @@ def _p(a):
 class OracleExtractor:
     """Mirror of ORB_SLAM2::ORBextractor backed by the C oracle."""
 
-    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7):
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, semantics=0):
         self._L = lib()
         self.nfeatures, self.nlevels = nfeatures, nlevels
         self._h = self._L.oo_create(nfeatures, scale_factor, nlevels, ini_th, min_th)
         if not self._h:
             raise ValueError("bad extractor parameters")
+        if self._L.oo_set_semantics(self._h, int(semantics)) != 0:
+            raise ValueError(f"unknown semantics flags {semantics:#x}")
+        self.semantics = int(semantics)
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -447,17 +452,17 @@ def descriptor_distance(a, b) -> int:
     return lib().oo_descriptor_distance(_p(a), _p(b))
 
 
-def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+def resize_linear(src: np.ndarray, dw: int, dh: int, semantics: int = 0) -> np.ndarray:
     src = np.ascontiguousarray(src, np.uint8)
     dst = np.zeros((dh, dw), np.uint8)
-    lib().oo_resize_linear(_p(src), src.shape[1], src.shape[0], _p(dst), dw, dh)
+    lib().oo_resize_linear(_p(src), src.shape[1], src.shape[0], _p(dst), dw, dh, int(semantics))
     return dst
 
 
-def gaussian7(src: np.ndarray) -> np.ndarray:
+def gaussian7(src: np.ndarray, semantics: int = 0) -> np.ndarray:
     src = np.ascontiguousarray(src, np.uint8)
     dst = np.zeros_like(src)
-    lib().oo_gaussian7(_p(src), src.shape[1], src.shape[0], _p(dst))
+    lib().oo_gaussian7(_p(src), src.shape[1], src.shape[0], _p(dst), int(semantics))
     return dst
 
 

@@ -38,6 +38,7 @@ static void cv_push(oo_candvec* a, oo_cand c)
 
 struct oo_extractor {
     int nfeatures, nlevels, iniTh, minTh;
+    int sem;                                  /* OO_SEM_* (orb_oracle.h), default 0 */
     double scaleFactor;                       /* double member, src/ORBextractor.h:98 */
     float sf[OO_MAXLEVELS], isf[OO_MAXLEVELS], sig2[OO_MAXLEVELS], isig2[OO_MAXLEVELS];
     int nfeat[OO_MAXLEVELS];
@@ -105,6 +106,13 @@ void oo_destroy(oo_extractor* e)
 
 int oo_nlevels(const oo_extractor* e) { return e->nlevels; }
 
+int oo_set_semantics(oo_extractor* e, int sem)
+{
+    if (sem & ~OO_SEM_ALL || ((sem >> OO_SEM_BLUR_SHIFT) & 7) > 3) return -1;
+    e->sem = sem;
+    return 0;
+}
+
 void oo_scale_tables(const oo_extractor* e, float* scale, float* inv_scale, float* sigma2,
                      float* inv_sigma2, int* fpl, int* umax16)
 {
@@ -120,10 +128,16 @@ void oo_scale_tables(const oo_extractor* e, float* scale, float* inv_scale, floa
 
 /* ------------------------------------------------------------------------------------------------ */
 /* cv::resize INTER_LINEAR, CV_8UC1 (external; call site src/ORBextractor.cc:1120).  Generic           */
-/* fixed-point path, scalar vertical form.                                            */
+/* fixed-point path (resizeGeneric_ + HResizeLinear + VResizeLinear).  The vertical pass has two forms   */
+/* (sem & OO_SEM_RESIZE_FIXEDPT):                                                         */
+/*   0: OpenCV's VResizeLinear<uchar, int, short, FixedPtCast<int,uchar,22>, VResizeLinearVec_32s8u>      */
+/*      specialisation: ((b0*(D0>>4))>>16) + ((b1*(D1>>4))>>16) + 2) >> 2 -- the SSE2 mulhi body and the  */
+/*      scalar tail compute the same form, so no SIMD/tail split exists;                                 */
+/*   1: the generic template's FixedPtCast (b0*D0 + b1*D1 + 2^21) >> 22 (round-1 semantics).             */
 /* ------------------------------------------------------------------------------------------------ */
-void oo_resize_linear(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh)
+void oo_resize_linear(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh, int sem)
 {
+    const int fixedpt = (sem & OO_SEM_RESIZE_FIXEDPT) != 0;
     const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
     const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
     int* xofs = (int*)malloc(sizeof(int) * (size_t)dw);
@@ -160,7 +174,11 @@ void oo_resize_linear(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, 
         }
         uint8_t* o = dst + (size_t)dy * dw;
         for (int dx = 0; dx < dw; dx++) {
-            int val = (b0 * rows[dx] + b1 * rows[dw + dx] + (1 << 21)) >> 22;
+            int val;
+            if (fixedpt)
+                val = (b0 * rows[dx] + b1 * rows[dw + dx] + (1 << 21)) >> 22;
+            else
+                val = (((b0 * (rows[dx] >> 4)) >> 16) + ((b1 * (rows[dw + dx] >> 4)) >> 16) + 2) >> 2;
             o[dx] = (uint8_t)(val < 0 ? 0 : val > 255 ? 255 : val);
         }
     }
@@ -170,9 +188,19 @@ void oo_resize_linear(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, 
 }
 
 /* ------------------------------------------------------------------------------------------------ */
-/* cv::GaussianBlur 7x7 sigma 2 BORDER_REFLECT_101 on CV_8U (src/ORBextractor.cc:1086)              */
+/* cv::GaussianBlur 7x7 sigma 2 BORDER_REFLECT_101 on CV_8U (src/ORBextractor.cc:1086).  Separable      */
+/* integer kernel k (8 fractional bits), row sums exact; the column result by variant                  */
+/* ((sem >> OO_SEM_BLUR_SHIFT) & 7):                                                    */
+/*   0 SSE2_257: OpenCV 3.0-3.4.1 on x86-64 without IPP: FilterEngine with k = cvRound(256 g) =          */
+/*     [18,34,49,55,...] (sum 257); SymmColumnVec_32s8u converts the column sums to float (exact below   */
+/*     2^24) and rounds half-to-even (cvtps2dq) for x < 4*floor(w/4); the scalar tail x >= 4*floor(w/4)  */
+/*     uses FixedPtCastEx (S + 2^15) >> 16;                                                             */
+/*   1 SCALAR_257: the same kernel, FixedPtCastEx everywhere (a build without SSE2 vector ops);          */
+/*   2 BITEXACT_256: the fixed-point GaussianBlur, centre = 256 - 2*sum(sides): [18,34,49,54,...];       */
+/*   3 BITEXACT_ED: the fixed-point GaussianBlur with the error-diffused kernel [18,34,48,56,...].       */
+/* All: out = sat_u8(round(S / 2^16)), S = sum_y k_y sum_x k_x I.                                       */
 /* ------------------------------------------------------------------------------------------------ */
-static const int oo_gk[7] = {18, 34, 49, 55, 49, 34, 18}; /* cvRound(256*k), DESIGN.md §3.2 */
+static const int oo_gk_tab[4][4] = {{18, 34, 49, 55}, {18, 34, 49, 55}, {18, 34, 49, 54}, {18, 34, 48, 56}};
 
 static inline int oo_reflect101(int i, int n)
 {
@@ -184,20 +212,25 @@ static inline int oo_reflect101(int i, int n)
     return i;
 }
 
-void oo_gaussian7(const uint8_t* src, int w, int h, uint8_t* dst)
+void oo_gaussian7(const uint8_t* src, int w, int h, uint8_t* dst, int sem)
 {
+    const int var = (sem >> OO_SEM_BLUR_SHIFT) & 7;
+    const int* c = oo_gk_tab[var < 4 ? var : 0];
+    const int gk[7] = {c[0], c[1], c[2], c[3], c[2], c[1], c[0]};
+    const int xsimd = var == 0 ? (w & ~3) : 0;  /* columns whose result is rounded half-to-even */
     int* tmp = (int*)malloc(sizeof(int) * (size_t)w * (size_t)h);
     for (int y = 0; y < h; y++)
         for (int x = 0; x < w; x++) {
             int s = 0;
-            for (int k = -3; k <= 3; k++) s += oo_gk[k + 3] * src[(size_t)y * w + oo_reflect101(x + k, w)];
+            for (int k = -3; k <= 3; k++) s += gk[k + 3] * src[(size_t)y * w + oo_reflect101(x + k, w)];
             tmp[(size_t)y * w + x] = s;
         }
     for (int y = 0; y < h; y++)
         for (int x = 0; x < w; x++) {
             int s = 0;
-            for (int k = -3; k <= 3; k++) s += oo_gk[k + 3] * tmp[(size_t)oo_reflect101(y + k, h) * w + x];
+            for (int k = -3; k <= 3; k++) s += gk[k + 3] * tmp[(size_t)oo_reflect101(y + k, h) * w + x];
             int v = (s + (1 << 15)) >> 16;
+            if (x < xsimd && (s & 0x1ffff) == 0x8000) v--; /* tie with an even quotient: half-to-even */
             dst[(size_t)y * w + x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
         }
     free(tmp);
@@ -537,7 +570,7 @@ static float oo_ic_angle(const uint8_t* img, int stride, float px, float py, con
 }
 
 static void oo_orb_descriptor(float kx, float ky, float angle_deg, const uint8_t* img, int stride,
-                              uint8_t* desc)
+                              uint8_t* desc, int nofma)
 {
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float angle = angle_deg * factorPI;
@@ -551,9 +584,16 @@ static void oo_orb_descriptor(float kx, float ky, float angle_deg, const uint8_t
             int t[2];
             for (int q = 0; q < 2; q++) {
                 const float x = (float)pat[2 * q], y = (float)pat[2 * q + 1];
-                /* GCC -O3 -march=native contraction of the GET_VALUE expressions */
-                const int row = oo_cvround(fmaf(x, b, y * a));
-                const int col = oo_cvround(fmaf(x, a, -(y * b)));
+                /* GCC -O3 -march=native contraction of the GET_VALUE expressions, or the
+                 * separately rounded products of a build without FMA contraction (OO_SEM_BRIEF_NOFMA) */
+                int row, col;
+                if (nofma) {
+                    row = oo_cvround(x * b + y * a);
+                    col = oo_cvround(x * a - y * b);
+                } else {
+                    row = oo_cvround(fmaf(x, b, y * a));
+                    col = oo_cvround(fmaf(x, a, -(y * b)));
+                }
                 t[q] = center[row * stride + col];
             }
             val |= (t[0] < t[1]) << k;
@@ -585,7 +625,7 @@ int oo_extract(oo_extractor* e, const uint8_t* img, int cols, int rows, int step
         if (l == 0) {
             for (int y = 0; y < h; y++) memcpy(e->lev[0] + (size_t)y * w, img + (size_t)y * step, (size_t)w);
         } else {
-            oo_resize_linear(e->lev[l - 1], e->lw[l - 1], e->lh[l - 1], e->lev[l], w, h);
+            oo_resize_linear(e->lev[l - 1], e->lw[l - 1], e->lh[l - 1], e->lev[l], w, h, e->sem);
         }
     }
     /* ComputeKeyPointsOctTree */
@@ -656,10 +696,10 @@ int oo_extract(oo_extractor* e, const uint8_t* img, int cols, int rows, int step
     for (int l = 0; l < nl; l++) {
         if (nall[l] == 0) { free(all[l]); continue; }
         uint8_t* blurred = (uint8_t*)malloc((size_t)e->lw[l] * (size_t)e->lh[l]);
-        oo_gaussian7(e->lev[l], e->lw[l], e->lh[l], blurred);
+        oo_gaussian7(e->lev[l], e->lw[l], e->lh[l], blurred, e->sem);
         for (int i = 0; i < nall[l]; i++)
             oo_orb_descriptor(all[l][i].x, all[l][i].y, all[l][i].angle, blurred, e->lw[l],
-                              desc + (size_t)(off + i) * 32);
+                              desc + (size_t)(off + i) * 32, (e->sem & OO_SEM_BRIEF_NOFMA) != 0);
         free(blurred);
         if (l != 0) {
             const float s = e->sf[l];

@@ -11,8 +11,8 @@
  * vectors.  Individual pieces are pinned: glibc sincosf (exhaustive, tools/verify_sincosf.c), GCC's FMA
  * contraction of the rBRIEF rotation (tools/probe_contraction.sh), the FAST score against its
  * definition (tests/test_oracle_pins.py), the ORB sampling pattern against the reference source text.
- * The OpenCV primitives follow the semantics written down in DESIGN.md §3 (scalar resize, 257-sum
- * Gaussian kernel, scalar fastAtan2).
+ * The OpenCV primitives follow the semantics written down in DESIGN.md §3; the ones that differ between
+ * OpenCV versions/ISAs and compiler flags are selectable per extractor (oo_set_semantics, OO_SEM_*).
  */
 #ifndef ORB_ORACLE_H
 #define ORB_ORACLE_H
@@ -32,6 +32,16 @@ typedef struct {
 typedef struct oo_extractor oo_extractor;
 
 oo_extractor* oo_create(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST);
+
+/* OpenCV/compiler behaviours the pixels depend on; same bits as ORBGPU_SEM_* in the
+ * product's include/orbgpu.h (tests/test_oracle_pins.py checks the values agree).  0 = the default:
+ * OpenCV 3.0-3.4.1 on x86-64 (SSE2, no IPP) under the reference's -O3 -march=native on an FMA host. */
+#define OO_SEM_RESIZE_FIXEDPT 0x01 /* cv::resize vertical pass: generic FixedPtCast form, not the 8U form */
+#define OO_SEM_BLUR_SHIFT 2        /* GaussianBlur variant, 3 bits: 0 SSE2_257, 1 SCALAR_257, 2 BITEXACT_256, 3 ED */
+#define OO_SEM_BRIEF_NOFMA 0x20    /* rBRIEF rotation without FMA contraction */
+#define OO_SEM_ALL (OO_SEM_RESIZE_FIXEDPT | (7 << OO_SEM_BLUR_SHIFT) | OO_SEM_BRIEF_NOFMA)
+/* Returns 0, or -1 for an unknown flag combination (the extractor is unchanged then). */
+int oo_set_semantics(oo_extractor* e, int sem);
 void oo_destroy(oo_extractor* e);
 int oo_nlevels(const oo_extractor* e);
 void oo_scale_tables(const oo_extractor* e, float* scale, float* inv_scale, float* sigma2,
@@ -55,8 +65,8 @@ int oo_distribute_octree(const float* xy, const float* resp, int n, int minX, in
                          int N, float* out_xy, float* out_resp);
 
 /* Single-primitive entry points (used by tests to pin pieces). */
-void oo_resize_linear(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh);
-void oo_gaussian7(const uint8_t* src, int w, int h, uint8_t* dst);
+void oo_resize_linear(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh, int sem);
+void oo_gaussian7(const uint8_t* src, int w, int h, uint8_t* dst, int sem);
 int oo_fast_score(const uint8_t* img, int stride, int x, int y);      /* M-1 or -1 (see DESIGN) */
 float oo_fastatan2(float y, float x);
 void oo_sincos(float ang, float* s, float* c);

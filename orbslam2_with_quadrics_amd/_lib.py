@@ -32,8 +32,27 @@ EXPORTS = [
     "orbgpu_compute_stereo_from_rgbd", "orbgpu_compute_stereo_from_rgbd_batch",
     "orbgpu_vocabulary_load_text", "orbgpu_vocabulary_create", "orbgpu_vocabulary_destroy", "orbgpu_vocabulary_info",
     "orbgpu_compute_bow", "orbgpu_compute_bow_batch", "orbgpu_memcpy_h2d_async", "orbgpu_memcpy_d2h_async",
-    "orbgpu_cvt_color_to_gray_batch", "orbgpu_extract_color",
+    "orbgpu_cvt_color_to_gray_batch", "orbgpu_extract_color", "orbgpu_set_semantics", "orbgpu_get_semantics",
 ]
+
+# OpenCV / compiler semantics switch (include/orbgpu.h ORBGPU_SEM_*)
+SEM_DEFAULT = 0x00
+SEM_RESIZE_FIXEDPT = 0x01
+SEM_BLUR_SHIFT = 2
+SEM_BLUR_SSE2_257, SEM_BLUR_SCALAR_257, SEM_BLUR_BITEXACT_256, SEM_BLUR_BITEXACT_ED = (v << 2 for v in range(4))
+SEM_BRIEF_NOFMA = 0x20
+SEM_ROUND1 = SEM_RESIZE_FIXEDPT | SEM_BLUR_SCALAR_257
+# every valid combination: 2 resize forms x 4 blur variants x 2 rotation forms
+SEM_ALL_VARIANTS = [r | b | f for r in (0, SEM_RESIZE_FIXEDPT)
+                    for b in (SEM_BLUR_SSE2_257, SEM_BLUR_SCALAR_257, SEM_BLUR_BITEXACT_256, SEM_BLUR_BITEXACT_ED)
+                    for f in (0, SEM_BRIEF_NOFMA)]
+
+
+def semantics_name(flags: int) -> str:
+    """Human-readable name of a semantics combination (bench lines, test ids)."""
+    blur = ["sse2_257", "scalar_257", "bitexact_256", "bitexact_ed"][(flags >> SEM_BLUR_SHIFT) & 7]
+    return (f"resize={'fixedpt' if flags & SEM_RESIZE_FIXEDPT else 'opencv8u'},blur={blur},"
+            f"brief={'nofma' if flags & SEM_BRIEF_NOFMA else 'fma'}")
 
 # cv::cvtColor codes of the colour entry points (include/orbgpu.h ORBGPU_COLOR_*, OpenCV's values)
 COLOR_BGR2GRAY, COLOR_RGB2GRAY, COLOR_BGRA2GRAY, COLOR_RGBA2GRAY = 6, 7, 10, 11
@@ -93,6 +112,8 @@ def _declare(L):
     L.orbgpu_create.restype = vp
     L.orbgpu_create.argtypes = [i32, i32, f32, i32, i32, i32]
     L.orbgpu_destroy.argtypes = [vp]
+    L.orbgpu_set_semantics.argtypes = [vp, i32]
+    L.orbgpu_get_semantics.argtypes = [vp]
     L.orbgpu_get_levels.argtypes = [vp]
     L.orbgpu_get_scale_factor.restype = f32
     L.orbgpu_get_scale_factor.argtypes = [vp]

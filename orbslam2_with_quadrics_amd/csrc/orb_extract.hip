@@ -1,6 +1,7 @@
 // orb_extract.hip -- gfx950 kernels of ORBextractor::operator() (src/ORBextractor.cc:1043-1105).
 //
-//   k1 og_resize_kernel    : one chained pyramid level (cv::resize INTER_LINEAR 8U, scalar form)
+//   k1 og_resize_kernel    : one chained pyramid level (cv::resize INTER_LINEAR 8U; vertical form per
+//                            ORBGPU_SEM_RESIZE_*)
 //   k2 og_fast_blocks_kernel: one 512-thread workgroup per block of up to 2x2 FAST cells: ROI -> LDS,
 //                            threshold-free quick test, FAST-9 score, same-cell 3x3 NMS, the reference's
 //                            per-cell 20 -> 7 fallback, ballot compaction into the (frame, level) slots
@@ -34,6 +35,18 @@ __device__ __forceinline__ unsigned og_xcd_remap(unsigned orig, unsigned nwg)
 // ------------------------------------------------------------------------------------------------
 // k1: pyramid level l from level l-1 (src/ORBextractor.cc:1120)
 // ------------------------------------------------------------------------------------------------
+// cv::resize's vertical pass on the horizontal sums d0, d1 (<= 255 * 2048) with weights b0 + b1 = 2048:
+//   FX = false: OpenCV's 8U specialisation of VResizeLinear (SSE2 mulhi body and scalar tail alike):
+//               ((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2
+//   FX = true : the generic FixedPtCast form (b0 * d0 + b1 * d1 + 2^21) >> 22
+// All terms are >= 0 and < 2^32 (products < 2^27 after the shift, 2^31 before), results <= 255.
+template <bool FX>
+__device__ __forceinline__ uint32_t og_rz_vert(uint32_t b0, uint32_t d0, uint32_t b1, uint32_t d1)
+{
+    if (FX) return min((__umul24(b0, d0) + __umul24(b1, d1) + (1u << 21)) >> 22, 255u);
+    return min(((__umul24(b0, d0 >> 4) >> 16) + (__umul24(b1, d1 >> 4) >> 16) + 2u) >> 2, 255u);
+}
+
 #define RZ_NT 256
 #define RZ_TW 256                      // output columns per workgroup (64 lanes x 4)
 #define RZ_TH 16                       // output rows per workgroup (4 waves x 4 rows)
@@ -47,6 +60,7 @@ typedef unsigned short og_rz_u16x2 __attribute__((ext_vector_type(2)));
 // misalignment (mis[r]), so any pitch and any frame stride take the same path.  Each output pixel costs
 // 4 LDS byte reads; the arithmetic is the scalar fixed-point form of cv::resize INTER_LINEAR (DESIGN.md
 // §3.1).  The aligned 16-byte blocks read never leave the 16-byte block holding a pixel of the row.
+template <bool FX>
 __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restrict__ src, long long src_pitch,
                                                           long long src_fstride, uint8_t* __restrict__ dst,
                                                           long long dst_pitch, long long dst_fstride, int sw,
@@ -148,9 +162,7 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
                 const uint32_t p1 = __builtin_amdgcn_perm(R1[dwk[k] + 1], R1[dwk[k]], sel[k]);
                 const uint32_t d0 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[k], 0u, false);
                 const uint32_t d1 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[k], 0u, false);
-                // all terms >= 0 and < 2^32: yt.z, yt.w <= 2048, d <= 255 * 2049
-                const uint32_t v = (__umul24((unsigned)yt.z, d0) + __umul24((unsigned)yt.w, d1) + (1u << 21)) >> 22;
-                packed |= min(v, 255u) << (8 * k);
+                packed |= og_rz_vert<FX>((unsigned)yt.z, d0, (unsigned)yt.w, d1) << (8 * k);
             }
             store(r, packed);
         }
@@ -170,9 +182,7 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
             // (a1 == 0 at the right border, where sx+1 may be the column past the tile: reads 0-weighted)
             const int d0 = R0[sx[k]] * a0[k] + (a1[k] ? R0[sx[k] + 1] * a1[k] : 0);
             const int d1 = R1[sx[k]] * a0[k] + (a1[k] ? R1[sx[k] + 1] * a1[k] : 0);
-            int v = (yt.z * d0 + yt.w * d1 + (1 << 21)) >> 22;
-            v = v < 0 ? 0 : (v > 255 ? 255 : v);
-            packed |= (uint32_t)v << (8 * k);
+            packed |= og_rz_vert<FX>((unsigned)yt.z, (unsigned)d0, (unsigned)yt.w, (unsigned)d1) << (8 * k);
         }
         store(r, packed);
     }
@@ -185,11 +195,12 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
 // follows B's tiles through the source index of their first row/column (ytabB[y].x, xtabB[x].x, monotone):
 // tile [y0, y1) x [x0, x1) owns A rows [ytabB[y0].x, ytabB[y1].x) and columns [xtabB[x0].x, xtabB[x1].x),
 // the last tile of a row/column up to the level edge -- a partition of A, so every A pixel is stored once.
-// The arithmetic is og_resize_kernel's (cv::resize INTER_LINEAR, scalar fixed-point form).
+// The arithmetic is og_resize_kernel's (cv::resize INTER_LINEAR fixed point, og_rz_vert).
 // ------------------------------------------------------------------------------------------------
 
 // 4 horizontally adjacent outputs of one row from two LDS source rows: sx = byte offsets in the rows, weights
 // (a0, a1) per column (a1 = 0 at the right border), vertical weights (yz, yw)
+template <bool FX>
 __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t* R1, const int* sx,
                                                const og_rz_u16x2* wt, unsigned yz, unsigned yw)
 {
@@ -200,8 +211,7 @@ __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t*
         const uint32_t p1 = (uint32_t)R1[sx[k]] | ((uint32_t)R1[sx[k] + 1] << 16);
         const uint32_t d0 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[k], 0u, false);
         const uint32_t d1 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[k], 0u, false);
-        const uint32_t v = (__umul24(yz, d0) + __umul24(yw, d1) + (1u << 21)) >> 22;
-        packed |= min(v, 255u) << (8 * k);
+        packed |= og_rz_vert<FX>(yz, d0, yw, d1) << (8 * k);
     }
     return packed;
 }
@@ -227,6 +237,7 @@ __device__ __forceinline__ void og_rz_store4(uint8_t* Dr, uint32_t packed, int n
     }
 }
 
+template <bool FX>
 __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __restrict__ src, long long src_pitch,
                                                            long long src_fstride, uint8_t* __restrict__ dstA,
                                                            long long pitchA, uint8_t* __restrict__ dstB,
@@ -313,7 +324,7 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
             const int4 yt = YA[rr];
             const int r = ar0 + rr;
             const int r0 = yt.x - sr0, r1 = yt.y - sr0;
-            const uint32_t packed = og_rz_quad(S + r0 * g.SC + mis[r0], S + r1 * g.SC + mis[r1], sxA, wtA,
+            const uint32_t packed = og_rz_quad<FX>(S + r0 * g.SC + mis[r0], S + r1 * g.SC + mis[r1], sxA, wtA,
                                                (unsigned)yt.z, (unsigned)yt.w);
             *(uint32_t*)&A[rr * g.AC + 4 * qa] = packed;
             if (r < own_r1 && own_c) og_rz_store4(DA + (long long)r * pitchA + cA, packed, nown);
@@ -331,7 +342,7 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
         const int r = 4 * rg + q;
         if (r >= nyB) break;
         const int4 yt = YB[r];
-        const uint32_t packed = og_rz_quad(A + (yt.x - ar0) * g.AC, A + (yt.y - ar0) * g.AC, sxB, wtB, (unsigned)yt.z,
+        const uint32_t packed = og_rz_quad<FX>(A + (yt.x - ar0) * g.AC, A + (yt.y - ar0) * g.AC, sxB, wtB, (unsigned)yt.z,
                                            (unsigned)yt.w);
         og_rz_store4(DB + (long long)(by0 + r) * pitchB, packed, n);
     }
@@ -1248,6 +1259,11 @@ constexpr OgDisk og_make_disk()
     return d;
 }
 __constant__ OgDisk og_disk = og_make_disk();
+// GaussianBlur 7x7 sigma 2 integer kernels by ORBGPU_SEM_BLUR_* variant, c0 | c1 << 8 | c2 << 16 | c3 << 24 for
+// [c0,c1,c2,c3,c2,c1,c0]: cvRound(256 g) (sum 257) twice, the bit-exact kernel with centre 256 - 2 sum(sides),
+// the error-diffused bit-exact kernel
+__constant__ uint32_t og_blur_coefs[4] = {18u | 34u << 8 | 49u << 16 | 55u << 24, 18u | 34u << 8 | 49u << 16 | 55u << 24,
+                                          18u | 34u << 8 | 49u << 16 | 54u << 24, 18u | 34u << 8 | 48u << 16 | 56u << 24};
 
 #ifndef OG_DK_BLOCKSYNC
 #define OG_DK_BLOCKSYNC 0
@@ -1381,13 +1397,19 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     }
     const float angle = og_fast_atan2((float)m01, (float)m10);
     // ---- 7x7 Gaussian (sigma 2, BORDER_REFLECT_101) of the 37x37 window the tests can reach.  Integer
-    // weights gk[i]*gk[j] summed exactly and rounded once ((acc + 2^15) >> 16), so any factoring is exact:
+    // weights gk[i]*gk[j] summed exactly and rounded once, so any factoring is exact.  The kernel
+    // [c0,c1,c2,c3,c2,c1,c0] and the rounding follow the context's ORBGPU_SEM_BLUR_* variant:
+    // (acc + 2^15) >> 16, except that the SSE2 variant rounds ties half-to-even in columns x < 4*floor(w/4)
+    // (OpenCV 3.x SymmColumnVec_32s8u: float sums, cvtps2dq).
     // horizontal pass with v_dot4_u32_u8 (taps 0-3 and 4-6 of a byte window), vertical pass with
     // v_dot2_u32_u16 over row pairs of the horizontal sums (<= 257 * 255 = 65535, exact in u16).
     // horizontal: item = (row pair rp, 4-column group g): rows 2rp, 2rp+1, outputs 4g..4g+3, stored as
     // (row 2rp, row 2rp+1) u16 pairs Hp[rp][col]
+    const int bvar = (P.sem >> ORBGPU_SEM_BLUR_SHIFT) & 7;
+    const uint32_t gc = og_blur_coefs[bvar & 3];  // c0 | c1 << 8 | c2 << 16 | c3 << 24
+    const uint32_t c0 = gc & 0xff, c1 = (gc >> 8) & 0xff, c2 = (gc >> 16) & 0xff, c3 = gc >> 24;
     if (active) {
-        const uint32_t glo = 18u | (34u << 8) | (49u << 16) | (55u << 24), ghi = 49u | (34u << 8) | (18u << 16);
+        const uint32_t glo = gc, ghi = c2 | (c1 << 8) | (c0 << 16);
         for (int it = lane; it < HP_ROWS * 10; it += 64) {
             const int rp = it / 10, g = it - rp * 10;
             uint32_t hv[2][4];
@@ -1416,8 +1438,12 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     // (g0,g1)(g2,g3)(g4,g5)(g6,0), odd rows (0,g0)(g1,g2)(g3,g4)(g5,g6)
     if (active) {
         typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
-        const u16x2v e0 = {18, 34}, e1 = {49, 55}, e2 = {49, 34}, e3 = {18, 0};
-        const u16x2v o0 = {0, 18}, o1 = {34, 49}, o2 = {55, 49}, o3 = {34, 18};
+        const unsigned short s0 = (unsigned short)c0, s1 = (unsigned short)c1, s2 = (unsigned short)c2,
+                             s3 = (unsigned short)c3;
+        const u16x2v e0 = {s0, s1}, e1 = {s2, s3}, e2 = {s2, s1}, e3 = {s0, 0};
+        const u16x2v o0 = {0, s0}, o1 = {s1, s2}, o2 = {s3, s2}, o3 = {s1, s0};
+        // level column of window column c is cx - 18 + c (inside the level: keypoints sit >= 19 px from the edge)
+        const int xsimd = bvar == 0 ? ((lw & ~3) - (cx - 18)) : 0;  // window columns c < xsimd round half-to-even
         for (int it = lane; it < BL_W * 10; it += 64) {
             const int m = it / BL_W, c = it - m * BL_W;
             u16x2v pr[5];
@@ -1435,8 +1461,11 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
                 ao = __builtin_amdgcn_udot2(q[1], o1, ao, false);
                 ao = __builtin_amdgcn_udot2(q[2], o2, ao, false);
                 ao = __builtin_amdgcn_udot2(q[3], o3, ao, false);
-                if (r0 < BL_W) Bl[r0 * BL_W + c] = (uint8_t)min((ae + (1u << 15)) >> 16, 255u);
-                if (r0 + 1 < BL_W) Bl[(r0 + 1) * BL_W + c] = (uint8_t)min((ao + (1u << 15)) >> 16, 255u);
+                const bool rne = c < xsimd;  // a tie with an even quotient rounds down there
+                const uint32_t ve = ((ae + (1u << 15)) >> 16) - (rne && (ae & 0x1ffffu) == 0x8000u);
+                const uint32_t vo = ((ao + (1u << 15)) >> 16) - (rne && (ao & 0x1ffffu) == 0x8000u);
+                if (r0 < BL_W) Bl[r0 * BL_W + c] = (uint8_t)min(ve, 255u);
+                if (r0 + 1 < BL_W) Bl[(r0 + 1) * BL_W + c] = (uint8_t)min(vo, 255u);
             }
         }
     }
@@ -1447,6 +1476,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     float a, b;
     og_sincosf(angle * factorPI, &b, &a);
     const uint8_t* ctr = Bl + 18 * BL_W + 18;
+    const bool nofma = (P.sem & ORBGPU_SEM_BRIEF_NOFMA) != 0;
     u64 words[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
@@ -1456,8 +1486,10 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 #pragma unroll
         for (int q = 0; q < 2; q++) {
             const float x = (float)pt[2 * q], y = (float)pt[2 * q + 1];
-            const int row = og_cvround(__builtin_fmaf(x, b, y * a));
-            const int col = og_cvround(__builtin_fmaf(x, a, -(y * b)));
+            // GCC -O3 -march=native contracts the first product of GET_VALUE into an FMA; a
+            // build without contraction rounds both products (the kernels are compiled -ffp-contract=off)
+            const int row = nofma ? og_cvround(x * b + y * a) : og_cvround(__builtin_fmaf(x, b, y * a));
+            const int col = nofma ? og_cvround(x * a - y * b) : og_cvround(__builtin_fmaf(x, a, -(y * b)));
             val[q] = ctr[row * BL_W + col];
         }
         words[t] = __ballot(val[0] < val[1]);
@@ -1600,27 +1632,40 @@ hipError_t og_read_oct_prof(unsigned long long* out, int n)
 
 void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,
                       long long dst_pitch, long long dst_fstride, int sw, int sh, int dw, int dh, const int4* xtab,
-                      const int4* ytab, int xmax, int* status, int B)
+                      const int4* ytab, int xmax, int* status, int B, int sem)
 {
     dim3 grid((dw + RZ_TW - 1) / RZ_TW, (dh + RZ_TH - 1) / RZ_TH, B);
-    hipLaunchKernelGGL(og_resize_kernel, grid, dim3(RZ_NT), 0, s, src, src_pitch, src_fstride, dst, dst_pitch,
-                       dst_fstride, sw, sh, dw, dh, xtab, ytab, xmax, status);
+    if (sem & ORBGPU_SEM_RESIZE_FIXEDPT)
+        hipLaunchKernelGGL(og_resize_kernel<true>, grid, dim3(RZ_NT), 0, s, src, src_pitch, src_fstride, dst, dst_pitch,
+                           dst_fstride, sw, sh, dw, dh, xtab, ytab, xmax, status);
+    else
+        hipLaunchKernelGGL(og_resize_kernel<false>, grid, dim3(RZ_NT), 0, s, src, src_pitch, src_fstride, dst,
+                           dst_pitch, dst_fstride, sw, sh, dw, dh, xtab, ytab, xmax, status);
+}
+
+// the fused resize takes up to 64 KB of dynamic LDS: set once per device (the attribute is per device), from
+// orbgpu_create after hipSetDevice
+hipError_t og_prepare_device()
+{
+    hipError_t e = hipFuncSetAttribute((const void*)og_resize2_kernel<false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)og_resize2_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               64 * 1024);
 }
 
 void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dstA,
                        long long pitchA, uint8_t* dstB, long long pitchB, long long dst_fstride, const OgRz2Geom& g,
-                       int* status, int B)
+                       int* status, int B, int sem)
 {
     const size_t shm = og_rz2_lds_bytes(g.SR, g.SC, g.AR, g.AC);
-    static bool lds_attr = false;
-    if (!lds_attr) {
-        (void)hipFuncSetAttribute((const void*)og_resize2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  64 * 1024);
-        lds_attr = true;
-    }
     dim3 grid((g.bw + RZ_TW - 1) / RZ_TW, (g.bh + RZ2_TH - 1) / RZ2_TH, B);
-    hipLaunchKernelGGL(og_resize2_kernel, grid, dim3(RZ2_NT), shm, s, src, src_pitch, src_fstride, dstA, pitchA, dstB,
-                       pitchB, dst_fstride, g, status);
+    if (sem & ORBGPU_SEM_RESIZE_FIXEDPT)
+        hipLaunchKernelGGL(og_resize2_kernel<true>, grid, dim3(RZ2_NT), shm, s, src, src_pitch, src_fstride, dstA,
+                           pitchA, dstB, pitchB, dst_fstride, g, status);
+    else
+        hipLaunchKernelGGL(og_resize2_kernel<false>, grid, dim3(RZ2_NT), shm, s, src, src_pitch, src_fstride, dstA,
+                           pitchA, dstB, pitchB, dst_fstride, g, status);
 }
 
 void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,

@@ -48,6 +48,7 @@ struct orbgpu_ctx {
     hipEvent_t done = nullptr;
     // ORBextractor parameters and scale tables (src/ORBextractor.cc:410-470)
     int nfeatures = 0, nlevels = 0, iniTh = 0, minTh = 0;
+    int sem = ORBGPU_SEM_DEFAULT;  // OpenCV/compiler semantics (orbgpu_set_semantics)
     double scaleFactor = 0;  // `double scaleFactor` member, include/ORBextractor.h:98
     std::vector<float> sf, isf, sig2, isig2;
     std::vector<int> nfeat;
@@ -176,6 +177,7 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
     }
     OgPlan P{};
     P.nlevels = c->nlevels;
+    P.sem = c->sem;
     P.iniTh = c->iniTh;
     P.minTh = c->minTh;
     std::memcpy(P.umax, c->umax, sizeof(P.umax));
@@ -473,11 +475,11 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
                         c->tabs.p + Ln.xtab_off, c->tabs.p + Ln.ytab_off, Ln.xmax, L.fz_SR, L.fz_SC, L.fz_AR, L.fz_AC,
                         c->tabs.p + L.fz_tile_off};
             og_launch_resize2(s, src, sp, sfs, c->pyr.p + L.pyr_off, L.pitch, c->pyr.p + Ln.pyr_off, Ln.pitch,
-                              P.pyr_per_frame, g, c->status.p, B);
+                              P.pyr_per_frame, g, c->status.p, B, P.sem);
             l += 2;
         } else {
             og_launch_resize(s, src, sp, sfs, c->pyr.p + L.pyr_off, L.pitch, P.pyr_per_frame, Lp.w, Lp.h, L.w, L.h,
-                             c->tabs.p + L.xtab_off, c->tabs.p + L.ytab_off, L.xmax, c->status.p, B);
+                             c->tabs.p + L.xtab_off, c->tabs.p + L.ytab_off, L.xmax, c->status.p, B, P.sem);
             l += 1;
         }
     }
@@ -546,7 +548,8 @@ orbgpu_ctx* orbgpu_create(int device, int nfeatures, float scaleFactor, int nlev
     orbgpu_ctx* c = new orbgpu_ctx();
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess || og_upload_pattern(device) != hipSuccess) {
+        hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess || og_upload_pattern(device) != hipSuccess ||
+        og_prepare_device() != hipSuccess) {
         delete c;
         return nullptr;
     }
@@ -598,6 +601,20 @@ orbgpu_ctx* orbgpu_create(int device, int nfeatures, float scaleFactor, int nlev
     }
     return c;
 }
+
+int orbgpu_set_semantics(orbgpu_ctx* c, int flags)
+{
+    if (!c) return ORBGPU_ERR_ARG;
+    if ((flags & ~ORBGPU_SEM_ALL) || (flags & ORBGPU_SEM_BLUR_MASK) > ORBGPU_SEM_BLUR_BITEXACT_ED) {
+        c->err = "unknown semantics flags";
+        return ORBGPU_ERR_ARG;
+    }
+    c->sem = flags;
+    c->plan.sem = flags;  // the plan is passed by value to each launch: takes effect at the next extraction
+    return ORBGPU_OK;
+}
+
+int orbgpu_get_semantics(const orbgpu_ctx* c) { return c ? c->sem : ORBGPU_ERR_ARG; }
 
 void orbgpu_destroy(orbgpu_ctx* c)
 {

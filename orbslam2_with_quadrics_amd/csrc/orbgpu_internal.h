@@ -12,6 +12,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "../../include/orbgpu.h"  // ORBGPU_SEM_* (semantics switch)
+
 // umax of src/ORBextractor.cc:454-469 for HALF_PATCH_SIZE = 15 (the reference's constant); the describe
 // kernel's flattened IC_Angle disk is built from it at compile time
 #define OG_UMAX 15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3
@@ -57,6 +59,7 @@ struct OgCell {            // one FAST block of up to 2x2 cells (ROI union), src
 
 struct OgPlan {
     int nlevels;
+    int sem;               // ORBGPU_SEM_* of the context (include/orbgpu.h)
     int iniTh, minTh;
     int total_cells;
     int kcap_total;        // sum of kcap (octree slots per frame)

@@ -41,10 +41,11 @@ static inline size_t og_rz2_lds_bytes(int SR, int SC, int AR, int AC)
 }
 void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dstA,
                        long long pitchA, uint8_t* dstB, long long pitchB, long long dst_fstride, const OgRz2Geom& g,
-                       int* status, int B);
+                       int* status, int B, int sem);
 void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,
                       long long dst_pitch, long long dst_fstride, int sw, int sh, int dw, int dh, const int4* xtab,
-                      const int4* ytab, int xmax, int* status, int B);
+                      const int4* ytab, int xmax, int* status, int B, int sem);
+hipError_t og_prepare_device();  // per-device kernel attributes (call after hipSetDevice)
 void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,
                     long long fstride0, const uint8_t* pyr, unsigned long long* cand, int* cand_count, int* status,
                     int B);

@@ -25,12 +25,18 @@ class ORBextractor:
     """ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST) on HIP device `device`."""
 
     def __init__(self, nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int, minThFAST: int,
-                 device: int = 0):
+                 device: int = 0, semantics: int = _lib.SEM_DEFAULT):
         self._L = _lib.lib()
         self._ctx = self._L.orbgpu_create(device, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
         if not self._ctx:
             raise RuntimeError("orbgpu_create failed (no HIP device visible, or invalid parameters)")
         self.nfeatures, self.nlevels = nfeatures, nlevels
+        self.set_semantics(semantics)
+
+    def set_semantics(self, flags: int):
+        """OpenCV/compiler behaviours to reproduce (_lib.SEM_*, include/orbgpu.h ORBGPU_SEM_*)."""
+        _lib.check(self._ctx, self._L.orbgpu_set_semantics(self._ctx, int(flags)), "orbgpu_set_semantics")
+        self.semantics = int(flags)
 
     def close(self):
         if getattr(self, "_ctx", None):

@@ -2,7 +2,9 @@
 
 sincosf.json        : (angle, sinf, cosf) triples from the host libm's sincosf (glibc 2.35, FMA variant)
                       at angles the ORB path produces (fastAtan2 outputs * pi/180) plus edge cases.
-extract_golden.json : the oracle's ORB extraction of seeded synthetic frames (hashes + first rows).
+extract_golden.json : the oracle's ORB extraction of seeded synthetic frames (hashes + first rows), at the default
+                      semantics for every shape and at all 16 semantics variants (ORBGPU_SEM_*: resize form x
+                      GaussianBlur variant x rBRIEF FMA) for the config-2 and config-3 shapes.
                       This pins the oracle against regressions; it is NOT a reference-binary output
                       (the reference cannot be built here -- DESIGN.md §4).
 match_golden.json   : oracle SearchForInitialization on a seeded 1080p pair (match vector hash).
@@ -47,12 +49,17 @@ def sincos_vectors():
 
 
 def extract_cases():
+    from orbslam2_with_quadrics_amd import _lib
+
     cases = []
-    for fid, rows, cols, nf in [(3, 480, 640, 1000), (5, 376, 1241, 2000), (7, 1080, 1920, 2000)]:
+    todo = [(3, 480, 640, 1000, s) for s in _lib.SEM_ALL_VARIANTS] + [(5, 376, 1241, 2000, 0)] + \
+        [(7, 1080, 1920, 2000, s) for s in _lib.SEM_ALL_VARIANTS]
+    for fid, rows, cols, nf, sem in todo:
         img = synthetic.frame(fid, rows, cols)
-        k, d = O.OracleExtractor(nf)(img)
+        k, d = O.OracleExtractor(nf, semantics=sem)(img)
         head = np.stack([k["x"], k["y"], k["angle"], k["response"]], 1)[:12].astype(np.float64).tolist()
-        cases.append(dict(frame_id=fid, rows=rows, cols=cols, nfeatures=nf, n=int(len(k)),
+        cases.append(dict(frame_id=fid, rows=rows, cols=cols, nfeatures=nf, semantics=sem,
+                          semantics_name=_lib.semantics_name(sem), n=int(len(k)),
                           image_sha256=hashlib.sha256(img.tobytes()).hexdigest(),
                           kps_sha256=hashlib.sha256(k.tobytes()).hexdigest(),
                           desc_sha256=hashlib.sha256(d.tobytes()).hexdigest(), head=head))
@@ -77,6 +84,35 @@ def match_cases():
                           prev_sha256=hashlib.sha256(prev2.tobytes()).hexdigest()))
     json.dump({"generator": "oracle SearchForInitialization via tests/golden/make_golden.py", "cases": cases},
               open(os.path.join(OUT, "match_golden.json"), "w"), indent=1)
+
+
+def fma_probe_base(seed):
+    """Base image of the FMA-rotation probe (tools/find_fma_probe.py): flat 100 +- 3 texture, 24 bright 14-px
+    squares (180) whose top-left corner pixel (255) is the unique FAST maximum, each with a random rectangle in
+    the disk above-left of it so that the corners' IC angles differ.  Returns (image, corner list)."""
+    r = np.random.default_rng(seed)
+    img = np.full((480, 640), 100, np.int64)
+    corners = []
+    for i in range(4):
+        for j in range(6):
+            y0, x0 = 60 + i * 110, 60 + j * 95
+            img[y0:y0 + 14, x0:x0 + 14] = 180
+            h, w = r.integers(3, 9, 2)
+            oy, ox = r.integers(-13, -7, 2)
+            img[y0 + oy:y0 + oy + h, x0 + ox:x0 + ox + w] = r.integers(110, 250)
+            corners.append((x0, y0))
+    img = np.clip(img + r.integers(-3, 4, img.shape), 0, 255)
+    for (x0, y0) in corners:
+        img[y0, x0] = 255
+    return img.astype(np.uint8), corners
+
+
+def fma_probe_image(seed, mods):
+    """The probe image: the base plus the committed low-contrast dust [(x, y, delta), ...]."""
+    img = fma_probe_base(seed)[0].astype(np.int64)
+    for x, y, d in mods:
+        img[y, x] += d
+    return np.clip(img, 0, 255).astype(np.uint8)
 
 
 def config5_mappoints(k, d, M, seed):

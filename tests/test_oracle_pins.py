@@ -167,7 +167,7 @@ def test_oracle_golden_extraction(oracle):
     for case in g["cases"]:
         img = synthetic.frame(case["frame_id"], case["rows"], case["cols"])
         assert hashlib.sha256(img.tobytes()).hexdigest() == case["image_sha256"]
-        k, d = oracle.OracleExtractor(case["nfeatures"])(img)
+        k, d = oracle.OracleExtractor(case["nfeatures"], semantics=case.get("semantics", 0))(img)
         assert len(k) == case["n"]
         assert hashlib.sha256(k.tobytes()).hexdigest() == case["kps_sha256"]
         assert hashlib.sha256(d.tobytes()).hexdigest() == case["desc_sha256"]
@@ -204,3 +204,223 @@ def test_oracle_golden_tracking_and_stereo(oracle):
         assert n == case["nmatches"]
         assert hashlib.sha256(ur.tobytes()).hexdigest() == case["uright_sha256"]
         assert hashlib.sha256(de.tobytes()).hexdigest() == case["depth_sha256"]
+
+
+# ---------------------------------------------------------------------------------------------------------
+# OpenCV / compiler semantics variants (ORBGPU_SEM_*): each oracle form against an independent
+# numpy restatement of the OpenCV code path it stands for
+# ---------------------------------------------------------------------------------------------------------
+SEM_BLUR_SSE2_257, SEM_BLUR_SCALAR_257, SEM_BLUR_BITEXACT_256, SEM_BLUR_BITEXACT_ED = (v << 2 for v in range(4))
+
+
+def _resize_tables(n_src, n_dst):
+    """resizeGeneric_ coefficient tables of one axis (float32 fx, cvFloor, clamps, cvRound(x * 2048))."""
+    scale = 1.0 / (n_dst / n_src)
+    ofs, a0, a1, vmax = [], [], [], n_dst
+    for d in range(n_dst):
+        f = np.float32((d + 0.5) * scale - 0.5)
+        s = int(np.floor(f))
+        f = np.float32(f - np.float32(s))
+        if s < 0:
+            f, s = np.float32(0), 0
+        if s + 1 >= n_src:
+            vmax = min(vmax, d)
+            if s >= n_src - 1:
+                f, s = np.float32(0), n_src - 1
+        ofs.append(s)
+        a0.append(int(np.rint(np.float32(np.float32(1) - f) * np.float32(2048))))
+        a1.append(int(np.rint(f * np.float32(2048))))
+    return np.array(ofs), np.array(a0), np.array(a1), vmax
+
+
+def _sat16(v):
+    return np.clip(v, -32768, 32767)
+
+
+def _resize_sse2(src, dw, dh):
+    """cv::resize INTER_LINEAR 8U as OpenCV 3.x runs it on x86-64: HResizeLinear (exact int), then
+    VResizeLinearVec_32s8u's instruction sequence srai(4) / packs_epi32 / mulhi_epi16 / adds_epi16 /
+    adds(2) / srai(2) / packus_epi16, emulated lane by lane."""
+    sh, sw = src.shape
+    xo, xa0, xa1, xmax = _resize_tables(sw, dw)
+    yo, yb0, yb1, _ = _resize_tables(sh, dh)
+    S = src.astype(np.int64)
+    nx = np.minimum(xo + 1, sw - 1)
+    D = np.where(np.arange(dw) < xmax, S[:, xo] * xa0 + S[:, nx] * xa1, S[:, xo] * 2048)
+    out = np.zeros((dh, dw), np.uint8)
+    for y in range(dh):
+        r0 = min(max(yo[y], 0), sh - 1)
+        r1 = min(max(yo[y] + 1, 0), sh - 1)
+        x0, x1 = _sat16(D[r0] >> 4), _sat16(D[r1] >> 4)
+        m = _sat16(((x0 * yb0[y]) >> 16) + ((x1 * yb1[y]) >> 16))
+        out[y] = np.clip(_sat16(m + 2) >> 2, 0, 255)
+    return out
+
+
+def test_resize_opencv_8u_form_vs_sse2_sequence(oracle):
+    """Default resize semantics == OpenCV's SSE2 VResizeLinearVec_32s8u body over the whole row (its 8U
+    VResizeLinear specialisation makes the scalar tail compute the same form); the FIXEDPT variant is the
+    generic (b0*D0 + b1*D1 + 2^21) >> 22 and does differ from it."""
+    from orbslam2_with_quadrics_amd import synthetic
+
+    rng = np.random.default_rng(3)
+    differs = 0
+    for (h, w) in [(480, 640), (400, 533), (376, 1241), (1080, 1920), (97, 61)]:
+        src = synthetic.frame(int(rng.integers(1000)), h, w) if h > 100 else rng.integers(0, 256, (h, w), np.uint8)
+        dw, dh = int(np.rint(np.float32(w) / np.float32(1.2))), int(np.rint(np.float32(h) / np.float32(1.2)))
+        got = oracle.resize_linear(src, dw, dh, 0)
+        assert np.array_equal(got, _resize_sse2(src, dw, dh)), (h, w)
+        differs += int((oracle.resize_linear(src, dw, dh, 0x01) != got).sum())
+    assert differs > 0
+
+
+def _gauss_kernels():
+    """The integer 7x7 sigma-2 kernels of the three OpenCV generations, from the double-precision Gaussian."""
+    x = np.arange(7) - 3.0
+    g = np.exp(-0.125 * x * x)
+    g = g / g.sum()
+    legacy = [int(np.rint(np.float32(v) * 256)) for v in g.astype(np.float32)]   # cvRound(256 * float kernel)
+    sides = [int(np.rint(v * 256)) for v in g[:3]]
+    bitexact = sides + [256 - 2 * sum(sides)] + sides[::-1]                       # centre = 1 - sum(sides)
+    ed, err = [], 0.0                                                            # error-diffused rounding
+    for v in g[:3]:
+        adj = v * 256 + err
+        q = int(np.rint(adj))
+        err = adj - q
+        ed.append(q)
+    ed = ed + [256 - 2 * sum(ed)] + ed[::-1]
+    return legacy, bitexact, ed
+
+
+def test_gaussian_kernel_tables_all_variants():
+    legacy, bitexact, ed = _gauss_kernels()
+    assert legacy == [18, 34, 49, 55, 49, 34, 18]
+    assert bitexact == [18, 34, 49, 54, 49, 34, 18]
+    assert ed == [18, 34, 48, 56, 48, 34, 18]
+
+
+def _reflect101(i, n):
+    i = np.abs(i)
+    return np.where(i >= n, 2 * n - 2 - i, i)
+
+
+def _blur_rows(img, k):
+    h, w = img.shape
+    I = img.astype(np.int64)
+    xs = np.arange(w)
+    return sum(k[t] * I[:, _reflect101(xs + t - 3, w)] for t in range(7))
+
+
+def _blur_sse2(img):
+    """OpenCV 3.0-3.4.1 GaussianBlur on x86-64 (no IPP): exact integer row sums (SymmRowSmallVec_8u32s), then
+    SymmColumnVec_32s8u in float32 -- centre * f0 + (up_k + down_k) * f_k, f = k / 65536 -- rounded by cvtps2dq
+    (half-to-even) for x < 4 * floor(w / 4); SymmColumnFilter's scalar tail (S + 2^15) >> 16 after that."""
+    k = [18, 34, 49, 55, 49, 34, 18]
+    h, w = img.shape
+    R = _blur_rows(img, k)
+    ys = np.arange(h)
+    f = [np.float32(k[3 + t] / 65536.0) for t in range(4)]
+    s = R[_reflect101(ys, h)].astype(np.float32) * f[0]
+    for t in range(1, 4):
+        pair = (R[_reflect101(ys - t, h)] + R[_reflect101(ys + t, h)]).astype(np.float32)
+        s = (s + pair * f[t]).astype(np.float32)
+    vec = np.clip(np.rint(s), 0, 255)
+    S = sum(k[t] * R[_reflect101(ys + t - 3, h)] for t in range(7))
+    tail = np.clip((S + (1 << 15)) >> 16, 0, 255)
+    xs = np.arange(w)[None, :]
+    return np.where(xs < (w & ~3), vec, tail).astype(np.uint8)
+
+
+def _blur_fixed(img, k):
+    h, w = img.shape
+    R = _blur_rows(img, k)
+    S = sum(k[t] * R[_reflect101(np.arange(h) + t - 3, h)] for t in range(7))
+    return np.clip((S + (1 << 15)) >> 16, 0, 255).astype(np.uint8)
+
+
+def test_gaussian_variants_vs_restatements(oracle):
+    """Each GaussianBlur variant of the oracle against an independent restatement of its OpenCV code path;
+    binarised images make the half-to-even ties frequent, so the SSE2 and scalar variants do differ."""
+    from orbslam2_with_quadrics_amd import synthetic
+
+    legacy, bitexact, ed = _gauss_kernels()
+    ties = 0
+    for fid, (h, w) in enumerate([(480, 640), (313, 1034), (61, 43), (37, 41)]):
+        img = synthetic.frame(fid + 50, h, w) if h > 100 else np.random.default_rng(fid).integers(0, 256, (h, w))
+        img = (np.asarray(img, np.uint8) & 0x80) | 0x10 if fid % 2 == 0 else np.asarray(img, np.uint8)
+        sse2 = oracle.gaussian7(img, SEM_BLUR_SSE2_257)
+        assert np.array_equal(sse2, _blur_sse2(img)), (h, w)
+        scalar = oracle.gaussian7(img, SEM_BLUR_SCALAR_257)
+        assert np.array_equal(scalar, _blur_fixed(img, legacy))
+        assert np.array_equal(oracle.gaussian7(img, SEM_BLUR_BITEXACT_256), _blur_fixed(img, bitexact))
+        assert np.array_equal(oracle.gaussian7(img, SEM_BLUR_BITEXACT_ED), _blur_fixed(img, ed))
+        ties += int((sse2 != scalar).sum())
+    assert ties > 0
+
+
+def test_semantics_constants_agree():
+    """include/orbgpu.h ORBGPU_SEM_* and the oracle's OO_SEM_* use the same bits."""
+    hdr = open(os.path.join(ROOT, "include", "orbgpu.h")).read()
+    ora = open(os.path.join(ROOT, "oracle", "orb_oracle.h")).read()
+
+    def val(txt, name):
+        return int(re.search(r"#define " + name + r"\s+(0x[0-9a-fA-F]+|\d+)", txt).group(1), 0)
+
+    assert val(hdr, "ORBGPU_SEM_RESIZE_FIXEDPT") == val(ora, "OO_SEM_RESIZE_FIXEDPT") == 0x01
+    assert val(hdr, "ORBGPU_SEM_BLUR_SHIFT") == val(ora, "OO_SEM_BLUR_SHIFT") == 2
+    assert val(hdr, "ORBGPU_SEM_BRIEF_NOFMA") == val(ora, "OO_SEM_BRIEF_NOFMA") == 0x20
+    from orbslam2_with_quadrics_amd import _lib
+
+    assert (_lib.SEM_RESIZE_FIXEDPT, _lib.SEM_BLUR_SHIFT, _lib.SEM_BRIEF_NOFMA) == (0x01, 2, 0x20)
+
+
+def test_rbrief_fma_probe_golden(oracle):
+    """tests/golden/semantics_probe.json (tools/find_fma_probe.py): an image on which the FMA and the non-FMA
+    rBRIEF rotation give different descriptors; the oracle reproduces both committed hashes."""
+    sys.path.insert(0, GOLDEN)
+    import make_golden
+
+    g = json.load(open(os.path.join(GOLDEN, "semantics_probe.json")))
+    img = make_golden.fma_probe_image(g["seed"], g["mods"])
+    ka, da = oracle.OracleExtractor(g["nfeatures"])(img)
+    kb, db = oracle.OracleExtractor(g["nfeatures"], semantics=0x20)(img)
+    assert hashlib.sha256(ka.tobytes()).hexdigest() == hashlib.sha256(kb.tobytes()).hexdigest() == g["kps_sha256"]
+    assert hashlib.sha256(da.tobytes()).hexdigest() == g["desc_fma_sha256"]
+    assert hashlib.sha256(db.tobytes()).hexdigest() == g["desc_nofma_sha256"]
+    assert int((da != db).any(1).sum()) == g["descriptors_differing"] > 0
+
+
+def test_rbrief_nofma_form_vs_restatement(oracle):
+    """The non-FMA rotation recomputed in numpy float32 (two rounded products) from the oracle's own angle and
+    blurred level reproduces the oracle's NOFMA descriptors on the probe image; the FMA form with refpy's exact
+    fmaf reproduces the default ones."""
+    sys.path.insert(0, GOLDEN)
+    import make_golden
+
+    g = json.load(open(os.path.join(GOLDEN, "semantics_probe.json")))
+    img = make_golden.fma_probe_image(g["seed"], g["mods"])
+    ex = oracle.OracleExtractor(g["nfeatures"], semantics=0x20)
+    k, d_nofma = ex(img)
+    _, d_fma = oracle.OracleExtractor(g["nfeatures"])(img)
+    txt = open(os.path.join(ROOT, "oracle", "orb_pattern.inc")).read()
+    pat = np.array([int(v) for v in re.findall(r"-?\d+", txt[txt.index("{") + 1:txt.index("};")])]).reshape(256, 4)
+    blurred = oracle.gaussian7(ex.level(0), 0)
+    F = np.float32
+    rows = np.nonzero((d_nofma != d_fma).any(1) & (k["octave"] == 0))[0]
+    assert len(rows) > 0
+    for i in rows:
+        s, c = oracle.sincos(F(F(k["angle"][i]) * F(3.14159265358979323846 / 180.0)))
+        a, b = F(c), F(s)
+        cx, cy = int(np.rint(k["x"][i])), int(np.rint(k["y"][i]))
+        for form, want in (("nofma", d_nofma[i]), ("fma", d_fma[i])):
+            bits = []
+            for x0, y0, x1, y1 in pat:
+                v = []
+                for x, y in ((F(x0), F(y0)), (F(x1), F(y1))):
+                    if form == "nofma":
+                        r, q = F(F(x * b) + F(y * a)), F(F(x * a) - F(y * b))
+                    else:
+                        r, q = refpy.fmaf(x, b, F(y * a)), refpy.fmaf(x, a, -F(y * b))
+                    v.append(int(blurred[cy + int(np.rint(r)), cx + int(np.rint(q))]))
+                bits.append(v[0] < v[1])
+            assert np.array_equal(np.packbits(np.array(bits, np.uint8), bitorder="little"), want), (form, i)
