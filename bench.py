@@ -5,7 +5,8 @@ One step = one batch of B synthetic 1920x1080 frames already resident in HBM, pe
     src/ORBextractor.cc:1043-1105) -- pyramid, FAST cells, octree, orientation, blur + rBRIEF, grid;
   * vbPrevMatched := F1 keypoints (src/Tracking.cc:573-575) and SearchForInitialization(F1, F_b) for every
     frame b (src/ORBmatcher.cc:405-520; window 100, ratio 0.9, orientation check, src/Tracking.cc:599-600);
-  * (N > 1) RCCL all-gather of the per-frame keypoint counts (the only collective of the path).
+  * (N > 1) rank 0 extracts F1 and broadcasts it (RCCL, one ~120 KB record per step) to the other ranks, which
+    match their own frames against it; RCCL all-gather of the per-frame keypoint counts.
 Frames are independent, so N GPUs run N frame shards ("scaling": "weak"; value = all frames / max time).
 Within a GPU the B frames are split over S extractor contexts (--streams, one HIP stream each) whose
 kernels run concurrently.
@@ -65,6 +66,25 @@ def max_over_ranks(dist, value: float, device=None) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def shard_range(n_total: int, world: int, rank: int):
+    """Contiguous frame-to-rank split of a step's global frame set: (first global frame, frame count) of `rank`."""
+    base, rem = divmod(n_total, world)
+    return rank * base + min(rank, rem), base + (1 if rank < rem else 0)
+
+
+def broadcast_record(dist, rank: int, buf, pack, unpack, src: int = 0):
+    """A frame extracted once and shared by every rank (config 3: the initial frame F1 that every new frame is
+    matched against, src/Tracking.cc:563-635): the source rank packs it into `buf`, one broadcast (RCCL on the
+    GPU), the other ranks unpack it.  No-op on a single rank."""
+    if dist is None:
+        return
+    if rank == src:
+        pack(buf)
+    dist.broadcast(buf, src=src)
+    if rank != src:
+        unpack(buf)
 
 
 def allgather_counts(dist, counts, world: int):
@@ -154,12 +174,32 @@ def cpu_baseline(rows, cols, nfeat, seconds):
 # workloads: each sets up its contexts and device buffers and returns the timed step
 # ------------------------------------------------------------------------------------------------
 def _frames(synthetic, rows, cols, B, rank, seed_off=1000):
-    scene = synthetic.make_scene(synthetic.SEED_BASE + seed_off + rank, rows, cols)
+    """The initial frame (shared by all ranks) and this rank's B frames (global frames [rank*B, (rank+1)*B),
+    shard_range): one scene seen under 32 shifts with per-rank sensor noise, repeating with period 32."""
+    scene = synthetic.make_scene(synthetic.SEED_BASE + seed_off, rows, cols)
     nuniq = min(B, 32)
     uniq = [synthetic.render(scene, rows, cols, int(3 + 5 * (i % 8)), int(2 + 3 * (i // 8)),
                              noise_seed=rank * 100000 + 10 + i) for i in range(nuniq)]
-    f1 = synthetic.render(scene, rows, cols, 0, 0, noise_seed=rank * 100000 + 1)
+    f1 = synthetic.render(scene, rows, cols, 0, 0, noise_seed=1)
     return f1, np.stack([uniq[i % nuniq] for i in range(B)])
+
+
+def bench_golden(args, rank):
+    """Oracle hashes of this rank's config-3 frames (tests/golden/bench_golden.json, tests/golden/make_golden.py),
+    or None when the run's configuration is not the one the goldens were made for."""
+    path = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
+    if not os.path.exists(path):
+        return None
+    g = json.load(open(path))
+    if (g["rows"], g["cols"], g["nfeatures"], g["semantics"]) != (args.rows, args.cols, args.nfeatures, args.semantics):
+        return None
+    return next((r for r in g["ranks"] if r["rank"] == rank), None)
+
+
+def _sha(a) -> str:
+    import hashlib
+
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
 def setup_mono_init(args, env):
@@ -174,11 +214,12 @@ def setup_mono_init(args, env):
         raise SystemExit(f"--batch/--streams = {Bs} frames per stream must be a multiple of --chunks {K}")
     Bc = Bs // K
     f1, frames = _frames(synthetic, rows, cols, B, env["rank"])
-    ex_ref = ORBextractor(NF, 1.2, 8, 20, 7, device=dev)
-    exs = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev) for _ in range(S)]
+    ex_ref = ORBextractor(NF, 1.2, 8, 20, 7, device=dev, semantics=args.semantics)
+    exs = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev, semantics=args.semantics) for _ in range(S)]
     d_f1 = ex_ref.device_alloc(f1.nbytes)
     d_frames = exs[0].device_alloc(frames.nbytes)
     ex_ref.h2d(d_f1, f1)
+    dist, rank = env["dist"], env["rank"]
     exs[0].h2d(d_frames, frames)
     fbytes = rows * cols
     grid = _lib.GridGeom()
@@ -189,6 +230,19 @@ def setup_mono_init(args, env):
         e.synchronize()
     outs = [e.batch_outputs() for e in exs]
     cap = outs[0][3]
+    rec = None
+    if dist is not None:  # F1 record: extracted on rank 0, broadcast to the others once per step
+        import torch
+
+        rec = torch.empty(int(L.orbgpu_frame_record_bytes(ex_ref.ctx)), dtype=torch.uint8, device=f"cuda:{dev}")
+
+        def pack(buf):
+            _lib.check(ex_ref.ctx, L.orbgpu_frame_record_pack(ex_ref.ctx, 0, C_.c_void_p(buf.data_ptr())), "pack")
+            ex_ref.synchronize()
+
+        def unpack(buf):
+            torch.cuda.current_stream().synchronize()  # the broadcast has landed
+            _lib.check(ex_ref.ctx, L.orbgpu_frame_record_unpack(ex_ref.ctx, C_.c_void_p(buf.data_ptr())), "unpack")
     d_prev = [e.device_alloc(Bc * cap * 2 * 4) for e in exs]
     d_m12 = [e.device_alloc(Bc * cap * 4) for e in exs]
     d_nm = [e.device_alloc(Bc * 4) for e in exs]
@@ -202,7 +256,10 @@ def setup_mono_init(args, env):
                     desc=[torch.empty(Bc * cap * 32, dtype=torch.uint8).pin_memory() for _ in exs])
 
     def step():
-        ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
+        if rank == 0:
+            ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
+        if rec is not None:
+            broadcast_record(dist, rank, rec, pack, unpack)
         for r in range(K):
             for s_, e in enumerate(exs):
                 off = (s_ * Bs + r * Bc) * fbytes
@@ -225,6 +282,49 @@ def setup_mono_init(args, env):
                     _lib.check(e.ctx, L.orbgpu_memcpy_d2h_async(e.ctx, C_.c_void_p(host["desc"][s_].data_ptr()),
                                                                 C_.c_void_p(outs[s_][1]), Bc * cap * 32), "d2h")
 
+    def verify():
+        """Parity of the timed path itself: every frame of the last step's last chunk (and the initial frame)
+        against the oracle's hashes of the same frame -- keypoints, descriptors, vnMatches12, nmatches and the
+        updated vbPrevMatched (src/ORBmatcher.cc:405-520)."""
+        g = bench_golden(args, env["rank"])
+        if g is None:
+            return {"status": "no oracle golden for this configuration/rank", "frames": 0, "mismatches": None}
+        nuniq = min(B, 32)
+        ex_ref.synchronize()
+        o_ref = ex_ref.batch_outputs()
+        n1 = np.zeros(1, np.int32)
+        ex_ref.d2h(n1, o_ref[2])
+        n1 = int(n1[0])
+        k1 = np.zeros(n1 * 28, np.uint8)
+        d1 = np.zeros(n1 * 32, np.uint8)
+        ex_ref.d2h(k1, o_ref[0])
+        ex_ref.d2h(d1, o_ref[1])
+        bad = int(_sha(k1) != g["f1"]["kps_sha256"] or _sha(d1) != g["f1"]["desc_sha256"] or n1 != g["f1"]["n"])
+        checked = 0
+        for s_, e in enumerate(exs):
+            e.synchronize()
+            kp, de, cn, cap_ = outs[s_]
+            kps = np.zeros(Bc * cap_ * 28, np.uint8)
+            desc = np.zeros(Bc * cap_ * 32, np.uint8)
+            cnt = np.zeros(Bc, np.int32)
+            m12 = np.zeros(Bc * cap_, np.int32)
+            prev = np.zeros(Bc * cap_ * 2, np.float32)
+            nm = np.zeros(Bc, np.int32)
+            for dst, src in ((kps, kp), (desc, de), (cnt, cn), (m12, d_m12[s_]), (prev, d_prev[s_]), (nm, d_nm[s_])):
+                e.d2h(dst, src)
+            for b in range(Bc):
+                gf = g["frames"][(s_ * Bs + (K - 1) * Bc + b) % nuniq]
+                n = int(cnt[b])
+                ok = (n == gf["n"] and nm[b] == gf["nmatches"] and
+                      _sha(kps[b * cap_ * 28:(b * cap_ + n) * 28]) == gf["kps_sha256"] and
+                      _sha(desc[b * cap_ * 32:(b * cap_ + n) * 32]) == gf["desc_sha256"] and
+                      _sha(m12[b * cap_:b * cap_ + n1]) == gf["matches12_sha256"] and
+                      _sha(prev[2 * b * cap_:2 * (b * cap_ + n1)]) == gf["prev_sha256"])
+                bad += int(not ok)
+                checked += 1
+        return {"status": "checked", "frames": checked + 1, "unique_frames": nuniq + 1, "mismatches": bad,
+                "against": "oracle hashes of the same frames (tests/golden/bench_golden.json)"}
+
     def post():  # the last chunk of every context
         counts = np.zeros(Bc, np.int32)
         nm = np.zeros(Bc, np.int32)
@@ -246,7 +346,8 @@ def setup_mono_init(args, env):
         ex_ref.device_free(d_f1)
 
     metric = METRIC if host is None else METRIC + " (PCIe-inclusive: frames H2D, keypoints + descriptors D2H)"
-    return dict(metric=metric, exs=exs, step=step, post=post, free=free, Bs=Bc, per_stream=Bs, frames_per_step=B,
+    return dict(metric=metric, exs=exs, sync_extra=[ex_ref], step=step, post=post, free=free, verify=verify, Bs=Bc,
+                per_stream=Bs, frames_per_step=B,
                 counts=d_cnt,
                 workload=f"config 3: {cols}x{rows} mono, {NF} features, ORB extract + SearchForInitialization "
                          f"(window 100, ratio 0.9, checkOri) of every frame against an initial frame",
@@ -259,7 +360,7 @@ def setup_extract(args, env):
     rows, cols, B, NF, S, dev = args.rows, args.cols, args.batch, args.nfeatures, args.streams, env["dev"]
     Bs = B // S
     _, frames = _frames(synthetic, rows, cols, B, env["rank"], 2000)
-    exs = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev) for _ in range(S)]
+    exs = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev, semantics=args.semantics) for _ in range(S)]
     d_frames = exs[0].device_alloc(frames.nbytes)
     exs[0].h2d(d_frames, frames)
     fbytes = rows * cols
@@ -295,8 +396,8 @@ def setup_stereo(args, env):
     pairs = [synthetic.stereo_pair(3000 + env["rank"] * 100 + i, rows, cols) for i in range(nuniq)]
     left = np.stack([pairs[i % nuniq][0] for i in range(B)])
     right = np.stack([pairs[i % nuniq][1] for i in range(B)])
-    exL = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev) for _ in range(S)]
-    exR = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev) for _ in range(S)]
+    exL = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev, semantics=args.semantics) for _ in range(S)]
+    exR = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev, semantics=args.semantics) for _ in range(S)]
     dL = exL[0].device_alloc(left.nbytes)
     dR = exL[0].device_alloc(right.nbytes)
     exL[0].h2d(dL, left)
@@ -398,7 +499,7 @@ def setup_tracking(args, env):
     M = args.mappoints
     Bs = B // S
     _, frames = _frames(synthetic, rows, cols, B, env["rank"], 5000)
-    exs = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev) for _ in range(S)]
+    exs = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev, semantics=args.semantics) for _ in range(S)]
     d_frames = exs[0].device_alloc(frames.nbytes)
     exs[0].h2d(d_frames, frames)
     fbytes = rows * cols
@@ -532,6 +633,8 @@ def main():
     ap.add_argument("--cols", type=int, default=None)
     ap.add_argument("--nfeatures", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--semantics", type=lambda v: int(v, 0), default=0,
+                    help="ORBGPU_SEM_* flags (include/orbgpu.h): which OpenCV/compiler behaviours to reproduce")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     args = ap.parse_args()
@@ -550,7 +653,8 @@ def main():
     dist = dist_init(world, "nccl")
     dev = local
     torch.cuda.set_device(dev)
-    env = dict(L=_lib.lib(), _lib=_lib, ORBextractor=ORBextractor, synthetic=synthetic, dev=dev, rank=rank)
+    env = dict(L=_lib.lib(), _lib=_lib, ORBextractor=ORBextractor, synthetic=synthetic, dev=dev, rank=rank,
+               dist=dist, world=world)
     t = time.time()
     W = WORKLOADS[args.workload](args, env)
     log(f"rank {rank}: {args.workload} set up in {time.time() - t:.1f}s")
@@ -564,7 +668,7 @@ def main():
             for s_, dc in enumerate(W["counts"]):
                 _lib.check(exs[s_].ctx, _lib.lib().orbgpu_memcpy_d2d_async(
                     exs[s_].ctx, C.c_void_p(counts_t.data_ptr() + 4 * s_ * Bps), C.c_void_p(dc), Bps * 4), "d2d")
-        for e in exs:
+        for e in exs + W.get("sync_extra", []):  # every context's capacity-guard flags are read each step
             e.synchronize()
         if dist is not None:
             allgather_counts(dist, counts_t, world)
@@ -611,6 +715,13 @@ def main():
     # one context's Bs frames)
     cand_total = sum(_lib.lib().orbgpu_batch_candidate_total(e.ctx) for e in exs) / len(exs)
     extra, kp_total = W["post"]()
+    parity = W["verify"]() if "verify" in W else None
+    if parity is not None and dist is not None and parity["mismatches"] is not None:
+        import torch
+
+        t = torch.tensor([parity["frames"], parity["mismatches"]], dtype=torch.int64, device=f"cuda:{dev}")
+        dist.all_reduce(t)
+        parity = dict(parity, frames=int(t[0]), mismatches=int(t[1]), ranks=world)
     P = level_pixels(args.cols, args.rows, exs[0].GetInverseScaleFactors())
     stages = {k: v[0] / max(v[1], 1) for k, v in stage_acc.items()}
     kernels = {k: v for k, v in stages.items()
@@ -668,6 +779,7 @@ def main():
             "frames_per_launch": Bs,
             "resolution": f"{args.cols}x{args.rows}",
             "nfeatures": args.nfeatures,
+            "semantics": _lib.semantics_name(args.semantics),
             "parallelism": f"frame-sharded x{world} GPUs, {S} streams per GPU (RCCL all-gather of keypoint "
                            f"counts only)",
         }, **extra),
@@ -685,6 +797,7 @@ def main():
             "launch_time": "union of the kernel's HIP-event intervals over the concurrent streams / launches",
             "valu": valu,
         },
+        "parity": parity,
         "stages_ms_per_launch": {k: round(v, 4) for k, v in stages.items()},
         "stages_busy_ms_per_step": {k: round(v / args.steps, 4) for k, v in union_acc.items()},
     }

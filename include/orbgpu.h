@@ -121,6 +121,16 @@ int orbgpu_batch_outputs(orbgpu_ctx* ctx, orbgpu_keypoint** d_kps, uint8_t** d_d
 int orbgpu_batch_download(orbgpu_ctx* ctx, int b, orbgpu_keypoint* kps, uint8_t* desc, int cap,
                           int* n);
 
+/* One extracted frame as a flat device record: count, keypoints, descriptors (and mvKeysUn with an
+ * undistortion model) at the context's frame capacity.  A multi-GPU run extracts the initial frame of
+ * Tracking::MonocularInitialization (src/Tracking.cc:563-635) on one rank and broadcasts this record (RCCL)
+ * to the others, which unpack it as frame 0 of a one-frame batch and match their frames against it
+ * (SURVEY §8(e)).  Both calls are enqueued on the context stream; unpack requires a context planned for the
+ * same image size and parameters, and records the event the matchers of other contexts wait for. */
+long long orbgpu_frame_record_bytes(const orbgpu_ctx* ctx);
+int orbgpu_frame_record_pack(orbgpu_ctx* ctx, int b, void* d_dst);
+int orbgpu_frame_record_unpack(orbgpu_ctx* ctx, const void* d_src);
+
 /* ---- Frame grid (src/Frame.cc:230-245, 327-392) ----------------------------------------------- */
 
 /* Grid geometry of ComputeImageBounds + grid scales (src/Frame.cc:207-223, 436-464) for an

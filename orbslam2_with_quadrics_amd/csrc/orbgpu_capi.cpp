@@ -390,6 +390,17 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
     return image_bounds(c, c->undist, c->und, W, H, &c->grid_geom);
 }
 
+// the device status word collects capacity-guard flags (atomicOr) from every launch until a status check reads
+// and clears it (check_status): zeroed once at allocation, never by a launch sequence, so a flag raised by one
+// chunk survives the next chunk's extraction
+static int ensure_status(orbgpu_ctx* c)
+{
+    if (c->status.p) return ORBGPU_OK;
+    HIP_TRY(c, ensure(c->status, 4));
+    HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(int) * 4, c->stream));
+    return ORBGPU_OK;
+}
+
 static int ensure_batch(orbgpu_ctx* c, int B)
 {
     if (c->Bcap >= B) return ORBGPU_OK;
@@ -408,7 +419,7 @@ static int ensure_batch(orbgpu_ctx* c, int B)
     HIP_TRY(c, ensure(c->counts, Bn));
     HIP_TRY(c, ensure(c->cell_start, Bn * (OG_GRID_CELLS + 1)));
     HIP_TRY(c, ensure(c->cell_items, Bn * (size_t)P.frame_cap));
-    HIP_TRY(c, ensure(c->status, 4));
+    if (int r = ensure_status(c)) return r;
     c->Bcap = B;
     return ORBGPU_OK;
 }
@@ -460,7 +471,6 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
     timer_begin(c);
     timer_mark(c, "start");
     HIP_TRY(c, hipMemsetAsync(c->cand_count.p, 0, sizeof(int) * (size_t)B * P.nlevels, s));
-    HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(int) * 4, s));
     // k1: chained pyramid, src/ORBextractor.cc:1107-1132
     // levels (1,2), (3,4), (5,6) in one launch each (og_resize2_kernel), a last odd level alone
     for (int l = 1; l < P.nlevels;) {
@@ -522,10 +532,13 @@ static int collect_timer(orbgpu_ctx* c)
 
 static int check_status(orbgpu_ctx* c)
 {
+    if (!c->status.p) return ORBGPU_OK;  // nothing launched yet
     int st[4] = {0};
     HIP_TRY(c, hipMemcpyAsync(st, c->status.p, sizeof(st), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (st[0]) {
+    if (st[0]) {  // read and clear: the flags of every launch since the last check
+        HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(st), c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
         c->err = "device capacity guard tripped (status " + std::to_string(st[0]) + ")";
         return ORBGPU_ERR_INTERNAL;
     }
@@ -712,6 +725,53 @@ int orbgpu_batch_outputs(orbgpu_ctx* c, orbgpu_keypoint** d_kps, uint8_t** d_des
     if (d_desc) *d_desc = c->desc.p;
     if (d_counts) *d_counts = c->counts.p;
     if (frame_cap) *frame_cap = c->plan.frame_cap;
+    return ORBGPU_OK;
+}
+
+// ---- one frame as a flat device record (the unit a multi-GPU run broadcasts: SURVEY §8(e), config 3's initial
+// frame).  Layout: int32 count, 12 pad bytes, frame_cap keypoints (28 B), frame_cap descriptors (32 B), and with an
+// undistortion model frame_cap mvKeysUn keypoints.
+static size_t ref_record_bytes(const orbgpu_ctx* c)
+{
+    return 16 + (size_t)c->plan.frame_cap * (28 + 32 + (c->undist ? 28 : 0));
+}
+
+long long orbgpu_frame_record_bytes(const orbgpu_ctx* c)
+{
+    if (!c || !c->planned) return ORBGPU_ERR_ARG;
+    return (long long)ref_record_bytes(c);
+}
+
+int orbgpu_frame_record_pack(orbgpu_ctx* c, int b, void* d_dst)
+{
+    if (!c || !c->planned || !d_dst || b < 0 || b >= c->last_B) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t cap = (size_t)c->plan.frame_cap, o = (size_t)b * cap;
+    uint8_t* d = (uint8_t*)d_dst;
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(d, c->counts.p + b, 4, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(d + 16, c->kps.p + o, cap * 28, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(d + 16 + cap * 28, c->desc.p + o * 32, cap * 32, hipMemcpyDeviceToDevice, s));
+    if (c->undist)
+        HIP_TRY(c, hipMemcpyAsync(d + 16 + cap * 60, c->kps_un.p + o, cap * 28, hipMemcpyDeviceToDevice, s));
+    return ORBGPU_OK;
+}
+
+int orbgpu_frame_record_unpack(orbgpu_ctx* c, const void* d_src)
+{
+    // frame 0 of a batch of one; the context must be planned for the record's geometry (same frame_cap)
+    if (!c || !c->planned || !d_src) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (int r = ensure_batch(c, 1)) return r;
+    const size_t cap = (size_t)c->plan.frame_cap;
+    const uint8_t* d = (const uint8_t*)d_src;
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(c->counts.p, d, 4, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(c->kps.p, d + 16, cap * 28, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(c->desc.p, d + 16 + cap * 28, cap * 32, hipMemcpyDeviceToDevice, s));
+    if (c->undist) HIP_TRY(c, hipMemcpyAsync(c->kps_un.p, d + 16 + cap * 60, cap * 28, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(c, hipEventRecord(c->done, s));  // matchers on other contexts wait for this record
+    c->last_B = std::max(c->last_B, 1);
     return ORBGPU_OK;
 }
 
@@ -904,8 +964,7 @@ int orbgpu_search_for_initialization(orbgpu_ctx* c, const orbgpu_frame_view* F1,
     }
     HIP_TRY(c, ensure(c->mlists, (size_t)cap1 * list_cap));
     HIP_TRY(c, ensure(c->mlist_n, (size_t)cap1));
-    HIP_TRY(c, ensure(c->status, 4));
-    HIP_TRY(c, hipMemsetAsync(c->status.p, 0, 16, s));
+    if (int r = ensure_status(c)) return r;
     og_launch_search_init(s, f1, 0, f2, G, nnratio, checkOri, windowSize, pv, 2 * cap1, m12, cap1, nm, c->mlists.p,
                           list_cap, c->mlist_n.p, c->status.p, 1);
     HIP_TRY(c, hipGetLastError());

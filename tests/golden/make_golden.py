@@ -8,6 +8,9 @@ extract_golden.json : the oracle's ORB extraction of seeded synthetic frames (ha
                       This pins the oracle against regressions; it is NOT a reference-binary output
                       (the reference cannot be built here -- DESIGN.md §4).
 match_golden.json   : oracle SearchForInitialization on a seeded 1080p pair (match vector hash).
+bench_golden.json   : the oracle's outputs on exactly the frames bench.py times (config 3: 1920x1080, 2000 features,
+                      default semantics; the initial frame and the 32 unique frames of every rank 0-7) --
+                      keypoint / descriptor / vnMatches12 / vbPrevMatched hashes, checked after the timed loop.
 tracking_golden.json: oracle SearchByProjection(F, 5000 map points, th 1) on a config-5 frame (1920x1080, 4000
                       features; SURVEY.md §8(d) map-point recipe) -- owner vector hash -- and oracle
                       Frame::ComputeStereoMatches on a KITTI-shape pair (mvuRight / mvDepth hashes).
@@ -155,11 +158,49 @@ def tracking_cases():
               open(os.path.join(OUT, "tracking_golden.json"), "w"), indent=1)
 
 
+def _bench_rank(rank):
+    sys.path.insert(0, ROOT)
+    import bench
+
+    rows, cols, nf = 1080, 1920, 2000
+    f1, frames = bench._frames(synthetic, rows, cols, 32, rank)
+    ex = O.OracleExtractor(nf)
+    k1, d1 = ex(f1)
+    sf = ex.tables()["scale"]
+    F1 = O.OracleFrame(k1, d1, cols, rows, sf)
+
+    def h(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+    out = dict(rank=rank, f1=dict(n=int(len(k1)), kps_sha256=h(k1), desc_sha256=h(d1)), frames=[])
+    for u in range(len(frames)):
+        k2, d2 = ex(frames[u])
+        prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+        n, m12, prev2 = O.search_for_initialization(F1, O.OracleFrame(k2, d2, cols, rows, sf), prev, 0.9, True, 100)
+        out["frames"].append(dict(n=int(len(k2)), kps_sha256=h(k2), desc_sha256=h(d2), nmatches=int(n),
+                                  matches12_sha256=h(m12.astype(np.int32)), prev_sha256=h(prev2.astype(np.float32))))
+    return out
+
+
+def bench_cases():
+    from multiprocessing import Pool
+
+    with Pool(8) as pool:
+        ranks = pool.map(_bench_rank, range(8))
+    json.dump({"generator": "oracle on bench.py's config-3 frames via tests/golden/make_golden.py",
+               "rows": 1080, "cols": 1920, "nfeatures": 2000, "semantics": 0, "unique_frames": 32,
+               "ranks": ranks}, open(os.path.join(OUT, "bench_golden.json"), "w"), indent=0)
+
+
 if __name__ == "__main__":
     O.build()
+    if "--only-bench" in sys.argv:
+        bench_cases()
+        sys.exit(0)
     if "--only-tracking" not in sys.argv:
         sincos_vectors()
         extract_cases()
         match_cases()
+        bench_cases()
     tracking_cases()
     print("golden fixtures written to", OUT)

@@ -1,5 +1,6 @@
-"""CPU test of the multi-rank plumbing bench.py uses (gloo, world_size 2): max-over-ranks timing and
-the per-frame keypoint-count all-gather (the path's only collective)."""
+"""CPU test of the multi-rank plumbing bench.py uses (gloo, world_size 2): the frame-to-rank split, the broadcast
+of the shared initial frame (config 3), max-over-ranks timing and the per-frame keypoint-count
+all-gather -- the same bench.py functions the GPU run calls, with a CPU stub in place of the extraction."""
 import os
 import socket
 import sys
@@ -47,6 +48,79 @@ def test_gloo_world2_allgather_and_max():
     for r, t, g in res:
         assert t == 2.0
         assert g == [0, 1, 2, 3, 100, 101, 102, 103]
+
+
+def _stub_extract(img):
+    """CPU stand-in for ORB extraction: a deterministic 'record' of the frame (count + bytes)."""
+    import numpy as np
+
+    rng = np.random.default_rng(int(img.sum()) % (2 ** 32))
+    n = int(rng.integers(100, 200))
+    return np.concatenate([np.array([n], np.int32).view(np.uint8), rng.integers(0, 256, 60 * n, np.uint8)])
+
+
+def _worker_share(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import torch
+
+    import bench
+    from orbslam2_with_quadrics_amd import synthetic
+
+    w, r, _ = bench.dist_env()
+    dist = bench.dist_init(w, "gloo")
+    B = 5
+    f1, frames = bench._frames(synthetic, 64, 96, B, r)  # the real frame generator, tiny frames
+    start, count = bench.shard_range(w * B, w, r)
+    record = {}
+    size = 4 + 60 * 200
+    buf = torch.zeros(size, dtype=torch.uint8)
+
+    def pack(b):
+        rec = _stub_extract(f1)  # only the source rank extracts F1
+        b.zero_()
+        b[:len(rec)] = torch.from_numpy(rec)
+        record["f1"] = b.clone()
+
+    def unpack(b):
+        record["f1"] = b.clone()
+
+    bench.broadcast_record(dist, r, buf, pack, unpack)
+    counts = torch.tensor([int(_stub_extract(f)[:4].view(np.int32)[0]) for f in frames], dtype=torch.int32)
+    g = bench.allgather_counts(dist, counts, w)
+    q.put((r, start, count, __import__("hashlib").sha256(f1.tobytes()).hexdigest(), record["f1"].numpy().tobytes(), g.tolist(), counts.tolist()))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_shared_initial_frame_split_and_gather():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_share, args=(r, 2, port, q)) for r in range(2)]
+    [p.start() for p in ps]
+    res = sorted(q.get(timeout=180) for _ in range(2))
+    [p.join(timeout=60) for p in ps]
+    (r0, s0, c0, h0, rec0, g0, n0), (r1, s1, c1, h1, rec1, g1, n1) = res
+    assert (s0, c0, s1, c1) == (0, 5, 5, 5)      # the global frame set [0, 10) split without overlap
+    assert h0 == h1                              # every rank renders the same initial frame
+    assert rec0 == rec1 and any(rec0)            # rank 1 holds rank 0's record after the broadcast
+    assert g0 == g1 == n0 + n1                   # all-gathered keypoint counts, rank order
+    assert n0 != n1                              # the ranks' frames differ (per-rank sensor noise)
+
+
+def test_shard_range_partitions():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for n in (0, 1, 7, 512, 1000):
+        for w in (1, 2, 3, 8):
+            got = [bench.shard_range(n, w, r) for r in range(w)]
+            assert sum(c for _, c in got) == n
+            assert all(got[i][0] + got[i][1] == got[i + 1][0] for i in range(w - 1))
 
 
 def test_single_rank_is_collective_free():

@@ -1,0 +1,98 @@
+"""The headline timed path at its own shape (bench.py config 3): 1920x1080, 2000 features, 256 frames per launch on
+each of two concurrently running extractor contexts (HIP streams), SearchForInitialization of every frame against
+the initial frame.  Every one of the 512 frames is checked against the oracle's hashes of the same frame
+(tests/golden/bench_golden.json, made by tests/golden/make_golden.py from bench._frames), and frames 0, 1, 128 and
+255 of each stream field by field against a live oracle run."""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIELDS = ("x", "y", "size", "angle", "response", "octave", "class_id")
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_bench_shape_two_streams_b256(gpu, oracle):
+    import ctypes as C
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from orbslam2_with_quadrics_amd import _lib, synthetic
+    from orbslam2_with_quadrics_amd.extractor import KP_DTYPE
+
+    rows, cols, NF, S, Bs = 1080, 1920, 2000, 2, 256
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_golden.json")))["ranks"][0]
+    f1, frames = bench._frames(synthetic, rows, cols, S * Bs, 0)
+    L = _lib.lib()
+    ex_ref = gpu.ORBextractor(NF, 1.2, 8, 20, 7)
+    exs = [gpu.ORBextractor(NF, 1.2, 8, 20, 7) for _ in range(S)]
+    fb = rows * cols
+    d_f1 = ex_ref.device_alloc(f1.nbytes)
+    d_frames = exs[0].device_alloc(frames.nbytes)
+    bufs = []
+    try:
+        ex_ref.h2d(d_f1, f1)
+        exs[0].h2d(d_frames, frames)
+        grid = _lib.GridGeom()
+        L.orbgpu_grid_geom_for_image(cols, rows, C.byref(grid))
+        ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, fb)
+        for s, e in enumerate(exs):  # both streams enqueued before either is waited on: they run concurrently
+            e.extract_batch_device(d_frames + s * Bs * fb, Bs, cols, rows, cols, fb)
+        outs = [e.batch_outputs() for e in exs]
+        cap = outs[0][3]
+        for s, e in enumerate(exs):
+            prev, m12, nm = (e.device_alloc(Bs * cap * 8), e.device_alloc(Bs * cap * 4), e.device_alloc(Bs * 4))
+            bufs.append((e, prev, m12, nm))
+            _lib.check(e.ctx, L.orbgpu_prev_matched_from_frame(ex_ref.ctx, 0, e.ctx, C.c_void_p(prev)), "prev")
+            _lib.check(e.ctx, L.orbgpu_search_for_initialization_batch(ex_ref.ctx, 0, e.ctx, grid, 0.9, 1, 100,
+                                                                         C.c_void_p(prev), C.c_void_p(m12),
+                                                                         C.c_void_p(nm)), "search")
+        for e in exs + [ex_ref]:
+            e.synchronize()
+        k1, d1 = ex_ref.batch_download(0)
+        assert _sha(k1) == g["f1"]["kps_sha256"] and _sha(d1) == g["f1"]["desc_sha256"]
+        n1 = len(k1)
+        oe = oracle.OracleExtractor(NF)
+        ko1, do1 = oe(f1)
+        F1 = oracle.OracleFrame(ko1, do1, cols, rows, oe.tables()["scale"])
+        bad = []
+        for s, (e, prev, m12, nm) in enumerate(bufs):
+            M = np.zeros(Bs * cap, np.int32)
+            P = np.zeros(Bs * cap * 2, np.float32)
+            NM = np.zeros(Bs, np.int32)
+            e.d2h(M, m12)
+            e.d2h(P, prev)
+            e.d2h(NM, nm)
+            for b in range(Bs):
+                k, d = e.batch_download(b)
+                gf = g["frames"][(s * Bs + b) % 32]
+                m, p = M[b * cap:b * cap + n1], P[2 * b * cap:2 * (b * cap + n1)]
+                if not (_sha(k) == gf["kps_sha256"] and _sha(d) == gf["desc_sha256"] and NM[b] == gf["nmatches"]
+                        and _sha(m) == gf["matches12_sha256"] and _sha(p) == gf["prev_sha256"]):
+                    bad.append((s, b))
+                if b in (0, 1, 128, 255):  # field by field against the live oracle
+                    ko, do = oe(frames[s * Bs + b])
+                    assert len(k) == len(ko)
+                    for f in FIELDS:
+                        assert np.array_equal(k[f].view(np.int32), ko[f].view(np.int32)), (s, b, f)
+                    assert np.array_equal(d, do)
+                    prev0 = np.stack([ko1["x"], ko1["y"]], 1).astype(np.float32)
+                    no, mo, po = oracle.search_for_initialization(
+                        F1, oracle.OracleFrame(ko, do, cols, rows, oe.tables()["scale"]), prev0, 0.9, True, 100)
+                    assert NM[b] == no and np.array_equal(m, mo) and np.array_equal(p.reshape(-1, 2), po), (s, b)
+        assert not bad, bad[:10]
+    finally:
+        for e, prev, m12, nm in bufs:
+            for q in (prev, m12, nm):
+                e.device_free(q)
+        exs[0].device_free(d_frames)
+        ex_ref.device_free(d_f1)
+    assert KP_DTYPE.itemsize == 28
