@@ -117,6 +117,10 @@ int orbgpu_extract_batch_device(orbgpu_ctx* ctx, const uint8_t* d_imgs, int B, i
  * counts[b] (final keypoint count of frame b).  Valid until the next batch call. */
 int orbgpu_batch_outputs(orbgpu_ctx* ctx, orbgpu_keypoint** d_kps, uint8_t** d_desc, int** d_counts,
                          int* frame_cap);
+/* Frame::mGrid of the last batch (Frame::AssignFeaturesToGrid, src/Frame.cc:230-245) as CSR per frame b:
+ * cell (ix, iy) -> items cell_items[b*frame_cap + cell_start[b*3073 + ix*48 + iy] .. + cell_start[.. + 1]),
+ * keypoint indices in ascending order (the reference's push_back order). */
+int orbgpu_batch_grid(orbgpu_ctx* ctx, int** d_cell_start, int** d_cell_items);
 /* Synchronise and copy frame b of the last batch to the host. */
 int orbgpu_batch_download(orbgpu_ctx* ctx, int b, orbgpu_keypoint* kps, uint8_t* desc, int cap,
                           int* n);

@@ -1262,7 +1262,7 @@ __constant__ OgDisk og_disk = og_make_disk();
 // GaussianBlur 7x7 sigma 2 integer kernels by ORBGPU_SEM_BLUR_* variant, c0 | c1 << 8 | c2 << 16 | c3 << 24 for
 // [c0,c1,c2,c3,c2,c1,c0]: cvRound(256 g) (sum 257) twice, the bit-exact kernel with centre 256 - 2 sum(sides),
 // the error-diffused bit-exact kernel
-__constant__ uint32_t og_blur_coefs[4] = {18u | 34u << 8 | 49u << 16 | 55u << 24, 18u | 34u << 8 | 49u << 16 | 55u << 24,
+constexpr uint32_t og_blur_coefs[4] = {18u | 34u << 8 | 49u << 16 | 55u << 24, 18u | 34u << 8 | 49u << 16 | 55u << 24,
                                           18u | 34u << 8 | 49u << 16 | 54u << 24, 18u | 34u << 8 | 48u << 16 | 56u << 24};
 
 #ifndef OG_DK_BLOCKSYNC
@@ -1284,6 +1284,9 @@ __device__ __forceinline__ void og_dk_sync()
 #endif
 }
 
+// BV = ORBGPU_SEM_BLUR_* variant >> ORBGPU_SEM_BLUR_SHIFT, NOFMA = ORBGPU_SEM_BRIEF_NOFMA: compile-time, so every
+// variant keeps its kernel taps as literal operands and only the SSE2 variant carries the tie test
+template <int BV, bool NOFMA>
 __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, const uint8_t* __restrict__ img0,
                                                                     long long pitch0, long long fstride0,
                                                                     const uint8_t* __restrict__ pyr,
@@ -1405,11 +1408,10 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     // v_dot2_u32_u16 over row pairs of the horizontal sums (<= 257 * 255 = 65535, exact in u16).
     // horizontal: item = (row pair rp, 4-column group g): rows 2rp, 2rp+1, outputs 4g..4g+3, stored as
     // (row 2rp, row 2rp+1) u16 pairs Hp[rp][col]
-    const int bvar = (P.sem >> ORBGPU_SEM_BLUR_SHIFT) & 7;
-    const uint32_t gc = og_blur_coefs[bvar & 3];  // c0 | c1 << 8 | c2 << 16 | c3 << 24
-    const uint32_t c0 = gc & 0xff, c1 = (gc >> 8) & 0xff, c2 = (gc >> 16) & 0xff, c3 = gc >> 24;
+    constexpr uint32_t gc = og_blur_coefs[BV];  // c0 | c1 << 8 | c2 << 16 | c3 << 24
+    constexpr uint32_t c0 = gc & 0xff, c1 = (gc >> 8) & 0xff, c2 = (gc >> 16) & 0xff, c3 = gc >> 24;
     if (active) {
-        const uint32_t glo = gc, ghi = c2 | (c1 << 8) | (c0 << 16);
+        constexpr uint32_t glo = gc, ghi = c2 | (c1 << 8) | (c0 << 16);
         for (int it = lane; it < HP_ROWS * 10; it += 64) {
             const int rp = it / 10, g = it - rp * 10;
             uint32_t hv[2][4];
@@ -1438,12 +1440,12 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     // (g0,g1)(g2,g3)(g4,g5)(g6,0), odd rows (0,g0)(g1,g2)(g3,g4)(g5,g6)
     if (active) {
         typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
-        const unsigned short s0 = (unsigned short)c0, s1 = (unsigned short)c1, s2 = (unsigned short)c2,
-                             s3 = (unsigned short)c3;
+        constexpr unsigned short s0 = (unsigned short)c0, s1 = (unsigned short)c1, s2 = (unsigned short)c2,
+                                 s3 = (unsigned short)c3;
         const u16x2v e0 = {s0, s1}, e1 = {s2, s3}, e2 = {s2, s1}, e3 = {s0, 0};
         const u16x2v o0 = {0, s0}, o1 = {s1, s2}, o2 = {s3, s2}, o3 = {s1, s0};
         // level column of window column c is cx - 18 + c (inside the level: keypoints sit >= 19 px from the edge)
-        const int xsimd = bvar == 0 ? ((lw & ~3) - (cx - 18)) : 0;  // window columns c < xsimd round half-to-even
+        const int xsimd = BV == 0 ? ((lw & ~3) - (cx - 18)) : 0;  // window columns c < xsimd round half-to-even
         for (int it = lane; it < BL_W * 10; it += 64) {
             const int m = it / BL_W, c = it - m * BL_W;
             u16x2v pr[5];
@@ -1461,9 +1463,15 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
                 ao = __builtin_amdgcn_udot2(q[1], o1, ao, false);
                 ao = __builtin_amdgcn_udot2(q[2], o2, ao, false);
                 ao = __builtin_amdgcn_udot2(q[3], o3, ao, false);
-                const bool rne = c < xsimd;  // a tie with an even quotient rounds down there
-                const uint32_t ve = ((ae + (1u << 15)) >> 16) - (rne && (ae & 0x1ffffu) == 0x8000u);
-                const uint32_t vo = ((ao + (1u << 15)) >> 16) - (rne && (ao & 0x1ffffu) == 0x8000u);
+                uint32_t ve, vo;
+                if (BV == 0) {  // half-to-even in the SIMD columns: + 0x7fff + bit 16 (the quotient's parity)
+                    const uint32_t up = c < xsimd ? 0u : 1u;  // the scalar tail rounds half-up
+                    ve = (ae + 0x7fffu + (__builtin_amdgcn_ubfe(ae, 16, 1) | up)) >> 16;
+                    vo = (ao + 0x7fffu + (__builtin_amdgcn_ubfe(ao, 16, 1) | up)) >> 16;
+                } else {
+                    ve = (ae + (1u << 15)) >> 16;
+                    vo = (ao + (1u << 15)) >> 16;
+                }
                 if (r0 < BL_W) Bl[r0 * BL_W + c] = (uint8_t)min(ve, 255u);
                 if (r0 + 1 < BL_W) Bl[(r0 + 1) * BL_W + c] = (uint8_t)min(vo, 255u);
             }
@@ -1476,7 +1484,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     float a, b;
     og_sincosf(angle * factorPI, &b, &a);
     const uint8_t* ctr = Bl + 18 * BL_W + 18;
-    const bool nofma = (P.sem & ORBGPU_SEM_BRIEF_NOFMA) != 0;
+    constexpr bool nofma = NOFMA;
     u64 words[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
@@ -1521,10 +1529,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 // ------------------------------------------------------------------------------------------------
 // k5: Frame::AssignFeaturesToGrid (src/Frame.cc:230-245, PosInGrid :382-392)
 // ------------------------------------------------------------------------------------------------
-#ifndef OG_GRID_SORT_LDS
-#define OG_GRID_SORT_LDS 1  // 0: sort in global memory
-#endif
-#define OG_GRID_LDS_ITEMS 8192
+// OG_GRID_LDS_ITEMS (orbgpu_internal.h): the frame capacity the plan enforces, so every frame's items fit in LDS
 // insertion sort of one cell's item indices [b, e) (a few items per cell)
 template <typename T>
 __device__ __forceinline__ void og_sort_cell(T* SI, int b, int e)
@@ -1542,14 +1547,12 @@ __device__ __forceinline__ void og_sort_cell(T* SI, int b, int e)
 __global__ __launch_bounds__(256) void og_grid_kernel(const orbgpu_kp_dev* __restrict__ kps,
                                                       const int* __restrict__ counts, int frame_cap,
                                                       OgGridGeom G, int* __restrict__ cell_start,
-                                                      int* __restrict__ cell_items)
+                                                      int* __restrict__ cell_items, int* __restrict__ status)
 {
     __shared__ int cnt[OG_GRID_CELLS + 1];
     __shared__ int wsum[32];
     __shared__ int starts[OG_GRID_CELLS + 1];
-#if OG_GRID_SORT_LDS
     __shared__ int sitems[OG_GRID_LDS_ITEMS];
-#endif
     const int f = blockIdx.x, tid = threadIdx.x;
     const int n = counts[f];
     const orbgpu_kp_dev* K = kps + (long long)f * frame_cap;
@@ -1589,22 +1592,32 @@ __global__ __launch_bounds__(256) void og_grid_kernel(const orbgpu_kp_dev* __res
     __syncthreads();
     __threadfence_block();
     // restore ascending index order inside each cell (push_back order of the reference): an insertion sort per
-    // cell (a few items each), in LDS when the frame's items fit (every frame of up to OG_GRID_LDS_ITEMS
-    // keypoints), so the dependent compare-and-shift chain costs LDS latency rather than global round trips
-    // (two explicit copies of the sort: no generic pointer selecting LDS or global memory)
+    // cell (a few items each) in LDS, so the dependent compare-and-shift chain costs LDS latency rather than global
+    // round trips.  Every frame's items fit: nin <= counts[f] <= frame_cap <= OG_GRID_LDS_ITEMS (build_plan).
+    // The ranges are checked, never trusted: DS instructions drop out-of-range LDS accesses silently, so a bad
+    // range raises status bit 64 (reported by the next status check) instead of passing unnoticed
+    // (the round-1 fault of the generic-pointer form).
     const int nin = starts[OG_GRID_CELLS];
-#if OG_GRID_SORT_LDS
-    if (nin <= OG_GRID_LDS_ITEMS) {
-        for (int p = tid; p < nin; p += 256) sitems[p] = CI[p];
-        __syncthreads();
-        for (int c = tid; c < OG_GRID_CELLS; c += 256) og_sort_cell(sitems, starts[c], starts[c + 1]);
-        __syncthreads();
-        for (int p = tid; p < nin; p += 256) CI[p] = sitems[p];
+    if (nin > min(n, OG_GRID_LDS_ITEMS)) {
+        if (tid == 0) atomicOr(status, 64);
         return;
     }
-#endif
-    (void)nin;
-    for (int c = tid; c < OG_GRID_CELLS; c += 256) og_sort_cell(CI, starts[c], starts[c + 1]);
+    for (int p = tid; p < nin; p += 256) sitems[p] = CI[p];
+    __syncthreads();
+    for (int c = tid; c < OG_GRID_CELLS; c += 256) {
+        const int b = starts[c], e = starts[c + 1];
+        if (b < 0 || b > e || e > nin) {
+            atomicOr(status, 64);
+            continue;
+        }
+        og_sort_cell(sitems, b, e);
+    }
+    __syncthreads();
+    for (int p = tid; p < nin; p += 256) {
+        const int v = sitems[p];
+        if (v < 0 || v >= n) atomicOr(status, 64);  // every item is a keypoint index of this frame
+        CI[p] = v;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1687,12 +1700,21 @@ void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, lon
                         orbgpu_kp_dev* kps, uint8_t* desc, int* counts, int B)
 {
     const int blocks = (P.frame_cap + DK_WAVES - 1) / DK_WAVES;
-    hipLaunchKernelGGL(og_describe_kernel, dim3(blocks, B), dim3(64 * DK_WAVES), 0, s, P, img0, pitch0, fstride0, pyr,
-                       oct_xy, oct_resp, oct_count, kps, desc, counts);
+    const int bv = (P.sem >> ORBGPU_SEM_BLUR_SHIFT) & 3;
+    const bool nofma = (P.sem & ORBGPU_SEM_BRIEF_NOFMA) != 0;
+    // the 8 (blur variant, rotation form) instantiations
+    using K = void (*)(OgPlan, const uint8_t*, long long, long long, const uint8_t*, const uint32_t*, const uint8_t*,
+                       const int*, orbgpu_kp_dev*, uint8_t*, int*);
+    static const K table[8] = {og_describe_kernel<0, false>, og_describe_kernel<1, false>, og_describe_kernel<2, false>,
+                               og_describe_kernel<3, false>, og_describe_kernel<0, true>,  og_describe_kernel<1, true>,
+                               og_describe_kernel<2, true>,  og_describe_kernel<3, true>};
+    hipLaunchKernelGGL(table[bv + 4 * nofma], dim3(blocks, B), dim3(64 * DK_WAVES), 0, s, P, img0, pitch0, fstride0,
+                       pyr, oct_xy, oct_resp, oct_count, kps, desc, counts);
 }
 
 void og_launch_grid(hipStream_t s, const orbgpu_kp_dev* kps, const int* counts, int frame_cap, OgGridGeom G,
-                    int* cell_start, int* cell_items, int B)
+                    int* cell_start, int* cell_items, int* status, int B)
 {
-    hipLaunchKernelGGL(og_grid_kernel, dim3(B), dim3(256), 0, s, kps, counts, frame_cap, G, cell_start, cell_items);
+    hipLaunchKernelGGL(og_grid_kernel, dim3(B), dim3(256), 0, s, kps, counts, frame_cap, G, cell_start, cell_items,
+                       status);
 }

@@ -370,6 +370,10 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
             return ORBGPU_ERR_UNSUPPORTED;
         }
     }
+    if (koff > OG_GRID_LDS_ITEMS) {
+        c->err = "more than " + std::to_string(OG_GRID_LDS_ITEMS) + " keypoints per frame (grid capacity)";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
     P.total_cells = (int)cells.size();
     P.kcap_total = koff;
     P.frame_cap = koff;
@@ -398,6 +402,20 @@ static int ensure_status(orbgpu_ctx* c)
     if (c->status.p) return ORBGPU_OK;
     HIP_TRY(c, ensure(c->status, 4));
     HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(int) * 4, c->stream));
+    return ORBGPU_OK;
+}
+
+// Frame::AssignFeaturesToGrid of host-supplied frames (single-frame matcher entry points): the grid kernel sorts a
+// frame's items in LDS, OG_GRID_LDS_ITEMS of them at most
+static int launch_host_grid(orbgpu_ctx* c, hipStream_t s, const orbgpu_kp_dev* k, const int* cnt, int cap, int n,
+                            const OgGridGeom& G, int* cs, int* ci)
+{
+    if (n > OG_GRID_LDS_ITEMS) {
+        c->err = "more than " + std::to_string(OG_GRID_LDS_ITEMS) + " keypoints in one frame (grid capacity)";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
+    if (int r = ensure_status(c)) return r;
+    og_launch_grid(s, k, cnt, cap, G, cs, ci, c->status.p, 1);
     return ORBGPU_OK;
 }
 
@@ -503,7 +521,8 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
                        c->desc.p, c->counts.p, B);
     timer_mark(c, "describe");
     if (c->undist) og_launch_undistort(s, c->kps.p, c->kps_un.p, c->counts.p, 0, P.frame_cap, c->und, B);
-    og_launch_grid(s, kps_match(c), c->counts.p, P.frame_cap, c->grid_geom, c->cell_start.p, c->cell_items.p, B);
+    og_launch_grid(s, kps_match(c), c->counts.p, P.frame_cap, c->grid_geom, c->cell_start.p, c->cell_items.p,
+                   c->status.p, B);
     timer_mark(c, "grid");
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(c->done, s));
@@ -736,6 +755,14 @@ static size_t ref_record_bytes(const orbgpu_ctx* c)
     return 16 + (size_t)c->plan.frame_cap * (28 + 32 + (c->undist ? 28 : 0));
 }
 
+int orbgpu_batch_grid(orbgpu_ctx* c, int** d_cell_start, int** d_cell_items)
+{
+    if (!c || !c->planned || !c->last_B) return ORBGPU_ERR_ARG;
+    if (d_cell_start) *d_cell_start = c->cell_start.p;
+    if (d_cell_items) *d_cell_items = c->cell_items.p;
+    return ORBGPU_OK;
+}
+
 long long orbgpu_frame_record_bytes(const orbgpu_ctx* c)
 {
     if (!c || !c->planned) return ORBGPU_ERR_ARG;
@@ -952,7 +979,7 @@ int orbgpu_search_for_initialization(orbgpu_ctx* c, const orbgpu_frame_view* F1,
     }
     HIP_TRY(c, hipMemcpyAsync(cnts, hc, sizeof(hc), hipMemcpyHostToDevice, s));
     const OgGridGeom G{F2->grid.minX, F2->grid.minY, F2->grid.maxX, F2->grid.maxY, F2->grid.invW, F2->grid.invH};
-    og_launch_grid(s, k2, cnts + 1, cap2, G, cs, ci, 1);
+    if (int r = launch_host_grid(c, s, k2, cnts + 1, cap2, F2->n, G, cs, ci)) return r;
     OgFrameDev f1{k1, d1, cnts, nullptr, nullptr, nullptr, cap1};
     OgFrameDev f2{k2, d2, cnts + 1, cs, ci, nullptr, cap2};
     int n2oct0 = 0;  // only octave-0 keypoints of F2 can be candidates (level1 == 0)
@@ -993,7 +1020,7 @@ int orbgpu_search_for_initialization_batch(orbgpu_ctx* cref, int ref, orbgpu_ctx
     const OgGridGeom G{grid.minX, grid.minY, grid.maxX, grid.maxY, grid.invW, grid.invH};
     if (std::memcmp(&G, &c->grid_geom, sizeof(G)) != 0) {
         c->grid_geom = G;
-        og_launch_grid(s, kps_match(c), c->counts.p, c->plan.frame_cap, G, c->cell_start.p, c->cell_items.p,
+        og_launch_grid(s, kps_match(c), c->counts.p, c->plan.frame_cap, G, c->cell_start.p, c->cell_items.p, c->status.p,
                        c->last_B);
     }
     OgFrameDev f1{kps_match(cref), cref->desc.p, cref->counts.p, nullptr, nullptr, nullptr, cref->plan.frame_cap};
@@ -1569,7 +1596,7 @@ int orbgpu_search_by_projection(orbgpu_ctx* c, const orbgpu_frame_view* F, const
     int hc = F->n;
     HIP_TRY(c, hipMemcpyAsync(cnts, &hc, sizeof(int), hipMemcpyHostToDevice, s));
     const OgGridGeom G{F->grid.minX, F->grid.minY, F->grid.maxX, F->grid.maxY, F->grid.invW, F->grid.invH};
-    og_launch_grid(s, k, cnts, n, G, cs, ci, 1);
+    if (int r = launch_host_grid(c, s, k, cnts, n, F->n, G, cs, ci)) return r;
     OgFrameDev fd{k, d, cnts, cs, ci, F->uright ? ur : nullptr, n};
     OgMapPointsDev mpd{mp->m, tiv, bad, lvl, vc, px, py, pxr, nobs, md};
     int r = run_projection(c, s, fd, G, sfd, mpd, m, 1, nnratio, th, own, obs, nm);
@@ -1767,7 +1794,7 @@ int orbgpu_search_by_projection_last_frame(orbgpu_ctx* c, const orbgpu_frame_vie
     int hc = F->n;
     HIP_TRY(c, hipMemcpyAsync(cnts, &hc, sizeof(int), hipMemcpyHostToDevice, s));
     const OgGridGeom G{F->grid.minX, F->grid.minY, F->grid.maxX, F->grid.maxY, F->grid.invW, F->grid.invH};
-    og_launch_grid(s, k, cnts, n, G, cs, ci, 1);
+    if (int r = launch_host_grid(c, s, k, cnts, n, F->n, G, cs, ci)) return r;
     OgFrameDev fd{k, d, cnts, cs, ci, F->uright ? ur : nullptr, n};
     OgLastFrameDev lfd{LF->n, lk, hm, ol, lp, lo, ld};
     const OgCameraDev cam = camera_dev(curc, G.minX, G.maxX, G.minY, G.maxY);
@@ -1842,7 +1869,7 @@ int orbgpu_search_by_projection_keyframe(orbgpu_ctx* c, const orbgpu_frame_view*
     int hc = F->n;
     HIP_TRY(c, hipMemcpyAsync(cnts, &hc, sizeof(int), hipMemcpyHostToDevice, s));
     const OgGridGeom G{F->grid.minX, F->grid.minY, F->grid.maxX, F->grid.maxY, F->grid.invW, F->grid.invH};
-    og_launch_grid(s, k, cnts, n, G, cs, ci, 1);
+    if (int r = launch_host_grid(c, s, k, cnts, n, F->n, G, cs, ci)) return r;
     OgFrameDev fd{k, d, cnts, cs, ci, nullptr, n};
     OgLastFrameDev kfd{KF->n, kk, kv, nullptr, kp3, nullptr, kd};
     OgCameraDev cam = camera_dev(curc, G.minX, G.maxX, G.minY, G.maxY);

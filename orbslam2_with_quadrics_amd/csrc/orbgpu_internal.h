@@ -26,6 +26,7 @@
 #define OG_GRID_CELLS (OG_GRID_COLS * OG_GRID_ROWS)
 #define OG_OCT_MAXL 1024   // max octree list length handled in LDS (N_l + 3 + slack)
 #define OG_MAX_CELL_W 64   // wCell <= 59 for any width (nCols = floor(w/30))
+#define OG_GRID_LDS_ITEMS 8192  // per-frame keypoint capacity (frame_cap) the grid kernel sorts in LDS
 
 struct OgLevel {
     int w, h;              // level size

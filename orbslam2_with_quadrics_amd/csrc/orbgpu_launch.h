@@ -56,7 +56,7 @@ void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, lon
                         const uint8_t* pyr, const uint32_t* oct_xy, const uint8_t* oct_resp, const int* oct_count,
                         orbgpu_kp_dev* kps, uint8_t* desc, int* counts, int B);
 void og_launch_grid(hipStream_t s, const orbgpu_kp_dev* kps, const int* counts, int frame_cap, OgGridGeom G,
-                    int* cell_start, int* cell_items, int B);
+                    int* cell_start, int* cell_items, int* status, int B);
 
 // matchers (orb_match.hip)
 struct OgFrameDev {        // device view of one or many frames (batch stride frame_cap)

@@ -96,3 +96,39 @@ def test_bench_shape_two_streams_b256(gpu, oracle):
         exs[0].device_free(d_frames)
         ex_ref.device_free(d_f1)
     assert KP_DTYPE.itemsize == 28
+
+
+def test_grid_csr_batch256_vs_oracle(gpu, oracle):
+    """Frame::AssignFeaturesToGrid of a 256-frame 1080p batch compared array by array with the oracle's grid
+    (cell starts and per-cell item lists, src/Frame.cc:230-245) -- the grid kernel's LDS sort at the batch size
+    where its round-1 generic-pointer form faulted."""
+    import ctypes as C
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from orbslam2_with_quadrics_amd import _lib, synthetic
+
+    rows, cols, NF, B = 1080, 1920, 2000, 256
+    _, frames = bench._frames(synthetic, rows, cols, B, 0)
+    ex = gpu.ORBextractor(NF, 1.2, 8, 20, 7)
+    d = ex.device_alloc(frames.nbytes)
+    try:
+        ex.h2d(d, frames)
+        ex.extract_batch_device(d, B, cols, rows, cols, rows * cols)
+        ex.synchronize()  # raises on a tripped range check (status bit 64)
+        cap = ex.batch_outputs()[3]
+        cs, ci = C.c_void_p(), C.c_void_p()
+        _lib.check(ex.ctx, _lib.lib().orbgpu_batch_grid(ex.ctx, C.byref(cs), C.byref(ci)), "grid")
+        CS = np.zeros(B * 3073, np.int32)
+        CI = np.zeros(B * cap, np.int32)
+        ex.d2h(CS, cs.value)
+        ex.d2h(CI, ci.value)
+        sf = ex.GetScaleFactors()
+        for b in range(0, B, 17):
+            k, dsc = ex.batch_download(b)
+            of = oracle.OracleFrame(k, dsc, cols, rows, sf)
+            s0 = CS[b * 3073:(b + 1) * 3073]
+            assert np.array_equal(s0, of.cell_start), b
+            assert np.array_equal(CI[b * cap:b * cap + s0[-1]], of.cell_items[:s0[-1]]), b
+    finally:
+        ex.device_free(d)
