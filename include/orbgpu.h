@@ -342,6 +342,12 @@ int orbgpu_compute_stereo_matches_batch(orbgpu_ctx* left, orbgpu_ctx* right, flo
  * sizes of the octree workgroup of (frame 0, level 0) of the last batch.  ORBGPU_ERR_UNSUPPORTED in the
  * product build. */
 int orbgpu_debug_octree_profile(orbgpu_ctx* ctx, unsigned long long* out, int n);
+/* Exhaustive pin of the device restatements of glibc sincosf (fn 0; src/ORBextractor.cc:113) and logf (fn 1;
+ * src/MapPoint.cc:410): every float bit pattern u in [begin, end) is evaluated on `device` and folded into
+ * out[(u >> chunk_log2) - (begin >> chunk_log2)] (nchunks entries) as the order-free hash of
+ * tools/libm_chunk_hash.c, which computes the same hashes from the host libm. */
+int orbgpu_debug_math_hash(int device, int fn, unsigned long long begin, unsigned long long end, int chunk_log2,
+                           unsigned long long* out, int nchunks);
 
 /* ---- Colour input: Tracking::GrabImage* -------------------------------------------------------------- */
 

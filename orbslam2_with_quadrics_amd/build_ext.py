@@ -14,7 +14,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "liborbgpu.so")
-SOURCES = ["orb_extract.hip", "orb_match.hip", "orb_stereo.hip", "orb_frame.hip", "orb_bow.hip", "orbgpu_capi.cpp"]
+SOURCES = ["orb_extract.hip", "orb_match.hip", "orb_stereo.hip", "orb_frame.hip", "orb_bow.hip", "orb_pins.hip",
+           "orbgpu_capi.cpp"]
 HEADERS = ["orbgpu_internal.h", "orbgpu_launch.h", "orb_math_dev.h", "orb_pattern.inc",
            os.path.join("..", "..", "include", "orbgpu.h")]
 ARCH = os.environ.get("ORBGPU_ARCH", "gfx950")

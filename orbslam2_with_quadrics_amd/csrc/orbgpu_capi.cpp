@@ -755,6 +755,22 @@ static size_t ref_record_bytes(const orbgpu_ctx* c)
     return 16 + (size_t)c->plan.frame_cap * (28 + 32 + (c->undist ? 28 : 0));
 }
 
+int orbgpu_debug_math_hash(int device, int fn, unsigned long long begin, unsigned long long end, int chunk_log2,
+                           unsigned long long* out, int nchunks)
+{
+    if (fn < 0 || fn > 1 || begin >= end || end > (1ull << 32) || chunk_log2 < 12 || chunk_log2 > 32 || !out)
+        return ORBGPU_ERR_ARG;
+    if ((long long)(((end - 1) >> chunk_log2) - (begin >> chunk_log2) + 1) != nchunks) return ORBGPU_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return ORBGPU_ERR_HIP;
+    unsigned long long* d = nullptr;
+    if (hipMalloc((void**)&d, (size_t)nchunks * 8) != hipSuccess) return ORBGPU_ERR_HIP;
+    hipError_t e = hipMemset(d, 0, (size_t)nchunks * 8);
+    if (e == hipSuccess) e = og_math_hash(fn, begin, end, chunk_log2, d, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d, (size_t)nchunks * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return e == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_HIP;
+}
+
 int orbgpu_batch_grid(orbgpu_ctx* c, int** d_cell_start, int** d_cell_items)
 {
     if (!c || !c->planned || !c->last_B) return ORBGPU_ERR_ARG;

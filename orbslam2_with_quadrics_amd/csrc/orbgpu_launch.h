@@ -15,6 +15,9 @@ struct OgGridGeom {
 };
 
 hipError_t og_upload_pattern(int device);
+// exhaustive pins of og_sincosf / og_logf (orb_pins.hip): chunked order-free hashes over a float bit range
+hipError_t og_math_hash(int fn, unsigned long long begin, unsigned long long end, int chunk_log2,
+                        unsigned long long* d_out, hipStream_t s);
 
 // two chained levels per launch (og_resize2_kernel): A = level l from S = level l-1, B = level l+1 from A
 struct OgRz2Geom {

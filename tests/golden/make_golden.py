@@ -8,6 +8,9 @@ extract_golden.json : the oracle's ORB extraction of seeded synthetic frames (ha
                       This pins the oracle against regressions; it is NOT a reference-binary output
                       (the reference cannot be built here -- DESIGN.md §4).
 match_golden.json   : oracle SearchForInitialization on a seeded 1080p pair (match vector hash).
+libm_chunks.json    : chunked hashes of the host libm (glibc 2.35) sincosf on every float in [0, 6.5) and logf on
+                      every positive finite float (tools/libm_chunk_hash.c); the GPU restatements are compared with
+                      them input by input (tests/test_gpu_pins.py).
 bench_golden.json   : the oracle's outputs on exactly the frames bench.py times (config 3: 1920x1080, 2000 features,
                       default semantics; the initial frame and the 32 unique frames of every rank 0-7) --
                       keypoint / descriptor / vnMatches12 / vbPrevMatched hashes, checked after the timed loop.
@@ -158,6 +161,29 @@ def tracking_cases():
               open(os.path.join(OUT, "tracking_golden.json"), "w"), indent=1)
 
 
+LIBM_RANGES = {"sincos": (0, 0x40D00000), "logf": (1, 0x7F800000)}
+LIBM_CHUNK_LOG2 = 22
+
+
+def libm_chunk_hashes(fn, begin, end, chunk_log2=LIBM_CHUNK_LOG2):
+    import subprocess
+    import tempfile
+
+    exe = os.path.join(tempfile.gettempdir(), "libm_chunk_hash")
+    subprocess.check_call(["gcc", "-O2", "-fopenmp", os.path.join(ROOT, "tools", "libm_chunk_hash.c"), "-o", exe,
+                           "-lm"])
+    out = subprocess.check_output([exe, fn, str(begin), str(end), str(chunk_log2)]).decode().split()
+    return [out[i + 1] for i in range(0, len(out), 2)]
+
+
+def libm_chunks():
+    g = {"generator": "tools/libm_chunk_hash.c (host libm, glibc 2.35 x86_64) via tests/golden/make_golden.py",
+         "chunk_log2": LIBM_CHUNK_LOG2, "functions": {}}
+    for fn, (b, e) in LIBM_RANGES.items():
+        g["functions"][fn] = dict(begin=b, end=e, hashes=libm_chunk_hashes(fn, b, e))
+    json.dump(g, open(os.path.join(OUT, "libm_chunks.json"), "w"), indent=0)
+
+
 def _bench_rank(rank):
     sys.path.insert(0, ROOT)
     import bench
@@ -194,6 +220,9 @@ def bench_cases():
 
 if __name__ == "__main__":
     O.build()
+    if "--only-libm" in sys.argv:
+        libm_chunks()
+        sys.exit(0)
     if "--only-bench" in sys.argv:
         bench_cases()
         sys.exit(0)
@@ -202,5 +231,6 @@ if __name__ == "__main__":
         extract_cases()
         match_cases()
         bench_cases()
+        libm_chunks()
     tracking_cases()
     print("golden fixtures written to", OUT)

@@ -445,3 +445,17 @@ def test_oracle_bench_golden_sample(oracle):
             k, d = ex(frames[i])
             assert hashlib.sha256(k.tobytes()).hexdigest() == gr["frames"][i]["kps_sha256"]
             assert hashlib.sha256(d.tobytes()).hexdigest() == gr["frames"][i]["desc_sha256"]
+
+
+def test_libm_chunk_golden_matches_host_libm():
+    """tests/golden/libm_chunks.json (the GPU pins' reference) re-derived from this host's libm on sample chunks."""
+    sys.path.insert(0, GOLDEN)
+    import make_golden
+
+    g = json.load(open(os.path.join(GOLDEN, "libm_chunks.json")))
+    cl = g["chunk_log2"]
+    for fn, spec in g["functions"].items():
+        for c in (0, len(spec["hashes"]) // 2, len(spec["hashes"]) - 1):
+            lo = max(spec["begin"], ((spec["begin"] >> cl) + c) << cl)
+            hi = min(spec["end"], ((spec["begin"] >> cl) + c + 1) << cl)
+            assert make_golden.libm_chunk_hashes(fn, lo, hi, cl) == [spec["hashes"][c]], (fn, c)
