@@ -1,0 +1,78 @@
+// Compile-check shim (tests/test_integration_compile.py only): declarations of the cv:: names the integration/
+// sources and the reference's include/ORBextractor.h use -- enough for `g++ -fsyntax-only`, nothing is defined
+// or executed.  Not OpenCV, not part of the product.
+#pragma once
+#include <cstddef>
+#include <vector>
+
+#define CV_8U 0
+#define CV_8UC1 0
+#define CV_32F 5
+
+namespace cv {
+template <typename T>
+struct Point_ {
+    T x, y;
+};
+typedef Point_<int> Point2i;
+typedef Point2i Point;
+typedef Point_<float> Point2f;
+
+struct KeyPoint {
+    Point2f pt;
+    float size, angle, response;
+    int octave, class_id;
+};
+
+struct Range {
+    int start, end;
+};
+
+class _OutputArray;
+typedef const _OutputArray& OutputArray;
+
+class Mat {
+public:
+    Mat();
+    Mat(int rows, int cols, int type);
+    Mat(int rows, int cols, int type, void* data, size_t step = 0);
+    int rows, cols;
+    size_t step;
+    unsigned char* data;
+    bool empty() const;
+    int type() const;
+    bool isContinuous() const;
+    void create(int rows, int cols, int type);
+    void release();
+    Mat clone() const;
+    void copyTo(OutputArray m) const;
+    Mat rowRange(int a, int b) const;
+    Mat colRange(int a, int b) const;
+    Mat col(int c) const;
+    Mat t() const;
+    template <typename T>
+    T& at(int i, int j = 0);
+    template <typename T>
+    const T& at(int i, int j = 0) const;
+    template <typename T>
+    T* ptr(int i = 0);
+    template <typename T>
+    const T* ptr(int i = 0) const;
+};
+
+class _InputArray {
+public:
+    _InputArray();
+    _InputArray(const Mat& m);
+    bool empty() const;
+    Mat getMat() const;
+};
+class _OutputArray : public _InputArray {
+public:
+    _OutputArray();
+    _OutputArray(Mat& m);
+    void release() const;
+    void create(int rows, int cols, int type) const;
+};
+typedef const _InputArray& InputArray;
+}  // namespace cv

@@ -13,6 +13,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "liborb_oracle.so")
+# ORB_ORACLE_FAST=1: the -O3 -march=native build (the reference's flags; bit-identical results) for CPU timing
+if os.environ.get("ORB_ORACLE_FAST") == "1":
+    LIB_PATH = os.path.join(HERE, "build", "liborb_oracle_fast.so")
 
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])

@@ -574,7 +574,7 @@ static void oo_orb_descriptor(float kx, float ky, float angle_deg, const uint8_t
 {
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float angle = angle_deg * factorPI;
-    float a, b;
+    float a = 0.f, b = 0.f; /* angle in [0, 2pi]: oo_sincosf always writes both (its |y| >= 120 branch is unreachable) */
     oo_sincosf(angle, &b, &a);
     const uint8_t* center = img + (size_t)oo_cvround(ky) * stride + oo_cvround(kx);
     const signed char* pat = oo_orb_pattern;
