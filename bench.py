@@ -138,36 +138,78 @@ def interval_union(iv):
 
 
 # ------------------------------------------------------------------------------------------------
-# CPU baseline: the oracle (a plain-C restatement of the reference path), single thread
+# CPU baseline: the oracle (a plain-C restatement of the reference path) built with the reference's flags
+# (-O3 -march=native, bit-identical to the checker build), on one pinned host core; median per frame after
+# warm-up frames (the full >= 200-frame and all-cores runs: tools/cpu_baseline.py)
 # ------------------------------------------------------------------------------------------------
-def cpu_baseline(rows, cols, nfeat, seconds):
+def _oracle_fast():
+    os.environ["ORB_ORACLE_FAST"] = "1"
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as O
-    from orbslam2_with_quadrics_amd import synthetic
 
     O.build()
+    return O
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def timed_cpu_frames(work, frame, seconds, warmup=3):
+    """Median seconds per frame of work(frame(i)) on one pinned core (the lowest core this process may use)."""
+    import statistics
+
+    prev = os.sched_getaffinity(0)
+    os.sched_setaffinity(0, {min(prev)})
+    try:
+        for i in range(warmup):
+            work(frame(i))
+        ts, spent = [], 0.0
+        i = warmup
+        while spent < seconds or len(ts) < 3:
+            f = frame(i)
+            t = time.perf_counter()
+            work(f)
+            ts.append(time.perf_counter() - t)
+            spent += ts[-1]
+            i += 1
+    finally:
+        os.sched_setaffinity(0, prev)
+    return statistics.median(ts), len(ts)
+
+
+def cpu_record(med, n, warmup, what):
+    return {"value": round(1.0 / med, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+            "sample": f"median of {n} frames after 3 warm-up frames, one pinned core: {what}; oracle built -O3 "
+                      f"-march=native (plain C, scalar; OpenCV's SIMD build of the reference would be faster)"}
+
+
+def cpu_baseline(rows, cols, nfeat, seconds):
+    O = _oracle_fast()
+    from orbslam2_with_quadrics_amd import synthetic
+
     ex = O.OracleExtractor(nfeat)
     scene = synthetic.make_scene(synthetic.SEED_BASE + 999, rows, cols)
     f1 = synthetic.render(scene, rows, cols, 0, 0, noise_seed=5)
-    spent = 0.0
-    ts = time.perf_counter()
     k1, d1 = ex(f1)
     sf = ex.tables()["scale"]
     F1 = O.OracleFrame(k1, d1, cols, rows, sf)
-    spent += time.perf_counter() - ts
-    frames = 0
-    while spent < seconds or frames < 2:
-        f2 = synthetic.render(scene, rows, cols, 3 + frames % 9, 2 + frames % 5, noise_seed=100 + frames)
-        ts = time.perf_counter()
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+
+    def work(f2):
         k2, d2 = ex(f2)
-        F2 = O.OracleFrame(k2, d2, cols, rows, sf)
-        O.search_for_initialization(F1, F2, np.stack([k1["x"], k1["y"]], 1), 0.9, True, 100)
-        spent += time.perf_counter() - ts
-        frames += 1
-    return {"value": round(frames / spent, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{frames} frames of {cols}x{rows}, {nfeat} features: oracle extract + "
-                      f"SearchForInitialization on one host thread (plain C, scalar; OpenCV's SIMD build "
-                      f"would be faster)"}
+        O.search_for_initialization(F1, O.OracleFrame(k2, d2, cols, rows, sf), prev.copy(), 0.9, True, 100)
+
+    med, n = timed_cpu_frames(work, lambda i: synthetic.render(scene, rows, cols, 3 + i % 9, 2 + i % 5,
+                                                                noise_seed=100 + i), seconds)
+    return cpu_record(med, n, 3, f"{cols}x{rows}, {nfeat} features, oracle extract + SearchForInitialization")
 
 
 # ------------------------------------------------------------------------------------------------
@@ -467,27 +509,24 @@ def tracking_mappoints(k, d, M, seed):
 
 
 def cpu_baseline_tracking(rows, cols, nfeat, M, seconds):
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle_py as O
+    O = _oracle_fast()
     from orbslam2_with_quadrics_amd import synthetic
 
-    O.build()
     ex = O.OracleExtractor(nfeat)
     sf = ex.tables()["scale"]
     scene = synthetic.make_scene(synthetic.SEED_BASE + 997, rows, cols)
-    spent, frames = 0.0, 0
-    while spent < seconds or frames < 2:
-        f = synthetic.render(scene, rows, cols, frames % 9, frames % 5, noise_seed=300 + frames)
-        k0, d0 = ex(f)
-        mp = tracking_mappoints(k0, d0, M, frames)
-        ts = time.perf_counter()
-        k, d = ex(f)
+    f = synthetic.render(scene, rows, cols, 0, 0, noise_seed=300)
+    k0, d0 = ex(f)
+    mp = tracking_mappoints(k0, d0, M, 0)
+
+    def work(img):
+        k, d = ex(img)
         O.search_by_projection(O.OracleFrame(k, d, cols, rows, sf), mp, 0.8, 1.0)
-        spent += time.perf_counter() - ts
-        frames += 1
-    return {"value": round(frames / spent, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{frames} frames of {cols}x{rows}, {nfeat} features: oracle extraction + SearchByProjection "
-                      f"vs {M} map points (th 1) on one host thread"}
+
+    med, n = timed_cpu_frames(work, lambda i: synthetic.render(scene, rows, cols, i % 3, i % 2, noise_seed=300 + i),
+                              seconds)
+    return cpu_record(med, n, 3, f"{cols}x{rows}, {nfeat} features, oracle extraction + SearchByProjection vs {M} "
+                                 f"map points (th 1)")
 
 
 def setup_tracking(args, env):
@@ -575,43 +614,33 @@ DEFAULT_SHAPE = {"mono_init": (1080, 1920, 2000), "extract": (480, 640, 1000), "
 
 
 def cpu_baseline_extract(rows, cols, nfeat, seconds):
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle_py as O
+    O = _oracle_fast()
     from orbslam2_with_quadrics_amd import synthetic
 
-    O.build()
     ex = O.OracleExtractor(nfeat)
     scene = synthetic.make_scene(synthetic.SEED_BASE + 998, rows, cols)
-    spent, frames = 0.0, 0
-    while spent < seconds or frames < 2:
-        f = synthetic.render(scene, rows, cols, frames % 9, frames % 5, noise_seed=100 + frames)
-        ts = time.perf_counter()
-        ex(f)
-        spent += time.perf_counter() - ts
-        frames += 1
-    return {"value": round(frames / spent, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{frames} frames of {cols}x{rows}, {nfeat} features: oracle extraction on one host thread"}
+    med, n = timed_cpu_frames(lambda f: ex(f), lambda i: synthetic.render(scene, rows, cols, i % 9, i % 5,
+                                                                          noise_seed=100 + i), seconds)
+    return cpu_record(med, n, 3, f"{cols}x{rows}, {nfeat} features, oracle extraction")
 
 
 def cpu_baseline_stereo(rows, cols, nfeat, seconds):
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle_py as O
+    O = _oracle_fast()
     from orbslam2_with_quadrics_amd import synthetic
 
-    O.build()
     exL, exR = O.OracleExtractor(nfeat), O.OracleExtractor(nfeat)
-    spent, frames = 0.0, 0
-    while spent < seconds or frames < 2:
-        l, r, _ = synthetic.stereo_pair(900 + frames % 4, rows, cols)
-        ts = time.perf_counter()
-        kL, dL = exL(l)
-        kR, dR = exR(r)
+    pairs = [synthetic.stereo_pair(900 + i, rows, cols) for i in range(4)]
+
+    def work(p):
+        kL, dL = exL(p[0])
+        kR, dR = exR(p[1])
         O.stereo_matches(exL, exR, kL, dL, kR, dR, 386.1448, 386.1448 / 718.856)
-        spent += time.perf_counter() - ts
-        frames += 1
-    return {"value": round(frames / spent, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{frames} stereo pairs of {cols}x{rows}, {nfeat} features: oracle L+R extraction + "
-                      f"ComputeStereoMatches on one host thread"}
+
+    med, n = timed_cpu_frames(work, lambda i: pairs[i % 4], seconds)
+    r = cpu_record(med, n, 3, f"{cols}x{rows} stereo pairs, {nfeat} features, oracle L+R extraction + "
+                              f"ComputeStereoMatches")
+    r["unit"] = "pairs/s"
+    return r
 
 
 def main():

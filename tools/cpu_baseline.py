@@ -99,16 +99,20 @@ def make_config(cfg):
 
 
 def single_core(cfg, n, warm, core=0):
+    prev = os.sched_getaffinity(0)
     os.sched_setaffinity(0, {core})
-    work, frame, desc = make_config(cfg)
-    frames = [frame(i) for i in range(warm + n)]
-    for f in frames[:warm]:
-        work(f)
-    ts = []
-    for f in frames[warm:]:
-        t = time.perf_counter()
-        work(f)
-        ts.append(time.perf_counter() - t)
+    try:
+        work, frame, desc = make_config(cfg)
+        frames = [frame(i) for i in range(warm + n)]
+        for f in frames[:warm]:
+            work(f)
+        ts = []
+        for f in frames[warm:]:
+            t = time.perf_counter()
+            work(f)
+            ts.append(time.perf_counter() - t)
+    finally:
+        os.sched_setaffinity(0, prev)
     return desc, ts
 
 
@@ -124,10 +128,10 @@ def _worker(args):
     return time.perf_counter() - t, len(frames)
 
 
-def all_cores(cfg, n):
+def all_cores(cfg, n, max_cores):
     from multiprocessing import get_context
 
-    cores = sorted(os.sched_getaffinity(0))
+    cores = sorted(os.sched_getaffinity(0))[:max_cores]
     per = max(1, n // len(cores))
     with get_context("spawn").Pool(len(cores)) as pool:
         t = time.perf_counter()
@@ -145,6 +149,7 @@ def main():
     ap.add_argument("--frames", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--configs", default="2,3,4,5")
+    ap.add_argument("--max-cores", type=int, default=16, help="workers of the all-cores run (the GPU box's CPU share)")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r02_cpu_baseline.json"))
     args = ap.parse_args()
     out = {"cpu_model": cpu_model(), "nproc": os.cpu_count(), "oracle_build": "gcc -O3 -march=native "
@@ -158,7 +163,7 @@ def main():
                                                   "median_ms": round(med * 1e3, 3),
                                                   "mean_ms": round(statistics.mean(ts) * 1e3, 3),
                                                   "frames_per_s_median": round(1 / med, 3), "pinned_core": 0}}
-        entry["all_cores"] = all_cores(cfg, args.frames)
+        entry["all_cores"] = all_cores(cfg, args.frames, args.max_cores)
         out["configs"][str(cfg)] = entry
         print(cfg, json.dumps(entry), flush=True)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
