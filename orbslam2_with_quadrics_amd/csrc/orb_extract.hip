@@ -865,34 +865,56 @@ __device__ unsigned long long og_oct_prof[256];
     } while (0)
 #endif
 
-__global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_octree_kernel(OgPlan P, const u64* __restrict__ cand,
+// exclusive block scan of NPT ints per thread, thread t holding items t*NPT .. t*NPT + NPT-1 (in order)
+template <int NPT>
+__device__ __forceinline__ void og_block_excl_scan_n(const int (&v)[NPT], int (&ex)[NPT], int* wsum, int* total)
+{
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < NPT; j++) s += v[j];
+    int e = og_block_excl_scan(s, wsum, total);
+#pragma unroll
+    for (int j = 0; j < NPT; j++) {
+        ex[j] = e;
+        e += v[j];
+    }
+}
+
+// MAXL = list capacity (OG_OCT_MAXL, or OG_OCT_MAXL_BIG for levels of more than ~1000 features, 2 list nodes per
+// thread); levels [l0, l0 + gridDim.x / frames) of the launch, level-major
+template <int MAXL>
+__global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_octree_kernel(OgPlan P, int l0, const u64* __restrict__ cand,
                                                            const int* __restrict__ cand_count,
                                                            uint16_t* __restrict__ node_of,
                                                            uint32_t* __restrict__ oct_xy,
                                                            uint8_t* __restrict__ oct_resp,
-                                                           int* __restrict__ oct_count, int* __restrict__ status)
+                                                           int* __restrict__ oct_count, int* __restrict__ status,
+                                                           int nlaunch)
 {
-    __shared__ OctNode nodes[2][OG_OCT_MAXL];
-    __shared__ uint8_t fresh[2][OG_OCT_MAXL];
-    __shared__ int splitRank[OG_OCT_MAXL];
-    __shared__ int splitNode[OG_OCT_MAXL];
-    __shared__ int newPos[OG_OCT_MAXL];
-    __shared__ int aux[OG_OCT_MAXL];
+    constexpr int OG_OCT_MAXL_T = MAXL;
+    constexpr int NPT = MAXL / OCT_NT;  // list nodes per thread in the per-node phases
+    static_assert(NPT * OCT_NT == MAXL, "list capacity is a multiple of the workgroup");
+    __shared__ OctNode nodes[2][MAXL];
+    __shared__ uint8_t fresh[2][MAXL];
+    __shared__ int splitRank[MAXL];
+    __shared__ int splitNode[MAXL];
+    __shared__ int newPos[MAXL];
+    __shared__ int aux[MAXL];
     // child counts, indexed 4*node + quadrant: one buffer -- a round's counts are consumed (split set,
     // children) before the key pass accumulates the next round's, with barriers in between; the last key
     // pass keeps the best key per node in the same storage.  ~74 KB of LDS in total: 2 workgroups per CU.
-    __shared__ __attribute__((aligned(16))) int childCnt[4 * OG_OCT_MAXL];
-    __shared__ __attribute__((aligned(16))) uint16_t childPos[4 * OG_OCT_MAXL];
+    __shared__ __attribute__((aligned(16))) int childCnt[4 * MAXL];
+    __shared__ __attribute__((aligned(16))) uint16_t childPos[4 * MAXL];
     // final-phase planning only: the candidates' (size, creation id) keys, in the previous round's (dead) childPos
     u64* skey = (u64*)childPos;
-    u64* best = (u64*)childCnt;  // [OG_OCT_MAXL], final key pass only
+    u64* best = (u64*)childCnt;  // [MAXL], final key pass only
     __shared__ int wsum[32];
     __shared__ int sv[16];
 
     // level-major dispatch order, level 0 first: the finest level has the most candidates (and rounds), so
     // its workgroups start in the first wave of residency instead of being interleaved with the short ones
-    const int nb = (int)gridDim.x / P.nlevels;  // frames in the launch
-    const int l = (int)blockIdx.x / nb, f = (int)blockIdx.x % nb, tid = threadIdx.x;
+    const int nb = (int)gridDim.x / nlaunch;  // frames in the launch
+    const int l = l0 + (int)blockIdx.x / nb, f = (int)blockIdx.x % nb, tid = threadIdx.x;
     const OgLevel& L = P.lv[l];
     const int C = min(cand_count[f * P.nlevels + l], L.cand_cap);
     const u64* K = cand + (long long)f * P.cand_per_frame + L.cand_off;
@@ -985,34 +1007,57 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const int* CC = childCnt;
         int* NCC = childCnt;
         __syncthreads();
-        // ---- the split set of this round and its order
-        const int i = tid;
+        // ---- the split set of this round and its order.  List node i = NPT * tid + j (j < NPT): each thread owns
+        // NPT consecutive nodes, so thread-local prefixes plus one block scan keep the list order.
         int S;
         if (mode == 0) {
-            const bool flag = i < Ln && cn[i].cnt > 1;
-            const int rank = og_block_excl_scan(flag ? 1 : 0, wsum, &S);
-            if (i < Ln) splitRank[i] = flag ? rank : -1;
-            if (flag) splitNode[rank] = i;
+            int fl[NPT], rk[NPT];
+#pragma unroll
+            for (int j = 0; j < NPT; j++) {
+                const int i = NPT * tid + j;
+                fl[j] = i < Ln && cn[i].cnt > 1;
+            }
+            og_block_excl_scan_n<NPT>(fl, rk, wsum, &S);
+#pragma unroll
+            for (int j = 0; j < NPT; j++) {
+                const int i = NPT * tid + j;
+                if (i < Ln) splitRank[i] = fl[j] ? rk[j] : -1;
+                if (fl[j]) splitNode[rk[j]] = i;
+            }
         } else {
             // vSizeAndPointerToNode of the previous round sorted ascending by (size, ptr) and walked from
             // the back (src/ORBextractor.cc:684-685): order = descending (cnt, creation id)
-            const bool flag = i < Ln && cf[i] && cn[i].cnt > 1;
-            const int c = og_block_excl_scan(flag ? 1 : 0, wsum, &S);
-            u64 mk = 0;
-            if (flag) {
-                mk = ((u64)(uint32_t)cn[i].cnt << 32) | (u64)(uint32_t)cn[i].cid;  // (size, ptr) order, unique
-                skey[c] = mk;
+            int fl[NPT], cx[NPT];
+            u64 mk[NPT];
+#pragma unroll
+            for (int j = 0; j < NPT; j++) {
+                const int i = NPT * tid + j;
+                fl[j] = i < Ln && cf[i] && cn[i].cnt > 1;
+            }
+            og_block_excl_scan_n<NPT>(fl, cx, wsum, &S);
+#pragma unroll
+            for (int j = 0; j < NPT; j++) {
+                const int i = NPT * tid + j;
+                mk[j] = 0;
+                if (fl[j]) {
+                    mk[j] = ((u64)(uint32_t)cn[i].cnt << 32) | (u64)(uint32_t)cn[i].cid;  // (size, ptr) order, unique
+                    skey[cx[j]] = mk[j];
+                }
             }
             __syncthreads();
-            if (i < Ln) splitRank[i] = -1;
-            if (flag) {
-                // rank = number of candidates with a larger key: every lane reads the same key (broadcast), no
-                // dependent lookups, so the loop pipelines
-                int rank = 0;
+#pragma unroll
+            for (int j = 0; j < NPT; j++) {
+                const int i = NPT * tid + j;
+                if (i < Ln) splitRank[i] = -1;
+                if (fl[j]) {
+                    // rank = number of candidates with a larger key: every lane reads the same key (broadcast), no
+                    // dependent lookups, so the loop pipelines
+                    int rank = 0;
 #pragma unroll 8
-                for (int q = 0; q < S; q++) rank += skey[q] > mk;
-                splitRank[i] = rank;
-                splitNode[rank] = i;
+                    for (int q = 0; q < S; q++) rank += skey[q] > mk[j];
+                    splitRank[i] = rank;
+                    splitNode[rank] = i;
+                }
             }
         }
         if (S == 0) {  // nothing to split: size == prevSize -> bFinish
@@ -1022,47 +1067,62 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         }
         __syncthreads();
         // ---- per split (in split order): non-empty children, the final phase's break point (:730-731)
-        int nc = 0, nexp = 0, sn = 0;
-        if (i < S) {
-            sn = splitNode[i];
+        int nc[NPT], nexp[NPT], sn[NPT], exNc[NPT];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int c = CC[4 * sn + q];
-                nc += c > 0;
-                nexp += c > 1;
+        for (int j = 0; j < NPT; j++) {
+            const int i = NPT * tid + j;
+            nc[j] = 0;
+            nexp[j] = 0;
+            sn[j] = 0;
+            if (i < S) {
+                sn[j] = splitNode[i];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int c = CC[4 * sn[j] + q];
+                    nc[j] += c > 0;
+                    nexp[j] += c > 1;
+                }
             }
         }
         int totNc;
-        const int exNc = og_block_excl_scan(nc, wsum, &totNc);
+        og_block_excl_scan_n<NPT>(nc, exNc, wsum, &totNc);
         int A = S;
         if (mode == 1) {
-            const bool reach = i < S && (Ln + exNc + nc - (i + 1) >= N);
             if (tid == 0) sv[5] = S;
             __syncthreads();
-            if (reach) atomicMin(&sv[5], i + 1);
+#pragma unroll
+            for (int j = 0; j < NPT; j++) {
+                const int i = NPT * tid + j;
+                if (i < S && (Ln + exNc[j] + nc[j] - (i + 1) >= N)) atomicMin(&sv[5], i + 1);
+            }
             __syncthreads();
             A = sv[5];
         }
-        if (i == A - 1) sv[6] = exNc + nc;
+#pragma unroll
+        for (int j = 0; j < NPT; j++)
+            if (NPT * tid + j == A - 1) sv[6] = exNc[j] + nc[j];
         __syncthreads();
         const int T = sv[6];
         // ---- children: groups in reverse split order, each n4,n3,n2,n1 (push_front, :621-660)
-        if (i < A) {
-            const OctNode par = cn[sn];
-            const int groupStart = T - (exNc + nc);
-            const int cidBase = sv[2] + exNc;
+#pragma unroll
+        for (int j = 0; j < NPT; j++) {
+            const int i = NPT * tid + j;
+            if (i >= A) continue;
+            const OctNode par = cn[sn[j]];
+            const int groupStart = T - (exNc[j] + nc[j]);
+            const int cidBase = sv[2] + exNc[j];
             // the key pass's remap record of node sn: its split point here, its children's positions below
-            newPos[sn] = (par.x0 + ((par.x1 - par.x0 + 1) >> 1)) | ((par.y0 + ((par.y1 - par.y0 + 1) >> 1)) << 16);
+            newPos[sn[j]] = (par.x0 + ((par.x1 - par.x0 + 1) >> 1)) | ((par.y0 + ((par.y1 - par.y0 + 1) >> 1)) << 16);
             int before = 0;  // non-empty children among q' < q (creation order n1..n4)
             for (int q = 0; q < 4; q++) {
-                const int c = CC[4 * sn + q];
+                const int c = CC[4 * sn[j] + q];
                 if (c > 0) {
-                    const int pos = groupStart + (nc - before - 1);
+                    const int pos = groupStart + (nc[j] - before - 1);
                     OctNode ch = og_child(par, q);
                     ch.cnt = c;
                     ch.cid = cidBase + before;
-                    childPos[4 * sn + q] = (uint16_t)pos;
-                    if (pos < OG_OCT_MAXL) {
+                    childPos[4 * sn[j] + q] = (uint16_t)pos;
+                    if (pos < MAXL) {
                         nn[pos] = ch;
                         nf[pos] = 1;
                     }
@@ -1071,23 +1131,32 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             }
         }
         // ---- kept nodes follow, in their old order
-        const bool kept = i < Ln && (splitRank[i] < 0 || splitRank[i] >= A);
+        int kept[NPT], kr[NPT], ne[NPT], dummy[NPT];
+#pragma unroll
+        for (int j = 0; j < NPT; j++) {
+            const int i = NPT * tid + j;
+            kept[j] = i < Ln && (splitRank[i] < 0 || splitRank[i] >= A);
+            ne[j] = i < A ? nexp[j] : 0;
+        }
         int keptTot;
-        const int kr = og_block_excl_scan(kept ? 1 : 0, wsum, &keptTot);
-        if (kept) {
-            const int pos = T + kr;
+        og_block_excl_scan_n<NPT>(kept, kr, wsum, &keptTot);
+#pragma unroll
+        for (int j = 0; j < NPT; j++) {
+            const int i = NPT * tid + j;
+            if (!kept[j]) continue;
+            const int pos = T + kr[j];
             // remap record of a kept node: split point (0, 0) selects quadrant 3, and all four entries are pos
             newPos[i] = 0;
             ((u64*)childPos)[i] = (u64)(uint16_t)pos * 0x0001000100010001ull;
-            if (pos < OG_OCT_MAXL) {
+            if (pos < MAXL) {
                 nn[pos] = cn[i];
                 nf[pos] = 0;
             }
         }
         int expTot;
-        (void)og_block_excl_scan(i < A ? nexp : 0, wsum, &expTot);
+        og_block_excl_scan_n<NPT>(ne, dummy, wsum, &expTot);
         const int Lnew = T + keptTot;
-        if (Lnew > OG_OCT_MAXL) {
+        if (Lnew > MAXL) {
             if (tid == 0) {
                 atomicOr(status, 2);
                 sv[3] = 1;
@@ -1197,6 +1266,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         }
         __syncthreads();
     }
+    (void)OG_OCT_MAXL_T;
     const int nout = min(Ln, L.kcap);
     for (int n = tid; n < nout; n += OCT_NT) {
         const u64 b = best[n];
@@ -1691,8 +1761,15 @@ void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const u
 void og_launch_octree(hipStream_t s, const OgPlan& P, const u64* cand, const int* cand_count, uint16_t* node_of,
                       uint32_t* oct_xy, uint8_t* oct_resp, int* oct_count, int* status, int B)
 {
-    hipLaunchKernelGGL(og_octree_kernel, dim3(P.nlevels * B), dim3(OCT_NT), 0, s, P, cand, cand_count, node_of, oct_xy,
-                       oct_resp, oct_count, status);
+    // levels whose list may exceed OG_OCT_MAXL (more than ~1000 features: the finest levels, P.oct_big of them)
+    // take the 2-nodes-per-thread kernel; the rest the 1-node-per-thread one
+    const int nbig = P.oct_big, nsmall = P.nlevels - P.oct_big;
+    if (nbig > 0)
+        hipLaunchKernelGGL(og_octree_kernel<OG_OCT_MAXL_BIG>, dim3(nbig * B), dim3(OCT_NT), 0, s, P, 0, cand,
+                           cand_count, node_of, oct_xy, oct_resp, oct_count, status, nbig);
+    if (nsmall > 0)
+        hipLaunchKernelGGL(og_octree_kernel<OG_OCT_MAXL>, dim3(nsmall * B), dim3(OCT_NT), 0, s, P, nbig, cand,
+                           cand_count, node_of, oct_xy, oct_resp, oct_count, status, nsmall);
 }
 
 void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, long long pitch0, long long fstride0,

@@ -283,9 +283,17 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
         }
         L.hX = (float)(L.maxBX - L.minB) / L.nIni;
         L.kcap = std::max(L.N + 3, 4 * L.nIni);
-        if (L.kcap > OG_OCT_MAXL - 8) {
-            c->err = "features per level exceed the LDS octree capacity";
+        if (L.kcap > OG_OCT_MAXL_BIG - 8) {
+            c->err = "features per level exceed the LDS octree capacity (" + std::to_string(OG_OCT_MAXL_BIG - 8) +
+                     " list nodes)";
             return ORBGPU_ERR_UNSUPPORTED;
+        }
+        if (L.kcap > OG_OCT_MAXL - 8) {
+            if (P.oct_big != l) {  // levels shrink with l: the big-list levels are a prefix
+                c->err = "octree: a large level after a small one";
+                return ORBGPU_ERR_INTERNAL;
+            }
+            P.oct_big = l + 1;
         }
         L.koff = koff;
         koff += L.kcap;

@@ -24,7 +24,8 @@
 #define OG_GRID_COLS 64
 #define OG_GRID_ROWS 48
 #define OG_GRID_CELLS (OG_GRID_COLS * OG_GRID_ROWS)
-#define OG_OCT_MAXL 1024   // max octree list length handled in LDS (N_l + 3 + slack)
+#define OG_OCT_MAXL 1024   // max octree list length handled in LDS (N_l + 3 + slack), one node per thread
+#define OG_OCT_MAXL_BIG 2048  // the same with two list nodes per thread (~143 KB of LDS): levels of up to ~2040 features
 #define OG_MAX_CELL_W 64   // wCell <= 59 for any width (nCols = floor(w/30))
 #define OG_GRID_LDS_ITEMS 8192  // per-frame keypoint capacity (frame_cap) the grid kernel sorts in LDS
 
@@ -61,6 +62,7 @@ struct OgCell {            // one FAST block of up to 2x2 cells (ROI union), src
 struct OgPlan {
     int nlevels;
     int sem;               // ORBGPU_SEM_* of the context (include/orbgpu.h)
+    int oct_big;           // levels 0 .. oct_big-1 run the OG_OCT_MAXL_BIG octree kernel (their lists may exceed OG_OCT_MAXL)
     int iniTh, minTh;
     int total_cells;
     int kcap_total;        // sum of kcap (octree slots per frame)

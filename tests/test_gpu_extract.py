@@ -167,15 +167,16 @@ def test_random_parameters_vs_oracle(gpu, oracle, seed):
     """Randomised extractor parameters and image shapes (scale factor up to the 1.6 the fused pyramid's LDS is
     sized for, 1-8 levels, thresholds, odd widths and pitches): keypoints, descriptors and the whole pyramid
     bit-exact.  Configurations the reference itself cannot run (a level narrower than one FAST cell, or zero
-    initial octree nodes) and levels of more than 1016 features must be rejected with ORBGPU_ERR_UNSUPPORTED."""
+    initial octree nodes) and levels of more than 2040 features must be rejected with ORBGPU_ERR_UNSUPPORTED."""
     rng = np.random.default_rng(1000 + seed)
     rows, cols = int(rng.integers(120, 1100)), int(rng.integers(160, 1300))
     scale = float(np.float32(rng.uniform(1.05, 1.6)))
     nlevels = int(rng.integers(1, 9))
-    # level 0 takes nf * (1 - 1/s) / (1 - s^-L) features (src/ORBextractor.cc:435-446): stay within 1000 of them
+    # level 0 takes nf * (1 - 1/s) / (1 - s^-L) features (src/ORBextractor.cc:435-446): up to 2000 of them (both
+    # octree list capacities)
     f = 1.0 / scale
     share0 = (1 - f) / (1 - f ** nlevels) if nlevels > 1 else 1.0
-    nf = int(rng.integers(100, max(101, int(1000 / share0))))
+    nf = int(rng.integers(100, max(101, int(2000 / share0))))
     ini = int(rng.integers(8, 40))
     mn = int(rng.integers(3, ini))
     img = synthetic.frame(300 + seed, rows, cols)
@@ -187,9 +188,9 @@ def test_random_parameters_vs_oracle(gpu, oracle, seed):
         ex = gpu.ORBextractor(nf, scale, nlevels, ini, mn)
         k, d = ex(img)
     except RuntimeError as e:
-        # the reference's own impossibilities, or more than 1016 features on one level (the LDS octree's list
+        # the reference's own impossibilities, or more than 2040 features on one level (the LDS octree's list
         # capacity): reported, never silently wrong
-        assert "FAST cell" in str(e) or "initial octree" in str(e) or "octree capacity" in str(e), str(e)
+        assert any(m in str(e) for m in ("FAST cell", "initial octree", "octree capacity", "grid capacity")), str(e)
         return
     oe = oracle.OracleExtractor(nf, scale, nlevels, ini, mn)
     ko, do = oe(np.ascontiguousarray(img))
@@ -198,9 +199,21 @@ def test_random_parameters_vs_oracle(gpu, oracle, seed):
         assert np.array_equal(ex.level(lvl), oe.level(lvl)), (lvl, rows, cols, scale, nlevels)
 
 
+@pytest.mark.parametrize("nf,shape", [(5000, (1080, 1920)), (8000, (1080, 1920)), (5000, (480, 640))])
+def test_many_features_vs_oracle(gpu, oracle, nf, shape):
+    """More than ~1016 features on one level: those levels run the 2048-node octree (two list nodes per thread,
+    OG_OCT_MAXL_BIG), the rest the 1024-node one; keypoints and descriptors bit-exact at 5000 and 8000 features."""
+    img = synthetic.frame(11, *shape)
+    ex = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
+    assert ex.features_per_level()[0] > 1016
+    k, d = ex(img)
+    ko, do = oracle.OracleExtractor(nf)(img)
+    assert_same(k, d, ko, do)
+
+
 def test_level_capacity_is_reported(gpu):
-    """More than 1016 features on one level exceeds the LDS octree list: ORBGPU_ERR_UNSUPPORTED with a message,
+    """More than 2040 features on one level exceeds the LDS octree list: ORBGPU_ERR_UNSUPPORTED with a message,
     never a silently different keypoint set."""
-    ex = gpu.ORBextractor(5000, 1.2, 8, 20, 7)  # level 0 budget 1085
+    ex = gpu.ORBextractor(12000, 1.2, 8, 20, 7)  # level 0 budget 2604
     with pytest.raises(RuntimeError, match="octree capacity"):
         ex(synthetic.frame(3, 480, 640))
