@@ -865,6 +865,362 @@ __device__ unsigned long long og_oct_prof[256];
     } while (0)
 #endif
 
+// levels [l0, l0 + gridDim.x / frames) of the launch, level-major, one list node per thread (OG_OCT_MAXL)
+__global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_octree_kernel(OgPlan P, int l0, const u64* __restrict__ cand,
+                                                           const int* __restrict__ cand_count,
+                                                           uint16_t* __restrict__ node_of,
+                                                           uint32_t* __restrict__ oct_xy,
+                                                           uint8_t* __restrict__ oct_resp,
+                                                           int* __restrict__ oct_count, int* __restrict__ status,
+                                                           int nlaunch)
+{
+    __shared__ OctNode nodes[2][OG_OCT_MAXL];
+    __shared__ uint8_t fresh[2][OG_OCT_MAXL];
+    __shared__ int splitRank[OG_OCT_MAXL];
+    __shared__ int splitNode[OG_OCT_MAXL];
+    __shared__ int newPos[OG_OCT_MAXL];
+    __shared__ int aux[OG_OCT_MAXL];
+    // child counts, indexed 4*node + quadrant: one buffer -- a round's counts are consumed (split set,
+    // children) before the key pass accumulates the next round's, with barriers in between; the last key
+    // pass keeps the best key per node in the same storage.  ~74 KB of LDS in total: 2 workgroups per CU.
+    __shared__ __attribute__((aligned(16))) int childCnt[4 * OG_OCT_MAXL];
+    __shared__ __attribute__((aligned(16))) uint16_t childPos[4 * OG_OCT_MAXL];
+    // final-phase planning only: the candidates' (size, creation id) keys, in the previous round's (dead) childPos
+    u64* skey = (u64*)childPos;
+    u64* best = (u64*)childCnt;  // [OG_OCT_MAXL], final key pass only
+    __shared__ int wsum[32];
+    __shared__ int sv[16];
+
+    // level-major dispatch order, level 0 first: the finest level has the most candidates (and rounds), so
+    // its workgroups start in the first wave of residency instead of being interleaved with the short ones
+    const int nb = (int)gridDim.x / nlaunch;  // frames in the launch
+    const int l = l0 + (int)blockIdx.x / nb, f = (int)blockIdx.x % nb, tid = threadIdx.x;
+    const OgLevel& L = P.lv[l];
+    const int C = min(cand_count[f * P.nlevels + l], L.cand_cap);
+    const u64* K = cand + (long long)f * P.cand_per_frame + L.cand_off;
+    const uint32_t* K32 = (const uint32_t*)K;  // [2k] = x | y << 16, [2k+1] = response
+    uint16_t* NO = node_of + (long long)f * P.cand_per_frame + L.cand_off;
+    const int N = L.N;
+    const int nIni = L.nIni;
+    const int H = L.maxBY - L.minB;
+
+    OCT_PROF(0, clock64());
+    OCT_PROF(1, (unsigned long long)C);
+    // ---- roots (src/ORBextractor.cc:552-585) and the children of the first pass's splits, in ONE key pass:
+    // each key's root r = x / hX and its quadrant in that root are counted together (childCnt[4r + q]); a root's
+    // size is the sum of its four quadrant counts.  NO[k] holds the root id until the first round's key pass,
+    // which maps it to the root's list position through aux[] (`noRoot`).
+    for (int q = tid; q < 4 * nIni; q += OCT_NT) childCnt[q] = 0;
+    __syncthreads();
+    for (int base = tid; base < C; base += OCT_NT * OCT_U) {
+        uint32_t kv[OCT_U];
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++) {
+            const int k = base + u * OCT_NT;
+            kv[u] = k < C ? K32[2 * k] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++) {
+            const int k = base + u * OCT_NT;
+            int a = 0;
+            if (k < C) {
+                const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
+                const int r = min((int)((float)x / L.hX), nIni - 1);
+                NO[k] = (uint16_t)r;
+                OctNode rn;
+                rn.x0 = (short)(int)(L.hX * (float)r);
+                rn.x1 = (short)(int)(L.hX * (float)(r + 1));
+                rn.y0 = 0;
+                rn.y1 = (short)H;
+                a = 4 * r + og_quadrant(x, y, rn);
+            }
+            og_wave_count(childCnt, a, k < C);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int Ln = 0;
+        for (int r = 0; r < nIni; r++) {
+            const int c0 = childCnt[4 * r], c1 = childCnt[4 * r + 1], c2 = childCnt[4 * r + 2], c3 = childCnt[4 * r + 3];
+            const int c = c0 + c1 + c2 + c3;
+            if (c > 0) {
+                OctNode n;
+                n.x0 = (short)(int)(L.hX * (float)r);
+                n.x1 = (short)(int)(L.hX * (float)(r + 1));
+                n.y0 = 0;
+                n.y1 = (short)H;
+                n.cnt = c;
+                n.cid = r;
+                nodes[0][Ln] = n;
+                fresh[0][Ln] = 0;
+                // quadrant counts follow the root to its list position (Ln <= r: a forward in-place move)
+                childCnt[4 * Ln] = c0;
+                childCnt[4 * Ln + 1] = c1;
+                childCnt[4 * Ln + 2] = c2;
+                childCnt[4 * Ln + 3] = c3;
+                aux[r] = Ln++;
+            } else {
+                aux[r] = -1;
+            }
+        }
+        for (int q = 4 * Ln; q < 4 * nIni; q++) childCnt[q] = 0;
+        sv[0] = Ln;      // list length
+        sv[1] = 0;       // mode of the coming round: 0 normal pass, 1 final phase
+        sv[2] = nIni;    // next creation id
+        sv[3] = Ln == 0; // done (an empty list can never grow)
+        sv[4] = 0;       // current node buffer
+        sv[8] = 0;       // `best` filled by a key pass
+    }
+    __syncthreads();
+    bool noRoot = true;  // NO[] holds root ids (workgroup-uniform)
+
+    OCT_PROF(2, clock64());
+    for (int round = 0; round < 4096; round++) {
+        if (sv[3]) break;
+        const int Ln = sv[0], mode = sv[1], cur = sv[4];
+        OCT_PROF(8 + 4 * round, clock64());
+        OCT_PROF(9 + 4 * round, (unsigned long long)Ln | ((unsigned long long)mode << 32));
+        OctNode* cn = nodes[cur];
+        uint8_t* cf = fresh[cur];
+        OctNode* nn = nodes[cur ^ 1];
+        uint8_t* nf = fresh[cur ^ 1];
+        const int* CC = childCnt;
+        int* NCC = childCnt;
+        __syncthreads();
+        // ---- the split set of this round and its order
+        const int i = tid;
+        int S;
+        if (mode == 0) {
+            const bool flag = i < Ln && cn[i].cnt > 1;
+            const int rank = og_block_excl_scan(flag ? 1 : 0, wsum, &S);
+            if (i < Ln) splitRank[i] = flag ? rank : -1;
+            if (flag) splitNode[rank] = i;
+        } else {
+            // vSizeAndPointerToNode of the previous round sorted ascending by (size, ptr) and walked from
+            // the back (src/ORBextractor.cc:684-685): order = descending (cnt, creation id)
+            const bool flag = i < Ln && cf[i] && cn[i].cnt > 1;
+            const int c = og_block_excl_scan(flag ? 1 : 0, wsum, &S);
+            u64 mk = 0;
+            if (flag) {
+                mk = ((u64)(uint32_t)cn[i].cnt << 32) | (u64)(uint32_t)cn[i].cid;  // (size, ptr) order, unique
+                skey[c] = mk;
+            }
+            __syncthreads();
+            if (i < Ln) splitRank[i] = -1;
+            if (flag) {
+                // rank = number of candidates with a larger key: every lane reads the same key (broadcast), no
+                // dependent lookups, so the loop pipelines
+                int rank = 0;
+#pragma unroll 8
+                for (int q = 0; q < S; q++) rank += skey[q] > mk;
+                splitRank[i] = rank;
+                splitNode[rank] = i;
+            }
+        }
+        if (S == 0) {  // nothing to split: size == prevSize -> bFinish
+            if (tid == 0) sv[3] = 1;
+            __syncthreads();
+            break;
+        }
+        __syncthreads();
+        // ---- per split (in split order): non-empty children, the final phase's break point (:730-731)
+        int nc = 0, nexp = 0, sn = 0;
+        if (i < S) {
+            sn = splitNode[i];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int c = CC[4 * sn + q];
+                nc += c > 0;
+                nexp += c > 1;
+            }
+        }
+        int totNc;
+        const int exNc = og_block_excl_scan(nc, wsum, &totNc);
+        int A = S;
+        if (mode == 1) {
+            const bool reach = i < S && (Ln + exNc + nc - (i + 1) >= N);
+            if (tid == 0) sv[5] = S;
+            __syncthreads();
+            if (reach) atomicMin(&sv[5], i + 1);
+            __syncthreads();
+            A = sv[5];
+        }
+        if (i == A - 1) sv[6] = exNc + nc;
+        __syncthreads();
+        const int T = sv[6];
+        // ---- children: groups in reverse split order, each n4,n3,n2,n1 (push_front, :621-660)
+        if (i < A) {
+            const OctNode par = cn[sn];
+            const int groupStart = T - (exNc + nc);
+            const int cidBase = sv[2] + exNc;
+            // the key pass's remap record of node sn: its split point here, its children's positions below
+            newPos[sn] = (par.x0 + ((par.x1 - par.x0 + 1) >> 1)) | ((par.y0 + ((par.y1 - par.y0 + 1) >> 1)) << 16);
+            int before = 0;  // non-empty children among q' < q (creation order n1..n4)
+            for (int q = 0; q < 4; q++) {
+                const int c = CC[4 * sn + q];
+                if (c > 0) {
+                    const int pos = groupStart + (nc - before - 1);
+                    OctNode ch = og_child(par, q);
+                    ch.cnt = c;
+                    ch.cid = cidBase + before;
+                    childPos[4 * sn + q] = (uint16_t)pos;
+                    if (pos < OG_OCT_MAXL) {
+                        nn[pos] = ch;
+                        nf[pos] = 1;
+                    }
+                    before++;
+                }
+            }
+        }
+        // ---- kept nodes follow, in their old order
+        const bool kept = i < Ln && (splitRank[i] < 0 || splitRank[i] >= A);
+        int keptTot;
+        const int kr = og_block_excl_scan(kept ? 1 : 0, wsum, &keptTot);
+        if (kept) {
+            const int pos = T + kr;
+            // remap record of a kept node: split point (0, 0) selects quadrant 3, and all four entries are pos
+            newPos[i] = 0;
+            ((u64*)childPos)[i] = (u64)(uint16_t)pos * 0x0001000100010001ull;
+            if (pos < OG_OCT_MAXL) {
+                nn[pos] = cn[i];
+                nf[pos] = 0;
+            }
+        }
+        int expTot;
+        (void)og_block_excl_scan(i < A ? nexp : 0, wsum, &expTot);
+        const int Lnew = T + keptTot;
+        if (Lnew > OG_OCT_MAXL) {
+            if (tid == 0) {
+                atomicOr(status, 2);
+                sv[3] = 1;
+                sv[0] = 0;
+            }
+            __syncthreads();
+            break;
+        }
+        // ---- termination / next mode (src/ORBextractor.cc:669-677, 734-735), decided before the key pass
+        int done = 0, nextMode = mode;
+        if (mode == 0) {
+            if (Lnew >= N || Lnew == Ln) done = 1;
+            else if (Lnew + expTot * 3 > N) nextMode = 1;
+        } else {
+            if (Lnew >= N || Lnew == Ln) done = 1;
+        }
+        for (int q = tid; q < 4 * Lnew; q += OCT_NT) NCC[q] = 0;
+        if (done) {
+            for (int q = tid; q < Lnew; q += OCT_NT) best[q] = 0ull;
+        } else {
+            // counting record of every node of the new list (splitRank is dead until the next round's plan):
+            // split point x | y << 15, bit 30 = the node is a split candidate of the next round
+            for (int q = tid; q < Lnew; q += OCT_NT) {
+                const OctNode& nd = nn[q];
+                const int countable = nd.cnt > 1 && (nextMode == 0 || nf[q]);
+                splitRank[q] = (nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1)) | ((nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1)) << 15) |
+                               (countable << 30);
+            }
+        }
+        __syncthreads();
+        OCT_PROF(10 + 4 * round, clock64());
+        OCT_PROF(11 + 4 * round, (unsigned long long)S | ((unsigned long long)A << 32));
+        // ---- one pass over the keys: move to the new list position, and either count the children of
+        // the next round's split candidates or (last round) keep the best key per node (:744-760)
+        for (int base = tid; base < C; base += OCT_NT * OCT_U) {
+            uint32_t kv[OCT_U];
+            int no[OCT_U];
+#pragma unroll
+            for (int u = 0; u < OCT_U; u++) {
+                const int k = base + u * OCT_NT;
+                kv[u] = k < C ? K32[2 * k] : 0u;
+                no[u] = k < C ? NO[k] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < OCT_U; u++) {
+                const int k = base + u * OCT_NT;
+                int a = 0;
+                bool cnt = false;
+                if (k < C) {
+                    const int n = noRoot ? aux[no[u]] : no[u];
+                    const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
+                    // remap record: the node's split point (newPos) and its four target positions (childPos)
+                    const int mm = newPos[n];
+                    const u64 tp = ((const u64*)childPos)[n];
+                    const int q = (x >= (mm & 0xffff) ? 1 : 0) | (y >= (mm >> 16) ? 2 : 0);  // og_quadrant
+                    const int n2 = (int)((tp >> (16 * q)) & 0xffffu);
+                    NO[k] = (uint16_t)n2;
+                    if (done) {
+                        const int resp = (int)(K32[2 * k + 1] & 0xff);
+                        atomicMax(&best[n2], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
+                    } else {
+                        const int rc = splitRank[n2];
+                        cnt = (rc >> 30) & 1;
+                        a = 4 * n2 + ((x >= (rc & 0x7fff) ? 1 : 0) | (y >= ((rc >> 15) & 0x7fff) ? 2 : 0));
+                    }
+                }
+                if (!done) og_wave_count(NCC, a, cnt);  // `done` is workgroup-uniform
+            }
+        }
+        __syncthreads();
+        noRoot = false;
+        if (tid == 0) {
+            sv[0] = Lnew;
+            sv[1] = nextMode;
+            sv[2] += T;
+            sv[3] = done;
+            sv[4] = cur ^ 1;
+            sv[8] = done;  // `best` is valid
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    OCT_PROF(3, clock64());
+    const int Ln = sv[0];
+    if (!sv[8]) {  // finished without a final key pass (empty split set): one pass for the best key
+        for (int n = tid; n < Ln; n += OCT_NT) best[n] = 0ull;
+        __syncthreads();
+        for (int base = tid; base < C; base += OCT_NT * OCT_U) {
+            u64 kv[OCT_U];
+            int no[OCT_U];
+#pragma unroll
+            for (int u = 0; u < OCT_U; u++) {
+                const int k = base + u * OCT_NT;
+                kv[u] = k < C ? K[k] : 0ull;
+                no[u] = k < C ? NO[k] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < OCT_U; u++) {
+                const int k = base + u * OCT_NT;
+                if (k < C) {
+                    const int x = (int)(kv[u] & 0xffff), y = (int)((kv[u] >> 16) & 0xffff);
+                    const int resp = (int)((kv[u] >> 32) & 0xff);
+                    atomicMax(&best[noRoot ? aux[no[u]] : no[u]],
+                              ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const int nout = min(Ln, L.kcap);
+    for (int n = tid; n < nout; n += OCT_NT) {
+        const u64 b = best[n];
+        const unsigned ord = 0xffffffffu - (unsigned)(b & 0xffffffffu);
+        const int lx = ord % L.wCell;
+        unsigned t2 = ord / L.wCell;
+        const int ly = t2 % L.hCell;
+        t2 /= L.hCell;
+        const int cj = t2 % L.nCols, ci = t2 / L.nCols;
+        const int x = cj * L.wCell + 3 + lx + L.minB, y = ci * L.hCell + 3 + ly + L.minB;
+        const long long o = (long long)f * P.kcap_total + L.koff + n;
+        oct_xy[o] = (uint32_t)x | ((uint32_t)y << 16);
+        oct_resp[o] = (uint8_t)(b >> 32);
+    }
+    if (tid == 0) {
+        oct_count[f * P.nlevels + l] = nout;
+        if (Ln > L.kcap) atomicOr(status, 4);
+    }
+    OCT_PROF(4, clock64());
+    OCT_PROF(5, (unsigned long long)Ln);
+}
+
 // exclusive block scan of NPT ints per thread, thread t holding items t*NPT .. t*NPT + NPT-1 (in order)
 template <int NPT>
 __device__ __forceinline__ void og_block_excl_scan_n(const int (&v)[NPT], int (&ex)[NPT], int* wsum, int* total)
@@ -880,10 +1236,12 @@ __device__ __forceinline__ void og_block_excl_scan_n(const int (&v)[NPT], int (&
     }
 }
 
-// MAXL = list capacity (OG_OCT_MAXL, or OG_OCT_MAXL_BIG for levels of more than ~1000 features, 2 list nodes per
-// thread); levels [l0, l0 + gridDim.x / frames) of the launch, level-major
+// og_octree_kernel with a list capacity of MAXL = OG_OCT_MAXL_BIG nodes, NPT = MAXL / OCT_NT of them per thread in the
+// per-node phases, for levels of more than ~1000 features (5000+ features per frame).  The 1024-node kernel above
+// keeps its own one-node-per-thread form: the generic one measured 22 % slower at NPT = 1 (0.60 -> 0.73 ms per 512
+// frames at config 3, same instruction count; not explained)
 template <int MAXL>
-__global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_octree_kernel(OgPlan P, int l0, const u64* __restrict__ cand,
+__global__ __launch_bounds__(OCT_NT) void og_octree_big_kernel(OgPlan P, int l0, const u64* __restrict__ cand,
                                                            const int* __restrict__ cand_count,
                                                            uint16_t* __restrict__ node_of,
                                                            uint32_t* __restrict__ oct_xy,
@@ -1765,10 +2123,10 @@ void og_launch_octree(hipStream_t s, const OgPlan& P, const u64* cand, const int
     // take the 2-nodes-per-thread kernel; the rest the 1-node-per-thread one
     const int nbig = P.oct_big, nsmall = P.nlevels - P.oct_big;
     if (nbig > 0)
-        hipLaunchKernelGGL(og_octree_kernel<OG_OCT_MAXL_BIG>, dim3(nbig * B), dim3(OCT_NT), 0, s, P, 0, cand,
+        hipLaunchKernelGGL(og_octree_big_kernel<OG_OCT_MAXL_BIG>, dim3(nbig * B), dim3(OCT_NT), 0, s, P, 0, cand,
                            cand_count, node_of, oct_xy, oct_resp, oct_count, status, nbig);
     if (nsmall > 0)
-        hipLaunchKernelGGL(og_octree_kernel<OG_OCT_MAXL>, dim3(nsmall * B), dim3(OCT_NT), 0, s, P, nbig, cand,
+        hipLaunchKernelGGL(og_octree_kernel, dim3(nsmall * B), dim3(OCT_NT), 0, s, P, nbig, cand,
                            cand_count, node_of, oct_xy, oct_resp, oct_count, status, nsmall);
 }
 
