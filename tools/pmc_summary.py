@@ -15,7 +15,8 @@ from collections import defaultdict
 
 
 def short(n):
-    return n.split("(")[0].replace("void ", "")
+    """Kernel name without arguments or template parameters (og_describe_kernel<0, false> -> og_describe_kernel)."""
+    return n.split("(")[0].replace("void ", "").split("<")[0].strip()
 
 
 STAGE = {"og_fast_blocks_kernel": "fast", "og_fast_cells_kernel": "fast", "og_octree_kernel": "octree", "og_describe_kernel": "describe",
