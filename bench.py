@@ -508,37 +508,95 @@ def tracking_mappoints(k, d, M, seed):
                 desc=d[src] ^ np.packbits(rng.random((M, 256)) < 0.05, axis=1))
 
 
+# config 5's camera model: a planar scene at depth RIG_DEPTH in front of pinhole cameras (fx = fy = RIG_F, principal
+# point at the image centre, monocular); frame slot b of a rank sees it from camera translation (-dx, -dy) * depth / f,
+# which moves every map point by the (dx, dy) pixel shift its synthetic frame was rendered with
+RIG_F, RIG_DEPTH = 1200.0, 5.0
+
+
+def frame_shift(i: int):
+    """Pixel shift (dx, dy) of unique frame i of _frames (period 32)."""
+    i %= 32
+    return int(3 + 5 * (i % 8)), int(2 + 3 * (i // 8))
+
+
+def rig_camera(cols, rows, dx, dy, scale_factor, nlevels):
+    """orbgpu_camera / oracle camera dict of the camera that sees the planar map shifted by (dx, dy) pixels."""
+    t = np.array([-dx * RIG_DEPTH / RIG_F, -dy * RIG_DEPTH / RIG_F, 0.0], np.float32)
+    return dict(Rcw=np.eye(3, dtype=np.float32), tcw=t, Ow=-t, fx=RIG_F, fy=RIG_F, cx=cols / 2.0, cy=rows / 2.0, mbf=0.0,
+                mb=0.0, scale_factor=float(scale_factor), nlevels=int(nlevels), cols=cols, rows=rows)
+
+
+def local_map(k, d, M, seed, cols, rows, scale_factors):
+    """SURVEY.md §8(d) config 5's local map as world points: M points sampled from the reference camera's extraction
+    (identity pose), back-projected onto the plane at RIG_DEPTH with N(0, 1 px) jitter, descriptor bits flipped with
+    p = 0.05; normal = viewing direction, mfMaxDistance = dist * scale^octave, mfMinDistance = max / scale^(L-1)
+    (MapPoint::UpdateNormalAndDepth, src/MapPoint.cc:340-383)."""
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, len(k), M)
+    u = (k["x"][src] + rng.normal(0, 1, M)).astype(np.float64)
+    v = (k["y"][src] + rng.normal(0, 1, M)).astype(np.float64)
+    pos = np.stack([(u - cols / 2.0) / RIG_F * RIG_DEPTH, (v - rows / 2.0) / RIG_F * RIG_DEPTH,
+                    np.full(M, RIG_DEPTH)], 1).astype(np.float32)
+    dist = np.linalg.norm(pos.astype(np.float64), axis=1).astype(np.float32)
+    sf = np.asarray(scale_factors, np.float32)
+    maxd = (dist * sf[k["octave"][src]]).astype(np.float32)
+    return dict(pos=pos, normal=(pos / dist[:, None]).astype(np.float32), max_dist=maxd,
+                min_dist=(maxd / sf[-1]).astype(np.float32), is_bad=np.zeros(M, np.uint8),
+                n_obs=np.full(M, 2, np.int32), desc=d[src] ^ np.packbits(rng.random((M, 256)) < 0.05, axis=1))
+
+
+MAP_FIELDS = (("pos", 12), ("normal", 12), ("max_dist", 4), ("min_dist", 4), ("is_bad", 1), ("n_obs", 4),
+              ("desc", 32))
+
+
+def pack_map(mp):
+    """The local map as one byte record (the unit rank 0 broadcasts once per step)."""
+    return np.concatenate([np.ascontiguousarray(mp[f]).view(np.uint8).reshape(-1) for f, _ in MAP_FIELDS])
+
+
 def cpu_baseline_tracking(rows, cols, nfeat, M, seconds):
     O = _oracle_fast()
     from orbslam2_with_quadrics_amd import synthetic
 
     ex = O.OracleExtractor(nfeat)
     sf = ex.tables()["scale"]
-    scene = synthetic.make_scene(synthetic.SEED_BASE + 997, rows, cols)
-    f = synthetic.render(scene, rows, cols, 0, 0, noise_seed=300)
-    k0, d0 = ex(f)
-    mp = tracking_mappoints(k0, d0, M, 0)
+    scene = synthetic.make_scene(synthetic.SEED_BASE + 5000, rows, cols)
+    k0, d0 = ex(synthetic.render(scene, rows, cols, 0, 0, noise_seed=1))
+    mp = local_map(k0, d0, M, 7000, cols, rows, sf)
 
-    def work(img):
-        k, d = ex(img)
-        O.search_by_projection(O.OracleFrame(k, d, cols, rows, sf), mp, 0.8, 1.0)
+    def work(i):
+        dx, dy = frame_shift(i)
+        k, d = ex(synthetic.render(scene, rows, cols, dx, dy, noise_seed=10 + i))
+        _, tr = O.is_in_frustum(rig_camera(cols, rows, dx, dy, 1.2, len(sf)), mp["pos"], mp["normal"],
+                                mp["max_dist"], mp["min_dist"], 0.5)
+        O.search_by_projection(O.OracleFrame(k, d, cols, rows, sf), dict(tr, is_bad=mp["is_bad"], n_obs=mp["n_obs"],
+                                                                          desc=mp["desc"]), 0.8, 1.0)
 
-    med, n = timed_cpu_frames(work, lambda i: synthetic.render(scene, rows, cols, i % 3, i % 2, noise_seed=300 + i),
-                              seconds)
-    return cpu_record(med, n, 3, f"{cols}x{rows}, {nfeat} features, oracle extraction + SearchByProjection vs {M} "
-                                 f"map points (th 1)")
+    med, n = timed_cpu_frames(work, lambda i: i, seconds)
+    return cpu_record(med, n, 3, f"{cols}x{rows}, {nfeat} features, oracle extraction + isInFrustum + "
+                                 f"SearchByProjection vs a {M}-point local map (th 1)")
 
 
 def setup_tracking(args, env):
-    """config 5 (8-camera 1920x1080 rig, 4000 features): per camera frame, ORB extraction and
-    SearchByProjection(F, local map points, th=1) (Tracking::SearchLocalPoints, src/Tracking.cc:1184-1191) against
-    --mappoints points; one camera per frame slot, cameras sharded over GPUs."""
+    """config 5 (8-camera 1920x1080 rig, 4000 features): per camera frame, ORB extraction, Frame::isInFrustum of every
+    local-map point for the camera's pose (src/Tracking.cc:1167-1180) and SearchByProjection(F, local map, th=1)
+    (Tracking::SearchLocalPoints, :1184-1191).  The local map (world points, SURVEY.md §8(d)) is built by rank 0 from
+    its reference frame and broadcast to every rank once per step; each rank's frames have their own
+    camera poses."""
+    import torch
+
     L, _lib, ORBextractor, synthetic = env["L"], env["_lib"], env["ORBextractor"], env["synthetic"]
+    dist, rank = env["dist"], env["rank"]
     rows, cols, B, NF, S, dev = args.rows, args.cols, args.batch, args.nfeatures, args.streams, env["dev"]
     M = args.mappoints
     Bs = B // S
-    _, frames = _frames(synthetic, rows, cols, B, env["rank"], 5000)
+    f_ref, frames = _frames(synthetic, rows, cols, B, rank, 5000)
     exs = [ORBextractor(NF, 1.2, 8, 20, 7, device=dev, semantics=args.semantics) for _ in range(S)]
+    sfac = exs[0].GetScaleFactors()
+    # the local map: rank 0 extracts its reference frame and builds it; the byte record is broadcast every step
+    k0, d0 = exs[0](f_ref)
+    mp = local_map(k0, d0, M, 7000, cols, rows, sfac)
     d_frames = exs[0].device_alloc(frames.nbytes)
     exs[0].h2d(d_frames, frames)
     fbytes = rows * cols
@@ -547,41 +605,57 @@ def setup_tracking(args, env):
         e.synchronize()
     outs = [e.batch_outputs() for e in exs]
     cap = outs[0][3]
-    # each camera's local map from its own extraction (host, once)
-    per = {}
-    mps_dev, own_dev = [], []
+    rec_h = pack_map(mp)
+    rec = torch.from_numpy(rec_h).to(f"cuda:{dev}")
+    offs, o = {}, 0
+    for f, w in MAP_FIELDS:
+        offs[f] = rec.data_ptr() + o
+        o += w * M
+    geom = _lib.MapPointGeomView(M, offs["pos"], offs["normal"], offs["max_dist"], offs["min_dist"])
+    grid = _lib.GridGeom()
+    L.orbgpu_grid_geom_for_image(cols, rows, C.byref(grid))
+    # per stream: cameras of its frame slots (device), the track fields (Bs x M), owners
+    per = []
     for s_, e in enumerate(exs):
-        arrs = {key: [] for key in MP_KEYS}
+        cams = np.zeros((Bs, 23), np.float32)
         for b in range(Bs):
-            fid = s_ * Bs + b
-            key = fid % min(B, 32)  # frames repeat with period min(B, 32) (_frames)
-            if key not in per:
-                k, d = e.batch_download(b)
-                per[key] = tracking_mappoints(k, d, M, 7000 + key + 1000 * env["rank"])
-            for kk in MP_KEYS:
-                arrs[kk].append(per[key][kk])
-        dp = {}
-        for kk in MP_KEYS:
-            a = np.ascontiguousarray(np.stack(arrs[kk]))
-            dp[kk] = e.device_alloc(a.nbytes)
-            e.h2d(dp[kk], a)
-        mps_dev.append(dp)
+            c = rig_camera(cols, rows, *frame_shift(s_ * Bs + b), 1.2, len(sfac))
+            cams[b, :9] = c["Rcw"].reshape(9)
+            cams[b, 9:12] = c["tcw"]
+            cams[b, 12:15] = c["Ow"]
+            cams[b, 15:22] = [c["fx"], c["fy"], c["cx"], c["cy"], c["mbf"], c["mb"], c["scale_factor"]]
+            cams[b, 22] = np.array([c["nlevels"]], np.int32).view(np.float32)[0]
+        d_cams = e.device_alloc(cams.nbytes)
+        e.h2d(d_cams, cams)
+        tr = {f: e.device_alloc(Bs * M * w) for f, w in (("iv", 1), ("px", 4), ("py", 4), ("pxr", 4), ("lv", 4),
+                                                          ("vc", 4))}
         d_none = e.device_alloc(Bs * cap * 4)  # mvpMapPoints all NULL at SearchLocalPoints time
         e.h2d(d_none, np.full(Bs * cap, -1, np.int32))
-        own_dev.append((d_none, e.device_alloc(Bs * cap * 4), e.device_alloc(Bs * cap * 4), e.device_alloc(Bs * 4)))
-    views = [_lib.MapPointsView(M, *[mps_dev[s_][kk] for kk in MP_KEYS]) for s_ in range(S)]
+        view = _lib.MapPointsView(M, tr["iv"], offs["is_bad"], tr["lv"], tr["vc"], tr["px"], tr["py"], tr["pxr"],
+                                  offs["n_obs"], offs["desc"])
+        per.append(dict(cams=d_cams, tr=tr, none=d_none, own=e.device_alloc(Bs * cap * 4),
+                        obs=e.device_alloc(Bs * cap * 4), nm=e.device_alloc(Bs * 4), view=view))
 
     def step():
+        if dist is not None:  # the local map from rank 0, once per step (before any frame is matched against it)
+            broadcast_record(dist, rank, rec, lambda buf: None, lambda buf: torch.cuda.current_stream().synchronize())
         for s_, e in enumerate(exs):
+            q = per[s_]
             e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
-            d_none, d_own, d_obs, _ = own_dev[s_]
-            _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C.c_void_p(d_own), C.c_void_p(d_none), Bs * cap * 4), "d2d")
-            _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C.c_void_p(d_obs), C.c_void_p(d_none), Bs * cap * 4), "d2d")
+            tr = q["tr"]
+            _lib.check(e.ctx, L.orbgpu_is_in_frustum_batch(e.ctx, C.c_void_p(q["cams"]), Bs, grid, C.byref(geom), 0.5,
+                                                           M, C.c_void_p(tr["iv"]), C.c_void_p(tr["px"]),
+                                                           C.c_void_p(tr["py"]), C.c_void_p(tr["pxr"]),
+                                                           C.c_void_p(tr["lv"]), C.c_void_p(tr["vc"])), "frustum")
+            _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C.c_void_p(q["own"]), C.c_void_p(q["none"]),
+                                                        Bs * cap * 4), "d2d")
+            _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C.c_void_p(q["obs"]), C.c_void_p(q["none"]),
+                                                        Bs * cap * 4), "d2d")
         for s_, e in enumerate(exs):
-            _, d_own, d_obs, d_nm = own_dev[s_]
-            _lib.check(e.ctx, L.orbgpu_search_by_projection_batch(e.ctx, C.byref(views[s_]), M, 0.8, 1.0, None,
-                                                                   C.c_void_p(d_own), C.c_void_p(d_obs),
-                                                                   C.c_void_p(d_nm)), "search_proj")
+            q = per[s_]
+            _lib.check(e.ctx, L.orbgpu_search_by_projection_batch_shared_map(
+                e.ctx, C.byref(q["view"]), M, 0.8, 1.0, None, C.c_void_p(q["own"]), C.c_void_p(q["obs"]),
+                C.c_void_p(q["nm"])), "search_proj")
 
     def post():
         counts = np.zeros(Bs, np.int32)
@@ -589,22 +663,26 @@ def setup_tracking(args, env):
         kp_all, nm_all = 0, 0
         for s_, e in enumerate(exs):
             e.d2h(counts, outs[s_][2])
-            e.d2h(nm, own_dev[s_][3])
+            e.d2h(nm, per[s_]["nm"])
             kp_all += int(counts.sum())
             nm_all += int(nm.sum())
-        return {"mean_keypoints_per_frame": round(kp_all / B, 1), "map_points_per_frame": M,
-                "mean_projection_matches_per_frame": round(nm_all / B, 1)}, kp_all / S
+        return {"mean_keypoints_per_frame": round(kp_all / B, 1), "map_points": M,
+                "mean_projection_matches_per_frame": round(nm_all / B, 1),
+                "local_map": "world points broadcast from rank 0 once per step; per-frame isInFrustum on the GPU"}, \
+            kp_all / S
 
     def free():
         for s_, e in enumerate(exs):
-            for p in list(mps_dev[s_].values()) + list(own_dev[s_]):
+            q = per[s_]
+            for p in [q["cams"], q["none"], q["own"], q["obs"], q["nm"]] + list(q["tr"].values()):
                 e.device_free(p)
         exs[0].device_free(d_frames)
 
-    return dict(metric=f"frames/sec ORB extract + SearchByProjection vs {M} map points @{cols}×{rows}, {NF} feat",
+    return dict(metric=f"frames/sec ORB extract + isInFrustum + SearchByProjection vs {M} map points "
+                       f"@{cols}×{rows}, {NF} feat",
                 exs=exs, step=step, post=post, free=free, Bs=Bs, frames_per_step=B, counts=[o[2] for o in outs],
-                workload=f"config 5: {cols}x{rows} camera frames, {NF} features, ORB extraction + SearchByProjection "
-                         f"(th 1, ratio 0.8) against {M} local-map points per camera",
+                workload=f"config 5: {cols}x{rows} camera frames, {NF} features, ORB extraction + isInFrustum + "
+                         f"SearchByProjection (th 1, ratio 0.8) against a {M}-point local map shared by all cameras",
                 cpu=lambda: cpu_baseline_tracking(rows, cols, NF, M, args.cpu_seconds))
 
 

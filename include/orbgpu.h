@@ -217,6 +217,13 @@ int orbgpu_search_by_projection_batch(orbgpu_ctx* ctx, const orbgpu_mappoints_vi
                                       float nnratio, float th, const float* d_uright, int32_t* d_owner,
                                       int32_t* d_owner_obs, int* d_nmatches);
 
+/* orbgpu_search_by_projection_batch with one local map shared by every frame of the batch: the track fields
+ * (track_in_view, level, view_cos, proj_x/y/xr) of frame b at element b*mp_stride + j, the map's own fields
+ * (is_bad, n_obs, desc) at element j for every frame (as orbgpu_is_in_frustum_batch produces them). */
+int orbgpu_search_by_projection_batch_shared_map(orbgpu_ctx* ctx, const orbgpu_mappoints_view* d_mp, int mp_stride,
+                                                 float nnratio, float th, const float* d_uright, int32_t* d_owner,
+                                                 int32_t* d_owner_obs, int* d_nmatches);
+
 /* ---- Frame post-processing: UndistortKeyPoints / ComputeImageBounds ---------------------------- */
 
 /* Replaces void Frame::UndistortKeyPoints() -- src/Frame.cc:404-434: mvKeysUn from mvKeys through
@@ -273,6 +280,16 @@ int orbgpu_is_in_frustum(orbgpu_ctx* ctx, const orbgpu_camera* cam, orbgpu_grid_
                          const orbgpu_mappoint_geom_view* mp, float viewingCosLimit, uint8_t* track_in_view,
                          float* proj_x, float* proj_y, float* proj_xr, int32_t* level, float* view_cos,
                          int* n_in_view);
+
+/* Device-resident batch form for frames sharing one local map (Tracking::SearchLocalPoints of a camera rig or of a
+ * frame batch, src/Tracking.cc:1143-1195): camera b = d_cams[b] (a DEVICE array of B orbgpu_camera) against the m
+ * points of *d_mp (device pointers, shared by all frames).  The five outputs of frame b go to element b*m_stride + j
+ * of each device array -- the track fields orbgpu_search_by_projection_batch_shared_map reads.  Enqueued on the
+ * context stream. */
+int orbgpu_is_in_frustum_batch(orbgpu_ctx* ctx, const orbgpu_camera* d_cams, int B, orbgpu_grid_geom bounds,
+                               const orbgpu_mappoint_geom_view* d_mp, float viewingCosLimit, int m_stride,
+                               uint8_t* d_in_view, float* d_px, float* d_py, float* d_pxr, int32_t* d_level,
+                               float* d_vc);
 
 /* LastFrame snapshot for the motion-model matcher. */
 typedef struct {

@@ -33,7 +33,8 @@ EXPORTS = [
     "orbgpu_vocabulary_load_text", "orbgpu_vocabulary_create", "orbgpu_vocabulary_destroy", "orbgpu_vocabulary_info",
     "orbgpu_compute_bow", "orbgpu_compute_bow_batch", "orbgpu_memcpy_h2d_async", "orbgpu_memcpy_d2h_async",
     "orbgpu_cvt_color_to_gray_batch", "orbgpu_extract_color", "orbgpu_set_semantics", "orbgpu_get_semantics",
-    "orbgpu_batch_grid", "orbgpu_debug_math_hash", "orbgpu_frame_record_bytes", "orbgpu_frame_record_pack", "orbgpu_frame_record_unpack",
+    "orbgpu_batch_grid", "orbgpu_debug_math_hash", "orbgpu_is_in_frustum_batch",
+    "orbgpu_search_by_projection_batch_shared_map", "orbgpu_frame_record_bytes", "orbgpu_frame_record_pack", "orbgpu_frame_record_unpack",
 ]
 
 # OpenCV / compiler semantics switch (include/orbgpu.h ORBGPU_SEM_*)
@@ -116,6 +117,10 @@ def _declare(L):
     L.orbgpu_set_semantics.argtypes = [vp, i32]
     L.orbgpu_get_semantics.argtypes = [vp]
     L.orbgpu_batch_grid.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
+    L.orbgpu_is_in_frustum_batch.argtypes = [vp, vp, i32, GridGeom, C.POINTER(MapPointGeomView), f32, i32, vp, vp, vp,
+                                             vp, vp, vp]
+    L.orbgpu_search_by_projection_batch_shared_map.argtypes = [vp, C.POINTER(MapPointsView), i32, f32, f32, vp, vp,
+                                                               vp, vp]
     L.orbgpu_debug_math_hash.argtypes = [i32, i32, C.c_ulonglong, C.c_ulonglong, i32, vp, i32]
     L.orbgpu_frame_record_bytes.restype = C.c_longlong
     L.orbgpu_frame_record_bytes.argtypes = [vp]

@@ -624,16 +624,17 @@ __device__ __forceinline__ OgFrameDev og_frame_of(const OgFrameDev& F, int b)
 __device__ __forceinline__ OgMapPointsDev og_mp_of(const OgMapPointsDev& mp, int b, int stride)
 {
     const long long o = (long long)b * stride;
+    const long long om = mp.shared_map ? 0 : o;  // the map's own fields: per frame, or one map for all frames
     OgMapPointsDev q = mp;
     q.track_in_view += o;
-    q.is_bad += o;
+    q.is_bad += om;
     q.level += o;
     q.view_cos += o;
     q.proj_x += o;
     q.proj_y += o;
     q.proj_xr += o;
-    q.n_obs += o;
-    q.desc += o * 32;
+    q.n_obs += om;
+    q.desc += om * 32;
     return q;
 }
 
@@ -874,11 +875,65 @@ __device__ __forceinline__ void og_rx_t(const float* R, const float* x, const fl
     }
 }
 
+__device__ __forceinline__ void og_frustum_point(const OgCameraDev& cam, const OgMapGeomDev& mp, int m, float limit,
+                                                OgFrustumOut out);
+
 __global__ __launch_bounds__(256) void og_frustum_kernel(OgCameraDev cam, OgMapGeomDev mp, float limit,
                                                          OgFrustumOut out)
 {
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= mp.m) return;
+    og_frustum_point(cam, mp, m, limit, out);
+}
+
+// one camera per blockIdx.y (the pose / intrinsics of orbgpu_camera, read from device memory), one shared map
+__global__ __launch_bounds__(256) void og_frustum_batch_kernel(const float* __restrict__ cams, float minX, float maxX,
+                                                               float minY, float maxY, OgMapGeomDev mp, float limit,
+                                                               OgFrustumOut out, int stride)
+{
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= mp.m) return;
+    const int b = blockIdx.y;
+    const float* c = cams + 23 * (long long)b;  // orbgpu_camera: 22 floats + int nlevels
+    OgCameraDev cam;
+#pragma unroll
+    for (int k = 0; k < 9; k++) cam.R[k] = c[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        cam.t[k] = c[9 + k];
+        cam.Ow[k] = c[12 + k];
+    }
+    cam.fx = c[15];
+    cam.fy = c[16];
+    cam.cx = c[17];
+    cam.cy = c[18];
+    cam.mbf = c[19];
+    cam.mb = c[20];
+    cam.scale_factor = c[21];
+    cam.nlevels = __float_as_int(c[22]);
+    cam.minX = minX;
+    cam.maxX = maxX;
+    cam.minY = minY;
+    cam.maxY = maxY;
+    const long long o = (long long)b * stride;
+    OgFrustumOut ob{out.in_view + o, out.proj_x + o, out.proj_y + o, out.proj_xr + o, out.level + o,
+                    out.view_cos + o, nullptr};
+    og_frustum_point(cam, mp, m, limit, ob);
+}
+
+void og_launch_frustum_batch(hipStream_t s, const void* d_cams, int B, float minX, float maxX, float minY, float maxY,
+                             OgMapGeomDev mp, float viewingCosLimit, OgFrustumOut out, int stride)
+{
+    if (mp.m > 0 && B > 0)
+        hipLaunchKernelGGL(og_frustum_batch_kernel, dim3((mp.m + 255) / 256, B), dim3(256), 0, s,
+                           (const float*)d_cams, minX, maxX, minY, maxY, mp, viewingCosLimit, out, stride);
+}
+
+// Frame::isInFrustum + MapPoint::PredictScale of map point m for one camera (src/Frame.cc:269-325,
+// src/MapPoint.cc:402-417)
+__device__ __forceinline__ void og_frustum_point(const OgCameraDev& cam, const OgMapGeomDev& mp, int m, float limit,
+                                                OgFrustumOut out)
+{
     bool in = false;
     float u = 0, v = 0, ur = 0, vc = 0;
     int lvl = 0;

@@ -1667,6 +1667,56 @@ int orbgpu_search_by_projection_batch(orbgpu_ctx* c, const orbgpu_mappoints_view
     return r;
 }
 
+int orbgpu_search_by_projection_batch_shared_map(orbgpu_ctx* c, const orbgpu_mappoints_view* d_mp, int mp_stride,
+                                                 float nnratio, float th, const float* d_uright, int32_t* d_owner,
+                                                 int32_t* d_owner_obs, int* d_nmatches)
+{
+    if (!c || !c->last_B || !d_mp || d_mp->m < 0 || mp_stride < d_mp->m || !d_owner || !d_owner_obs || !d_nmatches)
+        return ORBGPU_ERR_ARG;
+    if (d_mp->m && (!d_mp->track_in_view || !d_mp->is_bad || !d_mp->level || !d_mp->view_cos || !d_mp->proj_x ||
+                    !d_mp->proj_y || !d_mp->proj_xr || !d_mp->n_obs || !d_mp->desc))
+        return ORBGPU_ERR_ARG;
+    if ((size_t)2 * sizeof(int) * (size_t)c->plan.frame_cap > OG_INIT_LDS_MAX) {
+        c->err = "SearchByProjection: frame capacity exceeds the LDS-resident claim table";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    if (c->sf_dev.n < (size_t)c->nlevels) {
+        HIP_TRY(c, ensure(c->sf_dev, (size_t)c->nlevels));
+        HIP_TRY(c, hipMemcpyAsync(c->sf_dev.p, c->sf.data(), sizeof(float) * c->nlevels, hipMemcpyHostToDevice, s));
+    }
+    timer_mark(c, "match_proj");
+    OgFrameDev fd{kps_match(c), c->desc.p, c->counts.p, c->cell_start.p, c->cell_items.p, d_uright, c->plan.frame_cap};
+    OgMapPointsDev mpd{d_mp->m,      d_mp->track_in_view, d_mp->is_bad, d_mp->level, d_mp->view_cos, d_mp->proj_x,
+                       d_mp->proj_y, d_mp->proj_xr,       d_mp->n_obs,  d_mp->desc, 1};
+    int r = run_projection(c, s, fd, c->grid_geom, c->sf_dev.p, mpd, mp_stride, c->last_B, nnratio, th, d_owner,
+                           d_owner_obs, d_nmatches);
+    timer_mark(c, "search_proj");
+    return r;
+}
+
+int orbgpu_is_in_frustum_batch(orbgpu_ctx* c, const orbgpu_camera* d_cams, int B, orbgpu_grid_geom bounds,
+                               const orbgpu_mappoint_geom_view* d_mp, float viewingCosLimit, int m_stride,
+                               uint8_t* d_in_view, float* d_px, float* d_py, float* d_pxr, int32_t* d_level,
+                               float* d_vc)
+{
+    static_assert(sizeof(orbgpu_camera) == 23 * 4, "orbgpu_camera: 22 floats + int");
+    if (!c || !d_cams || B < 0 || !d_mp || d_mp->m < 0 || m_stride < d_mp->m) return ORBGPU_ERR_ARG;
+    if (d_mp->m && (!d_mp->pos || !d_mp->normal || !d_mp->max_dist || !d_mp->min_dist || !d_in_view || !d_px ||
+                    !d_py || !d_pxr || !d_level || !d_vc))
+        return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    timer_mark(c, "frustum0");
+    og_launch_frustum_batch(c->stream, d_cams, B, bounds.minX, bounds.maxX, bounds.minY, bounds.maxY,
+                            OgMapGeomDev{d_mp->m, d_mp->pos, d_mp->normal, d_mp->max_dist, d_mp->min_dist},
+                            viewingCosLimit, OgFrustumOut{d_in_view, d_px, d_py, d_pxr, d_level, d_vc, nullptr},
+                            m_stride);
+    HIP_TRY(c, hipGetLastError());
+    timer_mark(c, "frustum");
+    return ORBGPU_OK;
+}
+
 static OgCameraDev camera_dev(const orbgpu_camera* cam, float minX, float maxX, float minY, float maxY)
 {
     OgCameraDev d{};

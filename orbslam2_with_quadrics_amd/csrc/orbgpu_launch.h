@@ -95,6 +95,7 @@ struct OgMapPointsDev {
     const float* proj_xr;
     const int* n_obs;
     const uint8_t* desc;
+    int shared_map = 0;  // batched forms: 1 = is_bad / n_obs / desc are one map shared by every frame (stride 0)
 };
 
 struct OgProjCand;
@@ -149,6 +150,10 @@ struct OgMapGeomDev {
     const float* max_dist; // mfMaxDistance
     const float* min_dist; // mfMinDistance
 };
+// Frame::isInFrustum for B cameras (device array of orbgpu_camera's layout, the OgCameraDev prefix) against one shared
+// map; outputs of camera b at b*stride + j
+void og_launch_frustum_batch(hipStream_t s, const void* d_cams, int B, float minX, float maxX, float minY, float maxY,
+                             struct OgMapGeomDev mp, float viewingCosLimit, struct OgFrustumOut out, int stride);
 struct OgFrustumOut {
     uint8_t* in_view;
     float* proj_x;

@@ -88,9 +88,19 @@ def _worker_share(rank, world, port, q):
         record["f1"] = b.clone()
 
     bench.broadcast_record(dist, r, buf, pack, unpack)
+    # config 5: the local map (world points) built on rank 0 and broadcast as one byte record
+    import numpy as np
+
+    kp = np.zeros(50, [("x", "<f4"), ("y", "<f4"), ("octave", "<i4")])
+    kp["x"], kp["y"], kp["octave"] = np.arange(50) * 3.0 + 10 * (r == 0), 40.0, np.arange(50) % 8
+    mp = bench.local_map(kp, np.full((50, 32), r, np.uint8), 64, 7, 96, 64, 1.2 ** np.arange(8))
+    mrec = torch.from_numpy(bench.pack_map(mp).copy())
+    bench.broadcast_record(dist, r, mrec, lambda b: None, lambda b: None)
+    record["map"] = mrec.numpy().tobytes()
     counts = torch.tensor([int(_stub_extract(f)[:4].view(np.int32)[0]) for f in frames], dtype=torch.int32)
     g = bench.allgather_counts(dist, counts, w)
-    q.put((r, start, count, __import__("hashlib").sha256(f1.tobytes()).hexdigest(), record["f1"].numpy().tobytes(), g.tolist(), counts.tolist()))
+    q.put((r, start, count, __import__("hashlib").sha256(f1.tobytes()).hexdigest(), record["f1"].numpy().tobytes(),
+           g.tolist(), counts.tolist(), record["map"]))
     dist.destroy_process_group()
 
 
@@ -104,12 +114,13 @@ def test_gloo_world2_shared_initial_frame_split_and_gather():
     [p.start() for p in ps]
     res = sorted(q.get(timeout=180) for _ in range(2))
     [p.join(timeout=60) for p in ps]
-    (r0, s0, c0, h0, rec0, g0, n0), (r1, s1, c1, h1, rec1, g1, n1) = res
+    (r0, s0, c0, h0, rec0, g0, n0, m0), (r1, s1, c1, h1, rec1, g1, n1, m1) = res
     assert (s0, c0, s1, c1) == (0, 5, 5, 5)      # the global frame set [0, 10) split without overlap
     assert h0 == h1                              # every rank renders the same initial frame
     assert rec0 == rec1 and any(rec0)            # rank 1 holds rank 0's record after the broadcast
     assert g0 == g1 == n0 + n1                   # all-gathered keypoint counts, rank order
     assert n0 != n1                              # the ranks' frames differ (per-rank sensor noise)
+    assert m0 == m1                              # rank 1 holds rank 0's local map (it built a different one)
 
 
 def test_shard_range_partitions():

@@ -174,3 +174,89 @@ def test_search_by_projection_keyframe_vs_oracle(gpu, oracle, seed, shape, nf):
         wn, wown = oracle.search_by_projection_kf(Fo, cur, kf, th, orbdist, ori, owner0)
         assert gn == wn and gn > 10
         assert np.array_equal(gown, wown)
+
+
+def test_frustum_and_projection_batch_shared_map_vs_oracle(gpu, oracle):
+    """Config 5 as bench.py runs it: B camera frames (1080p, 4000 features) against ONE local map of 5000 world
+    points -- orbgpu_is_in_frustum_batch (a device camera array, src/Frame.cc:269-325) feeding
+    orbgpu_search_by_projection_batch_shared_map (src/ORBmatcher.cc:45-129) -- frame by frame against the oracle's
+    isInFrustum + SearchByProjection."""
+    import ctypes as C
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from orbslam2_with_quadrics_amd import _lib, synthetic
+
+    rows, cols, NF, M, B = 1080, 1920, 4000, 5000, 6
+    f_ref, frames = bench._frames(synthetic, rows, cols, B, 0, 5000)
+    ex = gpu.ORBextractor(NF, 1.2, 8, 20, 7)
+    sf = ex.GetScaleFactors()
+    k0, d0 = ex(f_ref)
+    mp = bench.local_map(k0, d0, M, 7000, cols, rows, sf)
+    L = _lib.lib()
+    ptrs = []
+
+    def dev(a):
+        a = np.ascontiguousarray(a)
+        p = ex.device_alloc(max(a.nbytes, 4))
+        ex.h2d(p, a)
+        ptrs.append(p)
+        return p
+
+    try:
+        d_img = dev(frames)
+        ex.extract_batch_device(d_img, B, cols, rows, cols, rows * cols)
+        cams = np.zeros((B, 23), np.float32)
+        camd = []
+        for b in range(B):
+            c = bench.rig_camera(cols, rows, *bench.frame_shift(b), 1.2, 8)
+            camd.append(c)
+            cams[b, :9], cams[b, 9:12], cams[b, 12:15] = c["Rcw"].reshape(9), c["tcw"], c["Ow"]
+            cams[b, 15:22] = [c["fx"], c["fy"], c["cx"], c["cy"], c["mbf"], c["mb"], c["scale_factor"]]
+            cams[b, 22] = np.array([8], np.int32).view(np.float32)[0]
+        geom = _lib.MapPointGeomView(M, dev(mp["pos"]), dev(mp["normal"]), dev(mp["max_dist"]), dev(mp["min_dist"]))
+        out = {f: ex.device_alloc(B * M * w) for f, w in (("iv", 1), ("px", 4), ("py", 4), ("pxr", 4), ("lv", 4),
+                                                          ("vc", 4))}
+        ptrs.extend(out.values())
+        grid = _lib.GridGeom()
+        L.orbgpu_grid_geom_for_image(cols, rows, C.byref(grid))
+        _lib.check(ex.ctx, L.orbgpu_is_in_frustum_batch(ex.ctx, C.c_void_p(dev(cams)), B, grid, C.byref(geom), 0.5, M,
+                                                        *[C.c_void_p(out[f]) for f in ("iv", "px", "py", "pxr", "lv",
+                                                                                       "vc")]), "frustum")
+        cap = ex.batch_outputs()[3]
+        own = dev(np.full(B * cap, -1, np.int32))
+        obs = dev(np.full(B * cap, -1, np.int32))
+        nm = dev(np.zeros(B, np.int32))
+        view = _lib.MapPointsView(M, out["iv"], dev(mp["is_bad"]), out["lv"], out["vc"], out["px"], out["py"],
+                                  out["pxr"], dev(mp["n_obs"]), dev(mp["desc"]))
+        _lib.check(ex.ctx, L.orbgpu_search_by_projection_batch_shared_map(ex.ctx, C.byref(view), M, 0.8, 1.0, None,
+                                                                          C.c_void_p(own), C.c_void_p(obs),
+                                                                          C.c_void_p(nm)), "search")
+        ex.synchronize()
+        IV = np.zeros(B * M, np.uint8)
+        PX = np.zeros(B * M, np.float32)
+        OWN = np.zeros(B * cap, np.int32)
+        NM = np.zeros(B, np.int32)
+        ex.d2h(IV, out["iv"])
+        ex.d2h(PX, out["px"])
+        ex.d2h(OWN, own)
+        ex.d2h(NM, nm)
+        total = 0
+        for b in range(B):
+            k, d = ex.batch_download(b)
+            n_in, tr = oracle.is_in_frustum(camd[b], mp["pos"], mp["normal"], mp["max_dist"], mp["min_dist"], 0.5)
+            iv = IV[b * M:(b + 1) * M]
+            assert np.array_equal(iv, tr["track_in_view"]), b
+            sel = iv == 1
+            assert np.array_equal(PX[b * M:(b + 1) * M][sel].view(np.int32), tr["proj_x"][sel].view(np.int32)), b
+            n, o, _ = oracle.search_by_projection(oracle.OracleFrame(k, d, cols, rows, sf),
+                                                  dict(tr, is_bad=mp["is_bad"], n_obs=mp["n_obs"], desc=mp["desc"]),
+                                                  0.8, 1.0)
+            assert NM[b] == n and np.array_equal(OWN[b * cap:b * cap + len(k)], o), b
+            total += n
+        assert total > 100 * B  # the map does project onto the frames' keypoints
+    finally:
+        for p in ptrs:
+            ex.device_free(p)
