@@ -23,6 +23,23 @@ typedef unsigned long long u64;
 __constant__ signed char og_pattern[1024];
 static bool g_pattern_uploaded_dev[64] = {false};
 
+// Lane masks straight from one v_cmp each (LLVM lowers ballot(a && b) as v_cmp(v_cndmask(mask), 0): two VALU
+// per ballot); compound conditions are ANDs of these masks on the scalar unit.  Inactive lanes read 0.
+#define OG_ICMP_EQ 32
+#define OG_ICMP_NE 33
+#define OG_ICMP_SGT 38
+#define OG_ICMP_SLT 40
+__device__ __forceinline__ u64 og_lanes_ne(unsigned a, unsigned b) { return __builtin_amdgcn_uicmp(a, b, OG_ICMP_NE); }
+__device__ __forceinline__ u64 og_lanes_eq(unsigned a, unsigned b) { return __builtin_amdgcn_uicmp(a, b, OG_ICMP_EQ); }
+__device__ __forceinline__ u64 og_lanes_lt(int a, int b) { return __builtin_amdgcn_sicmp(a, b, OG_ICMP_SLT); }
+__device__ __forceinline__ u64 og_lanes_gt(int a, int b) { return __builtin_amdgcn_sicmp(a, b, OG_ICMP_SGT); }
+__device__ __forceinline__ u64 og_ballot(bool b) { return __ballot(b); }
+// number of set bits of m below this lane (v_mbcnt: 2 VALU instead of masking and two popcounts)
+__device__ __forceinline__ int og_rank(u64 m, int base = 0)  // + base, for free
+{
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, (unsigned)base));
+}
+
 // XCD-aware bijective remap (cdna_hip_programming.md §5.5 T1): workgroups are dealt round-robin over
 // the 8 XCDs (separate L2s); give each XCD one contiguous chunk of the logical index space so that
 // neighbouring FAST cells / keypoints, which share cache lines, hit the same L2.  Speed only.
@@ -565,7 +582,6 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const int t1 = min(max(P.iniTh, 0), 255), t2 = min(max(P.minTh, 0), 255);
     const int tq = min(t1, t2);
     const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
-    const u64 lt_mask = (1ull << lane) - 1ull;
     // ---- stage 1: quick test on every detection pixel, two per lane: pair slot p -> row i, column c (pixels
     // (i, c) and (i, c + H)); wave w takes slots [64w, 64w + 64) + 512k; one LDS reservation per wave
     // iteration appends its survivors to the block's flat list (stages 2-4 then spread the list evenly)
@@ -584,23 +600,27 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             r[h] = make_uint2(0u, 0u);
             if (pp < npair) r[h] = og_fast_quick2(&T2[(ii[h] + 3) * FB_S2 + (cc[h] + 3)], FB_S2, tt);
         }
-        bool sv[2 * OG_FAST_SLOTS];
+        // polarity bits of each pixel (entry bits 14 = dark, 15 = bright): the halves of r.x / r.y are nonzero iff
+        // that polarity passes, min(half, 1) turns them into 0/1.  Survivor masks straight from v_cmp (og_lanes_*).
         int pol[2 * OG_FAST_SLOTS];
         u64 m[2 * OG_FAST_SLOTS];
-        int nn[2 * OG_FAST_SLOTS];
-#pragma unroll
-        for (int h = 0; h < OG_FAST_SLOTS; h++) {
-            pol[2 * h] = ((r[h].x & 0xffffu) ? 0x4000 : 0) | ((r[h].y & 0xffffu) ? 0x8000 : 0);
-            pol[2 * h + 1] = ((r[h].x >> 16) ? 0x4000 : 0) | ((r[h].y >> 16) ? 0x8000 : 0);
-            sv[2 * h] = pol[2 * h] != 0 && cc[h] < dw;
-            sv[2 * h + 1] = pol[2 * h + 1] != 0 && cc[h] + H < dw;
-        }
+        bool sv[2 * OG_FAST_SLOTS];  // bit `lane` of m (kept as a lane mask for the stores' exec)
         int n = 0;
 #pragma unroll
-        for (int q = 0; q < 2 * OG_FAST_SLOTS; q++) {
-            m[q] = __ballot(sv[q]);
-            nn[q] = __popcll(m[q]);
-            n += nn[q];
+        for (int h = 0; h < OG_FAST_SLOTS; h++) {
+            // v_pk_min_u16(x, 1) as asm: LLVM would otherwise turn min(half, 1) into per-half compares and selects
+            // (the splat 1 | 1 << 16 in a register: an inline constant would feed 0 to the high half)
+            uint32_t d1, b1;
+            __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r[h].x), "s"(0x00010001u));
+            __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r[h].y), "s"(0x00010001u));
+            const uint32_t pb = d1 | (b1 << 1);  // bits 0-1: first pixel (dark, bright), bits 16-17: second pixel
+            pol[2 * h] = (int)((pb << 14) & 0xc000u);
+            pol[2 * h + 1] = (int)((pb >> 2) & 0xc000u);
+            m[2 * h] = og_lanes_ne((unsigned)pol[2 * h], 0u) & og_lanes_lt(cc[h], dw);
+            m[2 * h + 1] = og_lanes_ne((unsigned)pol[2 * h + 1], 0u) & og_lanes_lt(cc[h], dw - H);
+            sv[2 * h] = pol[2 * h] != 0 && cc[h] < dw;
+            sv[2 * h + 1] = pol[2 * h + 1] != 0 && cc[h] < dw - H;
+            n += __popcll(m[2 * h]) + __popcll(m[2 * h + 1]);
         }
         if (n) {
             int b = 0;
@@ -609,9 +629,8 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 #pragma unroll
             for (int q = 0; q < 2 * OG_FAST_SLOTS; q++) {
                 const int h = q >> 1;
-                if (sv[q])
-                    lst[b + __popcll(m[q] & lt_mask)] = (uint16_t)(pol[q] | (ii[h] << 7) | (cc[h] + ((q & 1) ? H : 0)));
-                b += nn[q];
+                if (sv[q]) lst[og_rank(m[q], b)] = (uint16_t)(pol[q] | (ii[h] << 7) | (cc[h] + ((q & 1) ? H : 0)));
+                b += __popcll(m[q]);
             }
         }
     }
@@ -644,24 +663,24 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
     for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {  // same entry -> wave assignment as stage 4
         const int e = e0 + lane;
-        bool k1 = false, k2 = false;
-        int cell = 0;
+        int ent = 0, mc = 0, nb = 0;  // lanes past the end: score 0, never kept (tA, tB >= 1)
         if (e < ns) {
-            const int ent = lst[e] & 0x3fff;
-            const int i = ent >> 7, j = ent & 127;
-            const uint8_t* q = &Ms[og_ms_idx(i, j, wC, hC) - FB_MSW - 1];
-            const int m = q[FB_MSW + 1];
-            const int nb = max(max(max(q[0], q[1]), max(q[2], q[FB_MSW])),
-                               max(max(q[FB_MSW + 2], q[2 * FB_MSW]), max(q[2 * FB_MSW + 1], q[2 * FB_MSW + 2])));
-            k1 = m > tA && m > nb;
-            k2 = m > tB && m > nb;
-            cell = (i >= hC) * 2 + (j >= wC);
-            lst[e] = (uint16_t)(ent | (k1 ? 0x4000 : 0) | (k2 ? 0x8000 : 0));
+            ent = lst[e] & 0x3fff;
+            const uint8_t* q = &Ms[og_ms_idx(ent >> 7, ent & 127, wC, hC) - FB_MSW - 1];
+            mc = q[FB_MSW + 1];
+            nb = max(max(max(q[0], q[1]), max(q[2], q[FB_MSW])),
+                     max(max(q[FB_MSW + 2], q[2 * FB_MSW]), max(q[2 * FB_MSW + 1], q[2 * FB_MSW + 2])));
         }
+        // kept at t1 / t2 and the cell (row >= hCell, column >= wCell) as lane masks; per-cell counts on the SALU
+        const u64 top = og_lanes_gt(mc, nb);
+        const u64 K1 = og_lanes_gt(mc, tA) & top, K2 = og_lanes_gt(mc, tB) & top;
+        const u64 ci = og_lanes_gt(ent >> 7, hC - 1), cj = og_lanes_gt(ent & 127, wC - 1);
+        if (e < ns) lst[e] = (uint16_t)(ent | (mc > tA && mc > nb ? 0x4000 : 0) | (mc > tB && mc > nb ? 0x8000 : 0));
+        const u64 cm[4] = {~ci & ~cj, ~ci & cj, ci & ~cj, ci & cj};
 #pragma unroll
         for (int c = 0; c < 4; c++) {
-            c1[c] += __popcll(__ballot(k1 && cell == c));
-            c2[c] += __popcll(__ballot(k2 && cell == c));
+            c1[c] += __popcll(K1 & cm[c]);
+            c2[c] += __popcll(K2 & cm[c]);
         }
     }
     if (lane == 0) {
@@ -672,29 +691,29 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
     }
     __syncthreads();
-    // per cell: iniThFAST unless the cell is empty at it (src/ORBextractor.cc:809-816)
-    int tot1[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int w = 0; w < FB_NW; w++) {
-        const int4 a = *(const int4*)&wk[w][0];
-        tot1[0] += a.x;
-        tot1[1] += a.y;
-        tot1[2] += a.z;
-        tot1[3] += a.w;
-    }
+    // per cell: iniThFAST unless the cell is empty at it (src/ORBextractor.cc:809-816).  Lane-parallel: lane L < 32
+    // holds wave L/4's counts of cell L%4 (every wave computes the same block-uniform result; lanes >= 32 repeat
+    // lanes L - 32 and are masked off), so the bookkeeping is a few v_cmp / DPP ops and scalar sums instead of
+    // 16 LDS reads and ~80 adds and selects per wave
+    const int qw = (lane >> 2) & (FB_NW - 1), qc = lane & 3;
+    const int v1 = wk[qw][qc], v2 = wk[qw][4 + qc];
+    const u64 nz1 = og_lanes_ne((unsigned)v1, 0u) & 0xffffffffull;
     unsigned useT2 = 0;
 #pragma unroll
-    for (int c = 0; c < 4; c++) useT2 |= (tot1[c] ? 0u : 1u) << c;
-    // kept per wave (selected threshold per cell), this wave's offset and the block total
+    for (int c = 0; c < 4; c++) useT2 |= ((nz1 & (0x11111111ull << c)) ? 0u : 1u) << c;
+    const int kw = ((useT2 >> qc) & 1u) ? v2 : v1;
+    // one wave's four cells: sum over the quad (DPP quad_perm [1,0,3,2] then [2,3,0,1])
+    int ks = kw + __builtin_amdgcn_mov_dpp(kw, 0xb1, 0xf, 0xf, false);
+    ks = ks + __builtin_amdgcn_mov_dpp(ks, 0x4e, 0xf, 0xf, false);
+    // kept per wave, this wave's offset and the block total, on the scalar unit
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);
     int kept = 0, before = 0, total = 0;
 #pragma unroll
     for (int w = 0; w < FB_NW; w++) {
-        int kw = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) kw += ((useT2 >> c) & 1u) ? wk[w][4 + c] : wk[w][c];
-        before += w < wv ? kw : 0;
-        kept = w == wv ? kw : kept;
-        total += kw;
+        const int kwv = __builtin_amdgcn_readlane(ks, 4 * w);
+        before += w < wvu ? kwv : 0;
+        kept = w == wvu ? kwv : kept;
+        total += kwv;
     }
 #if OG_EXP_FAST_STOP == 3
     if (total == 12345) cand_count[0] = 1;
@@ -716,17 +735,13 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     int run = 0;
     for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
         const int e = e0 + lane;
-        bool keep = false;
-        int i = 0, j = 0;
-        if (e < ns) {
-            const int ent = lst[e];
-            i = (ent >> 7) & 127;
-            j = ent & 127;
-            const int cell = (i >= hC) * 2 + (j >= wC);
-            keep = (ent & (((useT2 >> cell) & 1u) ? 0x8000 : 0x4000)) != 0;
-        }
-        const u64 mask = __ballot(keep);
-        if (keep) out[run + __popcll(mask & lt_mask)] = og_pack_cand(ox + j, oy + i, Ms[og_ms_idx(i, j, wC, hC)] - 1);
+        int ent = 0;  // lanes past the end: no bits, not kept
+        if (e < ns) ent = lst[e];
+        const int i = (ent >> 7) & 127, j = ent & 127;
+        const int cell = (i >= hC) * 2 + (j >= wC);
+        const unsigned kb = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
+        const u64 mask = og_lanes_ne(kb, 0u);
+        if (kb) out[og_rank(mask, run)] = og_pack_cand(ox + j, oy + i, Ms[og_ms_idx(i, j, wC, hC)] - 1);
         run += __popcll(mask);
     }
 }
@@ -820,8 +835,8 @@ __device__ __forceinline__ void og_wave_count(int* ctr, int addr, bool act)
         const int a = act ? addr : -1;
         const int prev = __shfl_up(a, 1);
         const bool head = act && (lane == 0 || prev != a);
-        const u64 heads = __ballot(head);
-        const u64 actm = __ballot(act);
+        const u64 heads = og_ballot(head);
+        const u64 actm = og_ballot(act);
         if (head) {
             const u64 after = lane == 63 ? 0ull : (heads >> (lane + 1)) << (lane + 1);
             const int end = after ? __builtin_ctzll(after) : 64;  // next head (or past the wave)
@@ -831,7 +846,7 @@ __device__ __forceinline__ void og_wave_count(int* ctr, int addr, bool act)
         return;
     }
 #endif
-    u64 rem = __ballot(act);
+    u64 rem = og_ballot(act);
     const int lane = threadIdx.x & 63;
     // the two most common addresses of the wave are counted by one atomic each; lanes with any other
     // address (a wave spread over many nodes) fall back to plain atomics
@@ -839,7 +854,7 @@ __device__ __forceinline__ void og_wave_count(int* ctr, int addr, bool act)
     for (int it = 0; it < OCT_WC_IT && rem; it++) {
         const int ld = __builtin_ctzll(rem);
         const int a = __builtin_amdgcn_readlane(addr, ld);
-        const u64 m = __ballot(act && addr == a) & rem;
+        const u64 m = og_ballot(act && addr == a) & rem;
         if (lane == ld) atomicAdd(&ctr[a], (int)__popcll(m));
         rem &= ~m;
     }
@@ -1928,7 +1943,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             const int col = nofma ? og_cvround(x * a - y * b) : og_cvround(__builtin_fmaf(x, a, -(y * b)));
             val[q] = ctr[row * BL_W + col];
         }
-        words[t] = __ballot(val[0] < val[1]);
+        words[t] = og_ballot(val[0] < val[1]);
     }
     const long long o = (long long)f * P.frame_cap + g;
     if (lane < 4) {

@@ -33,7 +33,8 @@ def main():
         out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
         try:
             js = json.loads(out.stdout.strip().splitlines()[-1])
-            res[name] = dict(value=js["value"], ms_per_step=js["ms_per_step"], stages=js["stages_ms_per_launch"])
+            res[name] = dict(value=js["value"], ms_per_step=js["ms_per_step"], stages=js["stages_ms_per_launch"],
+                             parity=js.get("parity"))
         except Exception:
             res[name] = {"error": out.stderr[-600:]}
         print(name, json.dumps(res[name]), flush=True)
