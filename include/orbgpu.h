@@ -109,8 +109,9 @@ int orbgpu_get_level(orbgpu_ctx* ctx, int level, uint8_t* dst, size_t dst_step, 
 /* ---- batched, device-resident extraction (MI355X-native extension; same per-frame result) --- */
 
 /* Extract B frames that already live in HBM: frame b starts at d_imgs + b*frame_stride, rows are
- * `pitch` bytes apart.  Enqueued on the context stream; returns without synchronising.  Results stay
- * on the device (orbgpu_batch_outputs) until orbgpu_batch_download. */
+ * `pitch` bytes apart (pitch < 16 MiB, else ORBGPU_ERR_UNSUPPORTED).  Enqueued on the context stream;
+ * returns without synchronising.  Results stay on the device (orbgpu_batch_outputs) until
+ * orbgpu_batch_download. */
 int orbgpu_extract_batch_device(orbgpu_ctx* ctx, const uint8_t* d_imgs, int B, int cols, int rows,
                                 size_t pitch, size_t frame_stride);
 /* Device pointers of the last batch: kps[b*frame_cap + i], desc[(b*frame_cap + i)*32],

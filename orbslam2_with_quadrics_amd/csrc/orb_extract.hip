@@ -297,7 +297,13 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     const int dxt = bx0 + 4 * cth;
 #pragma unroll
     for (int k = 0; k < 4; k++) og_rz_weights(g.xtabA, g.xmaxA, min(cA + k, ac1), sc0, sxA, wtA, k);
-    const uint8_t* base = src + (long long)f * src_fstride;
+    // staging addresses: the region's first row (wave-uniform, SGPRs) rounded down to 16 bytes plus a 32-bit lane
+    // offset; chunk -> (row, chunk) with the exact float quotient (as in og_fast_blocks_kernel: nIt < 2^14)
+    const uint8_t* rbase = src + (long long)f * src_fstride + (long long)sr0 * src_pitch + sc0;
+    const unsigned mb = (unsigned)((uintptr_t)rbase & 15);
+    const uint8_t* abase = rbase - mb;
+    const unsigned upitch = (unsigned)src_pitch & (OG_MAX_PITCH - 1);  // < 2^24 (checked on the host)
+    const float rn = 1.0f / (float)nch, hn = 0.5f * rn;
     // RZ2_U chunks per thread per round, all loads issued before the first LDS store; the y-table rows of the
     // tile ride along (each pass below reads its vertical weights from LDS, not from a global load per row)
     const int nIt = nrS * nch;
@@ -310,22 +316,19 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
             const int it = it0 + u * RZ2_NT;
             v[u] = make_uint4(0u, 0u, 0u, 0u);
             if (it < nIt) {
-                const int r = it / nch, q = it - r * nch;
-                const uintptr_t a = (uintptr_t)(base + (long long)(sr0 + r) * src_pitch + sc0);
-                const uintptr_t a16 = a & ~(uintptr_t)15;
-                if (a16 + 16 * q <= a + (uintptr_t)(ncS - 1)) v[u] = *(const uint4*)(a16 + 16 * q);
+                const int r = (int)__builtin_fmaf((float)it, rn, hn) & 127, q = it - r * (nch & 0xfff);
+                const unsigned o = (unsigned)r * upitch + mb;      // row start relative to abase
+                const unsigned c16 = (o & ~15u) + 16u * (unsigned)q;  // this chunk, 16-byte aligned
+                if (c16 <= o + (unsigned)(ncS - 1)) v[u] = *(const uint4*)(abase + c16);
             }
         }
 #pragma unroll
         for (int u = 0; u < RZ2_U; u++) {
             const int it = it0 + u * RZ2_NT;
             if (it < nIt) {
-                const int r = it / nch, q = it - r * nch;
+                const int r = (int)__builtin_fmaf((float)it, rn, hn) & 127, q = it - r * (nch & 0xfff);
                 *(uint4*)&S[r * g.SC + 16 * q] = v[u];
-                if (q == 0) {
-                    const uintptr_t a = (uintptr_t)(base + (long long)(sr0 + r) * src_pitch + sc0);
-                    mis[r] = (int)(a & 15);
-                }
+                if (q == 0) mis[r] = (int)(((unsigned)r * upitch + mb) & 15u);
             }
         }
     }
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
             const uint32_t packed = og_rz_quad<FX>(S + r0 * g.SC + mis[r0], S + r1 * g.SC + mis[r1], sxA, wtA,
                                                (unsigned)yt.z, (unsigned)yt.w);
             *(uint32_t*)&A[rr * g.AC + 4 * qa] = packed;
-            if (r < own_r1 && own_c) og_rz_store4(DA + (long long)r * pitchA + cA, packed, nown);
+            if (r < own_r1 && own_c) og_rz_store4(DA + ((unsigned)r * (unsigned)pitchA + (unsigned)cA), packed, nown);
         }
     }
     __syncthreads();
@@ -361,7 +364,7 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
         const int4 yt = YB[r];
         const uint32_t packed = og_rz_quad<FX>(A + (yt.x - ar0) * g.AC, A + (yt.y - ar0) * g.AC, sxB, wtB, (unsigned)yt.z,
                                            (unsigned)yt.w);
-        og_rz_store4(DB + (long long)(by0 + r) * pitchB, packed, n);
+        og_rz_store4(DB + (unsigned)(by0 + r) * (unsigned)pitchB, packed, n);
     }
 }
 
@@ -478,7 +481,7 @@ __device__ __forceinline__ uint2 og_fast_quick2(const uint32_t* p, int st, og_u1
 #define FB_ROWS 86               // ROI rows (detection <= 80 + 6)
 #define FB_MW 80                 // detection width/height capacity of a block (2 x 40 or 1 x 64)
 #define FB_MSW (FB_MW + 3)       // score map stride: a zero gap column before, between and after the cells
-#define FB_MSZ ((FB_MSW * FB_MSW + 3) & ~3)
+#define FB_MSZ ((FB_MSW * FB_MSW + 15) & ~15)  // 16-byte multiple: zeroed by 16-byte stores
 
 // score-map index of detection pixel (i, j): one zero row/column separates the block's cells and surrounds
 // them, so a pixel's 8 neighbours outside its cell (or outside the detection area) read 0 without checks
@@ -523,7 +526,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     // H = the detection half-width rounded up to 4 (so both halves load from 4-byte aligned addresses).  The
     // dwords are read from global memory first (all loads issued before the LDS stores), then split with
     // v_perm into four pair dwords and stored as one 16-byte write.
-    const int H = (((dw + 1) >> 1) + 3) & ~3;
+    const int H = (((dw + 1) >> 1) + 3) & 0x7c;  // <= 44 (dw <= FB_MW); the 7-bit mask keeps its products 24-bit
     const uint8_t* row0 = img + (long long)cd.y0 * pitch + cd.x0;
     const bool aligned_rows = ((pitch & 3) == 0);
     const int mis = aligned_rows ? (int)((uintptr_t)row0 & 3) : 0;
@@ -532,29 +535,35 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const int nq = (H + 6 + mis + 3) >> 2;       // dword groups per row
         uint32_t blo[3], bhi[3];
         const int q = tid & 15;
+        // addresses: the block's uniform row base (SGPRs) plus a 32-bit per-lane offset, so the loads take the
+        // saddr + voffset form and no lane does 64-bit address arithmetic
+        const uint8_t* rbase = row0 - mis;
+        const unsigned upitch = (unsigned)pitch & (OG_MAX_PITCH - 1);  // < 2^24 (checked on the host)
+        const unsigned mb = (unsigned)((uintptr_t)rbase & 3);  // odd pitch: the rows' misalignment base
+        const uint8_t* abase = rbase - mb;                       // 4-byte aligned
 #pragma unroll
         for (int k = 0; k < 3; k++) {
             const int r = (tid >> 4) + 32 * k;
             blo[k] = 0u;
             bhi[k] = 0u;
             if (r < rh && q < nq) {
-                const uint8_t* rp = row0 + (long long)r * pitch - mis;
+                const unsigned off = (unsigned)r * upitch + 4u * (unsigned)q;
                 const int x = 4 * q - mis;          // ROI column of the dword's first byte
                 if (aligned_rows) {
-                    if (x < rw) blo[k] = *(const uint32_t*)(rp + 4 * q);
-                    if (x + H < rw) bhi[k] = *(const uint32_t*)(rp + 4 * q + H);
+                    if (x < rw) blo[k] = *(const uint32_t*)(rbase + off);
+                    if (x + H < rw) bhi[k] = *(const uint32_t*)(rbase + off + (unsigned)H);
                 } else {
                     // odd pitch: two aligned loads funnel-shifted by the row's offset.  Reads stay inside the
                     // row: an ROI starts >= 16 px from the left edge, ends >= 13 px before the right one.
                     if (x < rw) {
-                        const uint8_t* pp = rp + 4 * q;
-                        const uint32_t* a = (const uint32_t*)((uintptr_t)pp & ~(uintptr_t)3);
-                        blo[k] = __builtin_amdgcn_alignbyte(a[1], a[0], (unsigned)((uintptr_t)pp & 3));
+                        const unsigned o = off + mb;
+                        const uint32_t* a = (const uint32_t*)(abase + (o & ~3u));
+                        blo[k] = __builtin_amdgcn_alignbyte(a[1], a[0], o & 3u);
                     }
                     if (x + H < rw) {
-                        const uint8_t* pp = rp + 4 * q + H;
-                        const uint32_t* a = (const uint32_t*)((uintptr_t)pp & ~(uintptr_t)3);
-                        bhi[k] = __builtin_amdgcn_alignbyte(a[1], a[0], (unsigned)((uintptr_t)pp & 3));
+                        const unsigned o = off + (unsigned)H + mb;
+                        const uint32_t* a = (const uint32_t*)(abase + (o & ~3u));
+                        bhi[k] = __builtin_amdgcn_alignbyte(a[1], a[0], o & 3u);
                     }
                 }
             }
@@ -572,7 +581,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             }
         }
     }
-    for (int idx = tid * 4; idx < FB_MSZ; idx += FB_NT * 4) *(uint32_t*)&Ms[idx] = 0u;
+    for (int idx = tid * 16; idx < FB_MSZ; idx += FB_NT * 16) *(uint4*)&Ms[idx] = make_uint4(0u, 0u, 0u, 0u);
     if (tid == 0) sh_ns = 0;
     __syncthreads();
 #if OG_EXP_FAST_STOP == 1  // timing experiments only (tools/fast_variants.py): results are wrong
@@ -586,7 +595,10 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     // (i, c) and (i, c + H)); wave w takes slots [64w, 64w + 64) + 512k; one LDS reservation per wave
     // iteration appends its survivors to the block's flat list (stages 2-4 then spread the list evenly)
     const int npair = dh * H;
-    const unsigned invH = (1u << 20) / (unsigned)H + 1u;  // exact p / H for p < 3200, H <= 40
+    // p / H as trunc(fma(p, 1/H, 0.5/H)) with 1/H correctly rounded: (p + 1/2) / H is >= 1/(2H) away from an
+    // integer, far beyond the rounding error; exact for every p < 2^14 and H <= 128 (checked exhaustively,
+    // tests/test_oracle_pins.py::test_fast_slot_division_exact).  Full-rate VALU instead of a 32-bit multiply.
+    const float rH = 1.0f / (float)H, hH = 0.5f * rH;
     // two pair slots per lane per iteration (slots p and p + 512): twice the LDS reads in flight and one
     // reservation for the four survivor ballots
     for (int p0 = wv * 64; p0 < npair; p0 += OG_FAST_SLOTS * FB_NT) {
@@ -595,8 +607,8 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 #pragma unroll
         for (int h = 0; h < OG_FAST_SLOTS; h++) {
             const int pp = p0 + h * FB_NT + lane;
-            ii[h] = (int)(__umul24((unsigned)pp, invH) >> 20);
-            cc[h] = pp - (int)__umul24((unsigned)ii[h], (unsigned)H);
+            ii[h] = (int)__builtin_fmaf((float)pp, rH, hH) & 127;  // (< FB_ROWS; the mask lets the row offsets use 24-bit mads)
+            cc[h] = pp - ii[h] * H;
             r[h] = make_uint2(0u, 0u);
             if (pp < npair) r[h] = og_fast_quick2(&T2[(ii[h] + 3) * FB_S2 + (cc[h] + 3)], FB_S2, tt);
         }
@@ -1675,6 +1687,20 @@ __device__ __forceinline__ int og_reflect101(int i, int n)
     return i;
 }
 
+// sum over the 64 lanes (all active) with DPP: quad_perm [1,0,3,2] and [2,3,0,1] (quads), row_half_mirror (8),
+// row_mirror (16), row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3; lane 63 then holds the sum.
+// Six VALU ops instead of six ds_bpermute shuffles and adds.
+__device__ __forceinline__ int og_wave_sum(int v)
+{
+    v += __builtin_amdgcn_update_dpp(0, v, 0xb1, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4e, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 #ifndef DK_WAVES
 #define DK_WAVES 4
 #endif
@@ -1742,7 +1768,8 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 {
     __shared__ __attribute__((aligned(16))) uint8_t raw[DK_WAVES][RAW_W * RAW_S];
     __shared__ __attribute__((aligned(16))) uint32_t hp[DK_WAVES][HP_ROWS * HP_S];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // w is wave-uniform: made explicit, so the keypoint index, its level and its window origin live in SGPRs
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int f = (int)(lin / gridDim.x);
     const int g = (int)(lin % gridDim.x) * DK_WAVES + w;
@@ -1788,17 +1815,21 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             // the farthest byte read is x = cx + 26, inside the row (level starts are 256-B aligned, so the
             // rounded-down first load never precedes the image)
             // All 2 x 8 loads of a lane are issued before the first use (one memory round trip, not eight).
+            // Addresses: the window origin rounded down to 4 bytes (wave-uniform, SGPRs) plus a 32-bit lane offset.
             const uint8_t* src0 = img + (long long)(cy - 21) * pitch + (cx - 21);
+            const unsigned m0 = (unsigned)((uintptr_t)src0 & 3);
+            const uint8_t* abase = src0 - m0;
+            const unsigned upitch = (unsigned)pitch & (OG_MAX_PITCH - 1);  // < 2^24 (checked on the host)
             constexpr int NIT = (RAW_W * 11 + 63) / 64;
             uint32_t lo[NIT], hi[NIT];
             unsigned sh[NIT];
 #pragma unroll
             for (int k = 0; k < NIT; k++) {
                 const int idx = min(lane + 64 * k, RAW_W * 11 - 1);
-                const int r = idx / 11, q = idx - r * 11;
-                const uint8_t* p = src0 + (long long)r * pitch + 4 * q;
-                const uint32_t* a = (const uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
-                sh[k] = (unsigned)((uintptr_t)p & 3);
+                const int r = (idx * 5958) >> 16, q = idx - r * 11;  // idx / 11, exact for idx < 473 (5958 / 2^16 ~ 1/11)
+                const unsigned off = (unsigned)r * upitch + 4u * (unsigned)q + m0;
+                const uint32_t* a = (const uint32_t*)(abase + (off & ~3u));
+                sh[k] = off & 3u;
                 lo[k] = a[0];
                 hi[k] = a[1];
             }
@@ -1806,7 +1837,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             for (int k = 0; k < NIT; k++) {
                 const int idx = lane + 64 * k;
                 if (idx < RAW_W * 11) {
-                    const int r = idx / 11, q = idx - r * 11;
+                    const int r = (idx * 5958) >> 16, q = idx - r * 11;
                     *(uint32_t*)&R[r * RAW_S + 4 * q] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
                 }
             }
@@ -1835,11 +1866,8 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             m01 += v * (vp - vm);
             m10 += u * (vp + vm);
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            m01 += __shfl_xor(m01, o);
-            m10 += __shfl_xor(m10, o);
-        }
+        m01 = og_wave_sum(m01);
+        m10 = og_wave_sum(m10);
     }
     const float angle = og_fast_atan2((float)m01, (float)m10);
     // ---- 7x7 Gaussian (sigma 2, BORDER_REFLECT_101) of the 37x37 window the tests can reach.  Integer
@@ -1941,7 +1969,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             // build without contraction rounds both products (the kernels are compiled -ffp-contract=off)
             const int row = nofma ? og_cvround(x * b + y * a) : og_cvround(__builtin_fmaf(x, b, y * a));
             const int col = nofma ? og_cvround(x * a - y * b) : og_cvround(__builtin_fmaf(x, a, -(y * b)));
-            val[q] = ctr[row * BL_W + col];
+            val[q] = ctr[__mul24(row, BL_W) + col];  // |row| <= 18: a 24-bit multiply
         }
         words[t] = og_ballot(val[0] < val[1]);
     }

@@ -373,7 +373,8 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
         A.fz_SC = SC;
         A.fz_AR = AR;
         A.fz_AC = AC;
-        if (og_rz2_lds_bytes(SR, SC, AR, AC) > 64 * 1024) {
+        // SR <= 127 and SC <= 2048: og_resize2_kernel's row index (7 bits) and exact float chunk quotient
+        if (og_rz2_lds_bytes(SR, SC, AR, AC) > 64 * 1024 || SR > 127 || SC > 2048) {
             c->err = "fused resize region exceeds the LDS budget";
             return ORBGPU_ERR_UNSUPPORTED;
         }
@@ -737,6 +738,10 @@ int orbgpu_extract_batch_device(orbgpu_ctx* c, const uint8_t* d_imgs, int B, int
                                 size_t frame_stride)
 {
     if (!c || !d_imgs || B < 1 || cols <= 0 || rows <= 0 || pitch < (size_t)cols) return ORBGPU_ERR_ARG;
+    if (pitch >= OG_MAX_PITCH) {  // the kernels' per-lane row offsets are 24-bit products
+        c->err = "row pitch of 16 MiB or more";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
     HIP_TRY(c, hipSetDevice(c->device));
     int r = build_plan(c, cols, rows);
     if (r) return r;

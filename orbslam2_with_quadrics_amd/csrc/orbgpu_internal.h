@@ -27,6 +27,7 @@
 #define OG_OCT_MAXL 1024   // max octree list length handled in LDS (N_l + 3 + slack), one node per thread
 #define OG_OCT_MAXL_BIG 2048  // the same with two list nodes per thread (~143 KB of LDS): levels of up to ~2040 features
 #define OG_MAX_CELL_W 64   // wCell <= 59 for any width (nCols = floor(w/30))
+#define OG_MAX_PITCH (1u << 24)  // row pitches (bytes) below this: 24-bit row-offset products in the kernels
 #define OG_GRID_LDS_ITEMS 8192  // per-frame keypoint capacity (frame_cap) the grid kernel sorts in LDS
 
 struct OgLevel {

@@ -483,3 +483,17 @@ print(O.LIB_PATH, hashlib.sha256(k1.tobytes() + d1.tobytes() + k2.tobytes() + d2
         env = dict(os.environ, ORB_ORACLE_FAST=fast)
         outs.append(subprocess.check_output([sys.executable, "-c", code], env=env).decode().split())
     assert outs[0][0] != outs[1][0] and outs[0][1] == outs[1][1], outs
+
+
+def test_fast_slot_division_exact():
+    """og_fast_blocks_kernel maps a pair slot p to (row, column) with trunc(fma(p, 1/H, 0.5/H)) in float32
+    (csrc/orb_extract.hip, stage 1).  (p + 1/2)/H is at least 1/(2H) from an integer, far beyond the rounding of
+    the correctly rounded 1/H and of the fma, so the quotient is exact: checked for every p < 2^14 and H <= 128
+    (the kernel needs p < 80 * 44 and H <= 44).  The fma is evaluated exactly in float64 (a 24 x 24-bit product
+    is exact there) and rounded once to float32, as the hardware fma rounds."""
+    p = np.arange(0, 1 << 14, dtype=np.int64)
+    for H in range(1, 129):
+        rH = np.float32(1.0) / np.float32(H)
+        hH = np.float32(0.5) * rH
+        q = (p.astype(np.float64) * np.float64(rH) + np.float64(hH)).astype(np.float32)
+        assert np.array_equal(np.trunc(q).astype(np.int64), p // H), H
