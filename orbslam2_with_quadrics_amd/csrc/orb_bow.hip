@@ -214,12 +214,13 @@ void og_launch_bow(hipStream_t s, const OgVocDev& V, const uint8_t* desc, const 
                            frame_cap, levelsup, word, wt, nid);
     int P = 2;
     while (P < nmax) P <<= 1;
-    static bool lds_attr = false;
-    if (!lds_attr) {
-        (void)hipFuncSetAttribute((const void*)og_bow_reduce_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  BOW_MAXN * 8);
-        lds_attr = true;
-    }
     hipLaunchKernelGGL(og_bow_reduce_kernel, dim3(B), dim3(BOW_NT), (size_t)P * 8, s, V, counts, n_fixed, frame_cap,
                        word, wt, nid, words, values, nwords, nodes, node_off, feats, nnodes);
+}
+
+// dynamic-LDS attribute of the reduce kernel: per device, set from og_prepare_device (orbgpu_create)
+hipError_t og_prepare_device_bow()
+{
+    return hipFuncSetAttribute((const void*)og_bow_reduce_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               BOW_MAXN * 8);
 }

@@ -464,12 +464,6 @@ void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2,
 {
     hipLaunchKernelGGL(og_init_cand_kernel, dim3((F1.frame_cap + 3) / 4, B), dim3(256), 0, s, F1, ref, F2, G,
                        windowSize, og_init_keep_bound(nnratio), prev_xy, prev_stride, lists, list_cap, list_n);
-    static bool lds_attr = false;  // allow more than the default dynamic LDS per workgroup (benign race)
-    if (!lds_attr) {
-        (void)hipFuncSetAttribute((const void*)og_init_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  OG_INIT_LDS_MAX);
-        lds_attr = true;
-    }
     const size_t fixed = og_init_resolve_lds(F1.frame_cap, F2.frame_cap, 0);
     // staging for the (pruned, short) lists: a few KB keep several workgroups per CU; one list (<= list_cap)
     // must always fit, longer query ranges are staged in chunks
@@ -846,13 +840,7 @@ void og_launch_projb_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const fl
     if (mp.m > 0)
         hipLaunchKernelGGL(og_projb_fill_kernel, dim3((mp.m + 255) / 256, B), dim3(256), 0, s, F, G, sf, mp, stride, th,
                            og_proj_keep_bound(nnratio), off, base, cands, kept);
-    static bool lds_attr = false;
     const size_t shm = 2 * sizeof(int) * (size_t)F.frame_cap;
-    if (!lds_attr) {
-        (void)hipFuncSetAttribute((const void*)og_projb_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  OG_INIT_LDS_MAX);
-        lds_attr = true;
-    }
     hipLaunchKernelGGL(og_projb_resolve_kernel, dim3(B), dim3(PJ_NT), shm, s, mp, stride, off, base, kept, cands,
                        F.counts, F.frame_cap, nnratio, owner, owner_obs, nmatches, res, status);
 }
@@ -1251,4 +1239,14 @@ void og_launch_kf_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float
                            th, off, cands);
     hipLaunchKernelGGL(og_last_resolve_kernel, dim3(1), dim3(64), 0, s, F, KF, checkOri, 1, ORBdist, off, cands, ent,
                        owner, (int*)nullptr, nmatches);
+}
+
+// dynamic-LDS attributes (more than the default per workgroup): per device, set from og_prepare_device
+hipError_t og_prepare_device_match()
+{
+    hipError_t e = hipFuncSetAttribute((const void*)og_init_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       OG_INIT_LDS_MAX);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)og_projb_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               OG_INIT_LDS_MAX);
 }

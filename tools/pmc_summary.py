@@ -19,7 +19,7 @@ def short(n):
     return n.split("(")[0].replace("void ", "").split("<")[0].strip()
 
 
-STAGE = {"og_fast_blocks_kernel": "fast", "og_fast_cells_kernel": "fast", "og_octree_kernel": "octree", "og_describe_kernel": "describe",
+STAGE = {"og_fast_blocks_kernel": "fast", "og_fast_persist_kernel": "fast", "og_fast_cells_kernel": "fast", "og_octree_kernel": "octree", "og_describe_kernel": "describe",
          "og_search_init_kernel": "search_init", "og_grid_kernel": "grid", "og_resize_kernel": "pyramid"}
 
 
