@@ -24,7 +24,6 @@ typedef unsigned long long u64;
 #include "orb_pattern.inc"  // static const signed char oo_orb_pattern[1024]
 __constant__ signed char og_pattern[1024];
 static bool g_pattern_uploaded_dev[64] = {false};
-static int g_cu_count[64] = {0};  // CUs per device (og_prepare_device): persistent grid sizes
 
 // Lane masks straight from one v_cmp each (LLVM lowers ballot(a && b) as v_cmp(v_cndmask(mask), 0): two VALU
 // per ballot); compound conditions are ANDs of these masks on the scalar unit.  Inactive lanes read 0.
@@ -429,46 +428,13 @@ __device__ __forceinline__ int og_fast_M1(const E* p, int st, int fm)
 // polarity's test.
 typedef unsigned short og_u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ og_u16x2 og_as_u16x2(uint32_t x) { return __builtin_bit_cast(og_u16x2, x); }
-__device__ __forceinline__ uint2 og_fast_quick2(const uint32_t* p, int st, og_u16x2 tt)
-{
-    og_u16x2 c[16];
-    c[0] = og_as_u16x2(p[3 * st]);
-    c[1] = og_as_u16x2(p[1 + 3 * st]);
-    c[2] = og_as_u16x2(p[2 + 2 * st]);
-    c[3] = og_as_u16x2(p[3 + 1 * st]);
-    c[4] = og_as_u16x2(p[3]);
-    c[5] = og_as_u16x2(p[3 - 1 * st]);
-    c[6] = og_as_u16x2(p[2 - 2 * st]);
-    c[7] = og_as_u16x2(p[1 - 3 * st]);
-    c[8] = og_as_u16x2(p[-3 * st]);
-    c[9] = og_as_u16x2(p[-1 - 3 * st]);
-    c[10] = og_as_u16x2(p[-2 - 2 * st]);
-    c[11] = og_as_u16x2(p[-3 - 1 * st]);
-    c[12] = og_as_u16x2(p[-3]);
-    c[13] = og_as_u16x2(p[-3 + 1 * st]);
-    c[14] = og_as_u16x2(p[-2 + 2 * st]);
-    c[15] = og_as_u16x2(p[-1 + 3 * st]);
-    const og_u16x2 v = og_as_u16x2(p[0]);
-    og_u16x2 md = __builtin_elementwise_min(c[0], c[8]), mb = __builtin_elementwise_max(c[0], c[8]);
-#pragma unroll
-    for (int k = 1; k < 8; k++) {
-        md = __builtin_elementwise_max(md, __builtin_elementwise_min(c[k], c[k + 8]));
-        mb = __builtin_elementwise_min(mb, __builtin_elementwise_max(c[k], c[k + 8]));
-    }
-    // dark: md < v - t (saturated: v < t leaves no darker value), bright: mb > v + t (<= 510, no overflow)
-    const og_u16x2 dark = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, tt), md);
-    const og_u16x2 bright = __builtin_elementwise_sub_sat(mb, v + tt);
-    return make_uint2(__builtin_bit_cast(uint32_t, dark), __builtin_bit_cast(uint32_t, bright));
-}
-
-#ifndef OG_FAST_SLOTS
-#define OG_FAST_SLOTS 2  // pair slots per lane per stage-1 iteration
-#endif
 
 #ifndef OG_EXP_FAST_STOP
 #define OG_EXP_FAST_STOP 0
 #endif
-
+#ifndef OG_FAST_SLOT_BARRIER
+#define OG_FAST_SLOT_BARRIER 0  // 1: no scheduling across stage 1's two slots
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // k2': FAST over blocks of up to 2x2 cells.  The cells' detection areas tile a level without overlap
@@ -493,11 +459,105 @@ __device__ __forceinline__ int og_ms_idx(int i, int j, int wC, int hC)
     return (i + 1 + (i >= hC)) * FB_MSW + (j + 1 + (j >= wC));
 }
 
-__global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_fast_blocks_kernel(OgPlan P, const OgCell* __restrict__ blocks,
-                                                               const uint8_t* __restrict__ img0, long long pitch0,
-                                                               long long fstride0, const uint8_t* __restrict__ pyr,
-                                                               u64* __restrict__ cand, int* __restrict__ cand_count,
-                                                               int* __restrict__ status)
+// 1/H for the slot division of stage 1 (H = 4k <= 124), correctly rounded (compile-time IEEE division)
+__constant__ float og_fast_rcpH[32] = {
+    0.f,         1.f / 4.f,   1.f / 8.f,   1.f / 12.f,  1.f / 16.f,  1.f / 20.f,  1.f / 24.f,  1.f / 28.f,
+    1.f / 32.f,  1.f / 36.f,  1.f / 40.f,  1.f / 44.f,  1.f / 48.f,  1.f / 52.f,  1.f / 56.f,  1.f / 60.f,
+    1.f / 64.f,  1.f / 68.f,  1.f / 72.f,  1.f / 76.f,  1.f / 80.f,  1.f / 84.f,  1.f / 88.f,  1.f / 92.f,
+    1.f / 96.f,  1.f / 100.f, 1.f / 104.f, 1.f / 108.f, 1.f / 112.f, 1.f / 116.f, 1.f / 120.f, 1.f / 124.f};
+
+// The pair minima / maxima reduce as trees (depth 3 instead of a chain of 8): two slots' packed ops interleave
+// without hazard nops.
+__device__ __forceinline__ uint2 og_fast_quick2(const uint32_t* p, int st, og_u16x2 tt)
+{
+    og_u16x2 c[16];
+    c[0] = og_as_u16x2(p[3 * st]);
+    c[1] = og_as_u16x2(p[1 + 3 * st]);
+    c[2] = og_as_u16x2(p[2 + 2 * st]);
+    c[3] = og_as_u16x2(p[3 + 1 * st]);
+    c[4] = og_as_u16x2(p[3]);
+    c[5] = og_as_u16x2(p[3 - 1 * st]);
+    c[6] = og_as_u16x2(p[2 - 2 * st]);
+    c[7] = og_as_u16x2(p[1 - 3 * st]);
+    c[8] = og_as_u16x2(p[-3 * st]);
+    c[9] = og_as_u16x2(p[-1 - 3 * st]);
+    c[10] = og_as_u16x2(p[-2 - 2 * st]);
+    c[11] = og_as_u16x2(p[-3 - 1 * st]);
+    c[12] = og_as_u16x2(p[-3]);
+    c[13] = og_as_u16x2(p[-3 + 1 * st]);
+    c[14] = og_as_u16x2(p[-2 + 2 * st]);
+    c[15] = og_as_u16x2(p[-1 + 3 * st]);
+    const og_u16x2 v = og_as_u16x2(p[0]);
+    og_u16x2 mn[8], mx[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        mn[k] = __builtin_elementwise_min(c[k], c[k + 8]);
+        mx[k] = __builtin_elementwise_max(c[k], c[k + 8]);
+    }
+#pragma unroll
+    for (int w = 4; w >= 1; w >>= 1)
+#pragma unroll
+        for (int k = 0; k < w; k++) {
+            mn[k] = __builtin_elementwise_max(mn[k], mn[k + w]);
+            mx[k] = __builtin_elementwise_min(mx[k], mx[k + w]);
+        }
+    const og_u16x2 dark = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, tt), mn[0]);
+    const og_u16x2 bright = __builtin_elementwise_sub_sat(mx[0], v + tt);
+    return make_uint2(__builtin_bit_cast(uint32_t, dark), __builtin_bit_cast(uint32_t, bright));
+}
+
+// lanes whose u16 low half is nonzero (one v_cmp on the low 16 bits)
+__device__ __forceinline__ u64 og_lanes_lo16_nz(uint32_t a)
+{
+    u64 m;
+    __asm__("v_cmp_ne_u16_e64 %0, 0, %1" : "=s"(m) : "v"(a));
+    return m;
+}
+
+// ds_write_b16 from the lanes of `mask` only (exec = exec & mask around the store, restored after it)
+__device__ __forceinline__ void og_ds_write_b16_lanes(u64 mask, uint32_t lds_addr, uint32_t val)
+{
+    u64 sv;
+    __asm__ volatile("s_and_saveexec_b64 %0, %1\n\tds_write_b16 %2, %3\n\ts_mov_b64 exec, %0"
+                     : "=&s"(sv)
+                     : "s"(mask), "v"(lds_addr), "v"(val)
+                     : "memory");
+}
+
+// LDS byte address of a __shared__ object
+template <typename T>
+__device__ __forceinline__ uint32_t og_lds_addr(T* p)
+{
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)p;
+}
+
+// block table reads through the constant address space: uniform, so scalar loads (through a generic pointer the
+// compiler cannot prove the table unclobbered by the kernel's own stores and falls back to vector loads)
+__device__ __forceinline__ OgCell og_fast_block(const OgCell* blocks, int b)
+{
+    static_assert(sizeof(OgCell) == 16, "OgCell is read as one dwordx4");
+    // whole 16-byte records: the scalar unit has no 16-bit loads, so per-field short reads would go to the VMEM path
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint4 r = ((const __attribute__((address_space(4))) uint4*)blocks)[b];
+    return __builtin_bit_cast(OgCell, r);
+#else
+    return blocks[b];  // (host pass of the device function: never called)
+#endif
+}
+
+// floor(a / d) for 0 <= a < 2^24 and a quotient below 2^20, with rd ~ 1/d (v_rcp accuracy): the float product is
+// within 2^-10 of a / d, so one remainder correction makes it exact.  A few VALU instead of the ~40 scalar
+// instructions of a 32-bit integer division.
+__device__ __forceinline__ int og_div_small(int a, int d, float rd)
+{
+    int q = (int)((float)a * rd);
+    const int r = a - q * d;
+    return q + (r >= d) - (r < 0);
+}
+
+__global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_fast_blocks_kernel(
+    OgPlan P, const OgCell* __restrict__ blocks, const uint8_t* __restrict__ img0, long long pitch0, long long fstride0,
+    const uint8_t* __restrict__ pyr, u64* __restrict__ cand, int* __restrict__ cand_count, int* __restrict__ status)
 {
     __shared__ __attribute__((aligned(16))) uint32_t roi2[FB_ROWS * FB_S2];
     __shared__ __attribute__((aligned(16))) uint8_t Ms[FB_MSZ];
@@ -506,12 +566,14 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     __shared__ int sh_ns;
     __shared__ __attribute__((aligned(16))) int wk[FB_NW][8];  // per wave: kept at t1 per cell [0..3], at t2 [4..7]
     __shared__ int sh_base;
-    const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-    const int f = (int)(lin / gridDim.x);
-    const OgCell cd = blocks[lin % gridDim.x];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const unsigned nwg = gridDim.x * gridDim.y;
+    const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, nwg);
+    const int f = nwg < (1u << 24) ? og_div_small((int)lin, (int)gridDim.x, __builtin_amdgcn_rcpf((float)gridDim.x))
+                                   : (int)(lin / gridDim.x);
+    const OgCell cd = og_fast_block(blocks, (int)lin - f * (int)gridDim.x);
     const int l = cd.level;
     const OgLevel& L = P.lv[l];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint8_t* img;
     long long pitch;
     if (l == 0) {
@@ -594,70 +656,78 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const int t1 = min(max(P.iniTh, 0), 255), t2 = min(max(P.minTh, 0), 255);
     const int tq = min(t1, t2);
     const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
+    const int tA = max(t1, 1), tB = max(t2, 1);
+    const uint32_t a_ns = og_lds_addr(&sh_ns), a_lst = og_lds_addr(&lst[0]);
     // ---- stage 1: quick test on every detection pixel, two per lane: pair slot p -> row i, column c (pixels
-    // (i, c) and (i, c + H)); wave w takes slots [64w, 64w + 64) + 512k; one LDS reservation per wave
-    // iteration appends its survivors to the block's flat list (stages 2-4 then spread the list evenly)
-    const int npair = dh * H;
-    // p / H as trunc(fma(p, 1/H, 0.5/H)) with 1/H correctly rounded: (p + 1/2) / H is >= 1/(2H) away from an
-    // integer, far beyond the rounding error; exact for every p < 2^14 and H <= 128 (checked exhaustively,
-    // tests/test_oracle_pins.py::test_fast_slot_division_exact).  Full-rate VALU instead of a 32-bit multiply.
-    const float rH = 1.0f / (float)H, hH = 0.5f * rH;
-    // two pair slots per lane per iteration (slots p and p + 512): twice the LDS reads in flight and one
-    // reservation for the four survivor ballots
-    for (int p0 = wv * 64; p0 < npair; p0 += OG_FAST_SLOTS * FB_NT) {
-        int ii[OG_FAST_SLOTS], cc[OG_FAST_SLOTS];
-        uint2 r[OG_FAST_SLOTS];
+    // (i, c) and (i, c + H)); wave w takes slots [64w, 64w + 64) + 512k, two slots per iteration.  Branch-free:
+    // slots past the area test the last pair (clamped) and are masked out of the survivor masks.  One LDS
+    // reservation per wave iteration appends the survivors to the block's flat list (stages 2-4 then spread the
+    // list evenly); the stores take the survivor masks as exec.
+    const int npair = (dw > 0 && dh > 0) ? dh * H : 0;
+    const float rH = og_fast_rcpH[(H >> 2) & 31], hH = 0.5f * rH;
+    for (int p0 = wv * 64; p0 < npair; p0 += 2 * FB_NT) {
+        uint2 r[2];
+        int base[2];
+        u64 m[4];
 #pragma unroll
-        for (int h = 0; h < OG_FAST_SLOTS; h++) {
+        for (int h = 0; h < 2; h++) {
             const int pp = p0 + h * FB_NT + lane;
-            ii[h] = (int)__builtin_fmaf((float)pp, rH, hH) & 127;  // (< FB_ROWS; the mask lets the row offsets use 24-bit mads)
-            cc[h] = pp - ii[h] * H;
-            r[h] = make_uint2(0u, 0u);
-            if (pp < npair) r[h] = og_fast_quick2(&T2[(ii[h] + 3) * FB_S2 + (cc[h] + 3)], FB_S2, tt);
+            const int pc = min(pp, npair - 1);  // slots past the area test the last pair, masked below
+            const int ii = (int)__builtin_fmaf((float)pc, rH, hH) & 127;
+            const int cc = pc - ii * H;
+            base[h] = (ii << 7) | cc;
+            r[h] = og_fast_quick2(&T2[(ii + 3) * FB_S2 + (cc + 3)], FB_S2, tt);
+            const u64 valid = og_lanes_lt(pp, npair);
+            const uint32_t any = r[h].x | r[h].y;
+            m[2 * h] = og_lanes_lo16_nz(any) & valid & og_lanes_lt(cc, dw);
+            m[2 * h + 1] = og_lanes_gt((int)any, 0xffff) & valid & og_lanes_lt(cc, dw - H);
+#if OG_FAST_SLOT_BARRIER
+            __builtin_amdgcn_sched_barrier(0);  // one slot's 17 reads in flight at a time
+#endif
         }
-        // polarity bits of each pixel (entry bits 14 = dark, 15 = bright): the halves of r.x / r.y are nonzero iff
-        // that polarity passes, min(half, 1) turns them into 0/1.  Survivor masks straight from v_cmp (og_lanes_*).
-        int pol[2 * OG_FAST_SLOTS];
-        u64 m[2 * OG_FAST_SLOTS];
-        bool sv[2 * OG_FAST_SLOTS];  // bit `lane` of m (kept as a lane mask for the stores' exec)
-        int n = 0;
+        int cnt[4], n = 0;
 #pragma unroll
-        for (int h = 0; h < OG_FAST_SLOTS; h++) {
-            // v_pk_min_u16(x, 1) as asm: LLVM would otherwise turn min(half, 1) into per-half compares and selects
-            // (the splat 1 | 1 << 16 in a register: an inline constant would feed 0 to the high half)
-            uint32_t d1, b1;
-            __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r[h].x), "s"(0x00010001u));
-            __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r[h].y), "s"(0x00010001u));
-            const uint32_t pb = d1 | (b1 << 1);  // bits 0-1: first pixel (dark, bright), bits 16-17: second pixel
-            pol[2 * h] = (int)((pb << 14) & 0xc000u);
-            pol[2 * h + 1] = (int)((pb >> 2) & 0xc000u);
-            m[2 * h] = og_lanes_ne((unsigned)pol[2 * h], 0u) & og_lanes_lt(cc[h], dw);
-            m[2 * h + 1] = og_lanes_ne((unsigned)pol[2 * h + 1], 0u) & og_lanes_lt(cc[h], dw - H);
-            sv[2 * h] = pol[2 * h] != 0 && cc[h] < dw;
-            sv[2 * h + 1] = pol[2 * h + 1] != 0 && cc[h] < dw - H;
-            n += __popcll(m[2 * h]) + __popcll(m[2 * h + 1]);
+        for (int q = 0; q < 4; q++) {
+            cnt[q] = __popcll(m[q]);
+            n += cnt[q];
         }
         if (n) {
-            int b = 0;
-            if (lane == 0) b = atomicAdd(&sh_ns, n);
-            b = __builtin_amdgcn_readfirstlane(b);
+            // one LDS reservation per wave iteration from lane 0 (exec = lane 0 only; no atomic-optimizer code)
+            uint32_t old;
+            u64 sv;
+            __asm__ volatile(
+                "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_waitcnt lgkmcnt(0)\n\t"
+                "s_mov_b64 exec, %1"
+                : "=&v"(old), "=&s"(sv)
+                : "v"(a_ns), "v"(n)
+                : "memory");
+            int b = __builtin_amdgcn_readfirstlane(old);
 #pragma unroll
-            for (int q = 0; q < 2 * OG_FAST_SLOTS; q++) {
-                const int h = q >> 1;
-                if (sv[q]) lst[og_rank(m[q], b)] = (uint16_t)(pol[q] | (ii[h] << 7) | (cc[h] + ((q & 1) ? H : 0)));
-                b += __popcll(m[q]);
+            for (int h = 0; h < 2; h++) {
+                // entry bits 14 = dark, 15 = bright (halves of r.x / r.y nonzero, min(half, 1) per half)
+                uint32_t d1, b1;
+                __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r[h].x), "s"(0x00010001u));
+                __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r[h].y), "s"(0x00010001u));
+                const uint32_t pb = d1 | (b1 << 1);
+                const uint32_t elo = ((pb << 14) & 0xc000u) | (uint32_t)base[h];
+                const uint32_t ehi = ((pb >> 2) & 0xc000u) | (uint32_t)(base[h] + H);
+                og_ds_write_b16_lanes(m[2 * h], a_lst + 2u * (uint32_t)og_rank(m[2 * h], b), elo);
+                b += cnt[2 * h];
+                og_ds_write_b16_lanes(m[2 * h + 1], a_lst + 2u * (uint32_t)og_rank(m[2 * h + 1], b), ehi);
+                b += cnt[2 * h + 1];
             }
         }
     }
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm list stores are not tracked by the compiler
     __syncthreads();
     const int ns = sh_ns;
-#if OG_EXP_FAST_STOP == 2
+#if OG_EXP_FAST_STOP == 2  // timing experiments only (tools/fast_variants.py): results are wrong
     if (ns == 12345) cand_count[0] = 1;
     return;
 #endif
-    // ---- stage 2: exact M for every survivor of the wave (eager: ~92 % of 2x2 blocks hold a cell that falls
-    // back to minThFAST, so a lazy second pass costs more than it saves).  Single pixels are u16 reads of
-    // the pair layout (element step 2 per column).
+    // ---- stage 2: exact M for every survivor (eager: ~92 % of 2x2 blocks hold a cell that falls back to
+    // minThFAST, so a lazy second pass costs more than it saves).  Single pixels are u16 reads of the pair layout
+    // (element step 2 per column).
     const uint16_t* T16 = (const uint16_t*)T2;
     for (int e = tid; e < ns; e += FB_NT) {
         const int ent = lst[e];
@@ -667,18 +737,22 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const uint16_t* pc = &T16[2 * ((i + 3) * FB_S2 + (x + 3)) + hi];
         const bool dark = (ent & 0x4000) != 0, bright = (ent & 0x8000) != 0;
         int M = og_fast_M1<2>(pc, 2 * FB_S2, dark ? 0 : 0xff);
-        if (dark && bright) M = max(M, og_fast_M1<2>(pc, 2 * FB_S2, 0xff));  // rare: both polarities pass
+        if (dark && bright) {
+            // rare: both polarities pass.  The second pass re-reads its circle (the clobber stops the loads
+            // being merged with the first pass's, which would keep those 17 values live through it)
+            __asm__ volatile("" ::: "memory");
+            M = max(M, og_fast_M1<2>(pc, 2 * FB_S2, 0xff));
+        }
         Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)M;
     }
     __syncthreads();
     // ---- stage 3: same-cell 3x3 NMS at both thresholds.  cv::FAST keeps a corner (score M-1) iff its score
     // beats every neighbour's score, where non-corners score 0: with the gap layout and M <= t for every
     // non-corner, that is  M > max(t, 1)  and  M > max over the 8 neighbours of M.
-    const int tA = max(t1, 1), tB = max(t2, 1);
     int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
-    for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {  // same entry -> wave assignment as stage 4
+    for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
         const int e = e0 + lane;
-        int ent = 0, mc = 0, nb = 0;  // lanes past the end: score 0, never kept (tA, tB >= 1)
+        int ent = 0, mc = 0, nb = 0;
         if (e < ns) {
             ent = lst[e] & 0x3fff;
             const uint8_t* q = &Ms[og_ms_idx(ent >> 7, ent & 127, wC, hC) - FB_MSW - 1];
@@ -686,7 +760,6 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             nb = max(max(max(q[0], q[1]), max(q[2], q[FB_MSW])),
                      max(max(q[FB_MSW + 2], q[2 * FB_MSW]), max(q[2 * FB_MSW + 1], q[2 * FB_MSW + 2])));
         }
-        // kept at t1 / t2 and the cell (row >= hCell, column >= wCell) as lane masks; per-cell counts on the SALU
         const u64 top = og_lanes_gt(mc, nb);
         const u64 K1 = og_lanes_gt(mc, tA) & top, K2 = og_lanes_gt(mc, tB) & top;
         const u64 ci = og_lanes_gt(ent >> 7, hC - 1), cj = og_lanes_gt(ent & 127, wC - 1);
@@ -708,8 +781,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     __syncthreads();
     // per cell: iniThFAST unless the cell is empty at it (src/ORBextractor.cc:809-816).  Lane-parallel: lane L < 32
     // holds wave L/4's counts of cell L%4 (every wave computes the same block-uniform result; lanes >= 32 repeat
-    // lanes L - 32 and are masked off), so the bookkeeping is a few v_cmp / DPP ops and scalar sums instead of
-    // 16 LDS reads and ~80 adds and selects per wave
+    // lanes L - 32 and are masked off), so the bookkeeping is a few v_cmp / DPP ops and scalar sums
     const int qw = (lane >> 2) & (FB_NW - 1), qc = lane & 3;
     const int v1 = wk[qw][qc], v2 = wk[qw][4 + qc];
     const u64 nz1 = og_lanes_ne((unsigned)v1, 0u) & 0xffffffffull;
@@ -717,10 +789,8 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 #pragma unroll
     for (int c = 0; c < 4; c++) useT2 |= ((nz1 & (0x11111111ull << c)) ? 0u : 1u) << c;
     const int kw = ((useT2 >> qc) & 1u) ? v2 : v1;
-    // one wave's four cells: sum over the quad (DPP quad_perm [1,0,3,2] then [2,3,0,1])
     int ks = kw + __builtin_amdgcn_mov_dpp(kw, 0xb1, 0xf, 0xf, false);
     ks = ks + __builtin_amdgcn_mov_dpp(ks, 0x4e, 0xf, 0xf, false);
-    // kept per wave, this wave's offset and the block total, on the scalar unit
     const int wvu = __builtin_amdgcn_readfirstlane(wv);
     int kept = 0, before = 0, total = 0;
 #pragma unroll
@@ -734,494 +804,32 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     if (total == 12345) cand_count[0] = 1;
     return;
 #endif
-    if (total == 0) return;  // block-uniform
-    // ---- stage 4: one reservation per block (sh_base); each wave writes its kept entries at its offset (the
-    // octree orders candidates by position, not slot)
-    if (tid == 0) {
-        const int b = atomicAdd(&cand_count[f * P.nlevels + l], total);
-        if (b + total > L.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
-        sh_base = b;
-    }
-    __syncthreads();
-    const int base = sh_base + before;
-    if (sh_base + total > L.cand_cap || kept == 0) return;
-    u64* out = cand + (long long)f * P.cand_per_frame + L.cand_off + base;
-    const int ox = cd.x0 - L.minB + 3, oy = cd.y0 - L.minB + 3;
-    int run = 0;
-    for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
-        const int e = e0 + lane;
-        int ent = 0;  // lanes past the end: no bits, not kept
-        if (e < ns) ent = lst[e];
-        const int i = (ent >> 7) & 127, j = ent & 127;
-        const int cell = (i >= hC) * 2 + (j >= wC);
-        const unsigned kb = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
-        const u64 mask = og_lanes_ne(kb, 0u);
-        if (kb) out[og_rank(mask, run)] = og_pack_cand(ox + j, oy + i, Ms[og_ms_idx(i, j, wC, hC)] - 1);
-        run += __popcll(mask);
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// k2'': the same per-block algorithm as og_fast_blocks_kernel in a persistent grid (FP_WG_PER_CU workgroups
-// per CU, each walking a static list of (frame, block) items).  The ROI loads of the NEXT item are issued
-// into registers before the current item's stages run, so their latency hides behind stages 1-4 and the
-// next item starts with the LDS stores only; the per-workgroup setup (plan reads, thresholds) is paid once.
-// Stage 1 is branch-free: lanes past the detection area test garbage-free clamped slots and are masked out of
-// the survivor masks, both pair slots run interleaved (no dependent packed chains back to back), and the
-// survivor stores take their lane masks as exec directly.
-// ------------------------------------------------------------------------------------------------
-#ifndef OG_FAST_PERSIST
-#define OG_FAST_PERSIST 1
-#endif
-#define FP_WG_PER_CU 4  // 37.8 KB LDS and 8 waves per SIMD: four 512-thread workgroups per CU
-
-// 1/H for the slot division of stage 1 (H = 4k <= 124), correctly rounded (compile-time IEEE division)
-__constant__ float og_fast_rcpH[32] = {
-    0.f,         1.f / 4.f,   1.f / 8.f,   1.f / 12.f,  1.f / 16.f,  1.f / 20.f,  1.f / 24.f,  1.f / 28.f,
-    1.f / 32.f,  1.f / 36.f,  1.f / 40.f,  1.f / 44.f,  1.f / 48.f,  1.f / 52.f,  1.f / 56.f,  1.f / 60.f,
-    1.f / 64.f,  1.f / 68.f,  1.f / 72.f,  1.f / 76.f,  1.f / 80.f,  1.f / 84.f,  1.f / 88.f,  1.f / 92.f,
-    1.f / 96.f,  1.f / 100.f, 1.f / 104.f, 1.f / 108.f, 1.f / 112.f, 1.f / 116.f, 1.f / 120.f, 1.f / 124.f};
-
-// The quick test of og_fast_quick2 with the pair minima / maxima reduced as trees (depth 3 instead of a chain
-// of 8), so two slots' packed ops interleave without hazard nops.
-__device__ __forceinline__ uint2 og_fast_quick2t(const uint32_t* p, int st, og_u16x2 tt)
-{
-    og_u16x2 c[16];
-    c[0] = og_as_u16x2(p[3 * st]);
-    c[1] = og_as_u16x2(p[1 + 3 * st]);
-    c[2] = og_as_u16x2(p[2 + 2 * st]);
-    c[3] = og_as_u16x2(p[3 + 1 * st]);
-    c[4] = og_as_u16x2(p[3]);
-    c[5] = og_as_u16x2(p[3 - 1 * st]);
-    c[6] = og_as_u16x2(p[2 - 2 * st]);
-    c[7] = og_as_u16x2(p[1 - 3 * st]);
-    c[8] = og_as_u16x2(p[-3 * st]);
-    c[9] = og_as_u16x2(p[-1 - 3 * st]);
-    c[10] = og_as_u16x2(p[-2 - 2 * st]);
-    c[11] = og_as_u16x2(p[-3 - 1 * st]);
-    c[12] = og_as_u16x2(p[-3]);
-    c[13] = og_as_u16x2(p[-3 + 1 * st]);
-    c[14] = og_as_u16x2(p[-2 + 2 * st]);
-    c[15] = og_as_u16x2(p[-1 + 3 * st]);
-    const og_u16x2 v = og_as_u16x2(p[0]);
-    og_u16x2 mn[8], mx[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        mn[k] = __builtin_elementwise_min(c[k], c[k + 8]);
-        mx[k] = __builtin_elementwise_max(c[k], c[k + 8]);
-    }
-#pragma unroll
-    for (int w = 4; w >= 1; w >>= 1)
-#pragma unroll
-        for (int k = 0; k < w; k++) {
-            mn[k] = __builtin_elementwise_max(mn[k], mn[k + w]);
-            mx[k] = __builtin_elementwise_min(mx[k], mx[k + w]);
-        }
-    const og_u16x2 dark = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, tt), mn[0]);
-    const og_u16x2 bright = __builtin_elementwise_sub_sat(mx[0], v + tt);
-    return make_uint2(__builtin_bit_cast(uint32_t, dark), __builtin_bit_cast(uint32_t, bright));
-}
-
-// lanes whose u16 low half is nonzero (one v_cmp on the low 16 bits)
-__device__ __forceinline__ u64 og_lanes_lo16_nz(uint32_t a)
-{
-    u64 m;
-    __asm__("v_cmp_ne_u16_e64 %0, 0, %1" : "=s"(m) : "v"(a));
-    return m;
-}
-
-// ds_write_b16 from the lanes of `mask` only (exec = exec & mask around the store, restored after it)
-__device__ __forceinline__ void og_ds_write_b16_lanes(u64 mask, uint32_t lds_addr, uint32_t val)
-{
-    u64 sv;
-    __asm__ volatile("s_and_saveexec_b64 %0, %1\n\tds_write_b16 %2, %3\n\ts_mov_b64 exec, %0"
-                     : "=&s"(sv)
-                     : "s"(mask), "v"(lds_addr), "v"(val)
-                     : "memory");
-}
-
-// LDS byte address of a __shared__ object
-template <typename T>
-__device__ __forceinline__ uint32_t og_lds_addr(T* p)
-{
-    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)p;
-}
-
-// one FAST work item's ROI: block-uniform geometry and the in-flight loads of this thread's three dword pairs
-struct OgFastRoi {
-    int f, blk;        // frame, block index
-    int mis, H, nq, rh;
-    uint32_t lo[3], hi[3];
-};
-
-// block table reads through the constant address space: uniform, so scalar loads (through a generic pointer the
-// compiler cannot prove the table unclobbered by the kernel's own stores and falls back to vector loads)
-__device__ __forceinline__ OgCell og_fast_block(const OgCell* blocks, int b)
-{
-    static_assert(sizeof(OgCell) == 16, "OgCell is read as one dwordx4");
-    // whole 16-byte records: the scalar unit has no 16-bit loads, so per-field short reads would go to the VMEM path
-#if defined(__HIP_DEVICE_COMPILE__)
-    const uint4 r = ((const __attribute__((address_space(4))) uint4*)blocks)[b];
-    return __builtin_bit_cast(OgCell, r);
-#else
-    return blocks[b];  // (host pass of the device function: never called)
-#endif
-}
-
-// floor(a / d) for 0 <= a < 2^24 and a quotient below 2^20, with rd ~ 1/d (v_rcp accuracy): the float product is
-// within 2^-10 of a / d, so one remainder correction makes it exact.  A few VALU instead of the ~40 scalar
-// instructions of a 32-bit integer division.
-__device__ __forceinline__ int og_div_small(int a, int d, float rd)
-{
-    int q = (int)((float)a * rd);
-    const int r = a - q * d;
-    return q + (r >= d) - (r < 0);
-}
-
-__device__ __forceinline__ void og_fast_roi_issue(const OgPlan& P, const OgCell* __restrict__ blocks,
-                                                  const uint8_t* __restrict__ img0, long long pitch0,
-                                                  long long fstride0, const uint8_t* __restrict__ pyr, int item,
-                                                  float rtc, int tid, OgFastRoi& R)
-{
-    R.f = og_div_small(item, P.total_cells, rtc);
-    R.blk = item - R.f * P.total_cells;
-    const OgCell cd = og_fast_block(blocks, R.blk);
-    const OgLevel& L = P.lv[cd.level];
-    const uint8_t* img;
-    long long pitch;
-    if (cd.level == 0) {
-        img = img0 + (long long)R.f * fstride0;
-        pitch = pitch0;
-    } else {
-        img = pyr + (long long)R.f * P.pyr_per_frame + L.pyr_off;
-        pitch = L.pitch;
-    }
-    const int rw = cd.x1 - cd.x0, rh = cd.y1 - cd.y0, dw = rw - 6;
-    const int H = (((dw + 1) >> 1) + 3) & 0x7c;
-    const uint8_t* row0 = img + (long long)cd.y0 * pitch + cd.x0;
-    const bool aligned_rows = ((pitch & 3) == 0);
-    const int mis = aligned_rows ? (int)((uintptr_t)row0 & 3) : 0;
-    const int nq = (H + 6 + mis + 3) >> 2;
-    R.mis = mis;
-    R.H = H;
-    R.nq = nq;
-    R.rh = min(rh, FB_ROWS);
-    const int q = tid & 15;
-    const uint8_t* rbase = row0 - mis;
-    const unsigned upitch = (unsigned)pitch & (OG_MAX_PITCH - 1);
-    const unsigned mb = (unsigned)((uintptr_t)rbase & 3);
-    const uint8_t* abase = rbase - mb;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const int r = (tid >> 4) + 32 * k;
-        R.lo[k] = 0u;
-        R.hi[k] = 0u;
-        if (r < rh && q < nq) {
-            const unsigned off = (unsigned)r * upitch + 4u * (unsigned)q;
-            const int x = 4 * q - mis;
-            if (aligned_rows) {
-                if (x < rw) R.lo[k] = *(const uint32_t*)(rbase + off);
-                if (x + H < rw) R.hi[k] = *(const uint32_t*)(rbase + off + (unsigned)H);
-            } else {
-                if (x < rw) {
-                    const unsigned o = off + mb;
-                    const uint32_t* a = (const uint32_t*)(abase + (o & ~3u));
-                    R.lo[k] = __builtin_amdgcn_alignbyte(a[1], a[0], o & 3u);
-                }
-                if (x + H < rw) {
-                    const unsigned o = off + (unsigned)H + mb;
-                    const uint32_t* a = (const uint32_t*)(abase + (o & ~3u));
-                    R.hi[k] = __builtin_amdgcn_alignbyte(a[1], a[0], o & 3u);
-                }
-            }
-        }
-    }
-}
-
-// eighth x of n items (the og_xcd_remap split): [start, start + len)
-__device__ __forceinline__ void og_fast_eighth(int n, unsigned x, unsigned& start, unsigned& len)
-{
-    const unsigned q8 = (unsigned)n >> 3, r8 = (unsigned)n & 7;
-    start = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
-    len = q8 + (x < r8);
-}
-
-// dynamic schedule: v = the value a grab on eighth `ch` returned; item, or the next eighths' until all 8 from
-// `x0` are exhausted (-1)
-__device__ __forceinline__ int og_fast_grab_finish(int* work_q, int n, unsigned x0, unsigned& ch, int v)
-{
-    for (;;) {
-        unsigned start, len;
-        og_fast_eighth(n, ch & 7, start, len);
-        if ((unsigned)v < len) return (int)(start + (unsigned)v);
-        if (++ch >= x0 + 8) return -1;
-        v = atomicAdd(&work_q[32 * (ch & 7)], 1);
-    }
-}
-
-__global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_fast_persist_kernel(
-    OgPlan P, const OgCell* __restrict__ blocks, const uint8_t* __restrict__ img0, long long pitch0, long long fstride0,
-    const uint8_t* __restrict__ pyr, u64* __restrict__ cand, int* __restrict__ cand_count, int* __restrict__ status,
-    int nitems, int* __restrict__ work_q)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t roi2[FB_ROWS * FB_S2];
-    __shared__ __attribute__((aligned(16))) uint8_t Ms[FB_MSZ];
-    __shared__ uint16_t lst[FB_MW * FB_MW];
-    __shared__ int sh_ns;
-    __shared__ __attribute__((aligned(16))) int wk[FB_NW][8];
-    __shared__ int sh_base;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    // static XCD-aware schedule: the workgroups of XCD x (blockIdx % 8, as dispatched) walk one contiguous eighth
-    // of the item list, so neighbouring blocks (shared halo rows) run on one L2.  Speed only.
-    const unsigned G = gridDim.x, g = blockIdx.x, xcd = g & 7;
-#if OG_FAST_PERSIST == 3
-    // dynamic form: the eighth of XCD group x is drained through its own counter work_q[32x]; a group whose eighth
-    // is exhausted moves on to the next ones (workgroups that start late, behind another stream's kernels, simply
-    // take fewer items).  Thread 0 grabs; the next item's grab is in flight during stage 1.
-    __shared__ int sh_item;
-    unsigned ch = xcd;  // (thread 0) eighth being drained
-    if (tid == 0) sh_item = og_fast_grab_finish(work_q, nitems, xcd, ch, atomicAdd(&work_q[32 * xcd], 1));
-    __syncthreads();
-    int item = sh_item;
-    if (item < 0) return;  // workgroup-uniform
-#else
-    const unsigned nx = (G >> 3) + (xcd < (G & 7)), lg = g >> 3;
-    unsigned start, len;
-    og_fast_eighth(nitems, xcd, start, len);
-    unsigned k = lg;
-    if (k >= len) return;  // workgroup-uniform
-    int item = (int)(start + k);
-#endif
-    const int t1 = min(max(P.iniTh, 0), 255), t2 = min(max(P.minTh, 0), 255);
-    const int tq = min(t1, t2);
-    const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
-    const int tA = max(t1, 1), tB = max(t2, 1);
-    const uint32_t a_ns = og_lds_addr(&sh_ns), a_lst = og_lds_addr(&lst[0]);
-    const float rtc = __builtin_amdgcn_rcpf((float)P.total_cells);
-    OgFastRoi R;
-    og_fast_roi_issue(P, blocks, img0, pitch0, fstride0, pyr, item, rtc, tid, R);
-    for (;;) {
-
-        // ---- the item's ROI -> LDS (loads issued one item earlier), score map cleared, list emptied
-        {
-            const int q = tid & 15;
-#pragma unroll
-            for (int kk = 0; kk < 3; kk++) {
-                const int r = (tid >> 4) + 32 * kk;
-                if (r < R.rh && q < R.nq) {
-                    uint4 o;
-                    o.x = __builtin_amdgcn_perm(R.hi[kk], R.lo[kk], 0x0c040c00u);
-                    o.y = __builtin_amdgcn_perm(R.hi[kk], R.lo[kk], 0x0c050c01u);
-                    o.z = __builtin_amdgcn_perm(R.hi[kk], R.lo[kk], 0x0c060c02u);
-                    o.w = __builtin_amdgcn_perm(R.hi[kk], R.lo[kk], 0x0c070c03u);
-                    *(uint4*)&roi2[r * FB_S2 + 4 * q] = o;
-                }
-            }
-        }
-        for (int idx = tid * 16; idx < FB_MSZ; idx += FB_NT * 16) *(uint4*)&Ms[idx] = make_uint4(0u, 0u, 0u, 0u);
-        if (tid == 0) sh_ns = 0;
-        const int f = R.f;
-        const OgCell cd = og_fast_block(blocks, R.blk);
-        const int H = R.H;
-        const uint32_t* T2 = roi2 + R.mis;
-        __syncthreads();
-        const int l = cd.level;
-        const OgLevel& L = P.lv[l];
-        const int dw = cd.x1 - cd.x0 - 6, dh = cd.y1 - cd.y0 - 6;
-        const int wC = L.wCell, hC = L.hCell;
-        // ---- stage 1 (as og_fast_blocks_kernel), branch-free
-        const int npair = (dw > 0 && dh > 0) ? dh * H : 0;
-        const float rH = og_fast_rcpH[(H >> 2) & 31], hH = 0.5f * rH;
-        for (int p0 = wv * 64; p0 < npair; p0 += 2 * FB_NT) {
-            uint2 r[2];
-            int base[2];
-            u64 m[4];
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int pp = p0 + h * FB_NT + lane;
-                const int pc = min(pp, npair - 1);  // slots past the area test the last pair, masked below
-                const int ii = (int)__builtin_fmaf((float)pc, rH, hH) & 127;
-                const int cc = pc - ii * H;
-                base[h] = (ii << 7) | cc;
-                r[h] = og_fast_quick2t(&T2[(ii + 3) * FB_S2 + (cc + 3)], FB_S2, tt);
-                const u64 valid = og_lanes_lt(pp, npair);
-                const uint32_t any = r[h].x | r[h].y;
-                m[2 * h] = og_lanes_lo16_nz(any) & valid & og_lanes_lt(cc, dw);
-                m[2 * h + 1] = og_lanes_gt((int)any, 0xffff) & valid & og_lanes_lt(cc, dw - H);
-                __builtin_amdgcn_sched_barrier(0);  // one slot's 17 reads in flight at a time (VGPR budget 64)
-            }
-            int cnt[4], n = 0;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                cnt[q] = __popcll(m[q]);
-                n += cnt[q];
-            }
-            if (n) {
-                // one LDS reservation per wave iteration from lane 0 (exec = lane 0 only; no atomic-optimizer code)
-                uint32_t old;
-                u64 sv;
-                __asm__ volatile(
-                    "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_waitcnt lgkmcnt(0)\n\t"
-                    "s_mov_b64 exec, %1"
-                    : "=&v"(old), "=&s"(sv)
-                    : "v"(a_ns), "v"(n)
-                    : "memory");
-                int b = __builtin_amdgcn_readfirstlane(old);
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    // entry bits 14 = dark, 15 = bright (halves of r.x / r.y nonzero, min(half, 1) per half)
-                    uint32_t d1, b1;
-                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r[h].x), "s"(0x00010001u));
-                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r[h].y), "s"(0x00010001u));
-                    const uint32_t pb = d1 | (b1 << 1);
-                    const uint32_t elo = ((pb << 14) & 0xc000u) | (uint32_t)base[h];
-                    const uint32_t ehi = ((pb >> 2) & 0xc000u) | (uint32_t)(base[h] + H);
-                    og_ds_write_b16_lanes(m[2 * h], a_lst + 2u * (uint32_t)og_rank(m[2 * h], b), elo);
-                    b += cnt[2 * h];
-                    og_ds_write_b16_lanes(m[2 * h + 1], a_lst + 2u * (uint32_t)og_rank(m[2 * h + 1], b), ehi);
-                    b += cnt[2 * h + 1];
-                }
-            }
-        }
-        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm list stores are not tracked by the compiler
-        __syncthreads();
-        const int ns = sh_ns;
-#if OG_FAST_PERSIST == 3
-        // the next item's grab: in flight during stage 2 (whose loop holds no inline asm, which the compiler
-        // would wait in front of), consumed after it
-        // (inline asm, so the compiler's vmcnt bookkeeping does not wait for it inside stage 2; the explicit wait
-        // before the use carries the value as an operand)
-        uint32_t vq = 0;
-        if (tid == 0)
-            __asm__ volatile("global_atomic_add %0, %1, %2, %3 sc0"
-                             : "=v"(vq)
-                             : "v"(128u * (ch & 7)), "v"(1u), "s"(work_q)
-                             : "memory");
-#endif
-        // ---- stage 2: exact M of every survivor (as og_fast_blocks_kernel)
-        const uint16_t* T16 = (const uint16_t*)T2;
-        for (int e = tid; e < ns; e += FB_NT) {
-            const int ent = lst[e];
-            const int i = (ent >> 7) & 127, j = ent & 127;
-            const int hi = j >= H;
-            const int x = j - (hi ? H : 0);
-            const uint16_t* pc = &T16[2 * ((i + 3) * FB_S2 + (x + 3)) + hi];
-            const bool dark = (ent & 0x4000) != 0, bright = (ent & 0x8000) != 0;
-            int M = og_fast_M1<2>(pc, 2 * FB_S2, dark ? 0 : 0xff);
-            if (dark && bright) {
-                // rare: both polarities pass.  The second pass re-reads its circle (the clobber stops the loads
-                // being merged with the first pass's, which would keep those 17 values live through it)
-                __asm__ volatile("" ::: "memory");
-                M = max(M, og_fast_M1<2>(pc, 2 * FB_S2, 0xff));
-            }
-            Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)M;
-        }
-#if OG_FAST_PERSIST == 3
+    if (total != 0) {  // block-uniform
+        // ---- stage 4: one reservation per block; each wave writes its kept entries at its offset (the octree
+        // orders candidates by position, not slot)
         if (tid == 0) {
-            __asm__ volatile("s_waitcnt vmcnt(0)" : "+v"(vq) : : "memory");
-            sh_item = og_fast_grab_finish(work_q, nitems, xcd, ch, (int)vq);
-        }
-#endif
-        __syncthreads();
-#if OG_FAST_PERSIST == 3
-        const int nitem = sh_item;
-        const bool more = nitem >= 0;
-#else
-        const unsigned kn = k + nx;
-        const bool more = kn < len;
-        const int nitem = (int)(start + kn);
-#endif
-        // ---- next item's ROI loads in flight during this item's stages 3-4 (issued after the register-heavy
-        // stages 1-2, so the six load registers never raise the VGPR peak)
-#if OG_FAST_PERSIST == 2
-        (void)more;  // one item per workgroup: nothing to prefetch
-#else
-        // (unconditional, so the previous item's registers are dead here: the last item re-issues its own ROI)
-        og_fast_roi_issue(P, blocks, img0, pitch0, fstride0, pyr, more ? nitem : item, rtc, tid, R);
-#endif
-        // ---- stage 3: same-cell NMS at both thresholds, per-wave kept counts per cell
-        int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
-        for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
-            const int e = e0 + lane;
-            int ent = 0, mc = 0, nb = 0;
-            if (e < ns) {
-                ent = lst[e] & 0x3fff;
-                const uint8_t* q = &Ms[og_ms_idx(ent >> 7, ent & 127, wC, hC) - FB_MSW - 1];
-                mc = q[FB_MSW + 1];
-                nb = max(max(max(q[0], q[1]), max(q[2], q[FB_MSW])),
-                         max(max(q[FB_MSW + 2], q[2 * FB_MSW]), max(q[2 * FB_MSW + 1], q[2 * FB_MSW + 2])));
-            }
-            const u64 top = og_lanes_gt(mc, nb);
-            const u64 K1 = og_lanes_gt(mc, tA) & top, K2 = og_lanes_gt(mc, tB) & top;
-            const u64 ci = og_lanes_gt(ent >> 7, hC - 1), cj = og_lanes_gt(ent & 127, wC - 1);
-            if (e < ns) lst[e] = (uint16_t)(ent | (mc > tA && mc > nb ? 0x4000 : 0) | (mc > tB && mc > nb ? 0x8000 : 0));
-            const u64 cm[4] = {~ci & ~cj, ~ci & cj, ci & ~cj, ci & cj};
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                c1[c] += __popcll(K1 & cm[c]);
-                c2[c] += __popcll(K2 & cm[c]);
-            }
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                wk[wv][c] = c1[c];
-                wk[wv][4 + c] = c2[c];
-            }
+            const int b = atomicAdd(&cand_count[f * P.nlevels + l], total);
+            if (b + total > L.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
+            sh_base = b;
         }
         __syncthreads();
-        // per cell: iniThFAST unless the cell is empty at it (src/ORBextractor.cc:809-816), lane-parallel as in
-        // og_fast_blocks_kernel
-        const int qw = (lane >> 2) & (FB_NW - 1), qc = lane & 3;
-        const int v1 = wk[qw][qc], v2 = wk[qw][4 + qc];
-        const u64 nz1 = og_lanes_ne((unsigned)v1, 0u) & 0xffffffffull;
-        unsigned useT2 = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) useT2 |= ((nz1 & (0x11111111ull << c)) ? 0u : 1u) << c;
-        const int kw = ((useT2 >> qc) & 1u) ? v2 : v1;
-        int ks = kw + __builtin_amdgcn_mov_dpp(kw, 0xb1, 0xf, 0xf, false);
-        ks = ks + __builtin_amdgcn_mov_dpp(ks, 0x4e, 0xf, 0xf, false);
-        const int wvu = __builtin_amdgcn_readfirstlane(wv);
-        int kept = 0, before = 0, total = 0;
-#pragma unroll
-        for (int w = 0; w < FB_NW; w++) {
-            const int kwv = __builtin_amdgcn_readlane(ks, 4 * w);
-            before += w < wvu ? kwv : 0;
-            kept = w == wvu ? kwv : kept;
-            total += kwv;
-        }
-        if (total != 0) {  // block-uniform
-            // ---- stage 4: one reservation per block; each wave writes its kept entries at its offset
-            if (tid == 0) {
-                const int b = atomicAdd(&cand_count[f * P.nlevels + l], total);
-                if (b + total > L.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
-                sh_base = b;
-            }
-            __syncthreads();
-            const int sb = sh_base;
-            if (sb + total <= L.cand_cap && kept != 0) {
-                u64* out = cand + (long long)f * P.cand_per_frame + L.cand_off + sb + before;
-                const int ox = cd.x0 - L.minB + 3, oy = cd.y0 - L.minB + 3;
-                int run = 0;
-                for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
-                    const int e = e0 + lane;
-                    int ent = 0;
-                    if (e < ns) ent = lst[e];
-                    const int i = (ent >> 7) & 127, j = ent & 127;
-                    const int cell = (i >= hC) * 2 + (j >= wC);
-                    const unsigned kb = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
-                    const u64 mask = og_lanes_ne(kb, 0u);
-                    if (kb) out[og_rank(mask, run)] = og_pack_cand(ox + j, oy + i, Ms[og_ms_idx(i, j, wC, hC)] - 1);
-                    run += __popcll(mask);
-                }
+        const int sb = sh_base;
+        if (sb + total <= L.cand_cap && kept != 0) {
+            u64* out = cand + (long long)f * P.cand_per_frame + L.cand_off + sb + before;
+            const int ox = cd.x0 - L.minB + 3, oy = cd.y0 - L.minB + 3;
+            int run = 0;
+            for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
+                const int e = e0 + lane;
+                int ent = 0;
+                if (e < ns) ent = lst[e];
+                const int i = (ent >> 7) & 127, j = ent & 127;
+                const int cell = (i >= hC) * 2 + (j >= wC);
+                const unsigned kb = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
+                const u64 mask = og_lanes_ne(kb, 0u);
+                if (kb) out[og_rank(mask, run)] = og_pack_cand(ox + j, oy + i, Ms[og_ms_idx(i, j, wC, hC)] - 1);
+                run += __popcll(mask);
             }
         }
-        if (!more) break;  // workgroup-uniform
-        item = nitem;
-#if OG_FAST_PERSIST != 3
-        k = kn;
-#endif
-        __syncthreads();  // this item's LDS (roi2, Ms, lst, wk, sh_base) is dead before the next item's stores
     }
 }
 
@@ -2598,10 +2206,6 @@ void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, lo
 // orbgpu_create after hipSetDevice
 hipError_t og_prepare_device()
 {
-    int dev = 0, ncu = 0;
-    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 &&
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-        g_cu_count[dev] = ncu;
     hipError_t e = hipFuncSetAttribute((const void*)og_resize2_kernel<false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
     if (e == hipSuccess)
@@ -2627,34 +2231,10 @@ void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, l
 }
 
 void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,
-                    long long fstride0, const uint8_t* pyr, u64* cand, int* cand_count, int* status, int B,
-                    int* work_q)
+                    long long fstride0, const uint8_t* pyr, u64* cand, int* cand_count, int* status, int B)
 {
-#if OG_FAST_PERSIST
-    if ((long long)P.total_cells * B >= (1ll << 24)) {  // og_div_small's domain: the one-block-per-workgroup kernel
-        hipLaunchKernelGGL(og_fast_blocks_kernel, dim3(P.total_cells, B), dim3(FB_NT), 0, s, P, cells, img0, pitch0,
-                           fstride0, pyr, cand, cand_count, status);
-        return;
-    }
-    // persistent grid: FP_WG_PER_CU resident workgroups per CU (>= 8 whenever there are >= 8 items, so every
-    // XCD's eighth of the item list has a walker)
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const int ncu = (dev >= 0 && dev < 64 && g_cu_count[dev] > 0) ? g_cu_count[dev] : 256;
-    const long long nitems = (long long)P.total_cells * B;
-#if OG_FAST_PERSIST == 2
-    const int G = (int)nitems;  // one item per workgroup (the persistent kernel's code without the persistence)
-    (void)ncu;
-#else
-    const int G = (int)std::min<long long>((long long)FP_WG_PER_CU * ncu, nitems);
-#endif
-    if (G > 0)
-        hipLaunchKernelGGL(og_fast_persist_kernel, dim3(G), dim3(FB_NT), 0, s, P, cells, img0, pitch0, fstride0, pyr,
-                           cand, cand_count, status, (int)nitems, work_q);
-#else
     hipLaunchKernelGGL(og_fast_blocks_kernel, dim3(P.total_cells, B), dim3(FB_NT), 0, s, P, cells, img0, pitch0,
                        fstride0, pyr, cand, cand_count, status);
-#endif
 }
 
 void og_launch_octree(hipStream_t s, const OgPlan& P, const u64* cand, const int* cand_count, uint16_t* node_of,

@@ -435,8 +435,7 @@ static int ensure_batch(orbgpu_ctx* c, int B)
     const size_t Bn = (size_t)B;
     HIP_TRY(c, ensure(c->pyr, Bn * (size_t)P.pyr_per_frame));
     HIP_TRY(c, ensure(c->cand, Bn * (size_t)P.cand_per_frame));
-    // (frame, level) candidate counters, then (at a 128-B boundary) the FAST work counters
-    HIP_TRY(c, ensure(c->cand_count, ((Bn * (size_t)P.nlevels + 31) & ~(size_t)31) + OG_FAST_QWORDS));
+    HIP_TRY(c, ensure(c->cand_count, Bn * (size_t)P.nlevels));
     HIP_TRY(c, ensure(c->node_of, Bn * (size_t)P.cand_per_frame));
     HIP_TRY(c, ensure(c->oct_xy, Bn * (size_t)P.kcap_total));
     HIP_TRY(c, ensure(c->oct_resp, Bn * (size_t)P.kcap_total));
@@ -498,8 +497,7 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
     hipStream_t s = c->stream;
     timer_begin(c);
     timer_mark(c, "start");
-    const size_t q_off = ((size_t)B * P.nlevels + 31) & ~(size_t)31;
-    HIP_TRY(c, hipMemsetAsync(c->cand_count.p, 0, sizeof(int) * (q_off + OG_FAST_QWORDS), s));
+    HIP_TRY(c, hipMemsetAsync(c->cand_count.p, 0, sizeof(int) * (size_t)B * P.nlevels, s));
     // k1: chained pyramid, src/ORBextractor.cc:1107-1132
     // levels (1,2), (3,4), (5,6) in one launch each (og_resize2_kernel), a last odd level alone
     for (int l = 1; l < P.nlevels;) {
@@ -523,8 +521,7 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
         }
     }
     timer_mark(c, "pyramid");
-    og_launch_fast(s, P, c->cells.p, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p, c->status.p, B,
-                   c->cand_count.p + q_off);
+    og_launch_fast(s, P, c->cells.p, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p, c->status.p, B);
     timer_mark(c, "fast");
     og_launch_octree(s, P, c->cand.p, c->cand_count.p, c->node_of.p, c->oct_xy.p, c->oct_resp.p, c->oct_count.p,
                      c->status.p, B);
