@@ -435,6 +435,12 @@ __device__ __forceinline__ og_u16x2 og_as_u16x2(uint32_t x) { return __builtin_b
 #ifndef OG_FAST_SLOT_BARRIER
 #define OG_FAST_SLOT_BARRIER 0  // 1: no scheduling across stage 1's two slots
 #endif
+#ifndef OG_FAST_COLWALK
+#define OG_FAST_COLWALK 0  // 1: stage 1 as a column walk over a register window (measured slower)
+#endif
+#ifndef FB_R
+#define FB_R 8  // detection rows per column-walk item; divides FB_MW (the window never leaves roi2)
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // k2': FAST over blocks of up to 2x2 cells.  The cells' detection areas tile a level without overlap
@@ -451,6 +457,9 @@ __device__ __forceinline__ og_u16x2 og_as_u16x2(uint32_t x) { return __builtin_b
 #define FB_MW 80                 // detection width/height capacity of a block (2 x 40 or 1 x 64)
 #define FB_MSW (FB_MW + 3)       // score map stride: a zero gap column before, between and after the cells
 #define FB_MSZ ((FB_MSW * FB_MSW + 15) & ~15)  // 16-byte multiple: zeroed by 16-byte stores
+#if FB_MW % FB_R != 0 || FB_MW / FB_R > 16
+#error "FB_R must divide FB_MW into at most 16 segments"
+#endif
 
 // score-map index of detection pixel (i, j): one zero row/column separates the block's cells and surrounds
 // them, so a pixel's 8 neighbours outside its cell (or outside the detection area) read 0 without checks
@@ -468,31 +477,15 @@ __constant__ float og_fast_rcpH[32] = {
 
 // The pair minima / maxima reduce as trees (depth 3 instead of a chain of 8): two slots' packed ops interleave
 // without hazard nops.
-__device__ __forceinline__ uint2 og_fast_quick2(const uint32_t* p, int st, og_u16x2 tt)
+// c[k] = circle sample k (pair dwords, cv::FAST's offsets; only the opposite pairs {k, k+8} matter), pv = centre
+__device__ __forceinline__ uint2 og_fast_quick2v(const uint32_t (&c)[16], uint32_t pv, og_u16x2 tt)
 {
-    og_u16x2 c[16];
-    c[0] = og_as_u16x2(p[3 * st]);
-    c[1] = og_as_u16x2(p[1 + 3 * st]);
-    c[2] = og_as_u16x2(p[2 + 2 * st]);
-    c[3] = og_as_u16x2(p[3 + 1 * st]);
-    c[4] = og_as_u16x2(p[3]);
-    c[5] = og_as_u16x2(p[3 - 1 * st]);
-    c[6] = og_as_u16x2(p[2 - 2 * st]);
-    c[7] = og_as_u16x2(p[1 - 3 * st]);
-    c[8] = og_as_u16x2(p[-3 * st]);
-    c[9] = og_as_u16x2(p[-1 - 3 * st]);
-    c[10] = og_as_u16x2(p[-2 - 2 * st]);
-    c[11] = og_as_u16x2(p[-3 - 1 * st]);
-    c[12] = og_as_u16x2(p[-3]);
-    c[13] = og_as_u16x2(p[-3 + 1 * st]);
-    c[14] = og_as_u16x2(p[-2 + 2 * st]);
-    c[15] = og_as_u16x2(p[-1 + 3 * st]);
-    const og_u16x2 v = og_as_u16x2(p[0]);
+    const og_u16x2 v = og_as_u16x2(pv);
     og_u16x2 mn[8], mx[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        mn[k] = __builtin_elementwise_min(c[k], c[k + 8]);
-        mx[k] = __builtin_elementwise_max(c[k], c[k + 8]);
+        mn[k] = __builtin_elementwise_min(og_as_u16x2(c[k]), og_as_u16x2(c[k + 8]));
+        mx[k] = __builtin_elementwise_max(og_as_u16x2(c[k]), og_as_u16x2(c[k + 8]));
     }
 #pragma unroll
     for (int w = 4; w >= 1; w >>= 1)
@@ -504,6 +497,15 @@ __device__ __forceinline__ uint2 og_fast_quick2(const uint32_t* p, int st, og_u1
     const og_u16x2 dark = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, tt), mn[0]);
     const og_u16x2 bright = __builtin_elementwise_sub_sat(mx[0], v + tt);
     return make_uint2(__builtin_bit_cast(uint32_t, dark), __builtin_bit_cast(uint32_t, bright));
+}
+
+__device__ __forceinline__ uint2 og_fast_quick2(const uint32_t* p, int st, og_u16x2 tt)
+{
+    const uint32_t c[16] = {p[3 * st],      p[1 + 3 * st],  p[2 + 2 * st],  p[3 + 1 * st],
+                            p[3],           p[3 - 1 * st],  p[2 - 2 * st],  p[1 - 3 * st],
+                            p[-3 * st],     p[-1 - 3 * st], p[-2 - 2 * st], p[-3 - 1 * st],
+                            p[-3],          p[-3 + 1 * st], p[-2 + 2 * st], p[-1 + 3 * st]};
+    return og_fast_quick2v(c, p[0], tt);
 }
 
 // lanes whose u16 low half is nonzero (one v_cmp on the low 16 bits)
@@ -663,8 +665,79 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     // slots past the area test the last pair (clamped) and are masked out of the survivor masks.  One LDS
     // reservation per wave iteration appends the survivors to the block's flat list (stages 2-4 then spread the
     // list evenly); the stores take the survivor masks as exec.
-    const int npair = (dw > 0 && dh > 0) ? dh * H : 0;
     const float rH = og_fast_rcpH[(H >> 2) & 31], hH = 0.5f * rH;
+#if OG_FAST_COLWALK
+    // Column walk: item = (segment s of FB_R detection rows, pair column cc); the lanes of a wave run along the
+    // pair columns, so every window read is a row of consecutive dwords.  The item's (FB_R + 6) x 7 window of
+    // pair dwords sits in VGPRs and serves the FB_R quick tests of its column: 7 LDS reads per row instead of
+    // 17 per pixel pair, and one address per item.  Rows past dh read ROI rows the area does not cover (inside
+    // roi2: nseg * FB_R <= FB_MW) and are masked out.
+    {
+        const int nitem = ((dh + FB_R - 1) / FB_R) * H;
+        for (int it0 = wv * 64; it0 < nitem; it0 += FB_NT) {
+            const int it = it0 + lane;
+            const int itc = min(it, nitem - 1);
+            const int s = (int)__builtin_fmaf((float)itc, rH, hH) & 15;
+            const int cc = itc - s * H;
+            const int i0 = s * FB_R;
+            const uint32_t* q = &T2[i0 * FB_S2 + cc];  // window (r, x) = q[r * FB_S2 + x]: ROI row i0 + r, column cc + x
+            uint32_t win[FB_R + 6][7];
+#pragma unroll
+            for (int r = 0; r < FB_R + 6; r++)
+#pragma unroll
+                for (int x = 0; x < 7; x++) win[r][x] = q[r * FB_S2 + x];  // unused entries are dead loads
+            const u64 lane_ok = og_lanes_lt(it, nitem);
+            const u64 ok_lo = lane_ok & og_lanes_lt(cc, dw), ok_hi = lane_ok & og_lanes_lt(cc, dw - H);
+            // the survivor masks are counted here and re-derived from the polarity codes at the stores (16 masks
+            // held across the reservation would spill SGPRs)
+            uint32_t pb[FB_R];
+            int n = 0;
+#pragma unroll
+            for (int k = 0; k < FB_R; k++) {
+#define W_(dy, dx) win[k + 3 + (dy)][3 + (dx)]
+                const uint32_t c[16] = {W_(3, 0),   W_(3, 1),   W_(2, 2),   W_(1, 3),  W_(0, 3),  W_(-1, 3),
+                                        W_(-2, 2),  W_(-3, 1),  W_(-3, 0),  W_(-3, -1), W_(-2, -2), W_(-1, -3),
+                                        W_(0, -3),  W_(1, -3),  W_(2, -2),  W_(3, -1)};
+                const uint2 rr = og_fast_quick2v(c, W_(0, 0), tt);
+#undef W_
+                const u64 rowok = og_lanes_lt(i0 + k, dh);
+                const uint32_t any = rr.x | rr.y;
+                n += __popcll(og_lanes_lo16_nz(any) & ok_lo & rowok) + __popcll(og_lanes_gt((int)any, 0xffff) & ok_hi & rowok);
+                // polarity code per half: bit 0 dark, bit 1 bright (lo pixel bits 0-1, hi pixel bits 16-17)
+                uint32_t d1, b1;
+                __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(rr.x), "s"(0x00010001u));
+                __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(rr.y), "s"(0x00010001u));
+                pb[k] = d1 | (b1 << 1);
+            }
+            if (n) {
+                uint32_t old;
+                u64 sv;
+                __asm__ volatile(
+                    "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_waitcnt lgkmcnt(0)\n\t"
+                    "s_mov_b64 exec, %1"
+                    : "=&v"(old), "=&s"(sv)
+                    : "v"(a_ns), "v"(n)
+                    : "memory");
+                int b = __builtin_amdgcn_readfirstlane(old);
+                const uint32_t e0 = (uint32_t)((i0 << 7) | cc);
+#pragma unroll
+                for (int k = 0; k < FB_R; k++) {
+                    // entry (i << 7) | j with bits 14 = dark, 15 = bright; bits above 15 are not stored
+                    const uint32_t ek = e0 + (uint32_t)(k << 7);
+                    const uint32_t elo = (pb[k] << 14) | ek;
+                    const uint32_t ehi = (pb[k] >> 2) | (ek + (uint32_t)H);
+                    const u64 rowok = og_lanes_gt(dh - i0, k);
+                    const u64 mlo = og_lanes_lo16_nz(pb[k]) & ok_lo & rowok, mhi = og_lanes_gt((int)pb[k], 0xffff) & ok_hi & rowok;
+                    og_ds_write_b16_lanes(mlo, a_lst + 2u * (uint32_t)og_rank(mlo, b), elo);
+                    b += __popcll(mlo);
+                    og_ds_write_b16_lanes(mhi, a_lst + 2u * (uint32_t)og_rank(mhi, b), ehi);
+                    b += __popcll(mhi);
+                }
+            }
+        }
+    }
+#else
+    const int npair = (dw > 0 && dh > 0) ? dh * H : 0;
     for (int p0 = wv * 64; p0 < npair; p0 += 2 * FB_NT) {
         uint2 r[2];
         int base[2];
@@ -718,6 +791,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             }
         }
     }
+#endif
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm list stores are not tracked by the compiler
     __syncthreads();
     const int ns = sh_ns;
@@ -1782,6 +1856,11 @@ __device__ __forceinline__ int og_wave_sum(int v)
 #define RAW_W 43
 #define RAW_S 52  // 43 + 3 misalignment bytes, dword multiple; 13 dwords: conflict-free lane-per-row reads
 #define BL_W 37
+#ifndef OG_DK_VDWORD
+#define OG_DK_VDWORD 1  // vertical blur pass: 2 rows x 4 columns per item, dword stores (0: 4 rows x 1 column, bytes)
+#endif
+#define BL_S (OG_DK_VDWORD ? 40 : BL_W)  // blurred-window row stride in bytes
+static_assert(BL_W * BL_S <= RAW_W * RAW_S, "the blurred window aliases the raw one");
 #define HP_ROWS 22  // row pairs of the horizontal pass (43 rows -> 22 pairs)
 #define HP_S 40     // pair-row stride in dwords (10 groups of 4 columns)
 
@@ -1992,6 +2071,47 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         const u16x2v o0 = {0, s0}, o1 = {s1, s2}, o2 = {s3, s2}, o3 = {s1, s0};
         // level column of window column c is cx - 18 + c (inside the level: keypoints sit >= 19 px from the edge)
         const int xsimd = BV == 0 ? ((lw & ~3) - (cx - 18)) : 0;  // window columns c < xsimd round half-to-even
+#if OG_DK_VDWORD
+        // item = (row pair p, 4-column group g): rows 2p, 2p + 1 from pairs p .. p + 3 (one 16-byte read each),
+        // columns 4g .. 4g + 3 packed into one dword store per row (columns 37-39 are padding of the BL_S stride)
+        for (int it = lane; it < 19 * 10; it += 64) {
+            const int p = it / 10, g = it - p * 10;
+            uint4 pr4[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) pr4[k] = *(const uint4*)&Hp[(p + k) * HP_S + 4 * g];
+            uint32_t ve4 = 0, vo4 = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                u16x2v q[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t d = j == 0 ? pr4[k].x : j == 1 ? pr4[k].y : j == 2 ? pr4[k].z : pr4[k].w;
+                    q[k] = __builtin_bit_cast(u16x2v, d);
+                }
+                uint32_t ae = __builtin_amdgcn_udot2(q[0], e0, 0u, false);
+                ae = __builtin_amdgcn_udot2(q[1], e1, ae, false);
+                ae = __builtin_amdgcn_udot2(q[2], e2, ae, false);
+                ae = __builtin_amdgcn_udot2(q[3], e3, ae, false);
+                uint32_t ao = __builtin_amdgcn_udot2(q[0], o0, 0u, false);
+                ao = __builtin_amdgcn_udot2(q[1], o1, ao, false);
+                ao = __builtin_amdgcn_udot2(q[2], o2, ao, false);
+                ao = __builtin_amdgcn_udot2(q[3], o3, ao, false);
+                uint32_t ve, vo;
+                if (BV == 0) {
+                    const uint32_t up = 4 * g + j < xsimd ? 0u : 1u;
+                    ve = (ae + 0x7fffu + (__builtin_amdgcn_ubfe(ae, 16, 1) | up)) >> 16;
+                    vo = (ao + 0x7fffu + (__builtin_amdgcn_ubfe(ao, 16, 1) | up)) >> 16;
+                } else {
+                    ve = (ae + (1u << 15)) >> 16;
+                    vo = (ao + (1u << 15)) >> 16;
+                }
+                ve4 |= min(ve, 255u) << (8 * j);
+                vo4 |= min(vo, 255u) << (8 * j);
+            }
+            *(uint32_t*)&Bl[(2 * p) * BL_S + 4 * g] = ve4;
+            if (2 * p + 1 < BL_W) *(uint32_t*)&Bl[(2 * p + 1) * BL_S + 4 * g] = vo4;
+        }
+#else
         for (int it = lane; it < BL_W * 10; it += 64) {
             const int m = it / BL_W, c = it - m * BL_W;
             u16x2v pr[5];
@@ -2022,6 +2142,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
                 if (r0 + 1 < BL_W) Bl[(r0 + 1) * BL_W + c] = (uint8_t)min(vo, 255u);
             }
         }
+#endif
     }
     og_dk_sync();
     if (!active) return;
@@ -2029,7 +2150,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     float a, b;
     og_sincosf(angle * factorPI, &b, &a);
-    const uint8_t* ctr = Bl + 18 * BL_W + 18;
+    const uint8_t* ctr = Bl + 18 * BL_S + 18;
     constexpr bool nofma = NOFMA;
     u64 words[4];
 #pragma unroll
@@ -2044,7 +2165,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             // build without contraction rounds both products (the kernels are compiled -ffp-contract=off)
             const int row = nofma ? og_cvround(x * b + y * a) : og_cvround(__builtin_fmaf(x, b, y * a));
             const int col = nofma ? og_cvround(x * a - y * b) : og_cvround(__builtin_fmaf(x, a, -(y * b)));
-            val[q] = ctr[__mul24(row, BL_W) + col];  // |row| <= 18: a 24-bit multiply
+            val[q] = ctr[__mul24(row, BL_S) + col];  // |row| <= 18: a 24-bit multiply
         }
         words[t] = og_ballot(val[0] < val[1]);
     }
@@ -2230,10 +2351,12 @@ void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, l
                            pitchA, dstB, pitchB, dst_fstride, g, status);
 }
 
-void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,
-                    long long fstride0, const uint8_t* pyr, u64* cand, int* cand_count, int* status, int B)
+void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, int nblocks, const uint8_t* img0,
+                    long long pitch0, long long fstride0, const uint8_t* pyr, u64* cand, int* cand_count, int* status,
+                    int B)
 {
-    hipLaunchKernelGGL(og_fast_blocks_kernel, dim3(P.total_cells, B), dim3(FB_NT), 0, s, P, cells, img0, pitch0,
+    if (nblocks <= 0 || B <= 0) return;
+    hipLaunchKernelGGL(og_fast_blocks_kernel, dim3(nblocks, B), dim3(FB_NT), 0, s, P, cells, img0, pitch0,
                        fstride0, pyr, cand, cand_count, status);
 }
 

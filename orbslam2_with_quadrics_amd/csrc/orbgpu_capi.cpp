@@ -521,7 +521,7 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
         }
     }
     timer_mark(c, "pyramid");
-    og_launch_fast(s, P, c->cells.p, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p, c->status.p, B);
+    og_launch_fast(s, P, c->cells.p, P.total_cells, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p, c->status.p, B);
     timer_mark(c, "fast");
     og_launch_octree(s, P, c->cand.p, c->cand_count.p, c->node_of.p, c->oct_xy.p, c->oct_resp.p, c->oct_count.p,
                      c->status.p, B);

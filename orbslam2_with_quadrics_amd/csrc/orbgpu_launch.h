@@ -51,9 +51,10 @@ void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, lo
 hipError_t og_prepare_device();  // per-device kernel attributes (call after hipSetDevice)
 hipError_t og_prepare_device_match();  // (called by og_prepare_device)
 hipError_t og_prepare_device_bow();
-void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, const uint8_t* img0, long long pitch0,
-                    long long fstride0, const uint8_t* pyr, unsigned long long* cand, int* cand_count, int* status,
-                    int B);
+// nblocks entries of the block table from `cells` on, for each of B frames
+void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, int nblocks, const uint8_t* img0,
+                    long long pitch0, long long fstride0, const uint8_t* pyr, unsigned long long* cand, int* cand_count,
+                    int* status, int B);
 hipError_t og_read_oct_prof(unsigned long long* out, int n);  // OG_OCT_PROFILE builds only
 void og_launch_octree(hipStream_t s, const OgPlan& P, const unsigned long long* cand, const int* cand_count,
                       uint16_t* node_of, uint32_t* oct_xy, uint8_t* oct_resp, int* oct_count, int* status, int B);
