@@ -252,7 +252,9 @@ __device__ __forceinline__ void og_rz_store4(uint8_t* Dr, uint32_t packed, int n
     if (n == 4 && ((((uintptr_t)Dr) & 3) == 0)) {
         *(uint32_t*)Dr = packed;
     } else {
-        for (int k = 0; k < n; k++) Dr[k] = (uint8_t)(packed >> (8 * k));
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k < n) Dr[k] = (uint8_t)(packed >> (8 * k));
     }
 }
 
@@ -340,6 +342,7 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     // ---- level A region -> LDS (and the owned part -> HBM)
     uint8_t* DA = dstA + (long long)f * dst_fstride;
     if (rga < G) {
+        // ac0 is a multiple of 4 (host plan): every quad left of own_c1 is one aligned dword store
         const bool own_c = cA < own_c1;
         const int nown = min(4, own_c1 - cA);
         for (int rr = rga; rr < nrA; rr += G) {

@@ -354,7 +354,9 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
                 const int ar0 = yB[by0].x;
                 const int own_r1 = by0 + nyB == Bv.h ? A.h : yB[by0 + nyB].x;
                 const int ar1 = std::max(yB[by0 + nyB - 1].y, own_r1 - 1);
-                const int ac0 = xB[bx0].x;
+                // the region starts at a 4-column boundary, so the owned A quads are dword-aligned stores; the up
+                // to 3 extra columns are owned by the tile to the left, which stores the same values
+                const int ac0 = xB[bx0].x & ~3;
                 const int own_c1 = bx0 + nxB == Bv.w ? A.w : xB[bx0 + nxB].x;
                 const int ac1 = std::max(std::min(xB[bx0 + nxB - 1].x + 1, A.w - 1), own_c1 - 1);
                 const int sr0 = yA[ar0].x, sr1 = yA[ar1].y;
