@@ -757,8 +757,10 @@ def main():
 
     from orbslam2_with_quadrics_amd import ORBextractor, _lib, synthetic
 
-    dist = dist_init(world, "nccl")
-    dev = local
+    # RCCL ("nccl") is the backend; ORBGPU_BENCH_BACKEND=gloo rehearses the multi-rank path with more ranks than
+    # GPUs (ranks then share devices round-robin; RCCL refuses two ranks on one GPU)
+    dist = dist_init(world, os.environ.get("ORBGPU_BENCH_BACKEND", "nccl"))
+    dev = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev)
     env = dict(L=_lib.lib(), _lib=_lib, ORBextractor=ORBextractor, synthetic=synthetic, dev=dev, rank=rank,
                dist=dist, world=world)
