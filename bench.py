@@ -226,10 +226,11 @@ def _frames(synthetic, rows, cols, B, rank, seed_off=1000):
     return f1, np.stack([uniq[i % nuniq] for i in range(B)])
 
 
-def bench_golden(args, rank):
-    """Oracle hashes of this rank's config-3 frames (tests/golden/bench_golden.json, tests/golden/make_golden.py),
-    or None when the run's configuration is not the one the goldens were made for."""
-    path = os.path.join(ROOT, "tests", "golden", "bench_golden.json")
+def bench_golden(args, rank, name="bench_golden.json"):
+    """Oracle hashes of this rank's frames (tests/golden/bench_golden.json for config 3, bench_extract_golden.json
+    for config 2; tests/golden/make_golden.py), or None when the run's configuration is not the one the goldens
+    were made for."""
+    path = os.path.join(ROOT, "tests", "golden", name)
     if not os.path.exists(path):
         return None
     g = json.load(open(path))
@@ -423,7 +424,33 @@ def setup_extract(args, env):
             kp_all += int(counts.sum())
         return {"mean_keypoints_per_frame": round(kp_all / B, 1)}, kp_all / S
 
-    return dict(metric=f"frames/sec ORB extract @{cols}×{rows}, {NF} feat", exs=exs, step=step, post=post,
+    def verify():
+        """Parity of the timed path: keypoints and descriptors of every frame of the last step against the
+        oracle's hashes of the same frames (ORBextractor::operator(), src/ORBextractor.cc:1043-1105)."""
+        g = bench_golden(args, env["rank"], "bench_extract_golden.json")
+        if g is None:
+            return {"status": "no oracle golden for this configuration/rank", "frames": 0, "mismatches": None}
+        nuniq = min(B, 32)
+        bad = checked = 0
+        for s_, e in enumerate(exs):
+            e.synchronize()
+            kp, de, cn, cap_ = outs[s_]
+            kps = np.zeros(Bs * cap_ * 28, np.uint8)
+            desc = np.zeros(Bs * cap_ * 32, np.uint8)
+            cnt = np.zeros(Bs, np.int32)
+            for dst, src in ((kps, kp), (desc, de), (cnt, cn)):
+                e.d2h(dst, src)
+            for b in range(Bs):
+                gf = g["frames"][(s_ * Bs + b) % nuniq]
+                n = int(cnt[b])
+                ok = (n == gf["n"] and _sha(kps[b * cap_ * 28:(b * cap_ + n) * 28]) == gf["kps_sha256"] and
+                      _sha(desc[b * cap_ * 32:(b * cap_ + n) * 32]) == gf["desc_sha256"])
+                bad += int(not ok)
+                checked += 1
+        return {"status": "checked", "frames": checked, "unique_frames": nuniq, "mismatches": bad,
+                "against": "oracle hashes of the same frames (tests/golden/bench_extract_golden.json)"}
+
+    return dict(metric=f"frames/sec ORB extract @{cols}×{rows}, {NF} feat", exs=exs, step=step, post=post, verify=verify,
                 free=lambda: exs[0].device_free(d_frames), Bs=Bs, frames_per_step=B, counts=[o[2] for o in outs],
                 workload=f"config 2: {cols}x{rows}, {NF} features, ORB extraction (ORBextractor::operator())",
                 cpu=lambda: cpu_baseline_extract(rows, cols, NF, args.cpu_seconds))
@@ -825,12 +852,15 @@ def main():
     cand_total = sum(_lib.lib().orbgpu_batch_candidate_total(e.ctx) for e in exs) / len(exs)
     extra, kp_total = W["post"]()
     parity = W["verify"]() if "verify" in W else None
-    if parity is not None and dist is not None and parity["mismatches"] is not None:
+    if parity is not None and dist is not None:  # every rank joins the reduction, with or without goldens
         import torch
 
-        t = torch.tensor([parity["frames"], parity["mismatches"]], dtype=torch.int64, device=f"cuda:{dev}")
+        has = parity["mismatches"] is not None
+        t = torch.tensor([parity["frames"], parity["mismatches"] if has else 0, int(has)], dtype=torch.int64,
+                         device=f"cuda:{dev}")
         dist.all_reduce(t)
-        parity = dict(parity, frames=int(t[0]), mismatches=int(t[1]), ranks=world)
+        parity = dict(parity, frames=int(t[0]), mismatches=int(t[1]) if int(t[2]) else None, ranks=world,
+                      ranks_checked=int(t[2]))
     P = level_pixels(args.cols, args.rows, exs[0].GetInverseScaleFactors())
     stages = {k: v[0] / max(v[1], 1) for k, v in stage_acc.items()}
     kernels = {k: v for k, v in stages.items()

@@ -14,6 +14,8 @@ libm_chunks.json    : chunked hashes of the host libm (glibc 2.35) sincosf on ev
 bench_golden.json   : the oracle's outputs on exactly the frames bench.py times (config 3: 1920x1080, 2000 features,
                       default semantics; the initial frame and the 32 unique frames of every rank 0-7) --
                       keypoint / descriptor / vnMatches12 / vbPrevMatched hashes, checked after the timed loop.
+bench_extract_golden.json: the same for bench.py --workload extract (config 2: 640x480, 1000 features; the 32
+                      unique frames of every rank 0-7): keypoint / descriptor hashes.
 tracking_golden.json: oracle SearchByProjection(F, 5000 map points, th 1) on a config-5 frame (1920x1080, 4000
                       features; SURVEY.md §8(d) map-point recipe) -- owner vector hash -- and oracle
                       Frame::ComputeStereoMatches on a KITTI-shape pair (mvuRight / mvDepth hashes).
@@ -208,6 +210,34 @@ def _bench_rank(rank):
     return out
 
 
+def _bench_extract_rank(rank):
+    sys.path.insert(0, ROOT)
+    import bench
+
+    rows, cols, nf = 480, 640, 1000
+    _, frames = bench._frames(synthetic, rows, cols, 32, rank, 2000)
+    ex = O.OracleExtractor(nf)
+
+    def h(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+    out = dict(rank=rank, frames=[])
+    for u in range(len(frames)):
+        k, d = ex(frames[u])
+        out["frames"].append(dict(n=int(len(k)), kps_sha256=h(k), desc_sha256=h(d)))
+    return out
+
+
+def bench_extract_cases():
+    from multiprocessing import Pool
+
+    with Pool(8) as pool:
+        ranks = pool.map(_bench_extract_rank, range(8))
+    json.dump({"generator": "oracle on bench.py's config-2 frames (--workload extract) via tests/golden/make_golden.py",
+               "rows": 480, "cols": 640, "nfeatures": 1000, "semantics": 0, "unique_frames": 32,
+               "ranks": ranks}, open(os.path.join(OUT, "bench_extract_golden.json"), "w"), indent=0)
+
+
 def bench_cases():
     from multiprocessing import Pool
 
@@ -226,11 +256,15 @@ if __name__ == "__main__":
     if "--only-bench" in sys.argv:
         bench_cases()
         sys.exit(0)
+    if "--only-bench-extract" in sys.argv:
+        bench_extract_cases()
+        sys.exit(0)
     if "--only-tracking" not in sys.argv:
         sincos_vectors()
         extract_cases()
         match_cases()
         bench_cases()
+        bench_extract_cases()
         libm_chunks()
     tracking_cases()
     print("golden fixtures written to", OUT)
