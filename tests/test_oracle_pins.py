@@ -447,6 +447,26 @@ def test_oracle_bench_golden_sample(oracle):
             assert hashlib.sha256(d.tobytes()).hexdigest() == gr["frames"][i]["desc_sha256"]
 
 
+def test_oracle_bench_extract_golden_sample(oracle):
+    """tests/golden/bench_extract_golden.json (the config-2 frames bench.py --workload extract times): the oracle
+    reproduces frames of ranks 0 and 7 from bench._frames."""
+    from orbslam2_with_quadrics_amd import synthetic
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    g = json.load(open(os.path.join(GOLDEN, "bench_extract_golden.json")))
+    for rank, idx in ((0, (0, 31)), (7, (9,))):
+        gr = g["ranks"][rank]
+        _, frames = bench._frames(synthetic, g["rows"], g["cols"], 32, rank, 2000)
+        ex = oracle.OracleExtractor(g["nfeatures"])
+        for i in idx:
+            k, d = ex(frames[i])
+            assert len(k) == gr["frames"][i]["n"]
+            assert hashlib.sha256(k.tobytes()).hexdigest() == gr["frames"][i]["kps_sha256"]
+            assert hashlib.sha256(d.tobytes()).hexdigest() == gr["frames"][i]["desc_sha256"]
+
+
 def test_libm_chunk_golden_matches_host_libm():
     """tests/golden/libm_chunks.json (the GPU pins' reference) re-derived from this host's libm on sample chunks."""
     sys.path.insert(0, GOLDEN)
