@@ -504,6 +504,39 @@ def setup_stereo(args, env):
         return {"mean_left_keypoints_per_frame": round(kp_all / B, 1),
                 "mean_stereo_matches_per_frame": round(nm_all / B, 1)}, kp_all / S
 
+    def verify():
+        """Parity of the timed path: every pair of the last step -- left keypoints and descriptors, the number of
+        stereo matches and mvuRight / mvDepth as bit patterns (src/Frame.cc:466-640) -- against the oracle's hashes
+        of the same pairs."""
+        g = bench_golden(args, env["rank"], "bench_stereo_golden.json")
+        if g is None:
+            return {"status": "no oracle golden for this configuration/rank", "frames": 0, "mismatches": None}
+        bad = checked = 0
+        for s_ in range(S):
+            exL[s_].synchronize()
+            kp, de, cn, cap_ = outs[s_]
+            kps = np.zeros(Bs * cap_ * 28, np.uint8)
+            desc = np.zeros(Bs * cap_ * 32, np.uint8)
+            cnt = np.zeros(Bs, np.int32)
+            ur = np.zeros(Bs * cap_, np.float32)
+            dp = np.zeros(Bs * cap_, np.float32)
+            nm = np.zeros(Bs, np.int32)
+            for dst, src in ((kps, kp), (desc, de), (cnt, cn), (ur, d_out[s_]), (dp, d_out[s_] + Bs * cap_ * 4),
+                             (nm, d_out[s_] + Bs * cap_ * 8)):
+                exL[s_].d2h(dst, src)
+            for b in range(Bs):
+                gp = g["pairs"][(s_ * Bs + b) % nuniq]
+                n = int(cnt[b])
+                ok = (n == gp["n"] and int(nm[b]) == gp["nmatches"] and
+                      _sha(kps[b * cap_ * 28:(b * cap_ + n) * 28]) == gp["kps_sha256"] and
+                      _sha(desc[b * cap_ * 32:(b * cap_ + n) * 32]) == gp["desc_sha256"] and
+                      _sha(ur[b * cap_:b * cap_ + n]) == gp["uright_sha256"] and
+                      _sha(dp[b * cap_:b * cap_ + n]) == gp["depth_sha256"])
+                bad += int(not ok)
+                checked += 1
+        return {"status": "checked", "frames": checked, "unique_frames": nuniq, "mismatches": bad,
+                "against": "oracle hashes of the same pairs (tests/golden/bench_stereo_golden.json)"}
+
     def free():
         for s_ in range(S):
             exL[s_].device_free(d_out[s_])
@@ -511,7 +544,7 @@ def setup_stereo(args, env):
         exL[0].device_free(dR)
 
     return dict(metric=f"stereo frames/sec ORB extract L+R + ComputeStereoMatches @{cols}×{rows}, {NF} feat",
-                exs=exL + exR, step=step, post=post, free=free, Bs=Bs, frames_per_step=B,
+                exs=exL + exR, step=step, post=post, free=free, verify=verify, Bs=Bs, frames_per_step=B,
                 counts=[o[2] for o in outs],
                 workload=f"config 4: {cols}x{rows} rectified stereo pairs, {NF} features per image, "
                          f"left + right ORB extraction and Frame::ComputeStereoMatches (bf 386.1448)",

@@ -14,6 +14,8 @@ libm_chunks.json    : chunked hashes of the host libm (glibc 2.35) sincosf on ev
 bench_golden.json   : the oracle's outputs on exactly the frames bench.py times (config 3: 1920x1080, 2000 features,
                       default semantics; the initial frame and the 32 unique frames of every rank 0-7) --
                       keypoint / descriptor / vnMatches12 / vbPrevMatched hashes, checked after the timed loop.
+bench_stereo_golden.json: bench.py --workload stereo (config 4: KITTI 1241x376, 2000 features; the 16 unique pairs
+                      of every rank 0-7): left keypoint / descriptor hashes, nmatches, mvuRight / mvDepth hashes.
 bench_extract_golden.json: the same for bench.py --workload extract (config 2: 640x480, 1000 features; the 32
                       unique frames of every rank 0-7): keypoint / descriptor hashes.
 tracking_golden.json: oracle SearchByProjection(F, 5000 map points, th 1) on a config-5 frame (1920x1080, 4000
@@ -238,6 +240,35 @@ def bench_extract_cases():
                "ranks": ranks}, open(os.path.join(OUT, "bench_extract_golden.json"), "w"), indent=0)
 
 
+def _bench_stereo_rank(rank):
+    rows, cols, nf = 376, 1241, 2000
+    mbf, mb = 386.1448, 386.1448 / 718.856  # bench.setup_stereo (Examples/Stereo/KITTI00-02.yaml)
+    exL, exR = O.OracleExtractor(nf), O.OracleExtractor(nf)
+
+    def h(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+    out = dict(rank=rank, pairs=[])
+    for i in range(16):
+        left, right = synthetic.stereo_pair(3000 + rank * 100 + i, rows, cols)[:2]
+        kL, dL = exL(left)
+        kR, dR = exR(right)
+        n, ur, de = O.stereo_matches(exL, exR, kL, dL, kR, dR, mbf, mb)
+        out["pairs"].append(dict(n=int(len(kL)), kps_sha256=h(kL), desc_sha256=h(dL), nmatches=int(n),
+                                 uright_sha256=h(ur.astype(np.float32)), depth_sha256=h(de.astype(np.float32))))
+    return out
+
+
+def bench_stereo_cases():
+    from multiprocessing import Pool
+
+    with Pool(8) as pool:
+        ranks = pool.map(_bench_stereo_rank, range(8))
+    json.dump({"generator": "oracle on bench.py's config-4 pairs (--workload stereo) via tests/golden/make_golden.py",
+               "rows": 376, "cols": 1241, "nfeatures": 2000, "semantics": 0, "unique_frames": 16,
+               "ranks": ranks}, open(os.path.join(OUT, "bench_stereo_golden.json"), "w"), indent=0)
+
+
 def bench_cases():
     from multiprocessing import Pool
 
@@ -259,12 +290,16 @@ if __name__ == "__main__":
     if "--only-bench-extract" in sys.argv:
         bench_extract_cases()
         sys.exit(0)
+    if "--only-bench-stereo" in sys.argv:
+        bench_stereo_cases()
+        sys.exit(0)
     if "--only-tracking" not in sys.argv:
         sincos_vectors()
         extract_cases()
         match_cases()
         bench_cases()
         bench_extract_cases()
+        bench_stereo_cases()
         libm_chunks()
     tracking_cases()
     print("golden fixtures written to", OUT)

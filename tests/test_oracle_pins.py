@@ -467,6 +467,25 @@ def test_oracle_bench_extract_golden_sample(oracle):
             assert hashlib.sha256(d.tobytes()).hexdigest() == gr["frames"][i]["desc_sha256"]
 
 
+def test_oracle_bench_stereo_golden_sample(oracle):
+    """tests/golden/bench_stereo_golden.json (the config-4 pairs bench.py --workload stereo times): the oracle
+    reproduces one pair of rank 0 and one of rank 6."""
+    from orbslam2_with_quadrics_amd import synthetic
+
+    g = json.load(open(os.path.join(GOLDEN, "bench_stereo_golden.json")))
+    mbf, mb = 386.1448, 386.1448 / 718.856
+    for rank, i in ((0, 5), (6, 12)):
+        gp = g["ranks"][rank]["pairs"][i]
+        left, right = synthetic.stereo_pair(3000 + rank * 100 + i, g["rows"], g["cols"])[:2]
+        exL, exR = oracle.OracleExtractor(g["nfeatures"]), oracle.OracleExtractor(g["nfeatures"])
+        kL, dL = exL(left)
+        kR, dR = exR(right)
+        n, ur, de = oracle.stereo_matches(exL, exR, kL, dL, kR, dR, mbf, mb)
+        assert (len(kL), n) == (gp["n"], gp["nmatches"])
+        assert hashlib.sha256(ur.astype(np.float32).tobytes()).hexdigest() == gp["uright_sha256"]
+        assert hashlib.sha256(de.astype(np.float32).tobytes()).hexdigest() == gp["depth_sha256"]
+
+
 def test_libm_chunk_golden_matches_host_libm():
     """tests/golden/libm_chunks.json (the GPU pins' reference) re-derived from this host's libm on sample chunks."""
     sys.path.insert(0, GOLDEN)
