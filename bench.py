@@ -691,9 +691,11 @@ def setup_tracking(args, env):
                                                           ("vc", 4))}
         d_none = e.device_alloc(Bs * cap * 4)  # mvpMapPoints all NULL at SearchLocalPoints time
         e.h2d(d_none, np.full(Bs * cap, -1, np.int32))
+        d_zero = e.device_alloc(Bs * cap * 4)  # ... so no owner has observations (the oracle's convention: 0)
+        e.h2d(d_zero, np.zeros(Bs * cap, np.int32))
         view = _lib.MapPointsView(M, tr["iv"], offs["is_bad"], tr["lv"], tr["vc"], tr["px"], tr["py"], tr["pxr"],
                                   offs["n_obs"], offs["desc"])
-        per.append(dict(cams=d_cams, tr=tr, none=d_none, own=e.device_alloc(Bs * cap * 4),
+        per.append(dict(cams=d_cams, tr=tr, none=d_none, zero=d_zero, own=e.device_alloc(Bs * cap * 4),
                         obs=e.device_alloc(Bs * cap * 4), nm=e.device_alloc(Bs * 4), view=view))
 
     def step():
@@ -709,7 +711,7 @@ def setup_tracking(args, env):
                                                            C.c_void_p(tr["lv"]), C.c_void_p(tr["vc"])), "frustum")
             _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C.c_void_p(q["own"]), C.c_void_p(q["none"]),
                                                         Bs * cap * 4), "d2d")
-            _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C.c_void_p(q["obs"]), C.c_void_p(q["none"]),
+            _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C.c_void_p(q["obs"]), C.c_void_p(q["zero"]),
                                                         Bs * cap * 4), "d2d")
         for s_, e in enumerate(exs):
             q = per[s_]
@@ -731,16 +733,56 @@ def setup_tracking(args, env):
                 "local_map": "world points broadcast from rank 0 once per step; per-frame isInFrustum on the GPU"}, \
             kp_all / S
 
+    def verify():
+        """Parity of the timed path: every frame of the last step -- keypoints, descriptors, nmatches and the
+        mvpMapPoints owner / observation vectors of SearchByProjection after isInFrustum (src/ORBmatcher.cc:45-137,
+        src/Frame.cc:269-325) -- against the oracle's hashes of the same frames and cameras."""
+        g = bench_golden(args, env["rank"], "bench_tracking_golden.json")
+        if g is None or g.get("mappoints", M) != M:
+            return {"status": "no oracle golden for this configuration/rank", "frames": 0, "mismatches": None}
+        nuniq = min(B, 32)
+        bad = checked = 0
+        field_bad = {}
+        for s_, e in enumerate(exs):
+            e.synchronize()
+            q = per[s_]
+            kp, de, cn, cap_ = outs[s_]
+            kps = np.zeros(Bs * cap_ * 28, np.uint8)
+            desc = np.zeros(Bs * cap_ * 32, np.uint8)
+            cnt = np.zeros(Bs, np.int32)
+            own = np.zeros(Bs * cap_, np.int32)
+            obs = np.zeros(Bs * cap_, np.int32)
+            nm = np.zeros(Bs, np.int32)
+            for dst, src in ((kps, kp), (desc, de), (cnt, cn), (own, q["own"]), (obs, q["obs"]), (nm, q["nm"])):
+                e.d2h(dst, src)
+            for b in range(Bs):
+                gf = g["frames"][(s_ * Bs + b) % nuniq]
+                n = int(cnt[b])
+                fields = dict(n=n == gf["n"], nmatches=int(nm[b]) == gf["nmatches"],
+                              kps=_sha(kps[b * cap_ * 28:(b * cap_ + n) * 28]) == gf["kps_sha256"],
+                              desc=_sha(desc[b * cap_ * 32:(b * cap_ + n) * 32]) == gf["desc_sha256"],
+                              owner=_sha(own[b * cap_:b * cap_ + n]) == gf["owner_sha256"],
+                              owner_obs=_sha(obs[b * cap_:b * cap_ + n]) == gf["owner_obs_sha256"])
+                for k_, v in fields.items():
+                    field_bad[k_] = field_bad.get(k_, 0) + int(not v)
+                bad += int(not all(fields.values()))
+                checked += 1
+        if bad:
+            log(f"tracking parity: mismatching frames per field {field_bad}")
+        return {"status": "checked", "frames": checked, "unique_frames": nuniq, "mismatches": bad,
+                "against": "oracle hashes of the same frames and cameras (tests/golden/bench_tracking_golden.json)"}
+
     def free():
         for s_, e in enumerate(exs):
             q = per[s_]
-            for p in [q["cams"], q["none"], q["own"], q["obs"], q["nm"]] + list(q["tr"].values()):
+            for p in [q["cams"], q["none"], q["zero"], q["own"], q["obs"], q["nm"]] + list(q["tr"].values()):
                 e.device_free(p)
         exs[0].device_free(d_frames)
 
     return dict(metric=f"frames/sec ORB extract + isInFrustum + SearchByProjection vs {M} map points "
                        f"@{cols}×{rows}, {NF} feat",
-                exs=exs, step=step, post=post, free=free, Bs=Bs, frames_per_step=B, counts=[o[2] for o in outs],
+                exs=exs, step=step, post=post, free=free, verify=verify, Bs=Bs, frames_per_step=B,
+                counts=[o[2] for o in outs],
                 workload=f"config 5: {cols}x{rows} camera frames, {NF} features, ORB extraction + isInFrustum + "
                          f"SearchByProjection (th 1, ratio 0.8) against a {M}-point local map shared by all cameras",
                 cpu=lambda: cpu_baseline_tracking(rows, cols, NF, M, args.cpu_seconds))

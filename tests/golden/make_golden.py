@@ -16,6 +16,9 @@ bench_golden.json   : the oracle's outputs on exactly the frames bench.py times 
                       keypoint / descriptor / vnMatches12 / vbPrevMatched hashes, checked after the timed loop.
 bench_stereo_golden.json: bench.py --workload stereo (config 4: KITTI 1241x376, 2000 features; the 16 unique pairs
                       of every rank 0-7): left keypoint / descriptor hashes, nmatches, mvuRight / mvDepth hashes.
+bench_tracking_golden.json: bench.py --workload tracking (config 5: 1920x1080, 4000 features, isInFrustum and
+                      SearchByProjection(th 1) against the 5000-point local map; 32 unique frames of every rank 0-7):
+                      keypoint / descriptor hashes, nmatches, owner and owner-observation vectors.
 bench_extract_golden.json: the same for bench.py --workload extract (config 2: 640x480, 1000 features; the 32
                       unique frames of every rank 0-7): keypoint / descriptor hashes.
 tracking_golden.json: oracle SearchByProjection(F, 5000 map points, th 1) on a config-5 frame (1920x1080, 4000
@@ -269,6 +272,43 @@ def bench_stereo_cases():
                "ranks": ranks}, open(os.path.join(OUT, "bench_stereo_golden.json"), "w"), indent=0)
 
 
+def _bench_tracking_rank(rank):
+    sys.path.insert(0, ROOT)
+    import bench
+
+    rows, cols, nf, M = 1080, 1920, 4000, 5000
+    f_ref, frames = bench._frames(synthetic, rows, cols, 32, rank, 5000)
+    ex = O.OracleExtractor(nf)
+    sf = ex.tables()["scale"]
+    k0, d0 = ex(f_ref)
+    mp = bench.local_map(k0, d0, M, 7000, cols, rows, sf)
+
+    def h(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+    out = dict(rank=rank, frames=[])
+    for i in range(len(frames)):
+        dx, dy = bench.frame_shift(i)
+        k, d = ex(frames[i])
+        _, tr = O.is_in_frustum(bench.rig_camera(cols, rows, dx, dy, 1.2, len(sf)), mp["pos"], mp["normal"],
+                                mp["max_dist"], mp["min_dist"], 0.5)
+        n, own, obs = O.search_by_projection(O.OracleFrame(k, d, cols, rows, sf),
+                                             dict(tr, is_bad=mp["is_bad"], n_obs=mp["n_obs"], desc=mp["desc"]), 0.8, 1.0)
+        out["frames"].append(dict(n=int(len(k)), kps_sha256=h(k), desc_sha256=h(d), nmatches=int(n),
+                                  owner_sha256=h(own.astype(np.int32)), owner_obs_sha256=h(obs.astype(np.int32))))
+    return out
+
+
+def bench_tracking_cases():
+    from multiprocessing import Pool
+
+    with Pool(8) as pool:
+        ranks = pool.map(_bench_tracking_rank, range(8))
+    json.dump({"generator": "oracle on bench.py's config-5 frames (--workload tracking) via tests/golden/make_golden.py",
+               "rows": 1080, "cols": 1920, "nfeatures": 4000, "semantics": 0, "mappoints": 5000, "unique_frames": 32,
+               "ranks": ranks}, open(os.path.join(OUT, "bench_tracking_golden.json"), "w"), indent=0)
+
+
 def bench_cases():
     from multiprocessing import Pool
 
@@ -293,6 +333,9 @@ if __name__ == "__main__":
     if "--only-bench-stereo" in sys.argv:
         bench_stereo_cases()
         sys.exit(0)
+    if "--only-bench-tracking" in sys.argv:
+        bench_tracking_cases()
+        sys.exit(0)
     if "--only-tracking" not in sys.argv:
         sincos_vectors()
         extract_cases()
@@ -300,6 +343,7 @@ if __name__ == "__main__":
         bench_cases()
         bench_extract_cases()
         bench_stereo_cases()
+        bench_tracking_cases()
         libm_chunks()
     tracking_cases()
     print("golden fixtures written to", OUT)

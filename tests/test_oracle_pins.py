@@ -486,6 +486,33 @@ def test_oracle_bench_stereo_golden_sample(oracle):
         assert hashlib.sha256(de.astype(np.float32).tobytes()).hexdigest() == gp["depth_sha256"]
 
 
+def test_oracle_bench_tracking_golden_sample(oracle):
+    """tests/golden/bench_tracking_golden.json (the config-5 frames bench.py --workload tracking times): the oracle
+    reproduces one frame of rank 3 -- extraction, isInFrustum for its camera, SearchByProjection (th 1)."""
+    from orbslam2_with_quadrics_amd import synthetic
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    g = json.load(open(os.path.join(GOLDEN, "bench_tracking_golden.json")))
+    rank, i = 3, 21
+    rows, cols = g["rows"], g["cols"]
+    f_ref, frames = bench._frames(synthetic, rows, cols, 32, rank, 5000)
+    ex = oracle.OracleExtractor(g["nfeatures"])
+    sf = ex.tables()["scale"]
+    k0, d0 = ex(f_ref)
+    mp = bench.local_map(k0, d0, g["mappoints"], 7000, cols, rows, sf)
+    k, d = ex(frames[i])
+    _, tr = oracle.is_in_frustum(bench.rig_camera(cols, rows, *bench.frame_shift(i), 1.2, len(sf)), mp["pos"],
+                                 mp["normal"], mp["max_dist"], mp["min_dist"], 0.5)
+    n, own, obs = oracle.search_by_projection(oracle.OracleFrame(k, d, cols, rows, sf),
+                                              dict(tr, is_bad=mp["is_bad"], n_obs=mp["n_obs"], desc=mp["desc"]), 0.8, 1.0)
+    gf = g["ranks"][rank]["frames"][i]
+    assert (len(k), n) == (gf["n"], gf["nmatches"])
+    assert hashlib.sha256(own.astype(np.int32).tobytes()).hexdigest() == gf["owner_sha256"]
+    assert hashlib.sha256(obs.astype(np.int32).tobytes()).hexdigest() == gf["owner_obs_sha256"]
+
+
 def test_libm_chunk_golden_matches_host_libm():
     """tests/golden/libm_chunks.json (the GPU pins' reference) re-derived from this host's libm on sample chunks."""
     sys.path.insert(0, GOLDEN)
