@@ -1,12 +1,14 @@
 """bench.py -- frames/s of ORB extract + match @1920x1080, 2000 features (BASELINE.json metric).
 
 One step = one batch of B synthetic 1920x1080 frames already resident in HBM, per GPU:
-  * extract the initial frame F1 (Tracking::mInitialFrame) and the B new frames (ORBextractor::operator(),
-    src/ORBextractor.cc:1043-1105) -- pyramid, FAST cells, octree, orientation, blur + rBRIEF, grid;
+  * extract the B new frames (ORBextractor::operator(), src/ORBextractor.cc:1043-1105) -- pyramid, FAST cells,
+    octree, orientation, blur + rBRIEF, grid -- against the initial frame F1 (Tracking::mInitialFrame);
   * vbPrevMatched := F1 keypoints (src/Tracking.cc:573-575) and SearchForInitialization(F1, F_b) for every
     frame b (src/ORBmatcher.cc:405-520; window 100, ratio 0.9, orientation check, src/Tracking.cc:599-600);
-  * (N > 1) rank 0 extracts F1 and broadcasts it (RCCL, one ~120 KB record per step) to the other ranks, which
-    match their own frames against it; RCCL all-gather of the per-frame keypoint counts.
+  * F1 is extracted once at set-up, as Tracking extracts its initial frame once (src/Tracking.cc:571); with N > 1
+    rank 0 extracts it and broadcasts it once (RCCL, one ~120 KB record) to the other ranks, which match their own
+    frames against it; every step ends with the RCCL all-gather of the per-frame keypoint counts,
+    stream-ordered against the next step's count copies (no host synchronisation beyond the per-step one).
 Frames are independent, so N GPUs run N frame shards ("scaling": "weak"; value = all frames / max time).
 Within a GPU the B frames are split over S extractor contexts (--streams, one HIP stream each) whose
 kernels run concurrently.
@@ -85,6 +87,24 @@ def broadcast_record(dist, rank: int, buf, pack, unpack, src: int = 0):
     dist.broadcast(buf, src=src)
     if rank != src:
         unpack(buf)
+
+
+def multi_rank_step(work, exs, dist, world: int, counts, copy_counts, after_gather):
+    """One timed step: enqueue the workload on every context, copy each context's per-frame keypoint counts into
+    `counts` on that context's stream, synchronise every context once (the step's only host synchronisation: it
+    also reads the contexts' capacity-guard flags), then all-gather the counts over RCCL (north_star).  The
+    all-gather is left in flight; after_gather(s, e) orders context s's next count copy after it on the GPU.
+    Single rank: no copies, no collective."""
+    work()
+    if dist is not None:
+        for s_, e in enumerate(exs):
+            copy_counts(s_, e)
+    for e in exs:
+        e.synchronize()
+    if dist is not None:
+        allgather_counts(dist, counts, world)
+        for s_, e in enumerate(exs):
+            after_gather(s_, e)
 
 
 def allgather_counts(dist, counts, world: int):
@@ -267,14 +287,12 @@ def setup_mono_init(args, env):
     fbytes = rows * cols
     grid = _lib.GridGeom()
     L.orbgpu_grid_geom_for_image(cols, rows, C_.byref(grid))
-    ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
-    for s_, e in enumerate(exs):
-        e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bc, cols, rows, cols, fbytes)
-        e.synchronize()
-    outs = [e.batch_outputs() for e in exs]
-    cap = outs[0][3]
-    rec = None
-    if dist is not None:  # F1 record: extracted on rank 0, broadcast to the others once per step
+    # F1 (Tracking::mInitialFrame) is extracted once, at set-up (src/Tracking.cc:571); with N > 1 only rank 0
+    # extracts it and the others receive it as one frame record, also once
+    if rank == 0:
+        ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
+        ex_ref.synchronize()
+    if dist is not None:
         import torch
 
         rec = torch.empty(int(L.orbgpu_frame_record_bytes(ex_ref.ctx)), dtype=torch.uint8, device=f"cuda:{dev}")
@@ -286,6 +304,15 @@ def setup_mono_init(args, env):
         def unpack(buf):
             torch.cuda.current_stream().synchronize()  # the broadcast has landed
             _lib.check(ex_ref.ctx, L.orbgpu_frame_record_unpack(ex_ref.ctx, C_.c_void_p(buf.data_ptr())), "unpack")
+            ex_ref.synchronize()
+
+        broadcast_record(dist, rank, rec, pack, unpack)
+        del rec
+    for s_, e in enumerate(exs):
+        e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bc, cols, rows, cols, fbytes)
+        e.synchronize()
+    outs = [e.batch_outputs() for e in exs]
+    cap = outs[0][3]
     d_prev = [e.device_alloc(Bc * cap * 2 * 4) for e in exs]
     d_m12 = [e.device_alloc(Bc * cap * 4) for e in exs]
     d_nm = [e.device_alloc(Bc * 4) for e in exs]
@@ -299,10 +326,6 @@ def setup_mono_init(args, env):
                     desc=[torch.empty(Bc * cap * 32, dtype=torch.uint8).pin_memory() for _ in exs])
 
     def step():
-        if rank == 0:
-            ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
-        if rec is not None:
-            broadcast_record(dist, rank, rec, pack, unpack)
         for r in range(K):
             for s_, e in enumerate(exs):
                 off = (s_ * Bs + r * Bc) * fbytes
@@ -389,7 +412,7 @@ def setup_mono_init(args, env):
         ex_ref.device_free(d_f1)
 
     metric = METRIC if host is None else METRIC + " (PCIe-inclusive: frames H2D, keypoints + descriptors D2H)"
-    return dict(metric=metric, exs=exs, sync_extra=[ex_ref], step=step, post=post, free=free, verify=verify, Bs=Bc,
+    return dict(metric=metric, exs=exs, step=step, post=post, free=free, verify=verify, Bs=Bc,
                 per_stream=Bs, frames_per_step=B,
                 counts=d_cnt,
                 workload=f"config 3: {cols}x{rows} mono, {NF} features, ORB extract + SearchForInitialization "
@@ -610,9 +633,25 @@ MAP_FIELDS = (("pos", 12), ("normal", 12), ("max_dist", 4), ("min_dist", 4), ("i
               ("desc", 32))
 
 
+def map_offsets(M):
+    """Byte offset of each field inside the local-map record: fields in MAP_FIELDS order, each starting on a 16-byte
+    boundary (so the kernels' int32 / float loads stay aligned for any point count)."""
+    offs, o = {}, 0
+    for f, w in MAP_FIELDS:
+        offs[f] = o
+        o += (w * M + 15) & ~15
+    offs["_end"] = o
+    return offs
+
+
 def pack_map(mp):
-    """The local map as one byte record (the unit rank 0 broadcasts once per step)."""
-    return np.concatenate([np.ascontiguousarray(mp[f]).view(np.uint8).reshape(-1) for f, _ in MAP_FIELDS])
+    """The local map as one byte record (the unit rank 0 broadcasts once, at set-up); fields at map_offsets."""
+    M = len(mp["pos"])
+    offs = map_offsets(M)
+    rec = np.zeros(offs["_end"], np.uint8)
+    for f, w in MAP_FIELDS:
+        rec[offs[f]:offs[f] + w * M] = np.ascontiguousarray(mp[f]).view(np.uint8).reshape(-1)
+    return rec
 
 
 def cpu_baseline_tracking(rows, cols, nfeat, M, seconds):
@@ -642,7 +681,7 @@ def setup_tracking(args, env):
     """config 5 (8-camera 1920x1080 rig, 4000 features): per camera frame, ORB extraction, Frame::isInFrustum of every
     local-map point for the camera's pose (src/Tracking.cc:1167-1180) and SearchByProjection(F, local map, th=1)
     (Tracking::SearchLocalPoints, :1184-1191).  The local map (world points, SURVEY.md §8(d)) is built by rank 0 from
-    its reference frame and broadcast to every rank once per step; each rank's frames have their own
+    its reference frame and broadcast to every rank once, at set-up; each rank's frames have their own
     camera poses."""
     import torch
 
@@ -667,10 +706,10 @@ def setup_tracking(args, env):
     cap = outs[0][3]
     rec_h = pack_map(mp)
     rec = torch.from_numpy(rec_h).to(f"cuda:{dev}")
-    offs, o = {}, 0
-    for f, w in MAP_FIELDS:
-        offs[f] = rec.data_ptr() + o
-        o += w * M
+    # the local map from rank 0, once (before any frame is matched against it): rank 0's record overwrites the
+    # other ranks' (they built theirs from their own reference frame only to size the buffer)
+    broadcast_record(dist, rank, rec, lambda buf: None, lambda buf: torch.cuda.current_stream().synchronize())
+    offs = {f: rec.data_ptr() + o for f, o in map_offsets(M).items() if f != "_end"}
     geom = _lib.MapPointGeomView(M, offs["pos"], offs["normal"], offs["max_dist"], offs["min_dist"])
     grid = _lib.GridGeom()
     L.orbgpu_grid_geom_for_image(cols, rows, C.byref(grid))
@@ -699,8 +738,6 @@ def setup_tracking(args, env):
                         obs=e.device_alloc(Bs * cap * 4), nm=e.device_alloc(Bs * 4), view=view))
 
     def step():
-        if dist is not None:  # the local map from rank 0, once per step (before any frame is matched against it)
-            broadcast_record(dist, rank, rec, lambda buf: None, lambda buf: torch.cuda.current_stream().synchronize())
         for s_, e in enumerate(exs):
             q = per[s_]
             e.extract_batch_device(d_frames + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
@@ -730,7 +767,7 @@ def setup_tracking(args, env):
             nm_all += int(nm.sum())
         return {"mean_keypoints_per_frame": round(kp_all / B, 1), "map_points": M,
                 "mean_projection_matches_per_frame": round(nm_all / B, 1),
-                "local_map": "world points broadcast from rank 0 once per step; per-frame isInFrustum on the GPU"}, \
+                "local_map": "world points broadcast from rank 0 once at set-up; per-frame isInFrustum on the GPU"}, \
             kp_all / S
 
     def verify():
@@ -872,17 +909,19 @@ def main():
     exs, Bs, S, B = W["exs"], W["Bs"], args.streams, W["frames_per_step"]
     Bps = W.get("per_stream", Bs)  # frames per stream per step (Bs = frames per launch)
     counts_t = torch.zeros(B, dtype=torch.int32, device=f"cuda:{dev}")
+    streams = [torch.cuda.ExternalStream(e.stream(), device=f"cuda:{dev}") for e in exs]
+
+    def copy_counts(s_, e):
+        _lib.check(e.ctx, _lib.lib().orbgpu_memcpy_d2d_async(
+            e.ctx, C.c_void_p(counts_t.data_ptr() + 4 * s_ * Bps), C.c_void_p(W["counts"][s_]), Bps * 4), "d2d")
+
+    def after_gather(s_, e):
+        # the next step's copy into counts_t waits (on the GPU) for this step's all-gather, which reads it on the
+        # collective's stream: a stream wait, not a host synchronisation
+        streams[s_].wait_stream(torch.cuda.current_stream())
 
     def step():
-        W["step"]()
-        if dist is not None:  # north_star: all-gather of the per-frame keypoint counts over RCCL
-            for s_, dc in enumerate(W["counts"]):
-                _lib.check(exs[s_].ctx, _lib.lib().orbgpu_memcpy_d2d_async(
-                    exs[s_].ctx, C.c_void_p(counts_t.data_ptr() + 4 * s_ * Bps), C.c_void_p(dc), Bps * 4), "d2d")
-        for e in exs + W.get("sync_extra", []):  # every context's capacity-guard flags are read each step
-            e.synchronize()
-        if dist is not None:
-            allgather_counts(dist, counts_t, world)
+        multi_rank_step(W["step"], exs, dist, world, counts_t, copy_counts, after_gather)
 
     stage_acc = {}
     union_acc = {}  # stage -> total time with >= 1 launch of it running (union over the concurrent contexts)

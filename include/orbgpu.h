@@ -131,7 +131,10 @@ int orbgpu_batch_download(orbgpu_ctx* ctx, int b, orbgpu_keypoint* kps, uint8_t*
  * Tracking::MonocularInitialization (src/Tracking.cc:563-635) on one rank and broadcasts this record (RCCL)
  * to the others, which unpack it as frame 0 of a one-frame batch and match their frames against it
  * (SURVEY §8(e)).  Both calls are enqueued on the context stream; unpack requires a context planned for the
- * same image size and parameters, and records the event the matchers of other contexts wait for. */
+ * same image size and parameters, and records the event the matchers of other contexts wait for.  The record's
+ * 16-byte header holds the count, a magic word, frame_cap and the undistortion flag: unpack reads it back (a
+ * synchronising 16-byte read) and returns ORBGPU_ERR_ARG when it does not match the context's plan or the count
+ * exceeds frame_cap. */
 long long orbgpu_frame_record_bytes(const orbgpu_ctx* ctx);
 int orbgpu_frame_record_pack(orbgpu_ctx* ctx, int b, void* d_dst);
 int orbgpu_frame_record_unpack(orbgpu_ctx* ctx, const void* d_src);

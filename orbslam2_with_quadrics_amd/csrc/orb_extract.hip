@@ -14,6 +14,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstddef>
+#include <type_traits>
 
 #include "orb_math_dev.h"
 #include "orbgpu_internal.h"
@@ -438,14 +440,8 @@ __device__ __forceinline__ og_u16x2 og_as_u16x2(uint32_t x) { return __builtin_b
 #ifndef OG_FAST_SLOT_BARRIER
 #define OG_FAST_SLOT_BARRIER 0  // 1: no scheduling across stage 1's two slots
 #endif
-#ifndef OG_FAST_COLWALK
-#define OG_FAST_COLWALK 0  // 1: stage 1 as a column walk over a register window (measured slower)
-#endif
 #ifndef OG_FAST_F16
 #define OG_FAST_F16 1  // stage 1's quick test in packed f16 with the gfx950 3-input max/min (0: packed u16)
-#endif
-#ifndef FB_R
-#define FB_R 8  // detection rows per column-walk item; divides FB_MW (the window never leaves roi2)
 #endif
 
 // ------------------------------------------------------------------------------------------------
@@ -458,14 +454,12 @@ __device__ __forceinline__ og_u16x2 og_as_u16x2(uint32_t x) { return __builtin_b
 // ------------------------------------------------------------------------------------------------
 #define FB_NT 512
 #define FB_NW (FB_NT / 64)
-#define FB_S2 52                 // pair-ROI row stride in dwords (>= 40 + 6 + 3 misalignment, 4-dword multiple)
+#define FB_H 32                  // pair offset: roi2 dword (r, x) = ROI pixels (r, x) and (r, x + 32)
+#define FB_S2 52                 // pair-ROI row stride in dwords (>= 32 + 6 + 3 misalignment, 4-dword multiple)
 #define FB_ROWS 86               // ROI rows (detection <= 80 + 6)
-#define FB_MW 80                 // detection width/height capacity of a block (2 x 40 or 1 x 64)
+#define FB_MW 80                 // detection height capacity of a block (2 x 40 or 1 x 64); width <= 2 * FB_H
 #define FB_MSW (FB_MW + 3)       // score map stride: a zero gap column before, between and after the cells
 #define FB_MSZ ((FB_MSW * FB_MSW + 15) & ~15)  // 16-byte multiple: zeroed by 16-byte stores
-#if FB_MW % FB_R != 0 || FB_MW / FB_R > 16
-#error "FB_R must divide FB_MW into at most 16 segments"
-#endif
 
 // score-map index of detection pixel (i, j): one zero row/column separates the block's cells and surrounds
 // them, so a pixel's 8 neighbours outside its cell (or outside the detection area) read 0 without checks
@@ -473,13 +467,6 @@ __device__ __forceinline__ int og_ms_idx(int i, int j, int wC, int hC)
 {
     return (i + 1 + (i >= hC)) * FB_MSW + (j + 1 + (j >= wC));
 }
-
-// 1/H for the slot division of stage 1 (H = 4k <= 124), correctly rounded (compile-time IEEE division)
-__constant__ float og_fast_rcpH[32] = {
-    0.f,         1.f / 4.f,   1.f / 8.f,   1.f / 12.f,  1.f / 16.f,  1.f / 20.f,  1.f / 24.f,  1.f / 28.f,
-    1.f / 32.f,  1.f / 36.f,  1.f / 40.f,  1.f / 44.f,  1.f / 48.f,  1.f / 52.f,  1.f / 56.f,  1.f / 60.f,
-    1.f / 64.f,  1.f / 68.f,  1.f / 72.f,  1.f / 76.f,  1.f / 80.f,  1.f / 84.f,  1.f / 88.f,  1.f / 92.f,
-    1.f / 96.f,  1.f / 100.f, 1.f / 104.f, 1.f / 108.f, 1.f / 112.f, 1.f / 116.f, 1.f / 120.f, 1.f / 124.f};
 
 // The pair minima / maxima reduce as trees (depth 3 instead of a chain of 8): two slots' packed ops interleave
 // without hazard nops.
@@ -564,33 +551,47 @@ __device__ __forceinline__ uint32_t og_lds_addr(T* p)
     return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)p;
 }
 
-// block table reads through the constant address space: uniform, so scalar loads (through a generic pointer the
-// compiler cannot prove the table unclobbered by the kernel's own stores and falls back to vector loads)
-__device__ __forceinline__ OgCell og_fast_block(const OgCell* blocks, int b)
+// block table reads through the constant address space: uniform, so one scalar load (through a generic pointer
+// the compiler cannot prove the table unclobbered by the kernel's own stores and falls back to vector loads).  The
+// fields are taken from the 8 dwords with shifts (a bit_cast to the mixed-width struct costs ~50 scalar byte ops).
+typedef unsigned int og_u32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ og_u32x8 og_fast_block(const OgFastBlk* blocks, int b)
 {
-    static_assert(sizeof(OgCell) == 16, "OgCell is read as one dwordx4");
-    // whole 16-byte records: the scalar unit has no 16-bit loads, so per-field short reads would go to the VMEM path
+    static_assert(sizeof(OgFastBlk) == 32, "OgFastBlk is read as one dwordx8");
+    static_assert(offsetof(OgFastBlk, y0) == 8 && offsetof(OgFastBlk, rw) == 12 && offsetof(OgFastBlk, cand_off) == 16 &&
+                      offsetof(OgFastBlk, ox) == 24,
+                  "OgFastBlk field offsets");
 #if defined(__HIP_DEVICE_COMPILE__)
-    const uint4 r = ((const __attribute__((address_space(4))) uint4*)blocks)[b];
-    return __builtin_bit_cast(OgCell, r);
+    return ((const __attribute__((address_space(4))) og_u32x8*)blocks)[b];
 #else
-    return blocks[b];  // (host pass of the device function: never called)
+    og_u32x8 r;
+    __builtin_memcpy(&r, blocks + b, 32);  // (host pass of the device function: never called)
+    return r;
 #endif
 }
 
-// floor(a / d) for 0 <= a < 2^24 and a quotient below 2^20, with rd ~ 1/d (v_rcp accuracy): the float product is
-// within 2^-10 of a / d, so one remainder correction makes it exact.  A few VALU instead of the ~40 scalar
-// instructions of a 32-bit integer division.
-__device__ __forceinline__ int og_div_small(int a, int d, float rd)
+// Survivor stores of one stage-1 iteration: entry v_k to LDS byte address a_k from the lanes of m_k only.  One
+// exec save, then exec = saved & m_k around each store, one restore.
+__device__ __forceinline__ void og_ds_write_b16_x4(u64 m0, uint32_t a0, uint32_t v0, u64 m1, uint32_t a1, uint32_t v1,
+                                                   u64 m2, uint32_t a2, uint32_t v2, u64 m3, uint32_t a3, uint32_t v3)
 {
-    int q = (int)((float)a * rd);
-    const int r = a - q * d;
-    return q + (r >= d) - (r < 0);
+    u64 sv;
+    __asm__ volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_and_b64 exec, %0, %1\n\tds_write_b16 %2, %3\n\t"
+        "s_and_b64 exec, %0, %4\n\tds_write_b16 %5, %6\n\t"
+        "s_and_b64 exec, %0, %7\n\tds_write_b16 %8, %9\n\t"
+        "s_and_b64 exec, %0, %10\n\tds_write_b16 %11, %12\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(sv)
+        : "s"(m0), "v"(a0), "v"(v0), "s"(m1), "v"(a1), "v"(v1), "s"(m2), "v"(a2), "v"(v2), "s"(m3), "v"(a3), "v"(v3)
+        : "memory");
 }
 
 __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_fast_blocks_kernel(
-    OgPlan P, const OgCell* __restrict__ blocks, const uint8_t* __restrict__ img0, long long pitch0, long long fstride0,
-    const uint8_t* __restrict__ pyr, u64* __restrict__ cand, int* __restrict__ cand_count, int* __restrict__ status)
+    const OgFastBlk* __restrict__ blocks, const uint8_t* __restrict__ img0, long long pitch0, long long fstride0,
+    const uint8_t* __restrict__ pyr, long long pyr_per_frame, u64* __restrict__ cand, long long cand_per_frame,
+    int* __restrict__ cand_count, int nlevels, int thr, int* __restrict__ status)
 {
     __shared__ __attribute__((aligned(16))) uint32_t roi2[FB_ROWS * FB_S2];
     __shared__ __attribute__((aligned(16))) uint8_t Ms[FB_MSZ];
@@ -600,81 +601,81 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     __shared__ __attribute__((aligned(16))) int wk[FB_NW][8];  // per wave: kept at t1 per cell [0..3], at t2 [4..7]
     __shared__ int sh_base;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const unsigned nwg = gridDim.x * gridDim.y;
-    const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, nwg);
-    const int f = nwg < (1u << 24) ? og_div_small((int)lin, (int)gridDim.x, __builtin_amdgcn_rcpf((float)gridDim.x))
-                                   : (int)(lin / gridDim.x);
-    const OgCell cd = og_fast_block(blocks, (int)lin - f * (int)gridDim.x);
-    const int l = cd.level;
-    const OgLevel& L = P.lv[l];
-    const uint8_t* img;
-    long long pitch;
-    if (l == 0) {
-        img = img0 + (long long)f * fstride0;
-        pitch = pitch0;
-    } else {
-        img = pyr + (long long)f * P.pyr_per_frame + L.pyr_off;
-        pitch = L.pitch;
-    }
-    const int rw = cd.x1 - cd.x0, rh = cd.y1 - cd.y0;
+    // grid (blocks per frame, frames), dispatched in plan order (OgFastBlk)
+    const unsigned f = blockIdx.y;
+    const og_u32x8 bk = og_fast_block(blocks, (int)blockIdx.x);
+    const int l = (int)bk[2] >> 16;
+    if (l < 0) return;  // empty entry
+    const int rw = bk[3] & 255, rh = (bk[3] >> 8) & 255;
     const int dw = rw - 6, dh = rh - 6;
-    const int wC = L.wCell, hC = L.hCell;
-    if (dw <= 0 || dh <= 0) return;
+    const int wC = (bk[3] >> 16) & 255, hC = bk[3] >> 24;
+    const int cand_off = (int)bk[4], cand_cap = (int)bk[5];
+    const uint8_t* row0;
+    unsigned upitch;  // < 2^24 (checked on the host)
+    if (l == 0) {
+        upitch = (unsigned)pitch0 & (OG_MAX_PITCH - 1);
+        row0 = img0 + (unsigned long long)f * (unsigned long long)fstride0 +
+               (unsigned long long)((bk[2] & 0xffffu) * upitch) + bk[0];
+    } else {
+        upitch = bk[1];
+        row0 = pyr + (unsigned long long)f * (unsigned long long)pyr_per_frame + bk[0];
+    }
     // ---- ROI -> LDS as column pairs: roi2 dword (r, x) = ROI pixel (r, x) | ROI pixel (r, x + H) << 16, with
-    // H = the detection half-width rounded up to 4 (so both halves load from 4-byte aligned addresses).  The
-    // dwords are read from global memory first (all loads issued before the LDS stores), then split with
-    // v_perm into four pair dwords and stored as one 16-byte write.
-    const int H = (((dw + 1) >> 1) + 3) & 0x7c;  // <= 44 (dw <= FB_MW); the 7-bit mask keeps its products 24-bit
-    const uint8_t* row0 = img + (long long)cd.y0 * pitch + cd.x0;
-    const bool aligned_rows = ((pitch & 3) == 0);
+    // H = FB_H = 32 for every block (the host plans blocks of detection width <= 64), so a wave's 64 pair slots
+    // are two whole ROI rows and every stage-1 mask and address is a constant or a scalar.  The dwords are read
+    // from global memory first (all loads issued before the LDS stores), then split with v_perm into four pair
+    // dwords and stored as one 16-byte write.  The loads are unconditional (no exec branches): rows past the ROI
+    // re-read its last row, columns past it read image bytes to the right of the ROI (or the next row's first
+    // bytes: every ROI row has a row below it in the level), and both are masked to 0 / not stored.
+    constexpr int H = FB_H;
+    const bool aligned_rows = ((upitch & 3) == 0);
     const int mis = aligned_rows ? (int)((uintptr_t)row0 & 3) : 0;
     const uint32_t* T2 = roi2 + mis;                 // T2[r*FB_S2 + x] = pair (x, x + H) of ROI row r
-    {
+#ifndef OG_EXP_FAST_NOSTAGE
+#define OG_EXP_FAST_NOSTAGE 0  // timing experiments only: 1 = keep the previous block's stale ROI (results wrong)
+#endif
+    if (!OG_EXP_FAST_NOSTAGE) {
         const int nq = (H + 6 + mis + 3) >> 2;       // dword groups per row
         uint32_t blo[3], bhi[3];
         const int q = tid & 15;
+        const int x = 4 * q - mis;                   // ROI column of a lane's first byte
         // addresses: the block's uniform row base (SGPRs) plus a 32-bit per-lane offset, so the loads take the
         // saddr + voffset form and no lane does 64-bit address arithmetic
         const uint8_t* rbase = row0 - mis;
-        const unsigned upitch = (unsigned)pitch & (OG_MAX_PITCH - 1);  // < 2^24 (checked on the host)
         const unsigned mb = (unsigned)((uintptr_t)rbase & 3);  // odd pitch: the rows' misalignment base
         const uint8_t* abase = rbase - mb;                       // 4-byte aligned
+        const unsigned qq = 4u * (unsigned)min(q, nq - 1);
+#ifndef OG_FAST_STAGE_COND
+#define OG_FAST_STAGE_COND 0  // experiment switch: 1 = lanes outside the ROI issue no loads (exec-masked)
+#endif
 #pragma unroll
         for (int k = 0; k < 3; k++) {
-            const int r = (tid >> 4) + 32 * k;
-            blo[k] = 0u;
-            bhi[k] = 0u;
-            if (r < rh && q < nq) {
-                const unsigned off = (unsigned)r * upitch + 4u * (unsigned)q;
-                const int x = 4 * q - mis;          // ROI column of the dword's first byte
-                if (aligned_rows) {
-                    if (x < rw) blo[k] = *(const uint32_t*)(rbase + off);
-                    if (x + H < rw) bhi[k] = *(const uint32_t*)(rbase + off + (unsigned)H);
-                } else {
-                    // odd pitch: two aligned loads funnel-shifted by the row's offset.  Reads stay inside the
-                    // row: an ROI starts >= 16 px from the left edge, ends >= 13 px before the right one.
-                    if (x < rw) {
-                        const unsigned o = off + mb;
-                        const uint32_t* a = (const uint32_t*)(abase + (o & ~3u));
-                        blo[k] = __builtin_amdgcn_alignbyte(a[1], a[0], o & 3u);
-                    }
-                    if (x + H < rw) {
-                        const unsigned o = off + (unsigned)H + mb;
-                        const uint32_t* a = (const uint32_t*)(abase + (o & ~3u));
-                        bhi[k] = __builtin_amdgcn_alignbyte(a[1], a[0], o & 3u);
-                    }
-                }
+            const int r = min((tid >> 4) + 32 * k, rh - 1);
+            const unsigned off = (unsigned)r * upitch + qq;
+            blo[k] = bhi[k] = 0u;
+            if (OG_FAST_STAGE_COND && !((tid >> 4) + 32 * k < rh && q < nq)) continue;
+            if (aligned_rows) {  // block-uniform
+                blo[k] = *(const uint32_t*)(rbase + off);
+                bhi[k] = *(const uint32_t*)(rbase + off + (unsigned)H);
+            } else {
+                // odd pitch: two aligned loads funnel-shifted by the row's offset
+                const unsigned o = off + mb, o2 = o + (unsigned)H;
+                const uint32_t* a = (const uint32_t*)(abase + (o & ~3u));
+                const uint32_t* a2 = (const uint32_t*)(abase + (o2 & ~3u));
+                blo[k] = __builtin_amdgcn_alignbyte(a[1], a[0], o & 3u);
+                bhi[k] = __builtin_amdgcn_alignbyte(a2[1], a2[0], o2 & 3u);
             }
         }
 #pragma unroll
         for (int k = 0; k < 3; k++) {
             const int r = (tid >> 4) + 32 * k;
+            const uint32_t lo = x < rw ? blo[k] : 0u, hi = x + H < rw ? bhi[k] : 0u;
             if (r < rh && q < nq) {
                 uint4 o;
-                o.x = __builtin_amdgcn_perm(bhi[k], blo[k], 0x0c040c00u);
-                o.y = __builtin_amdgcn_perm(bhi[k], blo[k], 0x0c050c01u);
-                o.z = __builtin_amdgcn_perm(bhi[k], blo[k], 0x0c060c02u);
-                o.w = __builtin_amdgcn_perm(bhi[k], blo[k], 0x0c070c03u);
+                o.x = __builtin_amdgcn_perm(hi, lo, 0x0c040c00u);
+                o.y = __builtin_amdgcn_perm(hi, lo, 0x0c050c01u);
+                o.z = __builtin_amdgcn_perm(hi, lo, 0x0c060c02u);
+                o.w = __builtin_amdgcn_perm(hi, lo, 0x0c070c03u);
 #if OG_FAST_F16
                 o.x |= 0x64006400u;  // f16 1024 + pixel per half (og_fast_quick2v); the score differences cancel it
                 o.y |= 0x64006400u;
@@ -692,61 +693,53 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     if (roi2[tid] == 255u && roi2[tid + 1] == 254u) cand_count[0] = 1;
     return;
 #endif
-    const int t1 = min(max(P.iniTh, 0), 255), t2 = min(max(P.minTh, 0), 255);
+    const int t1 = thr & 255, t2 = (thr >> 8) & 255;  // clamped to [0, 255] on the host
     const int tq = min(t1, t2);
     const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
     const int tA = max(t1, 1), tB = max(t2, 1);
     const uint32_t a_ns = og_lds_addr(&sh_ns), a_lst = og_lds_addr(&lst[0]);
-    // ---- stage 1: quick test on every detection pixel, two per lane: pair slot p -> row i, column c (pixels
-    // (i, c) and (i, c + H)); wave w takes slots [64w, 64w + 64) + 512k, two slots per iteration.  Branch-free:
-    // slots past the area test the last pair (clamped) and are masked out of the survivor masks.  One LDS
-    // reservation per wave iteration appends the survivors to the block's flat list (stages 2-4 then spread the
-    // list evenly); the stores take the survivor masks as exec.
-    const float rH = og_fast_rcpH[(H >> 2) & 31], hH = 0.5f * rH;
-#if OG_FAST_COLWALK
-    // Column walk: item = (segment s of FB_R detection rows, pair column cc); the lanes of a wave run along the
-    // pair columns, so every window read is a row of consecutive dwords.  The item's (FB_R + 6) x 7 window of
-    // pair dwords sits in VGPRs and serves the FB_R quick tests of its column: 7 LDS reads per row instead of
-    // 17 per pixel pair, and one address per item.  Rows past dh read ROI rows the area does not cover (inside
-    // roi2: nseg * FB_R <= FB_MW) and are masked out.
+    // ---- stage 1: quick test on every detection pixel, two per lane.  Lane L of a wave holds pair column
+    // c = L & 31 of ROI pair row r0 + (L >> 5), i.e. pixels (i, c) and (i, c + 32); wave w takes the row pairs
+    // {2w, 2w + 1} + 16k, two row pairs (slots) per iteration.  Row and column validity are wave-uniform masks
+    // (scalar), addresses are a per-lane constant plus a scalar row offset.  Slots past the area re-test a
+    // clamped row and are masked out.  One LDS reservation per wave iteration appends the survivors to the
+    // block's flat list (stages 2-4 then spread the list evenly); the stores take the survivor masks as exec.
     {
-        const int nitem = ((dh + FB_R - 1) / FB_R) * H;
-        for (int it0 = wv * 64; it0 < nitem; it0 += FB_NT) {
-            const int it = it0 + lane;
-            const int itc = min(it, nitem - 1);
-            const int s = (int)__builtin_fmaf((float)itc, rH, hH) & 15;
-            const int cc = itc - s * H;
-            const int i0 = s * FB_R;
-            const uint32_t* q = &T2[i0 * FB_S2 + cc];  // window (r, x) = q[r * FB_S2 + x]: ROI row i0 + r, column cc + x
-            uint32_t win[FB_R + 6][7];
+        const int lrow = lane >> 5, lcol = lane & 31;
+        const uint32_t* Tl = &T2[(lrow + 3) * FB_S2 + (lcol + 3)];
+        const uint32_t e_lane = (uint32_t)((lrow << 7) | lcol);
+        // lanes whose column (lane & 31) is inside the detection width, for the low and the high pixel
+        const unsigned clo = dw >= 32 ? 0xffffffffu : ((1u << dw) - 1u);
+        const unsigned chi = dw >= 64 ? 0xffffffffu : (dw <= 32 ? 0u : ((1u << (dw - 32)) - 1u));
+        const u64 colLo = ((u64)clo << 32) | clo, colHi = ((u64)chi << 32) | chi;
+        // one iteration: pair rows r0, r0 + 1 (slot 0) and r0 + 16, r0 + 17 (slot 1); FULL: all four inside the area
+        auto iter = [&](auto full_tag, int r0) {
+            constexpr bool FULL = decltype(full_tag)::value;
+            uint2 r[2];
+            u64 m[4];
 #pragma unroll
-            for (int r = 0; r < FB_R + 6; r++)
+            for (int h = 0; h < 2; h++) {
+                const int rr = r0 + 2 * FB_NW * h;   // wave-uniform pair row of lanes 0-31
+                // (tail: rows past the area re-test row dh - 1 / dh and are masked out)
+                r[h] = og_fast_quick2(Tl + (FULL ? rr : min(rr, dh - 1)) * FB_S2, FB_S2, tt);
+                const uint32_t any = r[h].x | r[h].y;
+                if (FULL) {
+                    m[2 * h] = og_lanes_lo16_nz(any) & colLo;
+                    m[2 * h + 1] = og_lanes_gt((int)any, 0xffff) & colHi;
+                } else {
+                    const u64 rows = (rr < dh ? 0xffffffffull : 0ull) | (rr + 1 < dh ? 0xffffffff00000000ull : 0ull);
+                    m[2 * h] = og_lanes_lo16_nz(any) & rows & colLo;
+                    m[2 * h + 1] = og_lanes_gt((int)any, 0xffff) & rows & colHi;
+                }
+            }
+            int cnt[4], n = 0;
 #pragma unroll
-                for (int x = 0; x < 7; x++) win[r][x] = q[r * FB_S2 + x];  // unused entries are dead loads
-            const u64 lane_ok = og_lanes_lt(it, nitem);
-            const u64 ok_lo = lane_ok & og_lanes_lt(cc, dw), ok_hi = lane_ok & og_lanes_lt(cc, dw - H);
-            // the survivor masks are counted here and re-derived from the polarity codes at the stores (16 masks
-            // held across the reservation would spill SGPRs)
-            uint32_t pb[FB_R];
-            int n = 0;
-#pragma unroll
-            for (int k = 0; k < FB_R; k++) {
-#define W_(dy, dx) win[k + 3 + (dy)][3 + (dx)]
-                const uint32_t c[16] = {W_(3, 0),   W_(3, 1),   W_(2, 2),   W_(1, 3),  W_(0, 3),  W_(-1, 3),
-                                        W_(-2, 2),  W_(-3, 1),  W_(-3, 0),  W_(-3, -1), W_(-2, -2), W_(-1, -3),
-                                        W_(0, -3),  W_(1, -3),  W_(2, -2),  W_(3, -1)};
-                const uint2 rr = og_fast_quick2v(c, W_(0, 0), tt);
-#undef W_
-                const u64 rowok = og_lanes_lt(i0 + k, dh);
-                const uint32_t any = rr.x | rr.y;
-                n += __popcll(og_lanes_lo16_nz(any) & ok_lo & rowok) + __popcll(og_lanes_gt((int)any, 0xffff) & ok_hi & rowok);
-                // polarity code per half: bit 0 dark, bit 1 bright (lo pixel bits 0-1, hi pixel bits 16-17)
-                uint32_t d1, b1;
-                __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(rr.x), "s"(0x00010001u));
-                __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(rr.y), "s"(0x00010001u));
-                pb[k] = d1 | (b1 << 1);
+            for (int q = 0; q < 4; q++) {
+                cnt[q] = __popcll(m[q]);
+                n += cnt[q];
             }
             if (n) {
+                // one LDS reservation per wave iteration from lane 0 (exec = lane 0 only; no atomic-optimizer code)
                 uint32_t old;
                 u64 sv;
                 __asm__ volatile(
@@ -755,80 +748,34 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                     : "=&v"(old), "=&s"(sv)
                     : "v"(a_ns), "v"(n)
                     : "memory");
-                int b = __builtin_amdgcn_readfirstlane(old);
-                const uint32_t e0 = (uint32_t)((i0 << 7) | cc);
+                const uint32_t ab = a_lst + 2u * (uint32_t)__builtin_amdgcn_readfirstlane(old);
+                uint32_t a[4], v[4];
 #pragma unroll
-                for (int k = 0; k < FB_R; k++) {
-                    // entry (i << 7) | j with bits 14 = dark, 15 = bright; bits above 15 are not stored
-                    const uint32_t ek = e0 + (uint32_t)(k << 7);
-                    const uint32_t elo = (pb[k] << 14) | ek;
-                    const uint32_t ehi = (pb[k] >> 2) | (ek + (uint32_t)H);
-                    const u64 rowok = og_lanes_gt(dh - i0, k);
-                    const u64 mlo = og_lanes_lo16_nz(pb[k]) & ok_lo & rowok, mhi = og_lanes_gt((int)pb[k], 0xffff) & ok_hi & rowok;
-                    og_ds_write_b16_lanes(mlo, a_lst + 2u * (uint32_t)og_rank(mlo, b), elo);
-                    b += __popcll(mlo);
-                    og_ds_write_b16_lanes(mhi, a_lst + 2u * (uint32_t)og_rank(mhi, b), ehi);
-                    b += __popcll(mhi);
+                for (int h = 0; h < 2; h++) {
+                    // entry (i << 7) | j, bits 14 = dark, 15 = bright (halves of r.x / r.y nonzero, min(half, 1)
+                    // per half); only the low 16 bits are stored
+                    uint32_t d1, b1;
+                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r[h].x), "s"(0x00010001u));
+                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r[h].y), "s"(0x00020002u));
+                    const uint32_t pb = d1 | b1;
+                    const uint32_t base = e_lane + (uint32_t)((r0 + 2 * FB_NW * h) << 7);
+                    v[2 * h] = (pb << 14) | base;
+                    v[2 * h + 1] = (pb >> 2) | (base + (uint32_t)H);  // pb >> 2 holds only bits 14-15
                 }
+                // list slot of each survivor: the wave's reservation + the counts of the masks before + its rank
+                const uint32_t ab1 = ab + 2u * (uint32_t)cnt[0], ab2 = ab1 + 2u * (uint32_t)cnt[1],
+                               ab3 = ab2 + 2u * (uint32_t)cnt[2];
+                a[0] = ab + 2u * (uint32_t)og_rank(m[0]);
+                a[1] = ab1 + 2u * (uint32_t)og_rank(m[1]);
+                a[2] = ab2 + 2u * (uint32_t)og_rank(m[2]);
+                a[3] = ab3 + 2u * (uint32_t)og_rank(m[3]);
+                og_ds_write_b16_x4(m[0], a[0], v[0], m[1], a[1], v[1], m[2], a[2], v[2], m[3], a[3], v[3]);
             }
-        }
+        };
+        int r0 = 2 * __builtin_amdgcn_readfirstlane(wv);  // uniform
+        for (; r0 + 2 * FB_NW + 1 < dh; r0 += 4 * FB_NW) iter(std::true_type{}, r0);
+        if (r0 < dh) iter(std::false_type{}, r0);
     }
-#else
-    const int npair = (dw > 0 && dh > 0) ? dh * H : 0;
-    for (int p0 = wv * 64; p0 < npair; p0 += 2 * FB_NT) {
-        uint2 r[2];
-        int base[2];
-        u64 m[4];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int pp = p0 + h * FB_NT + lane;
-            const int pc = min(pp, npair - 1);  // slots past the area test the last pair, masked below
-            const int ii = (int)__builtin_fmaf((float)pc, rH, hH) & 127;
-            const int cc = pc - ii * H;
-            base[h] = (ii << 7) | cc;
-            r[h] = og_fast_quick2(&T2[(ii + 3) * FB_S2 + (cc + 3)], FB_S2, tt);
-            const u64 valid = og_lanes_lt(pp, npair);
-            const uint32_t any = r[h].x | r[h].y;
-            m[2 * h] = og_lanes_lo16_nz(any) & valid & og_lanes_lt(cc, dw);
-            m[2 * h + 1] = og_lanes_gt((int)any, 0xffff) & valid & og_lanes_lt(cc, dw - H);
-#if OG_FAST_SLOT_BARRIER
-            __builtin_amdgcn_sched_barrier(0);  // one slot's 17 reads in flight at a time
-#endif
-        }
-        int cnt[4], n = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            cnt[q] = __popcll(m[q]);
-            n += cnt[q];
-        }
-        if (n) {
-            // one LDS reservation per wave iteration from lane 0 (exec = lane 0 only; no atomic-optimizer code)
-            uint32_t old;
-            u64 sv;
-            __asm__ volatile(
-                "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_waitcnt lgkmcnt(0)\n\t"
-                "s_mov_b64 exec, %1"
-                : "=&v"(old), "=&s"(sv)
-                : "v"(a_ns), "v"(n)
-                : "memory");
-            int b = __builtin_amdgcn_readfirstlane(old);
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                // entry bits 14 = dark, 15 = bright (halves of r.x / r.y nonzero, min(half, 1) per half)
-                uint32_t d1, b1;
-                __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r[h].x), "s"(0x00010001u));
-                __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r[h].y), "s"(0x00010001u));
-                const uint32_t pb = d1 | (b1 << 1);
-                const uint32_t elo = ((pb << 14) & 0xc000u) | (uint32_t)base[h];
-                const uint32_t ehi = ((pb >> 2) & 0xc000u) | (uint32_t)(base[h] + H);
-                og_ds_write_b16_lanes(m[2 * h], a_lst + 2u * (uint32_t)og_rank(m[2 * h], b), elo);
-                b += cnt[2 * h];
-                og_ds_write_b16_lanes(m[2 * h + 1], a_lst + 2u * (uint32_t)og_rank(m[2 * h + 1], b), ehi);
-                b += cnt[2 * h + 1];
-            }
-        }
-    }
-#endif
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm list stores are not tracked by the compiler
     __syncthreads();
     const int ns = sh_ns;
@@ -919,15 +866,15 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         // ---- stage 4: one reservation per block; each wave writes its kept entries at its offset (the octree
         // orders candidates by position, not slot)
         if (tid == 0) {
-            const int b = atomicAdd(&cand_count[f * P.nlevels + l], total);
-            if (b + total > L.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
+            const int b = atomicAdd(&cand_count[f * nlevels + l], total);
+            if (b + total > cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
             sh_base = b;
         }
         __syncthreads();
         const int sb = sh_base;
-        if (sb + total <= L.cand_cap && kept != 0) {
-            u64* out = cand + (long long)f * P.cand_per_frame + L.cand_off + sb + before;
-            const int ox = cd.x0 - L.minB + 3, oy = cd.y0 - L.minB + 3;
+        if (sb + total <= cand_cap && kept != 0) {
+            u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(cand_off + sb + before);
+            const int ox = (int)(short)(bk[6] & 0xffffu), oy = (int)bk[6] >> 16;
             int run = 0;
             for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
                 const int e = e0 + lane;
@@ -1961,7 +1908,11 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     __shared__ __attribute__((aligned(16))) uint32_t hp[DK_WAVES][HP_ROWS * HP_S];
     // w is wave-uniform: made explicit, so the keypoint index, its level and its window origin live in SGPRs
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const unsigned lin = og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+#ifndef OG_DESC_XCD_REMAP
+#define OG_DESC_XCD_REMAP 1  // experiment switch: 0 = plain dispatch order
+#endif
+    const unsigned lin = OG_DESC_XCD_REMAP ? og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y)
+                                           : blockIdx.y * gridDim.x + blockIdx.x;
     const int f = (int)(lin / gridDim.x);
     const int g = (int)(lin % gridDim.x) * DK_WAVES + w;
     // which level does keypoint g belong to (levels concatenated 0..L-1, :1076-1104)
@@ -2388,13 +2339,14 @@ void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, l
                            pitchA, dstB, pitchB, dst_fstride, g, status);
 }
 
-void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, int nblocks, const uint8_t* img0,
+void og_launch_fast(hipStream_t s, const OgPlan& P, const OgFastBlk* blocks, int nblocks, const uint8_t* img0,
                     long long pitch0, long long fstride0, const uint8_t* pyr, u64* cand, int* cand_count, int* status,
                     int B)
 {
     if (nblocks <= 0 || B <= 0) return;
-    hipLaunchKernelGGL(og_fast_blocks_kernel, dim3(nblocks, B), dim3(FB_NT), 0, s, P, cells, img0, pitch0,
-                       fstride0, pyr, cand, cand_count, status);
+    const int thr = std::min(std::max(P.iniTh, 0), 255) | (std::min(std::max(P.minTh, 0), 255) << 8);
+    hipLaunchKernelGGL(og_fast_blocks_kernel, dim3(nblocks, B), dim3(FB_NT), 0, s, blocks, img0, pitch0, fstride0, pyr,
+                       P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels, thr, status);
 }
 
 void og_launch_octree(hipStream_t s, const OgPlan& P, const u64* cand, const int* cand_count, uint16_t* node_of,

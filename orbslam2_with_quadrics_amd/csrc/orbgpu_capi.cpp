@@ -46,6 +46,7 @@ struct orbgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    uint32_t rec_hdr[3] = {0, 0, 0};  // frame-record header staged for orbgpu_frame_record_pack's async copy
     // ORBextractor parameters and scale tables (src/ORBextractor.cc:410-470)
     int nfeatures = 0, nlevels = 0, iniTh = 0, minTh = 0;
     int sem = ORBGPU_SEM_DEFAULT;  // OpenCV/compiler semantics (orbgpu_set_semantics)
@@ -59,7 +60,7 @@ struct orbgpu_ctx {
     OgPlan plan{};
     std::vector<OgCell> cells_h;
     std::vector<int4> xtab_h, ytab_h;
-    DevBuf<OgCell> cells;
+    DevBuf<OgFastBlk> cells;  // the FAST kernel's block table
     DevBuf<int4> tabs;
     // batch buffers
     int Bcap = 0;
@@ -256,10 +257,11 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
                 c->err = "FAST cells do not form a rectangle";
                 return ORBGPU_ERR_INTERNAL;
             }
-            const int bs = (L.wCell <= 40 && L.hCell <= 40) ? 2 : 1;
-            for (int bi = 0; bi < nr; bi += bs)
-                for (int bj = 0; bj < ncl; bj += bs) {
-                    const int ni = std::min(bs, nr - bi), nj = std::min(bs, ncl - bj);
+            // the kernel's pair layout holds detection widths <= 2 * 32 and heights <= 80 (FB_H, FB_MW)
+            const int bsj = (2 * L.wCell <= 64) ? 2 : 1, bsi = (L.hCell <= 40) ? 2 : 1;
+            for (int bi = 0; bi < nr; bi += bsi)
+                for (int bj = 0; bj < ncl; bj += bsj) {
+                    const int ni = std::min(bsi, nr - bi), nj = std::min(bsj, ncl - bj);
                     const OgCell& a = lc[bi * ncl + bj];
                     const OgCell& right = lc[bi * ncl + bj + nj - 1];
                     const OgCell& below = lc[(bi + ni - 1) * ncl + bj];
@@ -267,6 +269,10 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
                     blk.pad = (short)((ni << 8) | nj);
                     blk.x1 = right.x1;
                     blk.y1 = below.y1;
+                    if (blk.x1 - blk.x0 - 6 > 64 || blk.y1 - blk.y0 - 6 > 80) {
+                        c->err = "FAST block larger than the kernel's LDS tile";
+                        return ORBGPU_ERR_INTERNAL;
+                    }
                     cells.push_back(blk);
                 }
         }
@@ -386,14 +392,51 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
         return ORBGPU_ERR_UNSUPPORTED;
     }
     P.total_cells = (int)cells.size();
+    // the FAST kernel's block table (OgFastBlk), in plan order: level-major, row-major blocks.  Hardware dispatch
+    // deals consecutive workgroups round-robin over the 8 XCDs; measured against giving every XCD a contiguous
+    // eighth of each frame (or whole frames, round 2's remap), plain order is 7-9 % faster
+    // (profiles/sweeps/r03_ab_fast_block_order.txt)
+    std::vector<OgFastBlk> fblk;
+    {
+        const int n = P.total_cells;
+        fblk.resize(n);
+        for (int p = 0; p < n; p++) {
+            OgFastBlk& r = fblk[p];
+            std::memset(&r, 0, sizeof(r));
+            const OgCell& cd = cells[p];
+            const OgLevel& L = P.lv[cd.level];
+            const int rw = cd.x1 - cd.x0, rh = cd.y1 - cd.y0;
+            if (rw - 6 > 64 || rh - 6 > 80 || rw < 7 || rh < 7 || L.wCell > 255 || L.hCell > 255) {
+                c->err = "FAST block outside the kernel's LDS tile";
+                return ORBGPU_ERR_INTERNAL;
+            }
+            r.lev = cd.level;
+            r.y0 = cd.y0;
+            r.pitch = cd.level == 0 ? 0 : L.pitch;
+            r.src_off = cd.level == 0 ? cd.x0 : (int)(L.pyr_off + (long long)cd.y0 * L.pitch + cd.x0);
+            r.rw = (unsigned char)rw;
+            r.rh = (unsigned char)rh;
+            r.wC = (unsigned char)L.wCell;
+            r.hC = (unsigned char)L.hCell;
+            r.cand_off = (int)L.cand_off;
+            r.cand_cap = L.cand_cap;
+            r.ox = (short)(cd.x0 - L.minB + 3);
+            r.oy = (short)(cd.y0 - L.minB + 3);
+        }
+        P.fast_blocks = n;
+        if (cand_off >= (1LL << 31) || std::max<long long>(pyr_off, 256) >= (1LL << 31)) {
+            c->err = "per-frame candidate or pyramid block of 2^31 or more";
+            return ORBGPU_ERR_UNSUPPORTED;
+        }
+    }
     P.kcap_total = koff;
     P.frame_cap = koff;
     P.cand_per_frame = cand_off;
     P.pyr_per_frame = std::max<long long>(pyr_off, 256);
     HIP_TRY(c, hipSetDevice(c->device));
-    HIP_TRY(c, ensure(c->cells, cells.size()));
+    HIP_TRY(c, ensure(c->cells, fblk.size()));
     HIP_TRY(c, ensure(c->tabs, tabs.size()));
-    HIP_TRY(c, hipMemcpyAsync(c->cells.p, cells.data(), cells.size() * sizeof(OgCell), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->cells.p, fblk.data(), fblk.size() * sizeof(OgFastBlk), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->tabs.p, tabs.data(), tabs.size() * sizeof(int4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     c->plan = P;
@@ -523,7 +566,7 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
         }
     }
     timer_mark(c, "pyramid");
-    og_launch_fast(s, P, c->cells.p, P.total_cells, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p, c->status.p, B);
+    og_launch_fast(s, P, c->cells.p, P.fast_blocks, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p, c->status.p, B);
     timer_mark(c, "fast");
     og_launch_octree(s, P, c->cand.p, c->cand_count.p, c->node_of.p, c->oct_xy.p, c->oct_resp.p, c->oct_count.p,
                      c->status.p, B);
@@ -808,6 +851,11 @@ int orbgpu_frame_record_pack(orbgpu_ctx* c, int b, void* d_dst)
     uint8_t* d = (uint8_t*)d_dst;
     hipStream_t s = c->stream;
     HIP_TRY(c, hipMemcpyAsync(d, c->counts.p + b, 4, hipMemcpyDeviceToDevice, s));
+    // header words 1-3: magic, frame_cap, undistortion flag -- unpack checks them against the receiving context
+    c->rec_hdr[0] = 0x5246474fu;  // "OGFR"
+    c->rec_hdr[1] = (uint32_t)c->plan.frame_cap;
+    c->rec_hdr[2] = c->undist ? 1u : 0u;
+    HIP_TRY(c, hipMemcpyAsync(d + 4, c->rec_hdr, 12, hipMemcpyHostToDevice, s));
     HIP_TRY(c, hipMemcpyAsync(d + 16, c->kps.p + o, cap * 28, hipMemcpyDeviceToDevice, s));
     HIP_TRY(c, hipMemcpyAsync(d + 16 + cap * 28, c->desc.p + o * 32, cap * 32, hipMemcpyDeviceToDevice, s));
     if (c->undist)
@@ -824,6 +872,17 @@ int orbgpu_frame_record_unpack(orbgpu_ctx* c, const void* d_src)
     const size_t cap = (size_t)c->plan.frame_cap;
     const uint8_t* d = (const uint8_t*)d_src;
     hipStream_t s = c->stream;
+    // the header must describe this context's plan (frame_cap, undistortion) and a count within it; a record from
+    // a differently planned context would otherwise be misread, and a larger count would send the matchers past
+    // the frame
+    uint32_t hdr[4];
+    HIP_TRY(c, hipMemcpyAsync(hdr, d, 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if (hdr[1] != 0x5246474fu || hdr[2] != (uint32_t)c->plan.frame_cap || hdr[3] != (c->undist ? 1u : 0u) ||
+        (int)hdr[0] < 0 || (int)hdr[0] > c->plan.frame_cap) {
+        c->err = "frame record does not match this context's plan (frame_cap / undistortion) or has a bad count";
+        return ORBGPU_ERR_ARG;
+    }
     HIP_TRY(c, hipMemcpyAsync(c->counts.p, d, 4, hipMemcpyDeviceToDevice, s));
     HIP_TRY(c, hipMemcpyAsync(c->kps.p, d + 16, cap * 28, hipMemcpyDeviceToDevice, s));
     HIP_TRY(c, hipMemcpyAsync(c->desc.p, d + 16 + cap * 28, cap * 32, hipMemcpyDeviceToDevice, s));

@@ -60,12 +60,28 @@ struct OgCell {            // one FAST block of up to 2x2 cells (ROI union), src
     short x0, y0, x1, y1;  // ROI [x0,x1) x [y0,y1) in level pixels
 };
 
+// One FAST block as the kernel reads it (og_fast_blocks_kernel): everything it needs from the block, its level and
+// the plan, precomputed on the host and read with one 32-byte scalar load (no per-wave level-table lookups).
+struct OgFastBlk {
+    int src_off;           // levels >= 1: byte offset of ROI pixel (0, 0) inside the frame's pyramid block;
+                           // level 0: the ROI's first column (the row term y0 * pitch0 is added at run time)
+    int pitch;             // row pitch of the level (levels >= 1); 0 for level 0 (the caller's pitch)
+    short y0, lev;         // ROI first row (level 0's row term), pyramid level (< 0: empty entry, skipped)
+    unsigned char rw, rh;  // ROI size (detection area + 6): rw - 6 <= 64, rh - 6 <= 80
+    unsigned char wC, hC;  // FAST cell size of the level
+    int cand_off;          // the level's candidate slots inside a frame (entries)
+    int cand_cap;          // ... and their number (the exact NMS bound)
+    short ox, oy;          // candidate coordinates of detection pixel (0, 0): x0 - minB + 3, y0 - minB + 3
+    int pad;
+};
+
 struct OgPlan {
     int nlevels;
     int sem;               // ORBGPU_SEM_* of the context (include/orbgpu.h)
     int oct_big;           // levels 0 .. oct_big-1 run the OG_OCT_MAXL_BIG octree kernel (their lists may exceed OG_OCT_MAXL)
     int iniTh, minTh;
     int total_cells;
+    int fast_blocks;       // entries of the OgFastBlk table per frame
     int kcap_total;        // sum of kcap (octree slots per frame)
     int frame_cap;         // final keypoints per frame (== kcap_total)
     long long cand_per_frame;

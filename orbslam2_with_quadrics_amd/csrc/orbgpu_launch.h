@@ -52,7 +52,7 @@ hipError_t og_prepare_device();  // per-device kernel attributes (call after hip
 hipError_t og_prepare_device_match();  // (called by og_prepare_device)
 hipError_t og_prepare_device_bow();
 // nblocks entries of the block table from `cells` on, for each of B frames
-void og_launch_fast(hipStream_t s, const OgPlan& P, const OgCell* cells, int nblocks, const uint8_t* img0,
+void og_launch_fast(hipStream_t s, const OgPlan& P, const OgFastBlk* blocks, int nblocks, const uint8_t* img0,
                     long long pitch0, long long fstride0, const uint8_t* pyr, unsigned long long* cand, int* cand_count,
                     int* status, int B);
 hipError_t og_read_oct_prof(unsigned long long* out, int n);  // OG_OCT_PROFILE builds only

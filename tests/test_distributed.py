@@ -123,6 +123,121 @@ def test_gloo_world2_shared_initial_frame_split_and_gather():
     assert m0 == m1                              # rank 1 holds rank 0's local map (it built a different one)
 
 
+def _worker_steady(rank, world, port, q):
+    """The real bench.multi_rank_step over 5 steady-state steps with stub contexts: count the host synchronisations
+    and the collectives each step issues."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as tdist
+
+    import bench
+
+    w, r, _ = bench.dist_env()
+    dist = bench.dist_init(w, "gloo")
+    calls = {"broadcast": 0, "all_gather": 0, "sync": 0, "after": 0, "work": 0}
+
+    class Dist:  # torch.distributed with the collectives counted
+        def __getattr__(self, name):
+            return getattr(tdist, name)
+
+        def broadcast(self, *a, **k):
+            calls["broadcast"] += 1
+            return tdist.broadcast(*a, **k)
+
+        def all_gather_into_tensor(self, *a, **k):
+            calls["all_gather"] += 1
+            return tdist.all_gather_into_tensor(*a, **k)
+
+    class Ctx:
+        def synchronize(self):
+            calls["sync"] += 1
+
+    exs = [Ctx(), Ctx()]
+    per = 3  # frames per context
+    counts = torch.zeros(len(exs) * per, dtype=torch.int32)
+    src = {}
+
+    def work():
+        calls["work"] += 1
+        for s_ in range(len(exs)):
+            src[s_] = torch.arange(per, dtype=torch.int32) + 1000 * r + 100 * s_ + 10 * calls["work"]
+
+    def copy_counts(s_, e):
+        counts[s_ * per:(s_ + 1) * per] = src[s_]
+
+    def after(s_, e):
+        calls["after"] += 1
+
+    per_step, gathered = [], []
+    D = Dist()
+    for _ in range(5):
+        before = dict(calls)
+        bench.multi_rank_step(work, exs, D, w, counts, copy_counts, after)
+        per_step.append({k: calls[k] - before[k] for k in calls})
+        gathered.append(bench.allgather_counts(D, counts, w).tolist())
+    q.put((r, per_step, gathered))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_steady_step_has_one_host_sync_and_no_broadcast():
+    """Verdict r02 item 3: the N > 1 step adds no host synchronisation and no broadcast beyond N = 1's per-step
+    context synchronisation; its only collective is the keypoint-count all-gather (the shared initial frame and the
+    local map are broadcast once, at set-up)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_steady, args=(r, 2, port, q)) for r in range(2)]
+    [p.start() for p in ps]
+    res = sorted(q.get(timeout=180) for _ in range(2))
+    [p.join(timeout=60) for p in ps]
+    for r, per_step, gathered in res:
+        for k, d in enumerate(per_step):
+            assert d == {"broadcast": 0, "all_gather": 1, "sync": 2, "after": 2, "work": 1}, (r, k, d)
+        for k, g in enumerate(gathered):
+            step = k + 1
+            want = [1000 * rr + 100 * s_ + 10 * step + i for rr in range(2) for s_ in range(2) for i in range(3)]
+            assert g == want
+
+
+def test_single_rank_step_is_collective_free():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    n = {"sync": 0, "copy": 0, "work": 0}
+
+    class Ctx:
+        def synchronize(self):
+            n["sync"] += 1
+
+    bench.multi_rank_step(lambda: n.__setitem__("work", n["work"] + 1), [Ctx(), Ctx()], None, 1, None,
+                          lambda s, e: n.__setitem__("copy", n["copy"] + 1), None)
+    assert n == {"sync": 2, "copy": 0, "work": 1}
+
+
+def test_map_record_fields_are_16_byte_aligned():
+    """every local-map field starts on a 16-byte boundary for any point count."""
+    sys.path.insert(0, ROOT)
+    import numpy as np
+
+    import bench
+
+    for M in (1, 3, 5, 4999, 5000, 5001):
+        offs = bench.map_offsets(M)
+        assert all(o % 16 == 0 for o in offs.values())
+        mp = dict(pos=np.arange(3 * M, dtype=np.float32).reshape(M, 3), normal=np.ones((M, 3), np.float32),
+                  max_dist=np.full(M, 2, np.float32), min_dist=np.full(M, 1, np.float32),
+                  is_bad=np.zeros(M, np.uint8), n_obs=np.arange(M, dtype=np.int32),
+                  desc=np.full((M, 32), 7, np.uint8))
+        rec = bench.pack_map(mp)
+        assert len(rec) == offs["_end"]
+        assert np.array_equal(rec[offs["n_obs"]:offs["n_obs"] + 4 * M].view(np.int32), mp["n_obs"])
+        assert np.array_equal(rec[offs["pos"]:offs["pos"] + 12 * M].view(np.float32), mp["pos"].reshape(-1))
+
+
 def test_shard_range_partitions():
     sys.path.insert(0, ROOT)
     import bench

@@ -1,0 +1,42 @@
+"""Frame records (orbgpu_frame_record_pack / _unpack, the unit bench.py broadcasts from rank 0 to the other ranks
+at set-up): a record unpacked into a second context reproduces the frame exactly, and a record
+that does not fit the receiving context's plan (frame_cap, undistortion) or carries a count above frame_cap is
+refused with ORBGPU_ERR_ARG."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_record_round_trip_and_plan_checks(gpu):
+    import torch
+
+    from orbslam2_with_quadrics_amd import _lib, synthetic
+
+    L = _lib.lib()
+    f1, _ = synthetic.frame_pair(31, 480, 640)
+    a = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    b = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    other = gpu.ORBextractor(1500, 1.2, 8, 20, 7)  # different per-frame capacity
+    ka, da = a(f1)
+    b(np.roll(f1, 5, axis=1))  # plans b for the same image size, with other contents
+    other(f1)
+    nbytes = int(L.orbgpu_frame_record_bytes(a.ctx))
+    assert nbytes == int(L.orbgpu_frame_record_bytes(b.ctx))
+    rec = torch.zeros(nbytes, dtype=torch.uint8, device="cuda:0")
+    _lib.check(a.ctx, L.orbgpu_frame_record_pack(a.ctx, 0, C.c_void_p(rec.data_ptr())), "pack")
+    a.synchronize()
+    _lib.check(b.ctx, L.orbgpu_frame_record_unpack(b.ctx, C.c_void_p(rec.data_ptr())), "unpack")
+    b.synchronize()
+    kb, db = b.batch_download(0)
+    assert kb.tobytes() == ka.tobytes() and np.array_equal(db, da)
+    # a context planned for another frame_cap refuses the record
+    assert L.orbgpu_frame_record_unpack(other.ctx, C.c_void_p(rec.data_ptr())) == _lib.ERR_ARG
+    # a count above frame_cap is refused
+    bad = rec.clone()
+    bad[:4] = torch.tensor([0x7fffffff], dtype=torch.int32).view(torch.uint8).to("cuda:0")
+    assert L.orbgpu_frame_record_unpack(b.ctx, C.c_void_p(bad.data_ptr())) == _lib.ERR_ARG
+    # a buffer that is not a record (no magic word) is refused
+    assert L.orbgpu_frame_record_unpack(b.ctx, C.c_void_p(torch.zeros_like(rec).data_ptr())) == _lib.ERR_ARG

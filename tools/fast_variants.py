@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VDIR = os.path.join(ROOT, "orbslam2_with_quadrics_amd", "variants")
 VARIANTS = {"full": [], "stop_roi": ["OG_EXP_FAST_STOP=1"], "stop_quick": ["OG_EXP_FAST_STOP=2"],
-            "stop_count": ["OG_EXP_FAST_STOP=3"]}
+            "stop_count": ["OG_EXP_FAST_STOP=3"], "nostage": ["OG_EXP_FAST_NOSTAGE=1"]}
 EXTRA = json.loads(os.environ.get("FAST_VARIANTS_EXTRA", "{}"))
 VARIANTS.update(EXTRA)
 
