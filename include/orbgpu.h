@@ -339,6 +339,16 @@ int orbgpu_search_by_projection_keyframe(orbgpu_ctx* ctx, const orbgpu_frame_vie
                                          const orbgpu_keyframe_view* KF, float th, int ORBdist, int checkOri,
                                          int32_t* owner, int* nmatches);
 
+/* The same matcher with the scale test done by the caller: pred_level[i] (KF.n ints) is
+ * pMP->PredictScale(dist3D, &CurrentFrame) when GetMinDistanceInvariance() <= dist3D <=
+ * GetMaxDistanceInvariance() and -1 otherwise (src/ORBmatcher.cc:1513-1523), computed by the binding with the
+ * reference's own MapPoint methods -- mfMaxDistance / mfMinDistance are protected (include/MapPoint.h:141-142), so
+ * a drop-in binding cannot snapshot them.  KF.max_dist / KF.min_dist are not read (may be NULL); everything else
+ * is as orbgpu_search_by_projection_keyframe. */
+int orbgpu_search_by_projection_keyframe_levels(orbgpu_ctx* ctx, const orbgpu_frame_view* F, const orbgpu_camera* cur,
+                                                const orbgpu_keyframe_view* KF, const int32_t* pred_level, float th,
+                                                int ORBdist, int checkOri, int32_t* owner, int* nmatches);
+
 /* ---- stereo ------------------------------------------------------------------------------------- */
 
 /* Replaces void Frame::ComputeStereoMatches() -- src/Frame.cc:466-640, called from the stereo Frame

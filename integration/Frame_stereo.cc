@@ -8,6 +8,9 @@
 #include "orbgpu.h"
 #include "orbgpu_binding.h"
 
+// marks this replacement as linked: integration/ORBextractor.cc then skips the host pyramid download
+extern "C" const int orbgpu_binding_device_stereo = 1;
+
 namespace ORB_SLAM2 {
 
 void Frame::ComputeStereoMatches()

@@ -6,6 +6,7 @@
 // private helpers (ComputePyramid, ComputeKeyPointsOctTree, DistributeOctTree, DivideNode) stay declared and
 // are no longer defined or called -- the whole of operator() runs on the GPU (src/ORBextractor.cc:1043-1105).
 #include <cassert>
+#include <cstdlib>
 #include <mutex>
 #include <stdexcept>
 #include <unordered_map>
@@ -18,12 +19,33 @@ namespace ORB_SLAM2 {
 
 static_assert(sizeof(cv::KeyPoint) == sizeof(orbgpu_keypoint), "cv::KeyPoint layout");
 
+// Linked from integration/Frame_stereo.cc when that replacement is part of the build: ComputeStereoMatches then reads
+// both pyramids in device memory and nothing else in ORB-SLAM2 reads mvImagePyramid (src/Frame.cc:473,563,575,580).
+extern "C" __attribute__((weak)) const int orbgpu_binding_device_stereo;
+
 namespace {
+struct Entry {
+    orbgpu_ctx* ctx;
+    bool host_pyramid;  // refresh mvImagePyramid after each call
+};
 std::mutex g_mu;
-std::unordered_map<const ORBextractor*, orbgpu_ctx*>& contexts()
+std::unordered_map<const ORBextractor*, Entry>& contexts()
 {
-    static std::unordered_map<const ORBextractor*, orbgpu_ctx*> m;
+    static std::unordered_map<const ORBextractor*, Entry> m;
     return m;
+}
+
+int env_int(const char* name, int dflt)
+{
+    const char* v = std::getenv(name);
+    return v && *v ? std::atoi(v) : dflt;
+}
+
+// Default for new extractors: download the pyramid only if something may read it -- i.e. unless the device stereo
+// matcher is linked; ORBGPU_HOST_PYRAMID=0/1 overrides (about 3 MB per 1080p frame over PCIe when on)
+bool default_host_pyramid()
+{
+    return env_int("ORBGPU_HOST_PYRAMID", &orbgpu_binding_device_stereo == nullptr ? 1 : 0) != 0;
 }
 }  // namespace
 
@@ -31,7 +53,23 @@ orbgpu_ctx* orbgpu_context_of(const ORBextractor* ex)
 {
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = contexts().find(ex);
-    return it == contexts().end() ? nullptr : it->second;
+    return it == contexts().end() ? nullptr : it->second.ctx;
+}
+
+void orbgpu_release_extractor(const ORBextractor* ex)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = contexts().find(ex);
+    if (it == contexts().end()) return;
+    orbgpu_destroy(it->second.ctx);
+    contexts().erase(it);
+}
+
+void orbgpu_set_host_pyramid(const ORBextractor* ex, bool on)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = contexts().find(ex);
+    if (it != contexts().end()) it->second.host_pyramid = on;
 }
 
 // src/ORBextractor.cc:410-470: the scale tables and per-level budgets come from the context (same arithmetic)
@@ -39,11 +77,18 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
     : nfeatures(_nfeatures), scaleFactor(_scaleFactor), nlevels(_nlevels), iniThFAST(_iniThFAST),
       minThFAST(_minThFAST)
 {
-    orbgpu_ctx* ctx = orbgpu_create(/*device*/ 0, nfeatures, _scaleFactor, nlevels, iniThFAST, minThFAST);
+    // device: ORBGPU_DEVICE (default 0), e.g. one SLAM process per GPU
+    orbgpu_ctx* ctx = orbgpu_create(env_int("ORBGPU_DEVICE", 0), nfeatures, _scaleFactor, nlevels, iniThFAST,
+                                    minThFAST);
     if (!ctx) throw std::runtime_error("orbgpu_create failed (no gfx950 device, or invalid parameters)");
     {
+        // the reference header's inline ~ORBextractor() cannot release the context: an extractor constructed at
+        // the address of a deleted one takes over the slot, and the old context is destroyed here
+        // (orbgpu_release_extractor releases one explicitly)
         std::lock_guard<std::mutex> lk(g_mu);
-        contexts()[this] = ctx;
+        auto it = contexts().find(this);
+        if (it != contexts().end()) orbgpu_destroy(it->second.ctx);
+        contexts()[this] = Entry{ctx, default_host_pyramid()};
     }
     mvScaleFactor.resize(nlevels);
     mvInvScaleFactor.resize(nlevels);
@@ -86,9 +131,14 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray _mask, std::
     } else {
         desc.rowRange(0, n).copyTo(_descriptors);
     }
-    // the public mvImagePyramid (include/ORBextractor.h:85), read by Frame::ComputeStereoMatches
-    // (src/Frame.cc:473,563,575,580); with integration/Frame_stereo.cc the stereo matcher reads the device pyramids
-    // and this download can go
+    // the public mvImagePyramid (include/ORBextractor.h:85), read only by Frame::ComputeStereoMatches
+    // (src/Frame.cc:473,563,575,580): downloaded when that reader may run on the CPU (default_host_pyramid)
+    bool host_pyramid;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        host_pyramid = contexts()[this].host_pyramid;
+    }
+    if (!host_pyramid) return;
     for (int l = 0; l < nlevels; ++l) {
         int w = 0, h = 0;
         orbgpu_get_level(ctx, l, nullptr, 0, &w, &h);

@@ -1,11 +1,12 @@
 // integration/ORBmatcher_perframe.cc -- the per-frame ORBmatcher methods on the gfx950 path.
 //
 // A maintainer deletes these bodies from the reference's src/ORBmatcher.cc and adds this file; the keyframe-rate
-// overloads (SearchByBoW, SearchByProjection(pKF, Scw, ..), SearchForTriangulation, SearchBySim3, Fuse) and the
-// relocalisation SearchByProjection(F, pKF, ..) keep their CPU bodies there.  Signatures are the reference's
+// overloads (SearchByBoW, SearchByProjection(pKF, Scw, ..), SearchForTriangulation, SearchBySim3, Fuse) keep their
+// CPU bodies there.  Signatures are the reference's
 // (include/ORBmatcher.h:40-69); tests/test_integration_compile.py compiles this file against the restated
 // declarations of integration/refdecl (checked line by line against the reference headers).
 #include <cstdint>
+#include <set>
 #include <stdexcept>
 #include <vector>
 
@@ -150,6 +151,52 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
         throw std::runtime_error("orbgpu_search_by_projection_last_frame");
     for (int i = 0; i < CurrentFrame.N; ++i)
         if (owner[i] >= 0 && owner[i] < L) CurrentFrame.mvpMapPoints[i] = LastFrame.mvpMapPoints[owner[i]];
+    return nmatches;
+}
+
+// src/ORBmatcher.cc:1472-1599, called from Tracking::Relocalization (src/Tracking.cc:1433,1467).  mfMaxDistance /
+// mfMinDistance are protected (include/MapPoint.h:141-142), so the scale gate runs here with the point's own public
+// methods -- GetMin/MaxDistanceInvariance and PredictScale on dist3D = cv::norm(x3Dw - Ow), exactly the reference's
+// :1477-1523 -- and the projection, window search, claims and rotation histogram run on the GPU
+// (orbgpu_search_by_projection_keyframe_levels).
+int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std::set<MapPoint*>& sAlreadyFound,
+                                   const float th, const int ORBdist)
+{
+    const cv::Mat Rcw = CurrentFrame.mTcw.rowRange(0, 3).colRange(0, 3);
+    const cv::Mat tcw = CurrentFrame.mTcw.rowRange(0, 3).col(3);
+    const cv::Mat Ow = -Rcw.t() * tcw;
+    const std::vector<MapPoint*> vpMPs = pKF->GetMapPointMatches();
+    const int L = (int)vpMPs.size();
+    std::vector<uint8_t> valid(L, 0), desc(32 * (size_t)L, 0);
+    std::vector<float> pos(3 * (size_t)L, 0.f);
+    std::vector<int32_t> level(L, -1), owner(CurrentFrame.N, -1);
+    for (int i = 0; i < L; ++i) {
+        MapPoint* pMP = vpMPs[i];
+        if (!pMP || pMP->isBad() || sAlreadyFound.count(pMP)) continue;
+        valid[i] = 1;
+        const cv::Mat x3Dw = pMP->GetWorldPos();
+        for (int k = 0; k < 3; ++k) pos[3 * i + k] = x3Dw.at<float>(k);
+        cv::Mat d(1, 32, CV_8U, &desc[32 * (size_t)i]);
+        pMP->GetDescriptor().copyTo(d);
+        const cv::Mat PO = x3Dw - Ow;
+        const float dist3D = cv::norm(PO);
+        const float maxDistance = pMP->GetMaxDistanceInvariance();
+        const float minDistance = pMP->GetMinDistanceInvariance();
+        if (dist3D < minDistance || dist3D > maxDistance) continue;  // level stays -1
+        level[i] = pMP->PredictScale(dist3D, &CurrentFrame);
+    }
+    for (int i = 0; i < CurrentFrame.N; ++i)  // any claim blocks the keypoint (:1532-1533)
+        if (CurrentFrame.mvpMapPoints[i]) owner[i] = L;
+    orbgpu_keyframe_view kf{L, reinterpret_cast<const orbgpu_keypoint*>(pKF->mvKeysUn.data()), valid.data(),
+                            pos.data(), nullptr, nullptr, desc.data()};
+    orbgpu_frame_view v = view_of(CurrentFrame);
+    orbgpu_camera cur = camera_of(CurrentFrame);
+    int nmatches = 0;
+    if (orbgpu_search_by_projection_keyframe_levels(ctx_of(CurrentFrame), &v, &cur, &kf, level.data(), th, ORBdist,
+                                                    mbCheckOrientation, owner.data(), &nmatches) != ORBGPU_OK)
+        throw std::runtime_error("orbgpu_search_by_projection_keyframe_levels");
+    for (int i = 0; i < CurrentFrame.N; ++i)
+        if (owner[i] >= 0 && owner[i] < L) CurrentFrame.mvpMapPoints[i] = vpMPs[owner[i]];
     return nmatches;
 }
 

@@ -75,4 +75,9 @@ public:
     void create(int rows, int cols, int type) const;
 };
 typedef const _InputArray& InputArray;
+// matrix expressions (OpenCV returns MatExpr, which converts to Mat) and cv::norm (default NORM_L2)
+Mat operator-(const Mat& a);
+Mat operator-(const Mat& a, const Mat& b);
+Mat operator*(const Mat& a, const Mat& b);
+double norm(InputArray src1, int normType = 4);
 }  // namespace cv

@@ -11,4 +11,9 @@ namespace ORB_SLAM2 {
 class ORBextractor;
 // the context created for `ex` by the replacement ORBextractor constructor (nullptr if none)
 orbgpu_ctx* orbgpu_context_of(const ORBextractor* ex);
+// destroy the context of `ex` (for integrators that delete extractors; the reference never does)
+void orbgpu_release_extractor(const ORBextractor* ex);
+// refresh ex->mvImagePyramid after each call (on by default unless integration/Frame_stereo.cc is linked;
+// ORBGPU_HOST_PYRAMID=0/1 sets the default)
+void orbgpu_set_host_pyramid(const ORBextractor* ex, bool on);
 }  // namespace ORB_SLAM2

@@ -3,6 +3,8 @@
 #include <opencv2/core/core.hpp>
 
 namespace ORB_SLAM2 {
+class Frame;
+class KeyFrame;
 class MapPoint
 {
 public:
@@ -10,6 +12,9 @@ public:
     int Observations();  // ref: include/MapPoint.h:52
     bool isBad();  // ref: include/MapPoint.h:61
     cv::Mat GetDescriptor();  // ref: include/MapPoint.h:75
+    float GetMinDistanceInvariance();  // ref: include/MapPoint.h:79
+    float GetMaxDistanceInvariance();  // ref: include/MapPoint.h:80
+    int PredictScale(const float &currentDist, Frame* pF);  // ref: include/MapPoint.h:82
     float mTrackProjX;  // ref: include/MapPoint.h:92
     float mTrackProjY;  // ref: include/MapPoint.h:93
     float mTrackProjXR;  // ref: include/MapPoint.h:94

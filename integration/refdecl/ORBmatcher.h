@@ -25,6 +25,7 @@ public:
     static int DescriptorDistance(const cv::Mat &a, const cv::Mat &b);  // ref: include/ORBmatcher.h:44
     int SearchByProjection(Frame &F, const std::vector<MapPoint*> &vpMapPoints, const float th=3);  // ref: include/ORBmatcher.h:48
     int SearchByProjection(Frame &CurrentFrame, const Frame &LastFrame, const float th, const bool bMono);  // ref: include/ORBmatcher.h:52
+    int SearchByProjection(Frame &CurrentFrame, KeyFrame* pKF, const std::set<MapPoint*> &sAlreadyFound, const float th, const int ORBdist);  // ref: include/ORBmatcher.h:56
     int SearchForInitialization(Frame &F1, Frame &F2, std::vector<cv::Point2f> &vbPrevMatched, std::vector<int> &vnMatches12, int windowSize=10);  // ref: include/ORBmatcher.h:69
     static const int TH_LOW;  // ref: include/ORBmatcher.h:87
     static const int TH_HIGH;  // ref: include/ORBmatcher.h:88

@@ -73,6 +73,7 @@ def lib():
         L.oo_search_by_projection.argtypes = [vp, vp, f32, f32, vp, vp]
         L.oo_is_in_frustum.restype = i32
         L.oo_is_in_frustum.argtypes = [vp, vp, f32, vp, vp, vp, vp, vp, vp]
+        L.oo_kf_predicted_levels.argtypes = [vp, vp, vp]
         L.oo_search_by_projection_kf.restype = i32
         L.oo_search_by_projection_kf.argtypes = [vp, vp, vp, f32, i32, i32, vp]
         L.oo_stereo_from_rgbd.argtypes = [vp, vp, i32, vp, i32, f32, vp, vp]
@@ -332,6 +333,23 @@ def search_by_projection_kf(f: OracleFrame, cur: dict, kf: dict, th=10.0, orbdis
     nm = lib().oo_search_by_projection_kf(C.byref(f._s), C.byref(c), C.byref(s), th, int(orbdist), int(check_ori),
                                           _p(owner) if n else None)
     return nm, owner
+
+
+def kf_predicted_levels(cur: dict, kf: dict):
+    """Per keyframe point the relocalisation matcher's predicted level, -1 outside the scale range or invalid
+    (oo_kf_predicted_levels; what a drop-in binding computes with MapPoint::PredictScale)."""
+    arrs = dict(kps=np.ascontiguousarray(kf["kps"]), valid=np.ascontiguousarray(kf["valid"], np.uint8),
+                pos=np.ascontiguousarray(kf["pos"], np.float32).reshape(-1, 3),
+                max_dist=np.ascontiguousarray(kf["max_dist"], np.float32),
+                min_dist=np.ascontiguousarray(kf["min_dist"], np.float32),
+                desc=np.ascontiguousarray(kf["desc"], np.uint8))
+    s = _OOKeyFrame()
+    s.n = len(arrs["kps"])
+    for k, v in arrs.items():
+        setattr(s, k, _p(v).value if v.size else None)
+    out = np.zeros(max(s.n, 1), np.int32)
+    lib().oo_kf_predicted_levels(C.byref(_camera(cur)), C.byref(s), _p(out))
+    return out[:s.n]
 
 
 def depth_u16_to_f32(depth_u16, factor):

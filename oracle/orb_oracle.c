@@ -1359,6 +1359,34 @@ void oo_compute_image_bounds(const float* K4, const float* dist, int ndist, int 
     *invH = (float)OO_GRID_ROWS / (*maxY - *minY);
 }
 
+/* The scale gate of the relocalisation matcher per keyframe point, as the drop-in binding computes it with the
+ * reference's own MapPoint methods (src/ORBmatcher.cc:1513-1523; PredictScale src/MapPoint.cc:402-417):
+ * level[i] = PredictScale(dist3D) when 0.8 * mfMinDistance <= dist3D <= 1.2 * mfMaxDistance, else -1 (and -1 for
+ * invalid points).  dist3D = ||X - Ow||, Ow = -Rcw^T tcw as below. */
+void oo_kf_predicted_levels(const oo_camera* cur, const oo_keyframe* KF, int* level)
+{
+    const float logsf = oo_logf(cur->scale_factor);
+    float Ow[3];
+    for (int j = 0; j < 3; j++) {
+        float s = cur->Rcw[j] * cur->tcw[0];
+        s = s + cur->Rcw[3 + j] * cur->tcw[1];
+        s = s + cur->Rcw[6 + j] * cur->tcw[2];
+        Ow[j] = -s;
+    }
+    for (int i = 0; i < KF->n; i++) {
+        level[i] = -1;
+        if (!KF->valid[i]) continue;
+        const float* X = KF->pos + 3 * (size_t)i;
+        const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
+        double ss = 0.0;
+        for (int k = 0; k < 3; k++) ss += (double)PO[k] * (double)PO[k];
+        const float dist3D = (float)sqrt(ss);
+        if (dist3D < 0.8f * KF->min_dist[i] || dist3D > 1.2f * KF->max_dist[i]) continue;
+        int l = (int)ceilf(oo_logf(KF->max_dist[i] / dist3D) / logsf);
+        level[i] = l < 0 ? 0 : (l >= cur->nlevels ? cur->nlevels - 1 : l);
+    }
+}
+
 /* ORBmatcher::SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)
  * (src/ORBmatcher.cc:1472-1599): relocalisation / loop matcher of the map points of one keyframe */
 int oo_search_by_projection_kf(const oo_frame* F, const oo_camera* cur, const oo_keyframe* KF, float th, int ORBdist,

@@ -184,6 +184,7 @@ typedef struct {
 /* ORBmatcher::SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)
  * (src/ORBmatcher.cc:1472-1599).  owner (F.n ints, in/out): keyframe index claiming the keypoint, -1 = NULL,
  * >= KF.n = other claims.  Returns nmatches. */
+void oo_kf_predicted_levels(const oo_camera* cur, const oo_keyframe* KF, int* level);
 int oo_search_by_projection_kf(const oo_frame* F, const oo_camera* cur, const oo_keyframe* KF, float th, int ORBdist,
                                int checkOri, int* owner);
 

@@ -29,6 +29,7 @@ EXPORTS = [
     "orbgpu_is_in_frustum", "orbgpu_search_by_projection_last_frame", "orbgpu_debug_octree_profile",
     "orbgpu_stage_marks", "orbgpu_undistort_keypoints", "orbgpu_compute_image_bounds", "orbgpu_set_undistortion",
     "orbgpu_batch_outputs_undistorted", "orbgpu_search_by_projection_keyframe",
+    "orbgpu_search_by_projection_keyframe_levels",
     "orbgpu_compute_stereo_from_rgbd", "orbgpu_compute_stereo_from_rgbd_batch",
     "orbgpu_vocabulary_load_text", "orbgpu_vocabulary_create", "orbgpu_vocabulary_destroy", "orbgpu_vocabulary_info",
     "orbgpu_compute_bow", "orbgpu_compute_bow_batch", "orbgpu_memcpy_h2d_async", "orbgpu_memcpy_d2h_async",
@@ -172,6 +173,9 @@ def _declare(L):
     L.orbgpu_debug_octree_profile.argtypes = [vp, vp, i32]
     L.orbgpu_search_by_projection_keyframe.argtypes = [vp, C.POINTER(FrameView), C.POINTER(Camera),
                                                        C.POINTER(KeyFrameView), f32, i32, i32, vp, C.POINTER(i32)]
+    L.orbgpu_search_by_projection_keyframe_levels.argtypes = [vp, C.POINTER(FrameView), C.POINTER(Camera),
+                                                              C.POINTER(KeyFrameView), vp, f32, i32, i32, vp,
+                                                              C.POINTER(i32)]
     L.orbgpu_compute_stereo_from_rgbd.argtypes = [vp, vp, i32, f32, sz, f32, vp, vp, i32, C.POINTER(i32)]
     L.orbgpu_compute_stereo_from_rgbd_batch.argtypes = [vp, vp, i32, f32, sz, sz, f32, vp, vp]
     L.orbgpu_vocabulary_load_text.restype = vp

@@ -1152,7 +1152,7 @@ void og_launch_last_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const flo
 template <bool FILL>
 __device__ int og_kf_enum(const OgFrameDev& F, const OgGridGeom& G, const float* sf, const OgCameraDev& cam,
                           const float* Ow, const OgLastFrameDev& KF, const float* max_dist, const float* min_dist,
-                          int i, float th, OgLastCand* out)
+                          const int* pred_level, int i, float th, OgLastCand* out)
 {
     if (!KF.has_mp[i]) return 0;
     const float X[3] = {KF.pos[3 * i], KF.pos[3 * i + 1], KF.pos[3 * i + 2]};
@@ -1164,15 +1164,22 @@ __device__ int og_kf_enum(const OgFrameDev& F, const OgGridGeom& G, const float*
     if (u < G.minX || u > G.maxX) return 0;
     if (v < G.minY || v > G.maxY) return 0;
     if (u != u || v != v) return 0;
-    const float PO[3] = {__fsub_rn(X[0], Ow[0]), __fsub_rn(X[1], Ow[1]), __fsub_rn(X[2], Ow[2])};
-    double ss = 0.0;
+    int lvl;
+    if (pred_level) {  // the caller's PredictScale (orbgpu_search_by_projection_keyframe_levels); -1: out of range
+        lvl = pred_level[i];
+        if (lvl < 0) return 0;
+        lvl = lvl >= cam.nlevels ? cam.nlevels - 1 : lvl;
+    } else {
+        const float PO[3] = {__fsub_rn(X[0], Ow[0]), __fsub_rn(X[1], Ow[1]), __fsub_rn(X[2], Ow[2])};
+        double ss = 0.0;
 #pragma unroll
-    for (int k = 0; k < 3; k++) ss = __dadd_rn(ss, __dmul_rn((double)PO[k], (double)PO[k]));
-    const float dist3D = (float)__dsqrt_rn(ss);
-    const float maxD = __fmul_rn(1.2f, max_dist[i]), minD = __fmul_rn(0.8f, min_dist[i]);
-    if (dist3D < minD || dist3D > maxD) return 0;
-    int lvl = (int)ceilf(__fdiv_rn(og_logf(__fdiv_rn(max_dist[i], dist3D)), og_logf(cam.scale_factor)));
-    lvl = lvl < 0 ? 0 : (lvl >= cam.nlevels ? cam.nlevels - 1 : lvl);
+        for (int k = 0; k < 3; k++) ss = __dadd_rn(ss, __dmul_rn((double)PO[k], (double)PO[k]));
+        const float dist3D = (float)__dsqrt_rn(ss);
+        const float maxD = __fmul_rn(1.2f, max_dist[i]), minD = __fmul_rn(0.8f, min_dist[i]);
+        if (dist3D < minD || dist3D > maxD) return 0;
+        lvl = (int)ceilf(__fdiv_rn(og_logf(__fdiv_rn(max_dist[i], dist3D)), og_logf(cam.scale_factor)));
+        lvl = lvl < 0 ? 0 : (lvl >= cam.nlevels ? cam.nlevels - 1 : lvl);
+    }
     const float radius = __fmul_rn(th, sf[lvl]);
     const int minLevel = lvl - 1, maxLevel = lvl + 1;
     const OgCellRange cr = og_cell_range(G, u, v, radius);
@@ -1202,41 +1209,44 @@ __device__ int og_kf_enum(const OgFrameDev& F, const OgGridGeom& G, const float*
 
 __global__ __launch_bounds__(256) void og_kf_count_kernel(OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
                                                           OgLastFrameDev KF, const float* max_dist,
-                                                          const float* min_dist, float th, int* cnt)
+                                                          const float* min_dist, const int* pred_level, float th,
+                                                          int* cnt)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= KF.n) return;
-    cnt[i] = og_kf_enum<false>(F, G, sf, cam, cam.Ow, KF, max_dist, min_dist, i, th, nullptr);
+    cnt[i] = og_kf_enum<false>(F, G, sf, cam, cam.Ow, KF, max_dist, min_dist, pred_level, i, th, nullptr);
 }
 
 __global__ __launch_bounds__(256) void og_kf_fill_kernel(OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
                                                          OgLastFrameDev KF, const float* max_dist,
-                                                         const float* min_dist, float th, const int* off,
-                                                         OgLastCand* cands)
+                                                         const float* min_dist, const int* pred_level, float th,
+                                                         const int* off, OgLastCand* cands)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= KF.n) return;
-    og_kf_enum<true>(F, G, sf, cam, cam.Ow, KF, max_dist, min_dist, i, th, cands + off[i]);
+    og_kf_enum<true>(F, G, sf, cam, cam.Ow, KF, max_dist, min_dist, pred_level, i, th, cands + off[i]);
 }
 
 void og_launch_kf_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
-                        OgLastFrameDev KF, const float* max_dist, const float* min_dist, float th, int* cnt, int* off)
+                        OgLastFrameDev KF, const float* max_dist, const float* min_dist, const int* pred_level,
+                        float th, int* cnt, int* off)
 {
     const int blocks = (KF.n + 255) / 256;
     if (blocks > 0)
         hipLaunchKernelGGL(og_kf_count_kernel, dim3(blocks), dim3(256), 0, s, F, G, sf, cam, KF, max_dist, min_dist,
-                           th, cnt);
+                           pred_level, th, cnt);
     hipLaunchKernelGGL(og_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, KF.n, off);
 }
 
 void og_launch_kf_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
-                          OgLastFrameDev KF, const float* max_dist, const float* min_dist, float th, int ORBdist,
-                          int checkOri, const int* off, OgLastCand* cands, int* ent, int* owner, int* nmatches)
+                          OgLastFrameDev KF, const float* max_dist, const float* min_dist, const int* pred_level,
+                          float th, int ORBdist, int checkOri, const int* off, OgLastCand* cands, int* ent, int* owner,
+                          int* nmatches)
 {
     const int blocks = (KF.n + 255) / 256;
     if (blocks > 0)
         hipLaunchKernelGGL(og_kf_fill_kernel, dim3(blocks), dim3(256), 0, s, F, G, sf, cam, KF, max_dist, min_dist,
-                           th, off, cands);
+                           pred_level, th, off, cands);
     hipLaunchKernelGGL(og_last_resolve_kernel, dim3(1), dim3(64), 0, s, F, KF, checkOri, 1, ORBdist, off, cands, ent,
                        owner, (int*)nullptr, nmatches);
 }

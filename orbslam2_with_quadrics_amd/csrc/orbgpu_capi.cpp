@@ -1958,15 +1958,15 @@ int orbgpu_search_by_projection_last_frame(orbgpu_ctx* c, const orbgpu_frame_vie
     return ORBGPU_OK;
 }
 
-int orbgpu_search_by_projection_keyframe(orbgpu_ctx* c, const orbgpu_frame_view* F, const orbgpu_camera* curc,
-                                         const orbgpu_keyframe_view* KF, float th, int ORBdist, int checkOri,
-                                         int32_t* owner, int* nmatches)
+static int search_by_projection_keyframe(orbgpu_ctx* c, const orbgpu_frame_view* F, const orbgpu_camera* curc,
+                                         const orbgpu_keyframe_view* KF, const int32_t* pred_level, float th,
+                                         int ORBdist, int checkOri, int32_t* owner, int* nmatches)
 {
     if (!c || !F || !curc || !KF || !nmatches || F->n < 0 || KF->n < 0) return ORBGPU_ERR_ARG;
     if (F->n && !owner) return ORBGPU_ERR_ARG;
     if (!F->scale_factors || F->nlevels < 1) return ORBGPU_ERR_ARG;
-    if (KF->n && (!KF->kps || !KF->valid || !KF->pos || !KF->max_dist || !KF->min_dist || !KF->desc))
-        return ORBGPU_ERR_ARG;
+    if (KF->n && (!KF->kps || !KF->valid || !KF->pos || !KF->desc)) return ORBGPU_ERR_ARG;
+    if (KF->n && !pred_level && (!KF->max_dist || !KF->min_dist)) return ORBGPU_ERR_ARG;
     if (KF->n >= (1 << 24) || F->n >= (1 << 24)) return ORBGPU_ERR_UNSUPPORTED;
     HIP_TRY(c, hipSetDevice(c->device));
     const int n = std::max(F->n, 1), L = std::max(KF->n, 1);
@@ -1984,7 +1984,7 @@ int orbgpu_search_by_projection_keyframe(orbgpu_ctx* c, const orbgpu_frame_view*
     orbgpu_kp_dev* kk = (orbgpu_kp_dev*)scratch_carve(cur, (size_t)L * 28);
     uint8_t* kv = scratch_carve(cur, (size_t)L);
     float* kp3 = (float*)scratch_carve(cur, (size_t)L * 12);
-    float* kmx = (float*)scratch_carve(cur, (size_t)L * 4);
+    float* kmx = (float*)scratch_carve(cur, (size_t)L * 4);  // (pred_level: the levels)
     float* kmn = (float*)scratch_carve(cur, (size_t)L * 4);
     uint8_t* kd = scratch_carve(cur, (size_t)L * 32);
     int* cnt = (int*)scratch_carve(cur, (size_t)L * 4);
@@ -2002,8 +2002,12 @@ int orbgpu_search_by_projection_keyframe(orbgpu_ctx* c, const orbgpu_frame_view*
         HIP_TRY(c, hipMemcpyAsync(kk, KF->kps, (size_t)KF->n * 28, hipMemcpyHostToDevice, s));
         HIP_TRY(c, hipMemcpyAsync(kv, KF->valid, (size_t)KF->n, hipMemcpyHostToDevice, s));
         HIP_TRY(c, hipMemcpyAsync(kp3, KF->pos, (size_t)KF->n * 12, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(kmx, KF->max_dist, (size_t)KF->n * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(kmn, KF->min_dist, (size_t)KF->n * 4, hipMemcpyHostToDevice, s));
+        if (pred_level) {
+            HIP_TRY(c, hipMemcpyAsync(kmx, pred_level, (size_t)KF->n * 4, hipMemcpyHostToDevice, s));
+        } else {
+            HIP_TRY(c, hipMemcpyAsync(kmx, KF->max_dist, (size_t)KF->n * 4, hipMemcpyHostToDevice, s));
+            HIP_TRY(c, hipMemcpyAsync(kmn, KF->min_dist, (size_t)KF->n * 4, hipMemcpyHostToDevice, s));
+        }
         HIP_TRY(c, hipMemcpyAsync(kd, KF->desc, (size_t)KF->n * 32, hipMemcpyHostToDevice, s));
     }
     int hc = F->n;
@@ -2019,12 +2023,13 @@ int orbgpu_search_by_projection_keyframe(orbgpu_ctx* c, const orbgpu_frame_view*
         t = t + curc->Rcw[6 + j] * curc->tcw[2];
         cam.Ow[j] = -t;
     }
-    og_launch_kf_count(s, fd, G, sfd, cam, kfd, kmx, kmn, th, cnt, off);
+    const int* lv = pred_level ? (const int*)kmx : nullptr;
+    og_launch_kf_count(s, fd, G, sfd, cam, kfd, kmx, kmn, lv, th, cnt, off);
     int total = 0;
     HIP_TRY(c, hipMemcpyAsync(&total, off + KF->n, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
     HIP_TRY(c, ensure(c->mcands, (size_t)std::max(total, 1) * sizeof(OgLastCand)));
-    og_launch_kf_resolve(s, fd, G, sfd, cam, kfd, kmx, kmn, th, ORBdist, checkOri, off, (OgLastCand*)c->mcands.p,
+    og_launch_kf_resolve(s, fd, G, sfd, cam, kfd, kmx, kmn, lv, th, ORBdist, checkOri, off, (OgLastCand*)c->mcands.p,
                          ent, own, nm);
     HIP_TRY(c, hipGetLastError());
     int hnm = 0;
@@ -2033,6 +2038,21 @@ int orbgpu_search_by_projection_keyframe(orbgpu_ctx* c, const orbgpu_frame_view*
     HIP_TRY(c, hipStreamSynchronize(s));
     *nmatches = hnm;
     return ORBGPU_OK;
+}
+
+int orbgpu_search_by_projection_keyframe(orbgpu_ctx* c, const orbgpu_frame_view* F, const orbgpu_camera* curc,
+                                         const orbgpu_keyframe_view* KF, float th, int ORBdist, int checkOri,
+                                         int32_t* owner, int* nmatches)
+{
+    return search_by_projection_keyframe(c, F, curc, KF, nullptr, th, ORBdist, checkOri, owner, nmatches);
+}
+
+int orbgpu_search_by_projection_keyframe_levels(orbgpu_ctx* c, const orbgpu_frame_view* F, const orbgpu_camera* curc,
+                                                const orbgpu_keyframe_view* KF, const int32_t* pred_level, float th,
+                                                int ORBdist, int checkOri, int32_t* owner, int* nmatches)
+{
+    if (KF && KF->n && !pred_level) return ORBGPU_ERR_ARG;
+    return search_by_projection_keyframe(c, F, curc, KF, pred_level, th, ORBdist, checkOri, owner, nmatches);
 }
 
 int orbgpu_debug_candidates(orbgpu_ctx* c, int b, int level, uint64_t* out, int cap)

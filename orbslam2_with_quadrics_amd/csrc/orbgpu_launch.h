@@ -190,11 +190,15 @@ void og_launch_last_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const flo
 
 // relocalisation SearchByProjection(F, pKF, sAlreadyFound, th, ORBdist): KF.has_mp = valid flag, KF.outlier and
 // KF.n_obs unused; cam.Ow = -Rcw^T tcw of the current frame as the reference computes it (:1478)
+// pred_level (may be NULL): per KF point the caller's PredictScale level, -1 = outside the scale range; when given,
+// max_dist / min_dist are not read
 void og_launch_kf_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
-                        OgLastFrameDev KF, const float* max_dist, const float* min_dist, float th, int* cnt, int* off);
+                        OgLastFrameDev KF, const float* max_dist, const float* min_dist, const int* pred_level,
+                        float th, int* cnt, int* off);
 void og_launch_kf_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgCameraDev cam,
-                          OgLastFrameDev KF, const float* max_dist, const float* min_dist, float th, int ORBdist,
-                          int checkOri, const int* off, OgLastCand* cands, int* ent, int* owner, int* nmatches);
+                          OgLastFrameDev KF, const float* max_dist, const float* min_dist, const int* pred_level,
+                          float th, int ORBdist, int checkOri, const int* off, OgLastCand* cands, int* ent, int* owner,
+                          int* nmatches);
 
 // Frame post-processing (orb_frame.hip): cv::undistortPoints of Frame::UndistortKeyPoints
 struct OgUndistort {

@@ -153,9 +153,11 @@ class ORBmatcher:
 
 
     def SearchByProjectionKeyFrame(self, CurrentFrame: Frame, cur: dict, KF: dict, th: float, ORBdist: int,
-                                   owner=None):
+                                   owner=None, pred_level=None):
         """ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>& sAlreadyFound,
         th, ORBdist) (src/ORBmatcher.cc:1472-1599).  KF: dict of kps, valid, pos, max_dist, min_dist, desc.
+        pred_level (optional, KF.n ints): the caller's PredictScale per point, -1 outside the scale range
+        (orbgpu_search_by_projection_keyframe_levels: max_dist / min_dist are then not read).
         Returns (nmatches, owner) -- owner = keyframe map-point index per keypoint, -1 = NULL."""
         n = CurrentFrame.N
         owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
@@ -172,9 +174,15 @@ class ORBmatcher:
         cc = camera_struct(cur)
         nm = C.c_int(0)
         ctx = self._ex.ctx
-        rc = _lib.lib().orbgpu_search_by_projection_keyframe(ctx, C.byref(fv), C.byref(cc), C.byref(kv), float(th),
-                                                             int(ORBdist), int(self.mbCheckOrientation),
-                                                             _p(owner) if n else None, C.byref(nm))
+        if pred_level is None:
+            rc = _lib.lib().orbgpu_search_by_projection_keyframe(ctx, C.byref(fv), C.byref(cc), C.byref(kv),
+                                                                 float(th), int(ORBdist), int(self.mbCheckOrientation),
+                                                                 _p(owner) if n else None, C.byref(nm))
+        else:
+            lv = np.ascontiguousarray(pred_level, np.int32)
+            rc = _lib.lib().orbgpu_search_by_projection_keyframe_levels(
+                ctx, C.byref(fv), C.byref(cc), C.byref(kv), _p(lv) if lv.size else None, float(th), int(ORBdist),
+                int(self.mbCheckOrientation), _p(owner) if n else None, C.byref(nm))
         _lib.check(ctx, rc, "orbgpu_search_by_projection_keyframe")
         return nm.value, owner
 

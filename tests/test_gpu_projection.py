@@ -174,6 +174,12 @@ def test_search_by_projection_keyframe_vs_oracle(gpu, oracle, seed, shape, nf):
         wn, wown = oracle.search_by_projection_kf(Fo, cur, kf, th, orbdist, ori, owner0)
         assert gn == wn and gn > 10
         assert np.array_equal(gown, wown)
+        # the drop-in binding's form: levels from the reference's MapPoint::PredictScale, computed by the caller
+        lv = oracle.kf_predicted_levels(cur, kf)
+        assert (lv >= 0).sum() > 10 and (lv < 0).sum() > 0
+        ln, lown = gpu.ORBmatcher(0.9, ori, context=ex).SearchByProjectionKeyFrame(F, cur, kf, th, orbdist, owner0,
+                                                                                  pred_level=lv)
+        assert ln == wn and np.array_equal(lown, wown)
 
 
 def test_frustum_and_projection_batch_shared_map_vs_oracle(gpu, oracle):
