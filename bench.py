@@ -141,6 +141,11 @@ def stage_bytes(stage, B, P, cand_total, kp_total, mappoints=0):
         return kp_total * 60 + B * 3073 * 4
     if stage == "search_proj":  # map-point snapshot (58 B per point) + keypoints + descriptors + grid
         return B * mappoints * 58 + kp_total * 60 + B * 3073 * 4
+    if stage == "frustum":  # the shared map's geometry (33 B per point) once + 21 B of track fields per (frame, point)
+        return mappoints * 33 + B * mappoints * 21
+    if stage == "stereo":  # left and right keypoints + descriptors, the 11x11 left window and 11x21 right band of
+        # each left keypoint, uRight / depth / SAD out (kp_total = left keypoints; right ones taken as many)
+        return kp_total * (2 * 60 + 121 + 231 + 12)
     return 0
 
 
@@ -882,7 +887,9 @@ def main():
     ap.add_argument("--semantics", type=lambda v: int(v, 0), default=0,
                     help="ORBGPU_SEM_* flags (include/orbgpu.h): which OpenCV/compiler behaviours to reproduce")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--pmc-json", default=None,
+                    help="PMC per-stage summary (tools/pmc_summary.py) the roofline's traffic comes from; default "
+                         "profiles/pmc_latest.json (mono_init) or profiles/pmc_latest_<workload>.json")
     args = ap.parse_args()
     r0, c0, n0 = DEFAULT_SHAPE[args.workload]
     args.rows = args.rows or r0
@@ -978,7 +985,8 @@ def main():
     P = level_pixels(args.cols, args.rows, exs[0].GetInverseScaleFactors())
     stages = {k: v[0] / max(v[1], 1) for k, v in stage_acc.items()}
     kernels = {k: v for k, v in stages.items()
-               if k in ("fast", "octree", "describe", "grid", "search_init", "search_proj")}
+               if k in ("pyramid", "fast", "octree", "describe", "grid", "search_init", "search_proj", "stereo",
+                        "frustum")}
     dom = max(kernels, key=kernels.get)
     # effective launch duration: time the GPU has >= 1 launch of the kernel running, per launch.  With
     # concurrent streams a launch's own event span also covers the co-running launches; the union does
@@ -990,9 +998,11 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
     valu = None
-    if args.workload == "mono_init" and os.path.exists(args.pmc_json):
+    pmc_json = args.pmc_json or os.path.join(ROOT, "profiles", "pmc_latest.json" if args.workload == "mono_init"
+                                             else f"pmc_latest_{args.workload}.json")
+    if os.path.exists(pmc_json):
         try:
-            pmc = json.load(open(args.pmc_json))
+            pmc = json.load(open(pmc_json))
             pk = pmc.get("kernels", {}).get(dom, {})
             scale = Bs / pmc["batch"] if pmc.get("batch", Bs) != Bs else 1.0  # per-frame linear in the batch
             traffic = pk.get("hbm_bytes_per_launch")
@@ -1004,7 +1014,7 @@ def main():
                 insts = pk["SQ_INSTS_VALU"] * scale
                 valu = {"insts_per_launch": int(insts),
                         "issue_frac": round(insts * 2 / (dom_ms * 1e-3 * VALU_CLK_HZ * VALU_SIMDS), 4),
-                        "note": "PMC SQ_INSTS_VALU (profiles/pmc_latest.json) x 2 cycles / (avg_launch_ms x "
+                        "note": f"PMC SQ_INSTS_VALU ({os.path.relpath(pmc_json, ROOT)}) x 2 cycles / (avg_launch_ms x "
                                 "2.4 GHz x 1024 SIMDs)"}
         except Exception:
             traffic = None

@@ -228,6 +228,167 @@ __global__ __launch_bounds__(256) void og_stereo_match_kernel(OgStereoDev S)
     }
 }
 
+// ---- og_stereo_match16_kernel: the same per-keypoint computation with 16 lanes per left keypoint (4 keypoints per
+// wave, 16 per 256-thread workgroup).  Every cross-lane step stays inside a 16-lane DPP row (row_ror / quad_perm
+// min and add reductions: VALU, no LDS round trips), and the SAD is computed from registers: lane r < 11 loads row
+// r - 5 of the 11-pixel left window and of the 21-pixel right band (all 11 window positions), then forms its 11 row
+// sums with v_sad_u32.
+__device__ __forceinline__ unsigned og_row16_min(unsigned v)
+{
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false));  // row_ror:8
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false));  // row_ror:4
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+    return v;
+}
+__device__ __forceinline__ int og_row16_sum(int v)
+{
+    v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4e, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0xb1, 0xf, 0xf, false);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void og_stereo_match16_kernel(OgStereoDev S)
+{
+    const int b = blockIdx.y, l = threadIdx.x & 15;
+    const int iL = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int N = S.L.counts[b];
+    if (iL >= N) return;  // whole 16-lane groups leave together
+    float* UR = S.uright + (long long)b * S.L.frame_cap;
+    float* DE = S.depth + (long long)b * S.L.frame_cap;
+    int* SAD = S.sad + (long long)b * S.L.frame_cap;
+    if (l == 0) {
+        UR[iL] = -1.0f;
+        DE[iL] = -1.0f;
+        SAD[iL] = -1;
+    }
+    const orbgpu_kp_dev kpL = S.L.kps[(long long)b * S.L.frame_cap + iL];
+    const orbgpu_kp_dev* KR = S.R.kps + (long long)b * S.R.frame_cap;
+    const int levelL = kpL.octave;
+    const float vL = kpL.y, uL = kpL.x;
+    const int row = (int)vL;
+    if (row < 0 || row >= S.nRows) return;
+    const int* RS = S.row_start + (long long)b * (S.nRows + 1);
+    const int* RI = S.row_items + (long long)b * S.row_cap;
+    const int cb = RS[row], ce = min(RS[row + 1], S.row_cap);
+    if (cb == ce) return;
+    const float minZ = S.mb, minD = 0;
+    const float maxD = S.mbf / minZ;
+    const float minU = uL - maxD, maxU = uL - minD;
+    if (maxU < 0) return;
+    // ---- row-band Hamming search: the first strict minimum below TH_HIGH in candidate order
+    uint4 da, db;
+    {
+        const uint4* q = (const uint4*)(S.L.desc + ((long long)b * S.L.frame_cap + iL) * 32);
+        da = q[0];
+        db = q[1];
+    }
+    unsigned best = 0xffffffffu;  // (dist << 16) | (candidate position): smallest distance, then first in order
+    for (int c = cb + l; c < ce; c += 16) {
+        const int iR = RI[c];
+        const orbgpu_kp_dev kpR = KR[iR];
+        if (!(kpR.octave < levelL - 1 || kpR.octave > levelL + 1)) {
+            const float uR = kpR.x;
+            if (uR >= minU && uR <= maxU) {
+                const uint4* q = (const uint4*)(S.R.desc + ((long long)b * S.R.frame_cap + iR) * 32);
+                const int dist = og_hamming(da, db, q[0], q[1]);
+                if (dist < ST_TH_HIGH) best = min(best, ((unsigned)dist << 16) | (unsigned)(c - cb));
+            }
+        }
+    }
+    best = og_row16_min(best);
+    const int thOrbDist = (ST_TH_HIGH + ST_TH_LOW) / 2;
+    if (best == 0xffffffffu || (int)(best >> 16) >= thOrbDist) return;
+    const int bestIdxR = RI[cb + (int)(best & 0xffffu)];
+    // ---- SAD sliding window on the keypoint's pyramid level (:552-592)
+    const float uR0 = KR[bestIdxR].x;
+    const float scaleFactor = S.isf[levelL];
+    const float scaleduL = roundf(kpL.x * scaleFactor);
+    const float scaledvL = roundf(kpL.y * scaleFactor);
+    const float scaleduR0 = roundf(uR0 * scaleFactor);
+    const int w = 5, Lw = 5;
+    const float iniu = scaleduR0 + Lw - w;
+    const float endu = scaleduR0 + Lw + w + 1;
+    const int rcols = S.lvl_w[levelL];
+    if (iniu < 0 || endu >= rcols) return;
+    const uint8_t* IL;
+    const uint8_t* IR;
+    long long pl, pr;
+    if (levelL == 0) {
+        IL = S.L0 + (long long)b * S.L0_fstride;
+        pl = S.L0_pitch;
+        IR = S.R0 + (long long)b * S.R0_fstride;
+        pr = S.R0_pitch;
+    } else {
+        IL = S.Lpyr + (long long)b * S.pyr_fstride + S.lvl_off[levelL];
+        IR = S.Rpyr + (long long)b * S.pyr_fstride + S.lvl_off[levelL];
+        pl = pr = S.lvl_pitch[levelL];
+    }
+    const int ivL = (int)scaledvL, iuL = (int)scaleduL, iuR0 = (int)scaleduR0;
+    const int ry = min(l, 2 * w) - w;  // window row of this lane (lanes 11-15 repeat row +5 and contribute 0)
+    const uint8_t* lrow = IL + (long long)(ivL + ry) * pl + (iuL - w);
+    const uint8_t* rrow = IR + (long long)(ivL + ry) * pr + (iuR0 - Lw - w);
+    const uint8_t* rctr = IR + (long long)ivL * pr + (iuR0 - Lw);
+    const int cL = IL[(long long)ivL * pl + iuL];
+    unsigned lv[11], rv[21], cR[11];
+#pragma unroll
+    for (int x = 0; x < 11; x++) lv[x] = lrow[x];
+#pragma unroll
+    for (int x = 0; x < 21; x++) rv[x] = rrow[x];
+#pragma unroll
+    for (int i = 0; i < 11; i++) cR[i] = rctr[i];
+    // |(L - cL) - (R - cR_i)| = |(L - cL + cR_i + 512) - (R + 512)|: both operands in [0, 1022], two window pixels
+    // per 16-bit half pair, so one v_sad_u16 adds two terms (the 11th pixel pairs with a zero half)
+    unsigned LP[6], RP[20];
+#pragma unroll
+    for (int p = 0; p < 5; p++) LP[p] = lv[2 * p] | (lv[2 * p + 1] << 16);
+    LP[5] = lv[10];
+#pragma unroll
+    for (int x = 0; x < 20; x++) RP[x] = (rv[x] | (rv[x + 1] << 16)) + 0x02000200u;
+    int sums[11];
+#pragma unroll
+    for (int i = 0; i < 11; i++) {
+        const unsigned off = cR[i] + 512u - (unsigned)cL;  // in [257, 767]
+        unsigned s = 0;
+#pragma unroll
+        for (int p = 0; p < 5; p++) s = __builtin_amdgcn_sad_u16(LP[p] + off * 0x10001u, RP[2 * p + i], s);
+        s = __builtin_amdgcn_sad_u16(LP[5] + off, rv[10 + i] + 512u, s);
+        sums[i] = l <= 2 * w ? (int)s : 0;
+    }
+    int bestD = INT_MAX, bestincR = 0;
+    float vDists[11];
+#pragma unroll
+    for (int i = 0; i < 11; i++) {
+        const float dist = (float)og_row16_sum(sums[i]);  // cv::norm(IL, IR, NORM_L1): exact integer
+        if (dist < bestD) {
+            bestD = (int)dist;
+            bestincR = i - Lw;
+        }
+        vDists[i] = dist;
+    }
+    if (bestincR == -Lw || bestincR == Lw) return;
+    const float dist1 = vDists[Lw + bestincR - 1];
+    const float dist2 = vDists[Lw + bestincR];
+    const float dist3 = vDists[Lw + bestincR + 1];
+    const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+    if (deltaR < -1 || deltaR > 1) return;
+    float bestuR = S.sf[levelL] * ((float)scaleduR0 + (float)bestincR + deltaR);
+    float disparity = (uL - bestuR);
+    if (disparity >= minD && disparity < maxD) {
+        if (disparity <= 0) {
+            disparity = 0.01f;
+            bestuR = (float)((double)uL - 0.01);
+        }
+        if (l == 0) {
+            DE[iL] = S.mbf / disparity;
+            UR[iL] = bestuR;
+            SAD[iL] = bestD;
+        }
+    }
+}
+
 // median of the valid SAD distances (radix select on 16-bit values: <= 121 * 510 = 61710), then the
 // 1.5 * 1.4 * median rejection, which removes exactly the entries with (float)dist >= thDist (:626-639)
 __global__ __launch_bounds__(256) void og_stereo_filter_kernel(OgStereoDev S)
@@ -307,6 +468,12 @@ __global__ __launch_bounds__(256) void og_stereo_filter_kernel(OgStereoDev S)
 void og_launch_stereo(hipStream_t s, const OgStereoDev& S, int B)
 {
     hipLaunchKernelGGL(og_stereo_rows_kernel, dim3(B), dim3(ST_NT), 0, s, S);
-    hipLaunchKernelGGL(og_stereo_match_kernel, dim3((S.L.frame_cap + 3) / 4, B), dim3(256), 0, s, S);
+#ifndef OG_STEREO16
+#define OG_STEREO16 1  // 1: og_stereo_match16_kernel (16 lanes per keypoint); 0: og_stereo_match_kernel (a wave each)
+#endif
+    if (OG_STEREO16)
+        hipLaunchKernelGGL(og_stereo_match16_kernel, dim3((S.L.frame_cap + 15) / 16, B), dim3(256), 0, s, S);
+    else
+        hipLaunchKernelGGL(og_stereo_match_kernel, dim3((S.L.frame_cap + 3) / 4, B), dim3(256), 0, s, S);
     hipLaunchKernelGGL(og_stereo_filter_kernel, dim3(B), dim3(256), 0, s, S);
 }
