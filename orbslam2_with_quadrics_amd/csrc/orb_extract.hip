@@ -971,6 +971,9 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 // Lane L of a wave takes quad column c = L & 15 of ROI row R + {0, 4, 1, 5}[L >> 4]: the two 16-lane row groups of
 // each 32-lane LDS access are 4 rows = 112 qwords = 16 (mod 32) apart, so every b64 access is bank-conflict free.
 // ------------------------------------------------------------------------------------------------
+#ifndef OG_FASTQ_KB
+#define OG_FASTQ_KB 1  // FAST blocks per quad-kernel workgroup; > 1 prefetches the next block's ROI during stage 2
+#endif
 #define FQ_S 28     // quad-ROI row stride in qwords (>= 16 + 6 + 3 misalignment; 4 * FQ_S = 16 mod 32)
 #define FQ_ROWS 86  // ROI rows (detection <= 80 + 6)
 
@@ -1007,7 +1010,7 @@ __device__ __forceinline__ void og_fastq_circle(uint32_t base, unsigned long lon
         : "memory");
 }
 
-__device__ __forceinline__ void og_fastq_roi_store(const OgFB& b, int tid, uint2* roiq)
+__device__ __forceinline__ void og_fastq_roi_load(const OgFB& b, int tid, uint32_t (&s)[2][4])
 {
     // item (row, group of 4 qwords): 4 dword loads (one per 16-column segment), 8 v_perm into 4 quads, two 16-byte
     // LDS stores.  Columns past the ROI hold image bytes to its right (never read by a detection pixel); rows past it
@@ -1017,14 +1020,18 @@ __device__ __forceinline__ void og_fastq_roi_store(const OgFB& b, int tid, uint2
     const uint8_t* rbase = b.row0 - b.mis;
     const unsigned mb = (unsigned)((uintptr_t)rbase & 3);
     const uint8_t* abase = rbase - mb;
-    uint32_t s[2][4];
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         const int r = min((tid >> 3) + 64 * k, b.rh - 1);
         const unsigned off = (unsigned)r * b.upitch + 4u * (unsigned)q4;
+#ifndef OG_EXP_FAST_NOMEM
+#define OG_EXP_FAST_NOMEM 0  // timing experiments only: 1 = a synthetic ROI instead of the global loads (results wrong)
+#endif
 #pragma unroll
         for (int g = 0; g < 4; g++) {
-            if (b.aligned) {
+            if (OG_EXP_FAST_NOMEM) {
+                s[k][g] = (off + 16u * g) * 0x9e3779b1u;
+            } else if (b.aligned) {
                 s[k][g] = *(const uint32_t*)(rbase + off + 16u * g);
             } else {
                 const unsigned o = off + 16u * g + mb;
@@ -1033,6 +1040,11 @@ __device__ __forceinline__ void og_fastq_roi_store(const OgFB& b, int tid, uint2
             }
         }
     }
+}
+
+__device__ __forceinline__ void og_fastq_roi_put(const OgFB& b, int tid, const uint32_t (&s)[2][4], uint2* roiq)
+{
+    const int nq4 = (16 + 6 + b.mis + 3) >> 2;
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         const int r = (tid >> 3) + 64 * k;
@@ -1067,16 +1079,18 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);
     const unsigned f = blockIdx.y;  // grid (blocks per frame, frames), plan order
-    const int p = blockIdx.x;
+    int p = blockIdx.x;
     if (p >= nb) return;
     const int t1 = thr & 255, t2 = (thr >> 8) & 255;  // clamped to [0, 255] on the host
     const int tq = min(t1, t2);
     const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
     const int tA = max(t1, 1), tB = max(t2, 1);
     const uint32_t a_ns = og_lds_addr(&sh_ns), a_lst = og_lds_addr(&lst[0]);
-    const OgFB b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
+    OgFB b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
     if (b.l < 0) return;
-    og_fastq_roi_store(b, tid, roiq);
+    uint32_t sroi[2][4];
+    og_fastq_roi_load(b, tid, sroi);
+    og_fastq_roi_put(b, tid, sroi, roiq);
     for (int idx = tid * 16; idx < FB_MSZ; idx += FB_NT * 16) *(uint4*)&Ms[idx] = make_uint4(0u, 0u, 0u, 0u);
     if (tid == 0) sh_ns = 0;
     __syncthreads();
@@ -1084,6 +1098,8 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     if (roiq[tid].x == 255u && roiq[tid + 1].x == 254u) cand_count[0] = 1;
     return;
 #endif
+#pragma unroll 1
+    for (int kb = 0;; kb++) {
     const int dw = b.dw, dh = b.dh, wC = b.wC, hC = b.hC;
     const uint2* Tq = roiq + b.mis;  // Tq[r * FQ_S + x] = quad (x, x + 16, x + 32, x + 48) of ROI row r
     // ---- stage 1: quick test on every detection pixel, four per lane.  Unit u = (row group g = u >> 1, half
@@ -1110,9 +1126,27 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             uint32_t c0[16], c1[16];
             unsigned long long w[17];
 #ifndef OG_FASTQ_READ2
-#define OG_FASTQ_READ2 0  // experiment switch: 1 = compiler-paired ds_read2_b64 (9 instructions, 8 cycles each)
+#define OG_FASTQ_READ2 2  // circle loads: 2 volatile ds_read_b64 in pair order, partial waits (kept, -2.5 %); 0 asm
+                          // ds_read_b64 + one full wait; 1 compiler-paired ds_read2_b64 (profiles/sweeps/r03_ab_*)
 #endif
-#if OG_FASTQ_READ2
+#if OG_FASTQ_READ2 == 2
+            {
+                // volatile 64-bit loads: never paired into ds_read2_b64, issued in order (opposite samples k, k + 8
+                // adjacent, centre first), each waited for only where it is used (partial lgkmcnt waits)
+                const int st = FQ_S;
+                const int off[17] = {3 * st,      1 + 3 * st,  2 + 2 * st,  3 + 1 * st, 3,          3 - 1 * st,
+                                     2 - 2 * st,  1 - 3 * st,  -3 * st,     -1 - 3 * st, -2 - 2 * st, -3 - 1 * st,
+                                     -3,          -3 + 1 * st, -2 + 2 * st, -1 + 3 * st, 0};
+                typedef const volatile __attribute__((address_space(3))) unsigned long long lds_u64;
+                lds_u64* q64 = (lds_u64*)(uintptr_t)og_lds_addr(q);
+                w[16] = q64[0];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    w[k] = q64[off[k]];
+                    w[k + 8] = q64[off[k + 8]];
+                }
+            }
+#elif OG_FASTQ_READ2
             {
                 const int st = FQ_S;
                 const int off[17] = {3 * st,      1 + 3 * st,  2 + 2 * st,  3 + 1 * st, 3,          3 - 1 * st,
@@ -1183,6 +1217,16 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             }
         }
     }
+    // prefetch (OG_FASTQ_KB > 1): the next block's record and ROI loads are issued now and land during stage 2
+    const int pn = p + (int)gridDim.x;
+    const bool has_next = kb + 1 < OG_FASTQ_KB && pn < nb;  // block-uniform
+    OgFB bn = b;
+    __builtin_amdgcn_sched_barrier(0);
+    if (has_next) {
+        bn = og_fast_decode(blocks, pn, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
+        og_fastq_roi_load(bn, tid, sroi);
+    }
+    __builtin_amdgcn_sched_barrier(0);
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm list stores are not tracked by the compiler
     __syncthreads();
     const int ns = sh_ns;
@@ -1205,6 +1249,9 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)M;
     }
     __syncthreads();
+    // roiq and sh_ns are free from here on: the next block's ROI goes in while this block finishes
+    if (tid == 0) sh_ns = 0;
+    if (has_next) og_fastq_roi_put(bn, tid, sroi, roiq);
     // ---- stage 3: same-cell 3x3 NMS at both thresholds (og_fast_blocks_kernel)
     int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
     for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
@@ -1258,30 +1305,40 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     if (total == 12345) cand_count[0] = 1;
     return;
 #endif
+    // ---- stage 4: one reservation per block; each wave writes its kept entries at its offset.  Every entry's
+    // score-map cell goes back to zero (the next block of this workgroup starts from a clean map).
+    int sb = 0;
     if (total != 0) {  // block-uniform
-        // ---- stage 4: one reservation per block; each wave writes its kept entries at its offset
         if (tid == 0) {
             const int bb = atomicAdd(&cand_count[f * nlevels + b.l], total);
             if (bb + total > b.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
             sh_base = bb;
         }
         __syncthreads();
-        const int sb = sh_base;
-        if (sb + total <= b.cand_cap && kept != 0) {
-            u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb + before);
-            int run = 0;
-            for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
-                const int e = e0 + lane;
-                int ent = 0;
-                if (e < ns) ent = lst[e];
-                const int i = (ent >> 7) & 127, j = ent & 127;
-                const int cell = (i >= hC) * 2 + (j >= wC);
-                const unsigned kb = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
-                const u64 mask = og_lanes_ne(kb, 0u);
-                if (kb) out[og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, Ms[og_ms_idx(i, j, wC, hC)] - 1);
-                run += __popcll(mask);
-            }
+        sb = sh_base;
+    }
+    const bool emit = total != 0 && sb + total <= b.cand_cap && kept != 0;
+    u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb + before);
+    int run = 0;
+    for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
+        const int e = e0 + lane;
+        int ent = 0;
+        if (e < ns) ent = lst[e];
+        const int i = (ent >> 7) & 127, j = ent & 127;
+        const int cell = (i >= hC) * 2 + (j >= wC);
+        const unsigned kbit = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
+        const u64 mask = og_lanes_ne(kbit, 0u);
+        if (e < ns) {
+            uint8_t* mcell = &Ms[og_ms_idx(i, j, wC, hC)];
+            if (emit && kbit) out[og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, *mcell - 1);
+            if (OG_FASTQ_KB > 1) *mcell = 0;
         }
+        run += __popcll(mask);
+    }
+    if (!has_next) break;
+    b = bn;
+    p = pn;
+    __syncthreads();  // score map back to zero, list consumed, next ROI stored
     }
 }
 
@@ -2743,7 +2800,8 @@ void og_launch_fast(hipStream_t s, const OgPlan& P, const OgFastBlk* blocks, int
 #define OG_FAST_QUAD 1  // 1: og_fast_quad_kernel (quad layout); 0: og_fast_blocks_kernel (pair layout)
 #endif
     if (OG_FAST_QUAD)
-        hipLaunchKernelGGL(og_fast_quad_kernel, dim3(nblocks, B), dim3(FB_NT), 0, s, blocks, nblocks, img0, pitch0,
+        hipLaunchKernelGGL(og_fast_quad_kernel, dim3((nblocks + OG_FASTQ_KB - 1) / OG_FASTQ_KB, B), dim3(FB_NT), 0, s,
+                           blocks, nblocks, img0, pitch0,
                            fstride0, pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels, thr, status);
     else
         hipLaunchKernelGGL(og_fast_blocks_kernel, dim3((nblocks + OG_FAST_KB - 1) / OG_FAST_KB, B), dim3(FB_NT), 0, s,
