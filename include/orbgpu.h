@@ -73,7 +73,14 @@ void orbgpu_destroy(orbgpu_ctx* ctx);
 #define ORBGPU_SEM_BLUR_BITEXACT_ED (3 << ORBGPU_SEM_BLUR_SHIFT)
 #define ORBGPU_SEM_BLUR_MASK (7 << ORBGPU_SEM_BLUR_SHIFT)
 #define ORBGPU_SEM_BRIEF_NOFMA 0x20
-#define ORBGPU_SEM_ALL (ORBGPU_SEM_RESIZE_FIXEDPT | ORBGPU_SEM_BLUR_MASK | ORBGPU_SEM_BRIEF_NOFMA)
+/* Option, not a reference behaviour (off by default; also set at orbgpu_create by ORBGPU_SCORE_HARRIS=1):
+ * the octree ranks candidates by the Harris response of OpenCV's ORB HARRIS_SCORE (features2d orb.cpp
+ * HarrisResponses: 7x7 block, 3x3 Sobel-form gradients, k = 0.04, scale (1/(4*7*255))^4) at the FAST
+ * candidate's level pixel instead of by the FAST score, and the keypoint response is that float.
+ * ORB-SLAM2 itself always uses the FAST score (src/ORBextractor.cc:795-806, :621-632).  Parity of this
+ * option is unpinned: no reference fixture holds a Harris-ranked extraction. */
+#define ORBGPU_SEM_SCORE_HARRIS 0x40
+#define ORBGPU_SEM_ALL (ORBGPU_SEM_RESIZE_FIXEDPT | ORBGPU_SEM_BLUR_MASK | ORBGPU_SEM_BRIEF_NOFMA | ORBGPU_SEM_SCORE_HARRIS)
 /* the round-1 semantics of this build: generic resize form, 257-kernel rounded half-up, FMA rotation */
 #define ORBGPU_SEM_ROUND1 (ORBGPU_SEM_RESIZE_FIXEDPT | ORBGPU_SEM_BLUR_SCALAR_257)
 /* Select the semantics of later extractions on ctx.  ORBGPU_ERR_ARG for unknown bits or blur variants. */
@@ -469,10 +476,12 @@ int orbgpu_stage_marks(orbgpu_ctx* ctx, orbgpu_ctx* ref, const char** names, flo
 const char* orbgpu_last_error(const orbgpu_ctx* ctx);
 
 /* Introspection of the last batch (parity tests): FAST candidates of (frame b, level) as packed u64
- * {x-16:16, y-16:16, response:8} in arbitrary order, and the octree output of (b, level) in list order
- * as u32 {x:16, y:16} (level pixels) + u8 response.  Return the count (or < 0 on error). */
+ * {x-16:16, y-16:16, response key:32} in arbitrary order, and the octree output of (b, level) in list
+ * order as u32 {x:16, y:16} (level pixels) + u32 response key.  The key is the FAST score (0..255), or
+ * under ORBGPU_SEM_SCORE_HARRIS the order-preserving image of the float Harris response (bits ^ 0x80000000
+ * for >= +0, ~bits below).  Return the count (or < 0 on error). */
 int orbgpu_debug_candidates(orbgpu_ctx* ctx, int b, int level, uint64_t* out, int cap);
-int orbgpu_debug_octree(orbgpu_ctx* ctx, int b, int level, uint32_t* xy, uint8_t* resp, int cap);
+int orbgpu_debug_octree(orbgpu_ctx* ctx, int b, int level, uint32_t* xy, uint32_t* resp, int cap);
 
 /* Device memory helpers for callers without a HIP runtime of their own (tests, bench). */
 void* orbgpu_device_alloc(orbgpu_ctx* ctx, size_t bytes);

@@ -56,6 +56,8 @@ def lib():
         L.oo_set_semantics.argtypes = [vp, i32]
         L.oo_fast_score.restype = i32
         L.oo_fast_score.argtypes = [vp, i32, i32, i32]
+        L.oo_harris_response.restype = C.c_float
+        L.oo_harris_response.argtypes = [vp, i32, i32, i32]
         L.oo_fastatan2.restype = f32
         L.oo_fastatan2.argtypes = [f32, f32]
         L.oo_sincos.argtypes = [f32, C.POINTER(f32), C.POINTER(f32)]
@@ -490,6 +492,22 @@ def gaussian7(src: np.ndarray, semantics: int = 0) -> np.ndarray:
 def fast_score(img: np.ndarray, x: int, y: int) -> int:
     img = np.ascontiguousarray(img, np.uint8)
     return lib().oo_fast_score(_p(img), img.strides[0], x, y)
+
+
+def harris_response(img: np.ndarray, x: int, y: int) -> float:
+    """OpenCV ORB HARRIS_SCORE response at (x, y) (oracle/orb_oracle.c oo_harris_response; option, parity unpinned)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    if not (4 <= x < img.shape[1] - 4 and 4 <= y < img.shape[0] - 4):
+        raise ValueError("the 9x9 window must lie inside the image")
+    return float(lib().oo_harris_response(_p(img), img.strides[0], x, y))
+
+
+def harris_key(r: float) -> int:
+    """The device's order-preserving u32 image of a float response (include/orbgpu.h, orbgpu_debug_octree)."""
+    u = int(np.array([r], np.float32).view(np.uint32)[0])
+    if u == 0x80000000:
+        return 0x80000000
+    return (~u & 0xffffffff) if u & 0x80000000 else (u | 0x80000000)
 
 
 def fastatan2(y: float, x: float) -> float:

@@ -9,6 +9,7 @@
 
 #include <assert.h>
 #include <limits.h>
+#include <stddef.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -348,6 +349,36 @@ static void oo_fast_roi(const uint8_t* img, int stride, int x0, int y0, int x1, 
 }
 
 /* ------------------------------------------------------------------------------------------------ */
+/* Harris response (option OO_SEM_SCORE_HARRIS, not part of ORB-SLAM2, which ranks by the FAST score,    */
+/* src/ORBextractor.cc:795-806).  OpenCV's ORB HARRIS_SCORE (modules/features2d/src/orb.cpp               */
+/* HarrisResponses, OpenCV 3.x; OpenCV is an external dependency absent from /root/reference): over the  */
+/* blockSize x blockSize block centred on the pixel, the 3x3 Sobel-form gradients                        */
+/*   Ix = 2 (p[0,1] - p[0,-1]) + (p[-1,1] - p[-1,-1]) + (p[1,1] - p[1,-1]),  Iy likewise over rows,       */
+/* the integer sums a = sum Ix^2, b = sum Iy^2, c = sum Ix Iy, and the float response                     */
+/*   ((a*b - c*c) - k (a+b) (a+b)) * scale^4,  scale = 1 / (4 * blockSize * 255), k = 0.04, blockSize 7.   */
+/* Parity unpinned: no reference fixture holds a Harris response.                       */
+/* ------------------------------------------------------------------------------------------------ */
+float oo_harris_response(const uint8_t* img, int stride, int x, int y)
+{
+    const int bs = 7, r = bs / 2;
+    const float scale = 1.f / ((1 << 2) * bs * 255.f);
+    const float s4 = scale * scale * scale * scale;
+    int a = 0, b = 0, c = 0;
+    for (int i = -r; i <= r; i++)
+        for (int j = -r; j <= r; j++) {
+            const uint8_t* p = img + (ptrdiff_t)(y + i) * stride + (x + j);
+            const int ix = (p[1] - p[-1]) * 2 + (p[-stride + 1] - p[-stride - 1]) + (p[stride + 1] - p[stride - 1]);
+            const int iy = (p[stride] - p[-stride]) * 2 + (p[stride - 1] - p[-stride - 1]) +
+                           (p[stride + 1] - p[-stride + 1]);
+            a += ix * ix;
+            b += iy * iy;
+            c += ix * iy;
+        }
+    const float fa = (float)a, fb = (float)b, fc = (float)c;
+    return (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
 /* Octree: ExtractorNode::DivideNode + ORBextractor::DistributeOctTree,                               */
 /* src/ORBextractor.cc:481-537, 539-763.  std::list replaced by an index-linked list over a bump pool  */
 /* so that the (size, pointer) sort of :684 orders ties by creation order.            */
@@ -665,6 +696,9 @@ int oo_extract(oo_extractor* e, const uint8_t* img, int cols, int rows, int step
             }
         }
         free(cell.v);
+        if (e->sem & OO_SEM_SCORE_HARRIS) /* option: rank by the Harris response at the level pixel */
+            for (int k = 0; k < cand->n; k++)
+                cand->v[k].resp = oo_harris_response(im, lw, (int)cand->v[k].x + minBX, (int)cand->v[k].y + minBY);
         oo_cand* dist = (oo_cand*)malloc(sizeof(oo_cand) * (size_t)(cand->n + 1));
         const int nd = oo_distribute(cand, minBX, maxBX, minBY, maxBY, e->nfeat[l], dist);
         const int scaledPatchSize = (int)(OO_PATCH_SIZE * e->sf[l]);

@@ -39,9 +39,13 @@ oo_extractor* oo_create(int nfeatures, float scaleFactor, int nlevels, int iniTh
 #define OO_SEM_RESIZE_FIXEDPT 0x01 /* cv::resize vertical pass: generic FixedPtCast form, not the 8U form */
 #define OO_SEM_BLUR_SHIFT 2        /* GaussianBlur variant, 3 bits: 0 SSE2_257, 1 SCALAR_257, 2 BITEXACT_256, 3 ED */
 #define OO_SEM_BRIEF_NOFMA 0x20    /* rBRIEF rotation without FMA contraction */
-#define OO_SEM_ALL (OO_SEM_RESIZE_FIXEDPT | (7 << OO_SEM_BLUR_SHIFT) | OO_SEM_BRIEF_NOFMA)
+#define OO_SEM_SCORE_HARRIS 0x40   /* option (not ORB-SLAM2): octree ranks by the Harris response (oo_harris_response) */
+#define OO_SEM_ALL (OO_SEM_RESIZE_FIXEDPT | (7 << OO_SEM_BLUR_SHIFT) | OO_SEM_BRIEF_NOFMA | OO_SEM_SCORE_HARRIS)
 /* Returns 0, or -1 for an unknown flag combination (the extractor is unchanged then). */
 int oo_set_semantics(oo_extractor* e, int sem);
+/* Harris response of OpenCV's ORB HARRIS_SCORE at pixel (x, y) of an 8-bit image (blockSize 7, k 0.04); the
+ * pixel must lie >= 4 px inside the image. */
+float oo_harris_response(const uint8_t* img, int stride, int x, int y);
 void oo_destroy(oo_extractor* e);
 int oo_nlevels(const oo_extractor* e);
 void oo_scale_tables(const oo_extractor* e, float* scale, float* inv_scale, float* sigma2,

@@ -44,6 +44,7 @@ SEM_RESIZE_FIXEDPT = 0x01
 SEM_BLUR_SHIFT = 2
 SEM_BLUR_SSE2_257, SEM_BLUR_SCALAR_257, SEM_BLUR_BITEXACT_256, SEM_BLUR_BITEXACT_ED = (v << 2 for v in range(4))
 SEM_BRIEF_NOFMA = 0x20
+SEM_SCORE_HARRIS = 0x40  # option, not a reference behaviour: rank by the Harris response (parity unpinned)
 SEM_ROUND1 = SEM_RESIZE_FIXEDPT | SEM_BLUR_SCALAR_257
 # every valid combination: 2 resize forms x 4 blur variants x 2 rotation forms
 SEM_ALL_VARIANTS = [r | b | f for r in (0, SEM_RESIZE_FIXEDPT)
@@ -55,7 +56,7 @@ def semantics_name(flags: int) -> str:
     """Human-readable name of a semantics combination (bench lines, test ids)."""
     blur = ["sse2_257", "scalar_257", "bitexact_256", "bitexact_ed"][(flags >> SEM_BLUR_SHIFT) & 7]
     return (f"resize={'fixedpt' if flags & SEM_RESIZE_FIXEDPT else 'opencv8u'},blur={blur},"
-            f"brief={'nofma' if flags & SEM_BRIEF_NOFMA else 'fma'}")
+            f"brief={'nofma' if flags & SEM_BRIEF_NOFMA else 'fma'}" + (",score=harris" if flags & SEM_SCORE_HARRIS else ""))
 
 # cv::cvtColor codes of the colour entry points (include/orbgpu.h ORBGPU_COLOR_*, OpenCV's values)
 COLOR_BGR2GRAY, COLOR_RGB2GRAY, COLOR_BGRA2GRAY, COLOR_RGBA2GRAY = 6, 7, 10, 11

@@ -741,6 +741,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const int tA = max(t1, 1), tB = max(t2, 1);
     const uint32_t a_ns = og_lds_addr(&sh_ns), a_lst = og_lds_addr(&lst[0]);
     OgFB b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
+    if (b.l < 0) return;  // padding entry
     uint32_t blo[3], bhi[3];
     og_fast_roi_load(b, tid, blo, bhi);
     og_fast_roi_store(b, tid, blo, bhi, roi2);
@@ -833,11 +834,12 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
         // prefetch: the next block's record and ROI loads are issued now and land during stages 2-4
         const int pn = p + (int)gridDim.x;
-        const bool has_next = k + 1 < OG_FAST_KB && pn < nb;  // block-uniform
+        bool has_next = k + 1 < OG_FAST_KB && pn < nb;  // block-uniform
         OgFB bn = b;
         if (has_next) {
             bn = og_fast_decode(blocks, pn, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
-            og_fast_roi_load(bn, tid, blo, bhi);
+            has_next = bn.l >= 0;  // a padding entry ends the chain (the table pads each level to 8 entries)
+            if (has_next) og_fast_roi_load(bn, tid, blo, bhi);
         }
         __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm list stores are not tracked by the compiler
         __syncthreads();
@@ -1219,12 +1221,13 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     }
     // prefetch (OG_FASTQ_KB > 1): the next block's record and ROI loads are issued now and land during stage 2
     const int pn = p + (int)gridDim.x;
-    const bool has_next = kb + 1 < OG_FASTQ_KB && pn < nb;  // block-uniform
+    bool has_next = kb + 1 < OG_FASTQ_KB && pn < nb;  // block-uniform
     OgFB bn = b;
     __builtin_amdgcn_sched_barrier(0);
     if (has_next) {
         bn = og_fast_decode(blocks, pn, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
-        og_fastq_roi_load(bn, tid, sroi);
+        has_next = bn.l >= 0;  // a padding entry ends the chain (the table pads each level to 8 entries)
+        if (has_next) og_fastq_roi_load(bn, tid, sroi);
     }
     __builtin_amdgcn_sched_barrier(0);
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm list stores are not tracked by the compiler
@@ -1339,6 +1342,107 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     b = bn;
     p = pn;
     __syncthreads();  // score map back to zero, list consumed, next ROI stored
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k2b (option ORBGPU_SEM_SCORE_HARRIS, include/orbgpu.h; not part of ORB-SLAM2): the Harris response of every
+// FAST candidate replaces its FAST score as the octree's ranking key.  The response is OpenCV's ORB
+// HARRIS_SCORE (features2d orb.cpp HarrisResponses, blockSize 7, harris_k 0.04) at the candidate's level pixel;
+// the candidate keeps its slot, only the key word (bits 32-63) is rewritten.
+// ------------------------------------------------------------------------------------------------
+// float -> u32 with the same order (the octree's atomicMax ranks keys); -0 (not produced: a, b >= 0) as +0
+__device__ __forceinline__ unsigned og_harris_key(float r)
+{
+    const unsigned u = __float_as_uint(r);
+    if (u == 0x80000000u) return 0x80000000u;
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float og_harris_unkey(unsigned k)
+{
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// the response from the integer structure-tensor sums, in the published operation order, each product and sum
+// rounded to float (no contraction): ((a*b - c*c) - (k*(a+b))*(a+b)) * scale^4, scale = 1/(4*7*255)
+__device__ __forceinline__ float og_harris_response(int a, int b, int c)
+{
+#pragma clang fp contract(off)
+    const float scale = 1.f / ((1 << 2) * 7 * 255.f);
+    const float s4 = scale * scale * scale * scale;
+    const float fa = (float)a, fb = (float)b, fc = (float)c;
+    return (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
+}
+
+#define HR_NT 256
+// workgroups per (frame, level): one per 2^15 candidate slots (the level's area / 4), 1 .. 32
+__host__ __device__ inline int og_harris_groups(int cand_cap)
+{
+    const int g = cand_cap >> 15;
+    return g < 1 ? 1 : (g > 32 ? 32 : g);
+}
+
+// one thread per candidate of levels [lb, le); grid (sum over those levels of og_harris_groups, B)
+__global__ __launch_bounds__(HR_NT) void og_harris_kernel(OgPlan P, const uint8_t* __restrict__ img0, long long pitch0,
+                                                          long long fstride0, const uint8_t* __restrict__ pyr,
+                                                          u64* __restrict__ cand, const int* __restrict__ cand_count,
+                                                          int lb, int le)
+{
+    const int f = blockIdx.y;
+    int l = lb, g = blockIdx.x, ng = 1;
+    for (; l < le; l++) {
+        ng = og_harris_groups(P.lv[l].cand_cap);
+        if (g < ng) break;
+        g -= ng;
+    }
+    if (l >= le) return;
+    const OgLevel& L = P.lv[l];
+    const int n = min(cand_count[f * P.nlevels + l], L.cand_cap);
+    const uint8_t* img;
+    long long pitch;
+    if (l == 0) {
+        img = img0 + (long long)f * fstride0;
+        pitch = pitch0;
+    } else {
+        img = pyr + (long long)f * P.pyr_per_frame + L.pyr_off;
+        pitch = L.pitch;
+    }
+    uint32_t* K32 = (uint32_t*)(cand + (long long)f * P.cand_per_frame + L.cand_off);
+    for (int k = g * HR_NT + (int)threadIdx.x; k < n; k += ng * HR_NT) {
+        const uint32_t xy = K32[2 * k];
+        // candidates lie >= 19 px inside the level (minB + 3), the 9 x 9 window reaches 4: no border handling
+        const int x = (int)(xy & 0xffff) + L.minB, y = (int)(xy >> 16) + L.minB;
+        int p[9][9];
+#pragma unroll
+        for (int r = 0; r < 9; r++) {
+            // row r of the window from three aligned dwords (any pitch: each row has its own misalignment)
+            const uint8_t* rp = img + (long long)(y - 4 + r) * pitch + (x - 4);
+            const unsigned m = (unsigned)((uintptr_t)rp & 3);
+            const uint32_t* q = (const uint32_t*)(rp - m);
+            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, m), w1 = __builtin_amdgcn_alignbyte(d2, d1, m);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                p[r][j] = (int)((w0 >> (8 * j)) & 0xff);
+                p[r][4 + j] = (int)((w1 >> (8 * j)) & 0xff);
+            }
+            p[r][8] = (int)((d2 >> (8 * m)) & 0xff);
+        }
+        // 7 x 7 block of 3x3 Sobel-form gradients (integer sums: any order)
+        int sa = 0, sb = 0, sc = 0;
+#pragma unroll
+        for (int i = 1; i < 8; i++)
+#pragma unroll
+            for (int j = 1; j < 8; j++) {
+                const int ix = (p[i][j + 1] - p[i][j - 1]) * 2 + (p[i - 1][j + 1] - p[i - 1][j - 1]) +
+                               (p[i + 1][j + 1] - p[i + 1][j - 1]);
+                const int iy = (p[i + 1][j] - p[i - 1][j]) * 2 + (p[i + 1][j - 1] - p[i - 1][j - 1]) +
+                               (p[i + 1][j + 1] - p[i - 1][j + 1]);
+                sa += ix * ix;
+                sb += iy * iy;
+                sc += ix * iy;
+            }
+        K32[2 * k + 1] = og_harris_key(og_harris_response(sa, sb, sc));
     }
 }
 
@@ -1481,7 +1585,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                                                            const int* __restrict__ cand_count,
                                                            uint16_t* __restrict__ node_of,
                                                            uint32_t* __restrict__ oct_xy,
-                                                           uint8_t* __restrict__ oct_resp,
+                                                           uint32_t* __restrict__ oct_resp,
                                                            int* __restrict__ oct_count, int* __restrict__ status,
                                                            int nlaunch)
 {
@@ -1759,7 +1863,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                     const int n2 = (int)((tp >> (16 * q)) & 0xffffu);
                     NO[k] = (uint16_t)n2;
                     if (done) {
-                        const int resp = (int)(K32[2 * k + 1] & 0xff);
+                        const unsigned resp = K32[2 * k + 1];
                         atomicMax(&best[n2], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
                     } else {
                         const int rc = splitRank[n2];
@@ -1802,7 +1906,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 const int k = base + u * OCT_NT;
                 if (k < C) {
                     const int x = (int)(kv[u] & 0xffff), y = (int)((kv[u] >> 16) & 0xffff);
-                    const int resp = (int)((kv[u] >> 32) & 0xff);
+                    const unsigned resp = (unsigned)(kv[u] >> 32);
                     atomicMax(&best[noRoot ? aux[no[u]] : no[u]],
                               ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
                 }
@@ -1822,7 +1926,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const int x = cj * L.wCell + 3 + lx + L.minB, y = ci * L.hCell + 3 + ly + L.minB;
         const long long o = (long long)f * P.kcap_total + L.koff + n;
         oct_xy[o] = (uint32_t)x | ((uint32_t)y << 16);
-        oct_resp[o] = (uint8_t)(b >> 32);
+        oct_resp[o] = (uint32_t)(b >> 32);
     }
     if (tid == 0) {
         oct_count[f * P.nlevels + l] = nout;
@@ -1856,7 +1960,7 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_big_kernel(OgPlan P, int l0,
                                                            const int* __restrict__ cand_count,
                                                            uint16_t* __restrict__ node_of,
                                                            uint32_t* __restrict__ oct_xy,
-                                                           uint8_t* __restrict__ oct_resp,
+                                                           uint32_t* __restrict__ oct_resp,
                                                            int* __restrict__ oct_count, int* __restrict__ status,
                                                            int nlaunch)
 {
@@ -2184,7 +2288,7 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_big_kernel(OgPlan P, int l0,
                     const int n2 = (int)((tp >> (16 * q)) & 0xffffu);
                     NO[k] = (uint16_t)n2;
                     if (done) {
-                        const int resp = (int)(K32[2 * k + 1] & 0xff);
+                        const unsigned resp = K32[2 * k + 1];
                         atomicMax(&best[n2], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
                     } else {
                         const int rc = splitRank[n2];
@@ -2227,7 +2331,7 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_big_kernel(OgPlan P, int l0,
                 const int k = base + u * OCT_NT;
                 if (k < C) {
                     const int x = (int)(kv[u] & 0xffff), y = (int)((kv[u] >> 16) & 0xffff);
-                    const int resp = (int)((kv[u] >> 32) & 0xff);
+                    const unsigned resp = (unsigned)(kv[u] >> 32);
                     atomicMax(&best[noRoot ? aux[no[u]] : no[u]],
                               ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
                 }
@@ -2248,7 +2352,7 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_big_kernel(OgPlan P, int l0,
         const int x = cj * L.wCell + 3 + lx + L.minB, y = ci * L.hCell + 3 + ly + L.minB;
         const long long o = (long long)f * P.kcap_total + L.koff + n;
         oct_xy[o] = (uint32_t)x | ((uint32_t)y << 16);
-        oct_resp[o] = (uint8_t)(b >> 32);
+        oct_resp[o] = (uint32_t)(b >> 32);
     }
     if (tid == 0) {
         oct_count[f * P.nlevels + l] = nout;
@@ -2349,7 +2453,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
                                                                     long long pitch0, long long fstride0,
                                                                     const uint8_t* __restrict__ pyr,
                                                                     const uint32_t* __restrict__ oct_xy,
-                                                                    const uint8_t* __restrict__ oct_resp,
+                                                                    const uint32_t* __restrict__ oct_resp,
                                                                     const int* __restrict__ oct_count,
                                                                     orbgpu_kp_dev* __restrict__ kps,
                                                                     uint8_t* __restrict__ desc,
@@ -2383,7 +2487,8 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     // the blurred window reuses the raw window's bytes: the raw window's last readers (IC angle, horizontal
     // pass) are done before the vertical pass writes Bl; 5.8 KB of LDS per wave keeps ~27 waves per CU resident
     uint8_t* Bl = raw[w];
-    int cx = 0, cy = 0, resp = 0, lw = 1, lh = 1;
+    int cx = 0, cy = 0, lw = 1, lh = 1;
+    unsigned resp = 0;  // response key (og_harris_key under ORBGPU_SEM_SCORE_HARRIS, else the FAST score)
     if (active) {
         const OgLevel& L = P.lv[l];
         const long long o = (long long)f * P.kcap_total + L.koff + li;
@@ -2625,7 +2730,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         k.y = y;
         k.size = (float)L.patch_size;
         k.angle = angle;
-        k.response = (float)resp;
+        k.response = (P.sem & ORBGPU_SEM_SCORE_HARRIS) ? og_harris_unkey(resp) : (float)resp;
         k.octave = l;
         k.class_id = -1;
         kps[o] = k;
@@ -2650,67 +2755,77 @@ __device__ __forceinline__ void og_sort_cell(T* SI, int b, int e)
         SI[q + 1] = v;
     }
 }
-__global__ __launch_bounds__(256) void og_grid_kernel(const orbgpu_kp_dev* __restrict__ kps,
-                                                      const int* __restrict__ counts, int frame_cap,
-                                                      OgGridGeom G, int* __restrict__ cell_start,
-                                                      int* __restrict__ cell_items, int* __restrict__ status)
+#define GRID_NT 1024
+// one 1024-thread workgroup per frame, everything in LDS (~72 KB): each keypoint's cell is computed once (kept in
+// cellOf), counted, scanned, scattered into LDS, and the per-cell insertion sort restores index order
+__global__ __launch_bounds__(GRID_NT) void og_grid_kernel(const orbgpu_kp_dev* __restrict__ kps,
+                                                          const int* __restrict__ counts, int frame_cap,
+                                                          OgGridGeom G, int* __restrict__ cell_start,
+                                                          int* __restrict__ cell_items, int* __restrict__ status)
 {
     __shared__ int cnt[OG_GRID_CELLS + 1];
     __shared__ int wsum[32];
     __shared__ int starts[OG_GRID_CELLS + 1];
     __shared__ int sitems[OG_GRID_LDS_ITEMS];
+    __shared__ uint16_t cellOf[OG_GRID_LDS_ITEMS];
     const int f = blockIdx.x, tid = threadIdx.x;
     const int n = counts[f];
     const orbgpu_kp_dev* K = kps + (long long)f * frame_cap;
     int* CS = cell_start + (long long)f * (OG_GRID_CELLS + 1);
     int* CI = cell_items + (long long)f * frame_cap;
-    for (int c = tid; c < OG_GRID_CELLS; c += 256) cnt[c] = 0;
-    __syncthreads();
-    for (int i = tid; i < n; i += 256) {
-        const int px = (int)roundf((K[i].x - G.minX) * G.invW);
-        const int py = (int)roundf((K[i].y - G.minY) * G.invH);
-        if (px >= 0 && px < OG_GRID_COLS && py >= 0 && py < OG_GRID_ROWS) atomicAdd(&cnt[px * OG_GRID_ROWS + py], 1);
-    }
-    __syncthreads();
-    // exclusive scan over 3072 cells, 12 per thread
-    const int per = OG_GRID_CELLS / 256;
-    int local[OG_GRID_CELLS / 256];
-    int s = 0;
-    for (int q = 0; q < per; q++) {
-        local[q] = s;
-        s += cnt[tid * per + q];
-    }
-    int tot;
-    const int ex = og_block_excl_scan(s, wsum, &tot);
-    for (int q = 0; q < per; q++) CS[tid * per + q] = starts[tid * per + q] = ex + local[q];
-    if (tid == 0) CS[OG_GRID_CELLS] = starts[OG_GRID_CELLS] = tot;
-    __syncthreads();
-    for (int q = 0; q < per; q++) cnt[tid * per + q] = ex + local[q];  // cursors
-    __syncthreads();
-    for (int i = tid; i < n; i += 256) {
-        const int px = (int)roundf((K[i].x - G.minX) * G.invW);
-        const int py = (int)roundf((K[i].y - G.minY) * G.invH);
-        if (px >= 0 && px < OG_GRID_COLS && py >= 0 && py < OG_GRID_ROWS) {
-            const int pos = atomicAdd(&cnt[px * OG_GRID_ROWS + py], 1);
-            CI[pos] = i;
-        }
-    }
-    __syncthreads();
-    __threadfence_block();
-    // restore ascending index order inside each cell (push_back order of the reference): an insertion sort per
-    // cell (a few items each) in LDS, so the dependent compare-and-shift chain costs LDS latency rather than global
-    // round trips.  Every frame's items fit: nin <= counts[f] <= frame_cap <= OG_GRID_LDS_ITEMS (build_plan).
-    // The ranges are checked, never trusted: DS instructions drop out-of-range LDS accesses silently, so a bad
-    // range raises status bit 64 (reported by the next status check) instead of passing unnoticed
-    // (the round-1 fault of the generic-pointer form).
-    const int nin = starts[OG_GRID_CELLS];
-    if (nin > min(n, OG_GRID_LDS_ITEMS)) {
+    // every frame's items fit: counts[f] <= frame_cap <= OG_GRID_LDS_ITEMS (build_plan); checked, never trusted
+    if (n < 0 || n > min(frame_cap, OG_GRID_LDS_ITEMS)) {
         if (tid == 0) atomicOr(status, 64);
         return;
     }
-    for (int p = tid; p < nin; p += 256) sitems[p] = CI[p];
+    constexpr int per = OG_GRID_CELLS / GRID_NT;
+    static_assert(per * GRID_NT == OG_GRID_CELLS, "cells per thread");
+#pragma unroll
+    for (int q = 0; q < per; q++) cnt[tid * per + q] = 0;
     __syncthreads();
-    for (int c = tid; c < OG_GRID_CELLS; c += 256) {
+    for (int i = tid; i < n; i += GRID_NT) {
+        const int px = (int)roundf((K[i].x - G.minX) * G.invW);
+        const int py = (int)roundf((K[i].y - G.minY) * G.invH);
+        int c = 0xffff;
+        if (px >= 0 && px < OG_GRID_COLS && py >= 0 && py < OG_GRID_ROWS) {  // PosInGrid, src/Frame.cc:382-392
+            c = px * OG_GRID_ROWS + py;
+            atomicAdd(&cnt[c], 1);
+        }
+        cellOf[i] = (uint16_t)c;
+    }
+    __syncthreads();
+    int local[per];
+    int sum = 0;
+#pragma unroll
+    for (int q = 0; q < per; q++) {
+        local[q] = sum;
+        sum += cnt[tid * per + q];
+    }
+    int tot;
+    const int ex = og_block_excl_scan(sum, wsum, &tot);
+#pragma unroll
+    for (int q = 0; q < per; q++) {
+        CS[tid * per + q] = starts[tid * per + q] = ex + local[q];
+        cnt[tid * per + q] = ex + local[q];  // cursors (each thread rewrites only its own cells)
+    }
+    if (tid == 0) CS[OG_GRID_CELLS] = starts[OG_GRID_CELLS] = tot;
+    __syncthreads();
+    const int nin = tot;
+    for (int i = tid; i < n; i += GRID_NT) {
+        const int c = cellOf[i];
+        if (c != 0xffff) {
+            const int pos = atomicAdd(&cnt[c], 1);
+            if (pos >= 0 && pos < nin) sitems[pos] = i;
+            else atomicOr(status, 64);
+        }
+    }
+    __syncthreads();
+    // restore ascending index order inside each cell (push_back order of the reference): an insertion sort per
+    // cell (a few items each) in LDS.  Ranges are checked: DS instructions drop out-of-range LDS accesses
+    // silently, so a bad range raises status bit 64 instead of passing unnoticed.
+#pragma unroll
+    for (int q = 0; q < per; q++) {
+        const int c = tid * per + q;
         const int b = starts[c], e = starts[c + 1];
         if (b < 0 || b > e || e > nin) {
             atomicOr(status, 64);
@@ -2719,7 +2834,7 @@ __global__ __launch_bounds__(256) void og_grid_kernel(const orbgpu_kp_dev* __res
         og_sort_cell(sitems, b, e);
     }
     __syncthreads();
-    for (int p = tid; p < nin; p += 256) {
+    for (int p = tid; p < nin; p += GRID_NT) {
         const int v = sitems[p];
         if (v < 0 || v >= n) atomicOr(status, 64);  // every item is a keypoint index of this frame
         CI[p] = v;
@@ -2809,29 +2924,41 @@ void og_launch_fast(hipStream_t s, const OgPlan& P, const OgFastBlk* blocks, int
                            cand_count, P.nlevels, thr, status);
 }
 
-void og_launch_octree(hipStream_t s, const OgPlan& P, const u64* cand, const int* cand_count, uint16_t* node_of,
-                      uint32_t* oct_xy, uint8_t* oct_resp, int* oct_count, int* status, int B)
+void og_launch_harris(hipStream_t s, const OgPlan& P, int lb, int le, const uint8_t* img0, long long pitch0,
+                      long long fstride0, const uint8_t* pyr, u64* cand, const int* cand_count, int B)
+{
+    le = std::min(le, P.nlevels);
+    int g = 0;
+    for (int l = lb; l < le; l++) g += og_harris_groups(P.lv[l].cand_cap);
+    if (g <= 0 || B <= 0) return;
+    hipLaunchKernelGGL(og_harris_kernel, dim3(g, B), dim3(HR_NT), 0, s, P, img0, pitch0, fstride0, pyr, cand,
+                       cand_count, lb, le);
+}
+
+void og_launch_octree(hipStream_t s, const OgPlan& P, int lb, int le, const u64* cand, const int* cand_count,
+                      uint16_t* node_of, uint32_t* oct_xy, uint32_t* oct_resp, int* oct_count, int* status, int B)
 {
     // levels whose list may exceed OG_OCT_MAXL (more than ~1000 features: the finest levels, P.oct_big of them)
     // take the 2-nodes-per-thread kernel; the rest the 1-node-per-thread one
-    const int nbig = P.oct_big, nsmall = P.nlevels - P.oct_big;
-    if (nbig > 0)
-        hipLaunchKernelGGL(og_octree_big_kernel<OG_OCT_MAXL_BIG>, dim3(nbig * B), dim3(OCT_NT), 0, s, P, 0, cand,
-                           cand_count, node_of, oct_xy, oct_resp, oct_count, status, nbig);
-    if (nsmall > 0)
-        hipLaunchKernelGGL(og_octree_kernel, dim3(nsmall * B), dim3(OCT_NT), 0, s, P, nbig, cand,
-                           cand_count, node_of, oct_xy, oct_resp, oct_count, status, nsmall);
+    le = std::min(le, P.nlevels);
+    const int b0 = lb, b1 = std::min(le, P.oct_big), s0 = std::max(lb, P.oct_big), s1 = le;
+    if (b1 > b0)
+        hipLaunchKernelGGL(og_octree_big_kernel<OG_OCT_MAXL_BIG>, dim3((b1 - b0) * B), dim3(OCT_NT), 0, s, P, b0, cand,
+                           cand_count, node_of, oct_xy, oct_resp, oct_count, status, b1 - b0);
+    if (s1 > s0)
+        hipLaunchKernelGGL(og_octree_kernel, dim3((s1 - s0) * B), dim3(OCT_NT), 0, s, P, s0, cand,
+                           cand_count, node_of, oct_xy, oct_resp, oct_count, status, s1 - s0);
 }
 
 void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, long long pitch0, long long fstride0,
-                        const uint8_t* pyr, const uint32_t* oct_xy, const uint8_t* oct_resp, const int* oct_count,
+                        const uint8_t* pyr, const uint32_t* oct_xy, const uint32_t* oct_resp, const int* oct_count,
                         orbgpu_kp_dev* kps, uint8_t* desc, int* counts, int B)
 {
     const int blocks = (P.frame_cap + DK_WAVES - 1) / DK_WAVES;
     const int bv = (P.sem >> ORBGPU_SEM_BLUR_SHIFT) & 3;
     const bool nofma = (P.sem & ORBGPU_SEM_BRIEF_NOFMA) != 0;
     // the 8 (blur variant, rotation form) instantiations
-    using K = void (*)(OgPlan, const uint8_t*, long long, long long, const uint8_t*, const uint32_t*, const uint8_t*,
+    using K = void (*)(OgPlan, const uint8_t*, long long, long long, const uint8_t*, const uint32_t*, const uint32_t*,
                        const int*, orbgpu_kp_dev*, uint8_t*, int*);
     static const K table[8] = {og_describe_kernel<0, false>, og_describe_kernel<1, false>, og_describe_kernel<2, false>,
                                og_describe_kernel<3, false>, og_describe_kernel<0, true>,  og_describe_kernel<1, true>,
@@ -2843,6 +2970,6 @@ void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, lon
 void og_launch_grid(hipStream_t s, const orbgpu_kp_dev* kps, const int* counts, int frame_cap, OgGridGeom G,
                     int* cell_start, int* cell_items, int* status, int B)
 {
-    hipLaunchKernelGGL(og_grid_kernel, dim3(B), dim3(256), 0, s, kps, counts, frame_cap, G, cell_start, cell_items,
+    hipLaunchKernelGGL(og_grid_kernel, dim3(B), dim3(GRID_NT), 0, s, kps, counts, frame_cap, G, cell_start, cell_items,
                        status);
 }

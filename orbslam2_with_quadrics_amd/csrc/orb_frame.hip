@@ -159,3 +159,36 @@ void og_launch_gray(hipStream_t s, const uint8_t* src, int cols, int rows, int c
     hipLaunchKernelGGL(og_gray_kernel, dim3((nq + 255) / 256, rows, B), dim3(256), 0, s, src, cols, rows, cn, bidx,
                        spitch, sfstride, dst, dpitch, dfstride);
 }
+
+// ------------------------------------------------------------------------------------------------
+// Single-frame host download (orbgpu_extract, the Frame::ExtractORB call of src/Frame.cc:247-253): one kernel
+// writes the status word, the keypoint count and the frame's `count` keypoints + descriptors straight into the
+// context's pinned host block, so the host waits once instead of four synchronous copies.
+// Host block: {status, count, 0, 0} (16 B), frame_cap keypoints (28 B), frame_cap descriptors (32 B).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void og_pack_host_kernel(const int* __restrict__ status, const int* __restrict__ counts,
+                                                          const uint32_t* __restrict__ kps,
+                                                          const uint32_t* __restrict__ desc, int frame_cap,
+                                                          uint32_t* __restrict__ host)
+{
+    const int n = min(max(counts[0], 0), frame_cap);
+    const int i0 = blockIdx.x * 256 + threadIdx.x;
+    if (i0 == 0) {
+        host[0] = (uint32_t)status[0];
+        host[1] = (uint32_t)counts[0];
+    }
+    const int nk = 7 * n, nd = 8 * n;  // dwords of the frame's keypoints / descriptors
+    uint32_t* hk = host + 4;
+    uint32_t* hd = host + 4 + 7 * frame_cap;
+    for (int i = i0; i < nk + nd; i += gridDim.x * 256) {
+        if (i < nk) hk[i] = kps[i];
+        else hd[i - nk] = desc[i - nk];
+    }
+}
+
+void og_launch_pack_host(hipStream_t s, const int* status, const int* counts, const orbgpu_kp_dev* kps,
+                         const uint8_t* desc, int frame_cap, void* host_dev)
+{
+    hipLaunchKernelGGL(og_pack_host_kernel, dim3(16), dim3(256), 0, s, status, counts, (const uint32_t*)kps,
+                       (const uint32_t*)desc, frame_cap, (uint32_t*)host_dev);
+}

@@ -46,6 +46,9 @@ struct orbgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    // small batches: level 0 on `stream`, pyramid + levels >= 1 on stream2 (run_batch), forked and joined by events
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     uint32_t rec_hdr[3] = {0, 0, 0};  // frame-record header staged for orbgpu_frame_record_pack's async copy
     // ORBextractor parameters and scale tables (src/ORBextractor.cc:410-470)
     int nfeatures = 0, nlevels = 0, iniTh = 0, minTh = 0;
@@ -69,7 +72,7 @@ struct orbgpu_ctx {
     DevBuf<int> cand_count;
     DevBuf<uint16_t> node_of;
     DevBuf<uint32_t> oct_xy;
-    DevBuf<uint8_t> oct_resp;
+    DevBuf<uint32_t> oct_resp;  // response keys (FAST score, or the Harris key under ORBGPU_SEM_SCORE_HARRIS)
     DevBuf<int> oct_count;
     DevBuf<orbgpu_kp_dev> kps;
     DevBuf<uint8_t> desc;
@@ -84,6 +87,9 @@ struct orbgpu_ctx {
     // single-frame host path
     DevBuf<uint8_t> in_img;
     DevBuf<uint8_t> in_color;  // colour frame staged by orbgpu_extract_color
+    uint8_t* hpin = nullptr;   // pinned download block of the single-frame path (og_launch_pack_host)
+    void* hpin_dev = nullptr;  // ... its device-side address
+    size_t hpin_size = 0;
     // matcher scratch
     DevBuf<uint8_t> mscratch;
     DevBuf<uint32_t> mlists;  // SearchForInitialization candidate lists {dist:16|i2:16}
@@ -392,18 +398,43 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
         return ORBGPU_ERR_UNSUPPORTED;
     }
     P.total_cells = (int)cells.size();
-    // the FAST kernel's block table (OgFastBlk), in plan order: level-major, row-major blocks.  Hardware dispatch
-    // deals consecutive workgroups round-robin over the 8 XCDs; measured against giving every XCD a contiguous
-    // eighth of each frame (or whole frames, round 2's remap), plain order is 7-9 % faster
-    // (profiles/sweeps/r03_ab_fast_block_order.txt)
+    // the FAST kernel's block table (OgFastBlk): level-major; each level's range is padded to a multiple of 8
+    // entries (empty entries, lev < 0, exit at once), so workgroup (f, w) of the launch runs on XCD w % 8 for every
+    // frame (dispatch deals consecutive workgroups round-robin over the 8 XCDs).  Within a level, ORBGPU_FAST_ORDER
+    // R (default 4) gives each XCD runs of R row-adjacent blocks: their ROIs share 128-byte lines, which are then
+    // fetched once into that XCD's L2 instead of once per XCD.  R = 1 is plain plan order; giving every XCD a
+    // contiguous eighth of each frame was 7-9 % slower (profiles/sweeps/r03_ab_fast_block_order.txt).
     std::vector<OgFastBlk> fblk;
     {
-        const int n = P.total_cells;
+        static const int R = [] {
+            const char* e = std::getenv("ORBGPU_FAST_ORDER");
+            const int v = e && *e ? std::atoi(e) : 4;
+            return v == 1 || v == 2 || v == 4 || v == 8 ? v : 4;
+        }();
+        std::vector<int> order;  // table entry -> cell index (-1 = padding)
+        for (int l = 0; l < P.nlevels; l++) {
+            OgLevel& L = P.lv[l];
+            L.fb_off = (int)order.size();
+            const int n = L.ncells, npad = (n + 7) & ~7, G = 8 * R;
+            for (int w = 0; w < npad; w++) {
+                int b = w;
+                if (w < n / G * G) {  // slot w = G q + 8 h + x -> block G q + R x + h
+                    const int q = w / G, h = (w % G) / 8, x = w % 8;
+                    b = G * q + R * x + h;
+                }
+                order.push_back(b < n ? L.cell_base + b : -1);
+            }
+        }
+        const int n = (int)order.size();
         fblk.resize(n);
         for (int p = 0; p < n; p++) {
             OgFastBlk& r = fblk[p];
             std::memset(&r, 0, sizeof(r));
-            const OgCell& cd = cells[p];
+            if (order[p] < 0) {
+                r.lev = -1;
+                continue;
+            }
+            const OgCell& cd = cells[order[p]];
             const OgLevel& L = P.lv[cd.level];
             const int rw = cd.x1 - cd.x0, rh = cd.y1 - cd.y0;
             if (rw - 6 > 64 || rh - 6 > 80 || rw < 7 || rh < 7 || L.wCell > 255 || L.hCell > 255) {
@@ -536,15 +567,11 @@ static void timer_mark(orbgpu_ctx* c, const char* name)
 // the keypoints the Frame-level code reads (mvKeysUn): undistorted when the context has a distortion model
 static const orbgpu_kp_dev* kps_match(const orbgpu_ctx* c) { return c->undist ? c->kps_un.p : c->kps.p; }
 
-static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitch, long long fstride)
+// k1: chained pyramid, src/ORBextractor.cc:1107-1132
+// levels (1,2), (3,4), (5,6) in one launch each (og_resize2_kernel), a last odd level alone
+static void launch_pyramid(orbgpu_ctx* c, hipStream_t s, const uint8_t* d_imgs, int B, long long pitch, long long fstride)
 {
     const OgPlan& P = c->plan;
-    hipStream_t s = c->stream;
-    timer_begin(c);
-    timer_mark(c, "start");
-    HIP_TRY(c, hipMemsetAsync(c->cand_count.p, 0, sizeof(int) * (size_t)B * P.nlevels, s));
-    // k1: chained pyramid, src/ORBextractor.cc:1107-1132
-    // levels (1,2), (3,4), (5,6) in one launch each (og_resize2_kernel), a last odd level alone
     for (int l = 1; l < P.nlevels;) {
         const OgLevel& L = P.lv[l];
         const OgLevel& Lp = P.lv[l - 1];
@@ -565,11 +592,65 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
             l += 1;
         }
     }
-    timer_mark(c, "pyramid");
-    og_launch_fast(s, P, c->cells.p, P.fast_blocks, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p, c->status.p, B);
-    timer_mark(c, "fast");
-    og_launch_octree(s, P, c->cand.p, c->cand_count.p, c->node_of.p, c->oct_xy.p, c->oct_resp.p, c->oct_count.p,
-                     c->status.p, B);
+}
+
+// FAST (+ the Harris option) and the octree of levels [lb, le) on stream s; the FAST block table is level-major,
+// so the levels' blocks are one contiguous range
+static void launch_levels(orbgpu_ctx* c, hipStream_t s, int lb, int le, const uint8_t* d_imgs, int B, long long pitch,
+                          long long fstride, bool marks)
+{
+    const OgPlan& P = c->plan;
+    const int p0 = P.lv[lb].fb_off, p1 = le < P.nlevels ? P.lv[le].fb_off : P.fast_blocks;
+    og_launch_fast(s, P, c->cells.p + p0, p1 - p0, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p,
+                   c->status.p, B);
+    if (marks) timer_mark(c, "fast");
+    if (P.sem & ORBGPU_SEM_SCORE_HARRIS) {  // option: rank by the Harris response (include/orbgpu.h)
+        og_launch_harris(s, P, lb, le, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p, B);
+        if (marks) timer_mark(c, "harris");
+    }
+    og_launch_octree(s, P, lb, le, c->cand.p, c->cand_count.p, c->node_of.p, c->oct_xy.p, c->oct_resp.p,
+                     c->oct_count.p, c->status.p, B);
+}
+
+// batches of up to this many frames run level 0's FAST + octree (the single-frame critical path, ~60 % of a
+// 1080p frame's device time) on the context stream while a second stream builds the pyramid and runs levels >= 1.
+// The fork and join cost more than they hide below ~1 MP (tools/latency.py: 1242x375 0.177 -> 0.211 ms forked,
+// 1920x1080 0.294 -> 0.238 ms), so only frames of at least ORBGPU_FORK_MIN_PIXELS (default 2^20) fork.
+#ifndef OG_FORK_MAX_B
+#define OG_FORK_MAX_B 4
+#endif
+static long long fork_min_pixels()
+{
+    static const long long v = [] {
+        const char* e = std::getenv("ORBGPU_FORK_MIN_PIXELS");
+        return e && *e ? std::atoll(e) : (1LL << 20);
+    }();
+    return v;
+}
+
+static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitch, long long fstride)
+{
+    const OgPlan& P = c->plan;
+    hipStream_t s = c->stream;
+    timer_begin(c);
+    timer_mark(c, "start");
+    HIP_TRY(c, hipMemsetAsync(c->cand_count.p, 0, sizeof(int) * (size_t)B * P.nlevels, s));
+    // stage timing and the debug sync keep the serial order (their marks are stage boundaries on one stream)
+    const bool fork = B <= OG_FORK_MAX_B && P.nlevels > 1 && !c->timer.on && !debug_sync() && c->stream2 &&
+                      (long long)c->W * c->H >= fork_min_pixels();
+    if (fork) {
+        HIP_TRY(c, hipEventRecord(c->ev_fork, s));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+        launch_levels(c, s, 0, 1, d_imgs, B, pitch, fstride, false);
+        launch_pyramid(c, c->stream2, d_imgs, B, pitch, fstride);
+        launch_levels(c, c->stream2, 1, P.nlevels, d_imgs, B, pitch, fstride, false);
+        HIP_TRY(c, hipEventRecord(c->ev_join, c->stream2));
+        HIP_TRY(c, hipStreamWaitEvent(s, c->ev_join, 0));
+    } else {
+        launch_pyramid(c, s, d_imgs, B, pitch, fstride);
+        timer_mark(c, "pyramid");
+        launch_levels(c, s, 0, P.nlevels, d_imgs, B, pitch, fstride, true);
+    }
     timer_mark(c, "octree");
     og_launch_describe(s, P, d_imgs, pitch, fstride, c->pyr.p, c->oct_xy.p, c->oct_resp.p, c->oct_count.p, c->kps.p,
                        c->desc.p, c->counts.p, B);
@@ -634,7 +715,10 @@ orbgpu_ctx* orbgpu_create(int device, int nfeatures, float scaleFactor, int nlev
     orbgpu_ctx* c = new orbgpu_ctx();
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess || og_upload_pattern(device) != hipSuccess ||
+        hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess || og_upload_pattern(device) != hipSuccess ||
         og_prepare_device() != hipSuccess) {
         delete c;
         return nullptr;
@@ -644,6 +728,8 @@ orbgpu_ctx* orbgpu_create(int device, int nfeatures, float scaleFactor, int nlev
     c->iniTh = iniThFAST;
     c->minTh = minThFAST;
     c->scaleFactor = (double)scaleFactor;
+    if (const char* e = std::getenv("ORBGPU_SCORE_HARRIS"))  // option, off by default (include/orbgpu.h)
+        if (e[0] == '1') c->sem |= ORBGPU_SEM_SCORE_HARRIS;
     // src/ORBextractor.cc:415-446
     c->sf.assign(nlevels, 0.f);
     c->sig2.assign(nlevels, 0.f);
@@ -724,6 +810,8 @@ void orbgpu_destroy(orbgpu_ctx* c)
     release(c->status);
     release(c->in_img);
     release(c->in_color);
+    if (c->hpin) (void)hipHostFree(c->hpin);
+    c->hpin = nullptr;
     release(c->mscratch);
     release(c->mlists);
     release(c->mlist_n);
@@ -742,7 +830,11 @@ void orbgpu_destroy(orbgpu_ctx* c)
     release(c->st_nm);
     release(c->st_out);
     for (hipEvent_t e : c->timer.ev) (void)hipEventDestroy(e);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->done) (void)hipEventDestroy(c->done);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -911,6 +1003,40 @@ int orbgpu_batch_download(orbgpu_ctx* c, int b, orbgpu_keypoint* kps, uint8_t* d
     return ORBGPU_OK;
 }
 
+// the single-frame download (orbgpu_extract*): one packing kernel into the pinned block, one wait
+static int download_single(orbgpu_ctx* c, orbgpu_keypoint* kps, uint8_t* desc, int cap, int* n)
+{
+    const size_t fc = (size_t)c->plan.frame_cap;
+    const size_t need = 16 + fc * 60;
+    if (c->hpin_size < need) {
+        if (c->hpin) HIP_TRY(c, hipHostFree(c->hpin));
+        c->hpin = nullptr;
+        c->hpin_size = 0;
+        HIP_TRY(c, hipHostMalloc((void**)&c->hpin, need, hipHostMallocDefault));
+        HIP_TRY(c, hipHostGetDevicePointer(&c->hpin_dev, c->hpin, 0));
+        c->hpin_size = need;
+    }
+    og_launch_pack_host(c->stream, c->status.p, c->counts.p, c->kps.p, c->desc.p, (int)fc, c->hpin_dev);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    collect_timer(c);
+    int hdr[2];
+    std::memcpy(hdr, c->hpin, sizeof(hdr));
+    if (hdr[0]) {  // capacity guard: read and clear, as check_status
+        HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(int) * 4, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        c->err = "device capacity guard tripped (status " + std::to_string(hdr[0]) + ")";
+        return ORBGPU_ERR_INTERNAL;
+    }
+    *n = hdr[1];
+    if (hdr[1] > cap) return ORBGPU_ERR_CAPACITY;
+    if (hdr[1] > 0) {
+        if (kps) std::memcpy(kps, c->hpin + 16, (size_t)hdr[1] * sizeof(orbgpu_kp_dev));
+        if (desc) std::memcpy(desc, c->hpin + 16 + fc * sizeof(orbgpu_kp_dev), (size_t)hdr[1] * 32);
+    }
+    return ORBGPU_OK;
+}
+
 int orbgpu_extract(orbgpu_ctx* c, const uint8_t* img, int cols, int rows, size_t step, orbgpu_keypoint* kps,
                    uint8_t* desc, int cap, int* n)
 {
@@ -921,13 +1047,18 @@ int orbgpu_extract(orbgpu_ctx* c, const uint8_t* img, int cols, int rows, size_t
     }
     if (step < (size_t)cols) return ORBGPU_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
-    const size_t pitch = ((size_t)cols + 63) & ~(size_t)63;
+    // a contiguous image (cv::Mat::isContinuous, the usual case) keeps its own pitch: one linear copy instead of
+    // a row-by-row 2-D copy (the kernels take any pitch)
+    const size_t pitch = step == (size_t)cols ? step : (((size_t)cols + 63) & ~(size_t)63);
     HIP_TRY(c, ensure(c->in_img, pitch * (size_t)rows));
-    HIP_TRY(c, hipMemcpy2DAsync(c->in_img.p, pitch, img, step, (size_t)cols, (size_t)rows, hipMemcpyHostToDevice,
-                                c->stream));
+    if (pitch == step)
+        HIP_TRY(c, hipMemcpyAsync(c->in_img.p, img, step * (size_t)rows, hipMemcpyHostToDevice, c->stream));
+    else
+        HIP_TRY(c, hipMemcpy2DAsync(c->in_img.p, pitch, img, step, (size_t)cols, (size_t)rows, hipMemcpyHostToDevice,
+                                    c->stream));
     int r = orbgpu_extract_batch_device(c, c->in_img.p, 1, cols, rows, pitch, pitch * (size_t)rows);
     if (r) return r;
-    return orbgpu_batch_download(c, 0, kps, desc, cap, n);
+    return download_single(c, kps, desc, cap, n);
 }
 
 static int og_color_code(int code, int* cn, int* bidx)
@@ -980,7 +1111,7 @@ int orbgpu_extract_color(orbgpu_ctx* c, const uint8_t* img, int cols, int rows, 
     if (r) return r;
     r = orbgpu_extract_batch_device(c, c->in_img.p, 1, cols, rows, pitch, pitch * (size_t)rows);
     if (r) return r;
-    return orbgpu_batch_download(c, 0, kps, desc, cap, n);
+    return download_single(c, kps, desc, cap, n);
 }
 
 int orbgpu_get_level(orbgpu_ctx* c, int level, uint8_t* dst, size_t dst_step, int* cols, int* rows)
@@ -2070,7 +2201,7 @@ int orbgpu_debug_candidates(orbgpu_ctx* c, int b, int level, uint64_t* out, int 
     return n;
 }
 
-int orbgpu_debug_octree(orbgpu_ctx* c, int b, int level, uint32_t* xy, uint8_t* resp, int cap)
+int orbgpu_debug_octree(orbgpu_ctx* c, int b, int level, uint32_t* xy, uint32_t* resp, int cap)
 {
     if (!c || !c->last_B || b < 0 || b >= c->last_B || level < 0 || level >= c->nlevels) return ORBGPU_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
@@ -2081,7 +2212,7 @@ int orbgpu_debug_octree(orbgpu_ctx* c, int b, int level, uint32_t* xy, uint8_t* 
     const size_t o = (size_t)b * c->plan.kcap_total + L.koff;
     const int m = std::min(n, cap);
     if (xy && m > 0) HIP_TRY(c, hipMemcpy(xy, c->oct_xy.p + o, (size_t)m * 4, hipMemcpyDeviceToHost));
-    if (resp && m > 0) HIP_TRY(c, hipMemcpy(resp, c->oct_resp.p + o, (size_t)m, hipMemcpyDeviceToHost));
+    if (resp && m > 0) HIP_TRY(c, hipMemcpy(resp, c->oct_resp.p + o, (size_t)m * 4, hipMemcpyDeviceToHost));
     return n;
 }
 

@@ -38,6 +38,7 @@ struct OgLevel {
     int minB, maxBX, maxBY;
     int nCols, nRows, wCell, hCell;
     int cell_base, ncells; // into the flat cell table
+    int fb_off;            // first entry of the level in the FAST block table (OgFastBlk, padded per level)
     // octree, src/ORBextractor.cc:539-563
     int N;                 // mnFeaturesPerLevel
     int nIni;

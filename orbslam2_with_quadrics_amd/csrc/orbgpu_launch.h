@@ -56,10 +56,15 @@ void og_launch_fast(hipStream_t s, const OgPlan& P, const OgFastBlk* blocks, int
                     long long pitch0, long long fstride0, const uint8_t* pyr, unsigned long long* cand, int* cand_count,
                     int* status, int B);
 hipError_t og_read_oct_prof(unsigned long long* out, int n);  // OG_OCT_PROFILE builds only
-void og_launch_octree(hipStream_t s, const OgPlan& P, const unsigned long long* cand, const int* cand_count,
-                      uint16_t* node_of, uint32_t* oct_xy, uint8_t* oct_resp, int* oct_count, int* status, int B);
+// ORBGPU_SEM_SCORE_HARRIS option: rewrite the response key of each candidate of levels [lb, le) with its Harris key
+void og_launch_harris(hipStream_t s, const OgPlan& P, int lb, int le, const uint8_t* img0, long long pitch0,
+                      long long fstride0, const uint8_t* pyr, unsigned long long* cand, const int* cand_count, int B);
+// octree of levels [lb, le)
+void og_launch_octree(hipStream_t s, const OgPlan& P, int lb, int le, const unsigned long long* cand,
+                      const int* cand_count, uint16_t* node_of, uint32_t* oct_xy, uint32_t* oct_resp, int* oct_count,
+                      int* status, int B);
 void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, long long pitch0, long long fstride0,
-                        const uint8_t* pyr, const uint32_t* oct_xy, const uint8_t* oct_resp, const int* oct_count,
+                        const uint8_t* pyr, const uint32_t* oct_xy, const uint32_t* oct_resp, const int* oct_count,
                         orbgpu_kp_dev* kps, uint8_t* desc, int* counts, int B);
 void og_launch_grid(hipStream_t s, const orbgpu_kp_dev* kps, const int* counts, int frame_cap, OgGridGeom G,
                     int* cell_start, int* cell_items, int* status, int B);
@@ -209,6 +214,10 @@ struct OgUndistort {
 void og_launch_undistort(hipStream_t s, const orbgpu_kp_dev* in, orbgpu_kp_dev* out, const int* counts, int n_fixed,
                          int frame_cap, const OgUndistort& U, int B);
 void og_launch_undistort_points(hipStream_t s, const float* xy, float* out, int n, const OgUndistort& U);
+// single-frame download: status, count, keypoints and descriptors of frame 0 into a pinned host block
+// {status, count, 0, 0, frame_cap x 28 B, frame_cap x 32 B} (host_dev: its device-side address)
+void og_launch_pack_host(hipStream_t s, const int* status, const int* counts, const orbgpu_kp_dev* kps,
+                         const uint8_t* desc, int frame_cap, void* host_dev);
 // Frame::ComputeStereoFromRGBD over B frames (counts == nullptr: one frame of n_fixed keypoints); depth rows
 // are `pitch` bytes apart, frames `fstride` bytes; is_u16: raw CV_16U scaled by `factor`, else CV_32F
 void og_launch_gray(hipStream_t s, const uint8_t* src, int cols, int rows, int cn, int bidx, long long spitch,

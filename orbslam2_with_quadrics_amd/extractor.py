@@ -25,13 +25,14 @@ class ORBextractor:
     """ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST) on HIP device `device`."""
 
     def __init__(self, nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int, minThFAST: int,
-                 device: int = 0, semantics: int = _lib.SEM_DEFAULT):
+                 device: int = 0, semantics: int | None = None):
         self._L = _lib.lib()
         self._ctx = self._L.orbgpu_create(device, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
         if not self._ctx:
             raise RuntimeError("orbgpu_create failed (no HIP device visible, or invalid parameters)")
         self.nfeatures, self.nlevels = nfeatures, nlevels
-        self.set_semantics(semantics)
+        # None: the context's own choice (SEM_DEFAULT, plus SEM_SCORE_HARRIS when ORBGPU_SCORE_HARRIS=1)
+        self.set_semantics(self._L.orbgpu_get_semantics(self._ctx) if semantics is None else semantics)
 
     def set_semantics(self, flags: int):
         """OpenCV/compiler behaviours to reproduce (_lib.SEM_*, include/orbgpu.h ORBGPU_SEM_*)."""
@@ -223,7 +224,7 @@ class ORBextractor:
         if n < 0:
             _lib.check(self._ctx, n, "orbgpu_debug_octree")
         xy = np.zeros(max(n, 1), np.uint32)
-        resp = np.zeros(max(n, 1), np.uint8)
+        resp = np.zeros(max(n, 1), np.uint32)  # response keys (FAST score, or the Harris key)
         self._L.orbgpu_debug_octree(self._ctx, b, level, _p(xy), _p(resp), n)
         return (xy[:n] & 0xFFFF).astype(np.int32), (xy[:n] >> 16).astype(np.int32), resp[:n]
 

@@ -107,7 +107,7 @@ def test_rbrief_rotation_probe(gpu, sem):
 
 def test_semantics_switch_rejects_unknown_flags(gpu):
     ex = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
-    for bad in (0x40, 0x80, 4 << 2, 7 << 2):
+    for bad in (0x80, 0x100, 4 << 2, 7 << 2):
         with pytest.raises(RuntimeError, match="semantics"):
             ex.set_semantics(bad)
     assert ex._L.orbgpu_get_semantics(ex.ctx) == 0
