@@ -1603,6 +1603,8 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     // final-phase planning only: the candidates' (size, creation id) keys, in the previous round's (dead) childPos
     u64* skey = (u64*)childPos;
     u64* best = (u64*)childCnt;  // [OG_OCT_MAXL], final key pass only
+    // table mode (below): each list node's index in the depth tables (childCnt) / position table (childPos)
+    __shared__ uint16_t npath[2][OG_OCT_MAXL];
     __shared__ int wsum[32];
     __shared__ int sv[16];
 
@@ -1621,10 +1623,126 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 
     OCT_PROF(0, clock64());
     OCT_PROF(1, (unsigned long long)C);
-    // ---- roots (src/ORBextractor.cc:552-585) and the children of the first pass's splits, in ONE key pass:
+    // ---- table mode.  A node's bounds follow from its root by the fixed halving of DivideNode (:481-537), so the
+    // node containing a key at depth d is a function of the key alone: path p_0 = root, p_d = 4 p_(d-1) + quadrant.
+    // ONE key pass counts every key at its depth-D node (D = the deepest depth whose tables of all depths fit the
+    // 4 x OG_OCT_MAXL ints of childCnt); the counts of depths < D are sums of their children.  The rounds then read
+    // their children counts from the tables instead of re-reading the keys (no per-round key pass), and NO[k] holds
+    // the key's depth-D table index.  The last pass maps that index to the key's final node through a position
+    // table (childPos) filled down from each listed node to its depth-D descendants.  A round whose next split
+    // candidates include a depth-D node leaves table mode: one key pass moves NO[] to list positions and counts the
+    // next children as the per-round passes below do (og_octree_profile: the level-0 workgroup's key passes were
+    // ~60 % of its time, and each re-read every key -- DESIGN.md §5).
+    int D = 0;
+    {
+        int tot = nIni, w = nIni;
+        while (D < 7 && tot + 4 * w <= 4 * OG_OCT_MAXL) {
+            w *= 4;
+            tot += w;
+            D++;
+        }
+    }
+    auto tbase = [nIni](int d) { return nIni * (((1 << (2 * d)) - 1) / 3); };  // first table index of depth d
+    auto tdepth = [&](int t) {  // depth of table index t
+        int d = 0;
+        while (d < D && t >= tbase(d + 1)) d++;
+        return d;
+    };
+    auto tchild = [&](int t, int q) {
+        const int d = tdepth(t);
+        return tbase(d + 1) + 4 * (t - tbase(d)) + q;
+    };
+    const int Ttot = tbase(D + 1);
+    bool tmode = D >= 1;  // workgroup-uniform
+    if (tmode) {
+        for (int q = tid; q < Ttot; q += OCT_NT) childCnt[q] = 0;
+        __syncthreads();
+        const int bD = tbase(D);
+        for (int base = tid; base < C; base += OCT_NT * OCT_U) {
+            uint32_t kv[OCT_U];
+#pragma unroll
+            for (int u = 0; u < OCT_U; u++) {
+                const int k = base + u * OCT_NT;
+                kv[u] = k < C ? K32[2 * k] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < OCT_U; u++) {
+                const int k = base + u * OCT_NT;
+                int a = 0;
+                if (k < C) {
+                    const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
+                    const int r = min((int)((float)x / L.hX), nIni - 1);
+                    int x0 = (int)(L.hX * (float)r), x1 = (int)(L.hX * (float)(r + 1)), y0 = 0, y1 = H;
+                    int pth = r;
+                    for (int d = 0; d < D; d++) {  // og_quadrant / og_child
+                        const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
+                        const int qx = x >= mx, qy = y >= my;
+                        x0 = qx ? mx : x0;
+                        x1 = qx ? x1 : mx;
+                        y0 = qy ? my : y0;
+                        y1 = qy ? y1 : my;
+                        pth = 4 * pth + qx + 2 * qy;
+                    }
+                    a = bD + pth;
+                    NO[k] = (uint16_t)a;
+                }
+                og_wave_count(childCnt, a, k < C);
+            }
+        }
+        __syncthreads();
+        for (int d = D - 1; d >= 0; d--) {  // counts of shallower depths: sums of the four children
+            const int b0 = tbase(d), b1 = tbase(d + 1), n = b1 - b0;
+            for (int e = tid; e < n; e += OCT_NT)
+                childCnt[b0 + e] = childCnt[b1 + 4 * e] + childCnt[b1 + 4 * e + 1] + childCnt[b1 + 4 * e + 2] +
+                                   childCnt[b1 + 4 * e + 3];
+            __syncthreads();
+        }
+        if (tid == 0) {
+            int Ln = 0;
+            for (int r = 0; r < nIni; r++) {
+                const int c = childCnt[r];
+                if (c > 0) {
+                    OctNode n;
+                    n.x0 = (short)(int)(L.hX * (float)r);
+                    n.x1 = (short)(int)(L.hX * (float)(r + 1));
+                    n.y0 = 0;
+                    n.y1 = (short)H;
+                    n.cnt = c;
+                    n.cid = r;
+                    nodes[0][Ln] = n;
+                    fresh[0][Ln] = 0;
+                    npath[0][Ln] = (uint16_t)r;
+                    Ln++;
+                }
+            }
+            sv[0] = Ln;
+            sv[1] = 0;
+            sv[2] = nIni;
+            sv[3] = Ln == 0;
+            sv[4] = 0;
+            sv[8] = 0;
+        }
+        __syncthreads();
+    }
+    // position table of list `lst` (childPos): every depth-D index -> the list position of its listed ancestor
+    auto pos_table = [&](int lst, int Lcount) {
+        uint16_t* PT = childPos;
+        for (int e = tid; e < Ttot; e += OCT_NT) PT[e] = 0xffff;
+        __syncthreads();
+        for (int q = tid; q < Lcount; q += OCT_NT) PT[npath[lst][q]] = (uint16_t)q;
+        __syncthreads();
+        for (int d = 1; d <= D; d++) {
+            const int b0 = tbase(d - 1), b1 = tbase(d), n = tbase(d + 1) - b1;
+            for (int e = tid; e < n; e += OCT_NT)
+                if (PT[b1 + e] == 0xffff) PT[b1 + e] = PT[b0 + (e >> 2)];
+            __syncthreads();
+        }
+    };
+    // ---- (no table mode) roots (src/ORBextractor.cc:552-585) and the children of the first pass's splits, in ONE key pass:
     // each key's root r = x / hX and its quadrant in that root are counted together (childCnt[4r + q]); a root's
     // size is the sum of its four quadrant counts.  NO[k] holds the root id until the first round's key pass,
     // which maps it to the root's list position through aux[] (`noRoot`).
+    if (!tmode) {
     for (int q = tid; q < 4 * nIni; q += OCT_NT) childCnt[q] = 0;
     __syncthreads();
     for (int base = tid; base < C; base += OCT_NT * OCT_U) {
@@ -1687,7 +1805,8 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         sv[8] = 0;       // `best` filled by a key pass
     }
     __syncthreads();
-    bool noRoot = true;  // NO[] holds root ids (workgroup-uniform)
+    }
+    bool noRoot = !tmode;  // NO[] holds root ids (workgroup-uniform)
 
     OCT_PROF(2, clock64());
     for (int round = 0; round < 4096; round++) {
@@ -1744,7 +1863,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             sn = splitNode[i];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const int c = CC[4 * sn + q];
+                const int c = tmode ? CC[tchild(npath[cur][sn], q)] : CC[4 * sn + q];
                 nc += c > 0;
                 nexp += c > 1;
             }
@@ -1771,17 +1890,20 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             // the key pass's remap record of node sn: its split point here, its children's positions below
             newPos[sn] = (par.x0 + ((par.x1 - par.x0 + 1) >> 1)) | ((par.y0 + ((par.y1 - par.y0 + 1) >> 1)) << 16);
             int before = 0;  // non-empty children among q' < q (creation order n1..n4)
+            const int tp = tmode ? (int)npath[cur][sn] : 0;
             for (int q = 0; q < 4; q++) {
-                const int c = CC[4 * sn + q];
+                const int tc = tmode ? tchild(tp, q) : 0;
+                const int c = tmode ? CC[tc] : CC[4 * sn + q];
                 if (c > 0) {
                     const int pos = groupStart + (nc - before - 1);
                     OctNode ch = og_child(par, q);
                     ch.cnt = c;
                     ch.cid = cidBase + before;
-                    childPos[4 * sn + q] = (uint16_t)pos;
+                    if (!tmode) childPos[4 * sn + q] = (uint16_t)pos;
                     if (pos < OG_OCT_MAXL) {
                         nn[pos] = ch;
                         nf[pos] = 1;
+                        npath[cur ^ 1][pos] = (uint16_t)tc;
                     }
                     before++;
                 }
@@ -1795,10 +1917,11 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             const int pos = T + kr;
             // remap record of a kept node: split point (0, 0) selects quadrant 3, and all four entries are pos
             newPos[i] = 0;
-            ((u64*)childPos)[i] = (u64)(uint16_t)pos * 0x0001000100010001ull;
+            if (!tmode) ((u64*)childPos)[i] = (u64)(uint16_t)pos * 0x0001000100010001ull;
             if (pos < OG_OCT_MAXL) {
                 nn[pos] = cn[i];
                 nf[pos] = 0;
+                npath[cur ^ 1][pos] = npath[cur][i];
             }
         }
         int expTot;
@@ -1821,7 +1944,20 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         } else {
             if (Lnew >= N || Lnew == Ln) done = 1;
         }
-        for (int q = tid; q < 4 * Lnew; q += OCT_NT) NCC[q] = 0;
+        // table mode: leave it when a next-round split candidate is a depth-D node (its children have no table)
+        bool leave = false;
+        if (tmode && !done) {
+            if (tid == 0) sv[10] = 0;
+            __syncthreads();
+            for (int q = tid; q < Lnew; q += OCT_NT) {
+                const OctNode& nd = nn[q];
+                if (nd.cnt > 1 && (nextMode == 0 || nf[q]) && tdepth(npath[cur ^ 1][q]) >= D) sv[10] = 1;
+            }
+            __syncthreads();
+            leave = sv[10] != 0;
+        }
+        if (!tmode || leave)
+            for (int q = tid; q < 4 * Lnew; q += OCT_NT) NCC[q] = 0;
         if (done) {
             for (int q = tid; q < Lnew; q += OCT_NT) best[q] = 0ull;
         } else {
@@ -1837,6 +1973,18 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         __syncthreads();
         OCT_PROF(10 + 4 * round, clock64());
         OCT_PROF(11 + 4 * round, (unsigned long long)S | ((unsigned long long)A << 32));
+        if (tmode && !done && !leave) {  // table mode: the next round's counts are in the tables, no key pass
+            if (tid == 0) {
+                sv[0] = Lnew;
+                sv[1] = nextMode;
+                sv[2] += T;
+                sv[3] = 0;
+                sv[4] = cur ^ 1;
+            }
+            __syncthreads();
+            continue;
+        }
+        if (tmode) pos_table(cur ^ 1, Lnew);  // NO[k] (depth-D index) -> new list position
         // ---- one pass over the keys: move to the new list position, and either count the children of
         // the next round's split candidates or (last round) keep the best key per node (:744-760)
         for (int base = tid; base < C; base += OCT_NT * OCT_U) {
@@ -1854,14 +2002,19 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 int a = 0;
                 bool cnt = false;
                 if (k < C) {
-                    const int n = noRoot ? aux[no[u]] : no[u];
                     const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
-                    // remap record: the node's split point (newPos) and its four target positions (childPos)
-                    const int mm = newPos[n];
-                    const u64 tp = ((const u64*)childPos)[n];
-                    const int q = (x >= (mm & 0xffff) ? 1 : 0) | (y >= (mm >> 16) ? 2 : 0);  // og_quadrant
-                    const int n2 = (int)((tp >> (16 * q)) & 0xffffu);
-                    NO[k] = (uint16_t)n2;
+                    int n2;
+                    if (tmode) {
+                        n2 = childPos[no[u]];
+                    } else {
+                        const int n = noRoot ? aux[no[u]] : no[u];
+                        // remap record: the node's split point (newPos) and its four target positions (childPos)
+                        const int mm = newPos[n];
+                        const u64 tp = ((const u64*)childPos)[n];
+                        const int q = (x >= (mm & 0xffff) ? 1 : 0) | (y >= (mm >> 16) ? 2 : 0);  // og_quadrant
+                        n2 = (int)((tp >> (16 * q)) & 0xffffu);
+                    }
+                    if (!done) NO[k] = (uint16_t)n2;
                     if (done) {
                         const unsigned resp = K32[2 * k + 1];
                         atomicMax(&best[n2], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
@@ -1876,6 +2029,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         }
         __syncthreads();
         noRoot = false;
+        tmode = false;  // NO[] now holds list positions (or the pass was the last one)
         if (tid == 0) {
             sv[0] = Lnew;
             sv[1] = nextMode;
@@ -1890,6 +2044,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     OCT_PROF(3, clock64());
     const int Ln = sv[0];
     if (!sv[8]) {  // finished without a final key pass (empty split set): one pass for the best key
+        if (tmode) pos_table(sv[4], Ln);  // (childPos: dead after the plan)
         for (int n = tid; n < Ln; n += OCT_NT) best[n] = 0ull;
         __syncthreads();
         for (int base = tid; base < C; base += OCT_NT * OCT_U) {
@@ -1907,7 +2062,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 if (k < C) {
                     const int x = (int)(kv[u] & 0xffff), y = (int)((kv[u] >> 16) & 0xffff);
                     const unsigned resp = (unsigned)(kv[u] >> 32);
-                    atomicMax(&best[noRoot ? aux[no[u]] : no[u]],
+                    atomicMax(&best[tmode ? (int)childPos[no[u]] : (noRoot ? aux[no[u]] : no[u])],
                               ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
                 }
             }
