@@ -1457,31 +1457,31 @@ struct OctNode {
 
 #define OCT_NT 1024
 
-// exclusive block scan of one int per thread; returns the exclusive prefix, *total = sum
+// inclusive scan over the 64 lanes (all active) with DPP, no LDS round trips: row_shr 1, 2, 4, 8 within rows of 16,
+// then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) carry the row totals
+__device__ __forceinline__ int og_wave_incl_scan(int x)
+{
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+    return x;
+}
+
+// exclusive block scan of one int per thread; returns the exclusive prefix, *total = sum.  Every wave scans the
+// per-wave totals itself (no third barrier for a wave-0 pass).
 __device__ __forceinline__ int og_block_excl_scan(int v, int* wsum, int* total)
 {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int x = og_wave_incl_scan(v);
     if (lane == 63) wsum[w] = x;
     __syncthreads();
-    if (w == 0) {
-        const int nw = blockDim.x >> 6;
-        int s = lane < nw ? wsum[lane] : 0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(s, o);
-            if (lane >= o) s += y;
-        }
-        if (lane < nw) wsum[lane] = s;  // inclusive per-wave totals
-    }
-    __syncthreads();
-    const int before = w ? wsum[w - 1] : 0;
-    *total = wsum[(blockDim.x >> 6) - 1];
+    const int nw = blockDim.x >> 6;
+    const int s = og_wave_incl_scan(lane < nw ? wsum[lane] : 0);
+    const int before = w ? __builtin_amdgcn_readlane(s, w - 1) : 0;
+    *total = __builtin_amdgcn_readlane(s, nw - 1);
     __syncthreads();
     return before + x - v;
 }
@@ -1516,6 +1516,43 @@ __device__ __forceinline__ unsigned og_cand_order(int x, int y, const OgLevel& L
     return (unsigned)(((ci * L.nCols + cj) * L.hCell + ly) * L.wCell + lx);
 }
 
+// og_cand_order with the two divisions as multiply-high by m = floor((2^32 - 1) / d) + 1 (exact for n < 2^16 and
+// d < 2^16; wCell, hCell <= 255 and level coordinates < 2^16 are checked by the plan)
+__device__ __forceinline__ unsigned og_cand_order_m(int x, int y, const OgLevel& L, unsigned mW, unsigned mH)
+{
+    const unsigned yy = (unsigned)(y - 3), xx = (unsigned)(x - 3);
+    const unsigned ci = __umulhi(yy, mH), cj = __umulhi(xx, mW);
+    const unsigned ly = yy - ci * (unsigned)L.hCell, lx = xx - cj * (unsigned)L.wCell;
+    return ((ci * (unsigned)L.nCols + cj) * (unsigned)L.hCell + ly) * (unsigned)L.wCell + lx;
+}
+
+// atomicMax(&ctr[addr], v) for every active lane, one LDS atomic per run of equal addresses: a segmented max with
+// DPP (row_shr 1/2/4/8, then row_bcast 15/31, each step taking the shifted lane's value only when its address is
+// the lane's own), after which the last lane of every run holds the run's maximum.  A shifted lane of another run
+// with the same address only adds a value of the same counter, so merging it is harmless.  Wave-uniform control
+// flow.  The final key pass's per-node maximum: its keys arrive in candidate order, so a wave's lanes fall into a
+// few nodes and plain atomics serialise on them (~45 % of that pass, tools/octree_profile.py --variant noatom).
+__device__ __forceinline__ void og_wave_max32(unsigned* ctr, int addr, unsigned v, bool act)
+{
+    const int a = act ? addr : -1;
+    unsigned x = act ? v : 0u;
+#define OG_SEGMAX_STEP(ctrl, rm)                                                                     \
+    {                                                                                                \
+        const int sa = __builtin_amdgcn_update_dpp(-2, a, ctrl, rm, 0xf, false);                     \
+        const unsigned sx = (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, rm, 0xf, false); \
+        x = (sa == a && sx > x) ? sx : x;                                                            \
+    }
+    OG_SEGMAX_STEP(0x111, 0xf)
+    OG_SEGMAX_STEP(0x112, 0xf)
+    OG_SEGMAX_STEP(0x114, 0xf)
+    OG_SEGMAX_STEP(0x118, 0xf)
+    OG_SEGMAX_STEP(0x142, 0xa)
+    OG_SEGMAX_STEP(0x143, 0xc)
+#undef OG_SEGMAX_STEP
+    const int nxt = __builtin_amdgcn_update_dpp(-2, a, 0x130, 0xf, 0xf, false);  // wave_shl:1 (lane + 1)
+    if (act && nxt != a) atomicMax(&ctr[addr], x);
+}
+
 // atomicAdd(&ctr[addr], 1) for every active lane, one LDS atomic per DISTINCT address of the wave: the
 // wave's keys are consecutive FAST outputs (one block's corners), so they fall into few nodes and plain
 // atomics would serialise on the same counters.  Wave-uniform control flow; exact counts.
@@ -1533,7 +1570,7 @@ __device__ __forceinline__ void og_wave_count(int* ctr, int addr, bool act)
     {
         const int lane = threadIdx.x & 63;
         const int a = act ? addr : -1;
-        const int prev = __shfl_up(a, 1);
+        const int prev = __builtin_amdgcn_update_dpp(-1, a, 0x138, 0xf, 0xf, false);  // wave_shr:1 (lane - 1)
         const bool head = act && (lane == 0 || prev != a);
         const u64 heads = og_ballot(head);
         const u64 actm = og_ballot(act);
@@ -1654,8 +1691,44 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     };
     const int Ttot = tbase(D + 1);
     bool tmode = D >= 1;  // workgroup-uniform
+    const unsigned mW = 0xffffffffu / (unsigned)L.wCell + 1u, mH = 0xffffffffu / (unsigned)L.hCell + 1u;
+    // the per-node best key in 32 bits when it fits: FAST score (8 bits) << 24 | 0xffffff - candidate order (the
+    // order is below nRows hCell nCols wCell <= 2^24); the Harris option's 32-bit keys keep the 64-bit form
+    const bool k32 = !(P.sem & ORBGPU_SEM_SCORE_HARRIS) &&
+                     (unsigned)(L.nRows * L.hCell) * (unsigned)(L.nCols * L.wCell) <= 0xffffffu;
+    unsigned* best32 = (unsigned*)childCnt;
     if (tmode) {
         for (int q = tid; q < Ttot; q += OCT_NT) childCnt[q] = 0;
+        // the depth-D path is separable: x alone picks the root and the x halves, y alone the y halves.  Per-column
+        // and per-row tables (in childPos, free until the position table) hold them with the quadrant bits already
+        // spread (x at even bit positions with the root above them, y at odd): path = XT[x] | YT[y]
+        const int Wx = L.maxBX - L.minB + 1, Hy = H + 1;
+        const bool xyt = Wx + Hy <= 4 * OG_OCT_MAXL;  // workgroup-uniform
+        uint16_t* XT = childPos;
+        uint16_t* YT = childPos + Wx;
+        if (xyt) {
+            for (int x = tid; x < Wx; x += OCT_NT) {
+                const int r = min((int)((float)x / L.hX), nIni - 1);
+                int x0 = (int)(L.hX * (float)r), x1 = (int)(L.hX * (float)(r + 1)), m = r;
+                for (int d = 0; d < D; d++) {
+                    const int mx = x0 + ((x1 - x0 + 1) >> 1), qx = x >= mx;
+                    x0 = qx ? mx : x0;
+                    x1 = qx ? x1 : mx;
+                    m = (m << 2) | qx;
+                }
+                XT[x] = (uint16_t)m;
+            }
+            for (int y = tid; y < Hy; y += OCT_NT) {
+                int y0 = 0, y1 = H, m = 0;
+                for (int d = 0; d < D; d++) {
+                    const int my = y0 + ((y1 - y0 + 1) >> 1), qy = y >= my;
+                    y0 = qy ? my : y0;
+                    y1 = qy ? y1 : my;
+                    m = (m << 2) | (qy << 1);
+                }
+                YT[y] = (uint16_t)m;
+            }
+        }
         __syncthreads();
         const int bD = tbase(D);
         for (int base = tid; base < C; base += OCT_NT * OCT_U) {
@@ -1671,17 +1744,22 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 int a = 0;
                 if (k < C) {
                     const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
-                    const int r = min((int)((float)x / L.hX), nIni - 1);
-                    int x0 = (int)(L.hX * (float)r), x1 = (int)(L.hX * (float)(r + 1)), y0 = 0, y1 = H;
-                    int pth = r;
-                    for (int d = 0; d < D; d++) {  // og_quadrant / og_child
-                        const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
-                        const int qx = x >= mx, qy = y >= my;
-                        x0 = qx ? mx : x0;
-                        x1 = qx ? x1 : mx;
-                        y0 = qy ? my : y0;
-                        y1 = qy ? y1 : my;
-                        pth = 4 * pth + qx + 2 * qy;
+                    int pth;
+                    if (xyt) {
+                        pth = XT[x] | YT[y];
+                    } else {
+                        const int r = min((int)((float)x / L.hX), nIni - 1);
+                        int x0 = (int)(L.hX * (float)r), x1 = (int)(L.hX * (float)(r + 1)), y0 = 0, y1 = H;
+                        pth = r;
+                        for (int d = 0; d < D; d++) {  // og_quadrant / og_child
+                            const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
+                            const int qx = x >= mx, qy = y >= my;
+                            x0 = qx ? mx : x0;
+                            x1 = qx ? x1 : mx;
+                            y0 = qy ? my : y0;
+                            y1 = qy ? y1 : my;
+                            pth = 4 * pth + qx + 2 * qy;
+                        }
                     }
                     a = bD + pth;
                     NO[k] = (uint16_t)a;
@@ -1820,13 +1898,15 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         uint8_t* nf = fresh[cur ^ 1];
         const int* CC = childCnt;
         int* NCC = childCnt;
+        if (tid == 0) sv[10] = 0;  // table-mode leave flags of this round
         __syncthreads();
         // ---- the split set of this round and its order
         const int i = tid;
-        int S;
+        int S, exSplit = 0;
         if (mode == 0) {
             const bool flag = i < Ln && cn[i].cnt > 1;
             const int rank = og_block_excl_scan(flag ? 1 : 0, wsum, &S);
+            exSplit = rank;
             if (i < Ln) splitRank[i] = flag ? rank : -1;
             if (flag) splitNode[rank] = i;
         } else {
@@ -1851,6 +1931,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 splitNode[rank] = i;
             }
         }
+        OCT_PROF(200 + 8 * (round & 3), clock64());
         if (S == 0) {  // nothing to split: size == prevSize -> bFinish
             if (tid == 0) sv[3] = 1;
             __syncthreads();
@@ -1868,9 +1949,12 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 nexp += c > 1;
             }
         }
-        int totNc;
-        const int exNc = og_block_excl_scan(nc, wsum, &totNc);
-        int A = S;
+        OCT_PROF(201 + 8 * (round & 3), clock64());
+        // one scan for the children counts and (mode 0) the expandable children: both sums <= 4 OG_OCT_MAXL < 2^16
+        int totP;
+        const int exP = og_block_excl_scan(nc | (nexp << 16), wsum, &totP);
+        const int exNc = exP & 0xffff;
+        int A = S, T = totP & 0xffff;
         if (mode == 1) {
             const bool reach = i < S && (Ln + exNc + nc - (i + 1) >= N);
             if (tid == 0) sv[5] = S;
@@ -1878,10 +1962,11 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             if (reach) atomicMin(&sv[5], i + 1);
             __syncthreads();
             A = sv[5];
+            if (i == A - 1) sv[6] = exNc + nc;
+            __syncthreads();
+            T = sv[6];
         }
-        if (i == A - 1) sv[6] = exNc + nc;
-        __syncthreads();
-        const int T = sv[6];
+        OCT_PROF(202 + 8 * (round & 3), clock64());
         // ---- children: groups in reverse split order, each n4,n3,n2,n1 (push_front, :621-660)
         if (i < A) {
             const OctNode par = cn[sn];
@@ -1905,14 +1990,20 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                         nf[pos] = 1;
                         npath[cur ^ 1][pos] = (uint16_t)tc;
                     }
+                    if (tmode && c > 1 && tdepth(tc) >= D) atomicOr(&sv[10], 1);  // a fresh split candidate at depth D
                     before++;
                 }
             }
         }
-        // ---- kept nodes follow, in their old order
+        // ---- kept nodes follow, in their old order (mode 0: every unsplit node, ranked by the split-set scan)
         const bool kept = i < Ln && (splitRank[i] < 0 || splitRank[i] >= A);
-        int keptTot;
-        const int kr = og_block_excl_scan(kept ? 1 : 0, wsum, &keptTot);
+        int keptTot, kr;
+        if (mode == 0) {
+            kr = i - exSplit;
+            keptTot = Ln - S;
+        } else {
+            kr = og_block_excl_scan(kept ? 1 : 0, wsum, &keptTot);
+        }
         if (kept) {
             const int pos = T + kr;
             // remap record of a kept node: split point (0, 0) selects quadrant 3, and all four entries are pos
@@ -1923,9 +2014,12 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 nf[pos] = 0;
                 npath[cur ^ 1][pos] = npath[cur][i];
             }
+            if (tmode && cn[i].cnt > 1 && tdepth(npath[cur][i]) >= D) atomicOr(&sv[10], 2);  // splits if mode 0
         }
-        int expTot;
-        (void)og_block_excl_scan(i < A ? nexp : 0, wsum, &expTot);
+        const int expTot = totP >> 16;  // mode 0 (A = S): expandable children of all splits
+        OCT_PROF(203 + 8 * (round & 3), clock64());
+        __syncthreads();  // the new list and the leave flags are complete
+        OCT_PROF(204 + 8 * (round & 3), clock64());
         const int Lnew = T + keptTot;
         if (Lnew > OG_OCT_MAXL) {
             if (tid == 0) {
@@ -1944,23 +2038,18 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         } else {
             if (Lnew >= N || Lnew == Ln) done = 1;
         }
-        // table mode: leave it when a next-round split candidate is a depth-D node (its children have no table)
+        // table mode: leave it when a next-round split candidate is a depth-D node (its children have no table):
+        // a fresh child with more than one key, or (the next round splits every such node) a kept one
         bool leave = false;
         if (tmode && !done) {
-            if (tid == 0) sv[10] = 0;
-            __syncthreads();
-            for (int q = tid; q < Lnew; q += OCT_NT) {
-                const OctNode& nd = nn[q];
-                if (nd.cnt > 1 && (nextMode == 0 || nf[q]) && tdepth(npath[cur ^ 1][q]) >= D) sv[10] = 1;
-            }
-            __syncthreads();
-            leave = sv[10] != 0;
+            const int lf = sv[10];
+            leave = (lf & 1) || (nextMode == 0 && (lf & 2));
         }
         if (!tmode || leave)
             for (int q = tid; q < 4 * Lnew; q += OCT_NT) NCC[q] = 0;
         if (done) {
             for (int q = tid; q < Lnew; q += OCT_NT) best[q] = 0ull;
-        } else {
+        } else if (!tmode || leave) {
             // counting record of every node of the new list (splitRank is dead until the next round's plan):
             // split point x | y << 15, bit 30 = the node is a split candidate of the next round
             for (int q = tid; q < Lnew; q += OCT_NT) {
@@ -2001,6 +2090,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 const int k = base + u * OCT_NT;
                 int a = 0;
                 bool cnt = false;
+                unsigned key32 = 0;
                 if (k < C) {
                     const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
                     int n2;
@@ -2017,14 +2107,31 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                     if (!done) NO[k] = (uint16_t)n2;
                     if (done) {
                         const unsigned resp = K32[2 * k + 1];
-                        atomicMax(&best[n2], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
+#ifndef OG_EXP_OCT_FINAL
+#define OG_EXP_OCT_FINAL 0  // timing experiments only (tools/octree_profile.py --variant): 1 no atomic, 2 no order
+#endif
+#if OG_EXP_OCT_FINAL == 1
+                        const u64 kk = ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order_m(x, y, L, mW, mH));
+                        if (kk == 0x123456789abcull) best[n2] = kk;
+#elif OG_EXP_OCT_FINAL == 2
+                        atomicMax(&best[n2], ((u64)resp << 32) | (u64)(unsigned)(x ^ y));
+#else
+                        if (k32) {
+                            key32 = (resp << 24) | (0xffffffu - og_cand_order_m(x, y, L, mW, mH));
+                            a = n2;
+                        } else {
+                            atomicMax(&best[n2],
+                                      ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order_m(x, y, L, mW, mH)));
+                        }
+#endif
                     } else {
                         const int rc = splitRank[n2];
                         cnt = (rc >> 30) & 1;
                         a = 4 * n2 + ((x >= (rc & 0x7fff) ? 1 : 0) | (y >= ((rc >> 15) & 0x7fff) ? 2 : 0));
                     }
                 }
-                if (!done) og_wave_count(NCC, a, cnt);  // `done` is workgroup-uniform
+                if (!done) og_wave_count(NCC, a, cnt);  // `done`, k32 are workgroup-uniform
+                else if (k32 && !OG_EXP_OCT_FINAL) og_wave_max32(best32, a, key32, k < C);
             }
         }
         __syncthreads();
@@ -2059,19 +2166,25 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 #pragma unroll
             for (int u = 0; u < OCT_U; u++) {
                 const int k = base + u * OCT_NT;
+                int n = 0;
+                unsigned key32 = 0;
                 if (k < C) {
                     const int x = (int)(kv[u] & 0xffff), y = (int)((kv[u] >> 16) & 0xffff);
                     const unsigned resp = (unsigned)(kv[u] >> 32);
-                    atomicMax(&best[tmode ? (int)childPos[no[u]] : (noRoot ? aux[no[u]] : no[u])],
-                              ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order(x, y, L)));
+                    n = tmode ? (int)childPos[no[u]] : (noRoot ? aux[no[u]] : no[u]);
+                    if (k32)
+                        key32 = (resp << 24) | (0xffffffu - og_cand_order_m(x, y, L, mW, mH));
+                    else
+                        atomicMax(&best[n], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order_m(x, y, L, mW, mH)));
                 }
+                if (k32) og_wave_max32(best32, n, key32, k < C);
             }
         }
         __syncthreads();
     }
     const int nout = min(Ln, L.kcap);
     for (int n = tid; n < nout; n += OCT_NT) {
-        const u64 b = best[n];
+        const u64 b = k32 ? ((u64)(best32[n] >> 24) << 32) | (0xff000000u | (best32[n] & 0xffffffu)) : best[n];
         const unsigned ord = 0xffffffffu - (unsigned)(b & 0xffffffffu);
         const int lx = ord % L.wCell;
         unsigned t2 = ord / L.wCell;

@@ -10,14 +10,17 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VLIB = os.path.join(ROOT, "orbslam2_with_quadrics_amd", "variants", "liborbgpu_octprof.so")
+# --variant NAME: timing experiments of the final key pass (results wrong): noatom (no atomicMax), noorder
+VARIANTS = {"": [], "noatom": ["OG_EXP_OCT_FINAL=1"], "noorder": ["OG_EXP_OCT_FINAL=2"]}
+VAR = sys.argv[sys.argv.index("--variant") + 1] if "--variant" in sys.argv else ""
+VLIB = os.path.join(ROOT, "orbslam2_with_quadrics_amd", "variants", f"liborbgpu_octprof{VAR}.so")
 
 
 def build():
     from orbslam2_with_quadrics_amd import build_ext
 
     os.makedirs(os.path.dirname(VLIB), exist_ok=True)
-    print(build_ext.build(force=True, defines=["OG_OCT_PROFILE=1"], out=VLIB))
+    print(build_ext.build(force=True, defines=["OG_OCT_PROFILE=1", *VARIANTS[VAR]], out=VLIB))
 
 
 def run():
@@ -49,6 +52,10 @@ def run():
               f"plan={tm - ts} keypass={nxt - tm} cycles")
         r += 1
     print("tail (final best pass + output)", int(buf[4]) - int(buf[3]), "cycles; total", int(buf[4]) - t0)
+    for r in range(min(r, 4)):  # plan phases of rounds 0-3: split set | S check | children scan | children+kept | barrier
+        ts = int(buf[8 + 4 * r])
+        marks = [int(buf[200 + 8 * r + j]) for j in range(5)]
+        print(f"round {r} plan phases:", [m - p for m, p in zip(marks, [ts] + marks[:-1])])
     ex.device_free(d)
 
 
