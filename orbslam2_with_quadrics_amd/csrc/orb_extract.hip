@@ -1679,15 +1679,12 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             D++;
         }
     }
-    auto tbase = [nIni](int d) { return nIni * (((1 << (2 * d)) - 1) / 3); };  // first table index of depth d
-    auto tdepth = [&](int t) {  // depth of table index t
-        int d = 0;
-        while (d < D && t >= tbase(d + 1)) d++;
-        return d;
-    };
-    auto tchild = [&](int t, int q) {
-        const int d = tdepth(t);
-        return tbase(d + 1) + 4 * (t - tbase(d)) + q;
+    // first table index of depth d: nIni (4^d - 1) / 3, and (4^d - 1) / 3 is 0b0101...01 (d ones)
+    auto tbase = [nIni](int d) { return nIni * (int)(0x55555555u & ((1u << (2 * d)) - 1u)); };
+    // a list node's npath entry: table index | depth << 12 (indices < 4 OG_OCT_MAXL = 2^12)
+    auto tchild = [&](int e, int q) {  // the npath entry of child q
+        const int t = e & 0xfff, d = e >> 12;
+        return (tbase(d + 1) + 4 * (t - tbase(d)) + q) | ((d + 1) << 12);
     };
     const int Ttot = tbase(D + 1);
     bool tmode = D >= 1;  // workgroup-uniform
@@ -1807,7 +1804,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         uint16_t* PT = childPos;
         for (int e = tid; e < Ttot; e += OCT_NT) PT[e] = 0xffff;
         __syncthreads();
-        for (int q = tid; q < Lcount; q += OCT_NT) PT[npath[lst][q]] = (uint16_t)q;
+        for (int q = tid; q < Lcount; q += OCT_NT) PT[npath[lst][q] & 0xfff] = (uint16_t)q;
         __syncthreads();
         for (int d = 1; d <= D; d++) {
             const int b0 = tbase(d - 1), b1 = tbase(d), n = tbase(d + 1) - b1;
@@ -1944,7 +1941,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             sn = splitNode[i];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const int c = tmode ? CC[tchild(npath[cur][sn], q)] : CC[4 * sn + q];
+                const int c = tmode ? CC[tchild(npath[cur][sn], q) & 0xfff] : CC[4 * sn + q];
                 nc += c > 0;
                 nexp += c > 1;
             }
@@ -1978,7 +1975,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             const int tp = tmode ? (int)npath[cur][sn] : 0;
             for (int q = 0; q < 4; q++) {
                 const int tc = tmode ? tchild(tp, q) : 0;
-                const int c = tmode ? CC[tc] : CC[4 * sn + q];
+                const int c = tmode ? CC[tc & 0xfff] : CC[4 * sn + q];
                 if (c > 0) {
                     const int pos = groupStart + (nc - before - 1);
                     OctNode ch = og_child(par, q);
@@ -1990,7 +1987,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                         nf[pos] = 1;
                         npath[cur ^ 1][pos] = (uint16_t)tc;
                     }
-                    if (tmode && c > 1 && tdepth(tc) >= D) atomicOr(&sv[10], 1);  // a fresh split candidate at depth D
+                    if (tmode && c > 1 && (tc >> 12) >= D) atomicOr(&sv[10], 1);  // a fresh split candidate at depth D
                     before++;
                 }
             }
@@ -2014,7 +2011,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 nf[pos] = 0;
                 npath[cur ^ 1][pos] = npath[cur][i];
             }
-            if (tmode && cn[i].cnt > 1 && tdepth(npath[cur][i]) >= D) atomicOr(&sv[10], 2);  // splits if mode 0
+            if (tmode && cn[i].cnt > 1 && (npath[cur][i] >> 12) >= D) atomicOr(&sv[10], 2);  // splits if mode 0
         }
         const int expTot = totP >> 16;  // mode 0 (A = S): expandable children of all splits
         OCT_PROF(203 + 8 * (round & 3), clock64());
