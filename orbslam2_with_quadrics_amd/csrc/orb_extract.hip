@@ -2074,12 +2074,12 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         // ---- one pass over the keys: move to the new list position, and either count the children of
         // the next round's split candidates or (last round) keep the best key per node (:744-760)
         for (int base = tid; base < C; base += OCT_NT * OCT_U) {
-            uint32_t kv[OCT_U];
+            u64 kv[OCT_U];  // the whole 8-byte key (its response is read by the last pass): same lines as its xy half
             int no[OCT_U];
 #pragma unroll
             for (int u = 0; u < OCT_U; u++) {
                 const int k = base + u * OCT_NT;
-                kv[u] = k < C ? K32[2 * k] : 0u;
+                kv[u] = k < C ? K[k] : 0ull;
                 no[u] = k < C ? NO[k] : 0;
             }
 #pragma unroll
@@ -2089,7 +2089,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 bool cnt = false;
                 unsigned key32 = 0;
                 if (k < C) {
-                    const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
+                    const int x = (int)(kv[u] & 0xffff), y = (int)((kv[u] >> 16) & 0xffff);
                     int n2;
                     if (tmode) {
                         n2 = childPos[no[u]];
@@ -2103,7 +2103,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                     }
                     if (!done) NO[k] = (uint16_t)n2;
                     if (done) {
-                        const unsigned resp = K32[2 * k + 1];
+                        const unsigned resp = (unsigned)(kv[u] >> 32);
 #ifndef OG_EXP_OCT_FINAL
 #define OG_EXP_OCT_FINAL 0  // timing experiments only (tools/octree_profile.py --variant): 1 no atomic, 2 no order
 #endif
