@@ -797,6 +797,9 @@ def setup_tracking(args, env):
             nm = np.zeros(Bs, np.int32)
             for dst, src in ((kps, kp), (desc, de), (cnt, cn), (own, q["own"]), (obs, q["obs"]), (nm, q["nm"])):
                 e.d2h(dst, src)
+            if os.environ.get("ORBGPU_BENCH_DUMP"):  # diagnostics: the downloaded arrays of this stream
+                np.savez(os.environ["ORBGPU_BENCH_DUMP"] + f"_s{s_}.npz", kps=kps, desc=desc, cnt=cnt, own=own, obs=obs,
+                         nm=nm, cap=cap_)
             for b in range(Bs):
                 gf = g["frames"][(s_ * Bs + b) % nuniq]
                 n = int(cnt[b])
@@ -824,7 +827,10 @@ def setup_tracking(args, env):
     return dict(metric=f"frames/sec ORB extract + isInFrustum + SearchByProjection vs {M} map points "
                        f"@{cols}×{rows}, {NF} feat",
                 exs=exs, step=step, post=post, free=free, verify=verify, Bs=Bs, frames_per_step=B,
-                counts=[o[2] for o in outs],
+                counts=[o[2] for o in outs], streams_state=per,
+                # the map record's device memory is read by every step's kernels through raw pointers (offs): the
+                # tensor must outlive set-up, or torch's caching allocator hands its memory to later tensors
+                map_record=rec,
                 workload=f"config 5: {cols}x{rows} camera frames, {NF} features, ORB extraction + isInFrustum + "
                          f"SearchByProjection (th 1, ratio 0.8) against a {M}-point local map shared by all cameras",
                 cpu=lambda: cpu_baseline_tracking(rows, cols, NF, M, args.cpu_seconds))

@@ -29,7 +29,7 @@ def _grid(ex, B):
     return CS, CI
 
 
-@pytest.mark.parametrize("shape,nf", [((480, 640), 1000), ((1080, 1920), 2000)])
+@pytest.mark.parametrize("shape,nf", [((480, 640), 1000), ((1080, 1920), 2000), ((1080, 1920), 4000)])
 def test_forked_small_batches_equal_serial(gpu, oracle, shape, nf):
     rows, cols = shape
     ex = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
