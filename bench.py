@@ -270,6 +270,40 @@ def _sha(a) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
+def pcie_peak(torch, dev, nbytes=256 << 20, reps=4):
+    """Measured link peak: pinned host <-> device copies of 256 MB (H2D, D2H, and both directions at once on two
+    streams), best of `reps`, GB/s.  The PCIe-inclusive bench line reports its transfer rate against these."""
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    h2 = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{dev}")
+    d2 = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{dev}")
+    s1, s2 = torch.cuda.Stream(device=f"cuda:{dev}"), torch.cuda.Stream(device=f"cuda:{dev}")
+    out = {}
+    for name, fn in (("h2d", lambda: d.copy_(h, non_blocking=True)), ("d2h", lambda: h2.copy_(d2, non_blocking=True))):
+        best = 0.0
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            with torch.cuda.stream(s1):
+                fn()
+            torch.cuda.synchronize()
+            best = max(best, nbytes / (time.perf_counter() - t) / 1e9)
+        out[name + "_GBps"] = round(best, 2)
+    best = 0.0
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        with torch.cuda.stream(s1):
+            d.copy_(h, non_blocking=True)
+        with torch.cuda.stream(s2):
+            h2.copy_(d2, non_blocking=True)
+        torch.cuda.synchronize()
+        best = max(best, 2 * nbytes / (time.perf_counter() - t) / 1e9)
+    out["bidir_GBps"] = round(best, 2)
+    del h, h2, d, d2
+    return out
+
+
 def setup_mono_init(args, env):
     """config 3: extract the initial frame and B frames, SearchForInitialization of each against it.  The B frames
     are split over S contexts (streams) and, per context, K sequential launches (--chunks; one launch is fastest,
@@ -326,19 +360,37 @@ def setup_mono_init(args, env):
     if args.host_io:  # frames from pinned host memory, keypoints + descriptors back to pinned host memory
         import torch
 
-        host = dict(frames=torch.from_numpy(frames).pin_memory(),
+        # the frames' device copy is a torch tensor (copied on a per-context side stream); d_frames stays the
+        # device_alloc buffer of set-up and is not read in this mode
+        dv = torch.empty(frames.nbytes, dtype=torch.uint8, device=f"cuda:{dev}")
+        host = dict(frames=torch.from_numpy(frames.reshape(-1)).pin_memory(), dev=dv,
                     kps=[torch.empty(Bc * cap * 28, dtype=torch.uint8).pin_memory() for _ in exs],
-                    desc=[torch.empty(Bc * cap * 32, dtype=torch.uint8).pin_memory() for _ in exs])
+                    desc=[torch.empty(Bc * cap * 32, dtype=torch.uint8).pin_memory() for _ in exs],
+                    # chunk r+1's upload runs on a side stream while chunk r computes; the compute stream waits for
+                    # the upload's event, and the next step's upload of a chunk waits for its compute to finish
+                    cs=[torch.cuda.Stream(device=f"cuda:{dev}") for _ in exs],
+                    xs=[torch.cuda.ExternalStream(e.stream(), device=f"cuda:{dev}") for e in exs],
+                    up=[[torch.cuda.Event() for _ in range(K)] for _ in exs],
+                    done=[[torch.cuda.Event() for _ in range(K)] for _ in exs])
+        host["peak"] = pcie_peak(torch, dev)
 
     def step():
         for r in range(K):
             for s_, e in enumerate(exs):
                 off = (s_ * Bs + r * Bc) * fbytes
+                src = d_frames
                 if host is not None:
-                    _lib.check(e.ctx, L.orbgpu_memcpy_h2d_async(e.ctx, C_.c_void_p(d_frames + off),
-                                                                C_.c_void_p(host["frames"].data_ptr() + off),
-                                                                Bc * fbytes), "h2d")
-                e.extract_batch_device(d_frames + off, Bc, cols, rows, cols, fbytes)
+                    import torch
+
+                    cs, xs = host["cs"][s_], host["xs"][s_]
+                    cs.wait_event(host["done"][s_][r])  # the previous step's compute of this chunk is done
+                    with torch.cuda.stream(cs):
+                        host["dev"][off:off + Bc * fbytes].copy_(host["frames"][off:off + Bc * fbytes],
+                                                                 non_blocking=True)
+                    host["up"][s_][r].record(cs)
+                    xs.wait_event(host["up"][s_][r])
+                    src = host["dev"].data_ptr()
+                e.extract_batch_device(src + off, Bc, cols, rows, cols, fbytes)
                 _lib.check(e.ctx, L.orbgpu_memcpy_d2d_async(e.ctx, C_.c_void_p(d_cnt[s_] + 4 * r * Bc),
                                                             C_.c_void_p(outs[s_][2]), Bc * 4), "d2d")
                 _lib.check(e.ctx, L.orbgpu_prev_matched_from_frame(ex_ref.ctx, 0, e.ctx, C_.c_void_p(d_prev[s_])),
@@ -352,6 +404,7 @@ def setup_mono_init(args, env):
                                                                 C_.c_void_p(outs[s_][0]), Bc * cap * 28), "d2h")
                     _lib.check(e.ctx, L.orbgpu_memcpy_d2h_async(e.ctx, C_.c_void_p(host["desc"][s_].data_ptr()),
                                                                 C_.c_void_p(outs[s_][1]), Bc * cap * 32), "d2h")
+                    host["done"][s_][r].record(host["xs"][s_])
 
     def verify():
         """Parity of the timed path itself: every frame of the last step's last chunk (and the initial frame)
@@ -405,9 +458,15 @@ def setup_mono_init(args, env):
             e.d2h(nm, d_nm[s_])
             kp_all += int(counts.sum())
             nm_all += int(nm.sum())
-        return {"mean_keypoints_per_frame": round(kp_all / (Bc * S), 1),
-                "mean_init_matches_per_frame": round(nm_all / (Bc * S), 1),
-                "chunks_per_stream": K}, kp_all / S
+        extra = {"mean_keypoints_per_frame": round(kp_all / (Bc * S), 1),
+                 "mean_init_matches_per_frame": round(nm_all / (Bc * S), 1),
+                 "chunks_per_stream": K}
+        if host is not None:
+            extra["pcie"] = {"h2d_bytes_per_step": int(frames.nbytes), "d2h_bytes_per_step": int(B * cap * 60),
+                             "link_peak": host["peak"],
+                             "note": "frames H2D on a side stream per context, overlapped with the previous chunk's "
+                                     "compute; keypoints + descriptors D2H on the compute stream"}
+        return extra, kp_all / S
 
     def free():
         for s_, e in enumerate(exs):
@@ -882,7 +941,9 @@ def main():
                     help="mono_init = BASELINE.json's config 3 (the headline metric); extract = config 2; "
                          "stereo = config 4; tracking = config 5")
     ap.add_argument("--mappoints", type=int, default=5000, help="local-map points per camera (tracking)")
-    ap.add_argument("--chunks", type=int, default=1, help="sequential launches per stream per step (mono_init)")
+    ap.add_argument("--chunks", type=int, default=None,
+                    help="sequential launches per stream per step (mono_init; default 1, with --host-io 8: chunk r+1 "
+                         "uploads while chunk r computes)")
     ap.add_argument("--host-io", action="store_true",
                     help="mono_init: frames come from pinned host memory and keypoints/descriptors go back to it "
                          "inside the timed step (the PCIe-inclusive rate; not the headline value)")
@@ -897,6 +958,8 @@ def main():
                     help="PMC per-stage summary (tools/pmc_summary.py) the roofline's traffic comes from; default "
                          "profiles/pmc_latest.json (mono_init) or profiles/pmc_latest_<workload>.json")
     args = ap.parse_args()
+    if args.chunks is None:
+        args.chunks = 8 if args.host_io else 1
     r0, c0, n0 = DEFAULT_SHAPE[args.workload]
     args.rows = args.rows or r0
     args.cols = args.cols or c0
@@ -1070,6 +1133,14 @@ def main():
         "stages_ms_per_launch": {k: round(v, 4) for k, v in stages.items()},
         "stages_busy_ms_per_step": {k: round(v / args.steps, 4) for k, v in union_acc.items()},
     }
+    if "pcie" in out["config"]:  # --host-io: the step's transfers against the measured link peak
+        pc = out["config"].pop("pcie")
+        step_s = dt / args.steps
+        h2d = pc["h2d_bytes_per_step"] / step_s / 1e9
+        both = (pc["h2d_bytes_per_step"] + pc["d2h_bytes_per_step"]) / step_s / 1e9
+        out["pcie"] = dict(pc, achieved_h2d_GBps=round(h2d, 2), achieved_total_GBps=round(both, 2),
+                           h2d_frac_of_peak=round(h2d / pc["link_peak"]["h2d_GBps"], 3),
+                           total_frac_of_bidir_peak=round(both / pc["link_peak"]["bidir_GBps"], 3))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("timing the CPU baseline (oracle, 1 thread)")
         out["cpu_baseline"] = W["cpu"]()
