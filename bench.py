@@ -70,6 +70,18 @@ def max_over_ranks(dist, value: float, device=None) -> float:
     return float(t.item())
 
 
+def per_rank_values(dist, value: float, device=None):
+    """Every rank's value (all-gather); [value] on a single rank."""
+    if dist is None:
+        return [value]
+    import torch
+
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
 def shard_range(n_total: int, world: int, rank: int):
     """Contiguous frame-to-rank split of a step's global frame set: (first global frame, frame count) of `rank`."""
     base, rem = divmod(n_total, world)
@@ -89,21 +101,23 @@ def broadcast_record(dist, rank: int, buf, pack, unpack, src: int = 0):
         unpack(buf)
 
 
-def multi_rank_step(work, exs, dist, world: int, counts, copy_counts, after_gather):
+def multi_rank_step(work, exs, dist, world: int, counts, copy_counts, after_gather, ncount=None):
     """One timed step: enqueue the workload on every context, copy each context's per-frame keypoint counts into
     `counts` on that context's stream, synchronise every context once (the step's only host synchronisation: it
     also reads the contexts' capacity-guard flags), then all-gather the counts over RCCL (north_star).  The
     all-gather is left in flight; after_gather(s, e) orders context s's next count copy after it on the GPU.
-    Single rank: no copies, no collective."""
+    Single rank: no copies, no collective.  ncount: the first ncount contexts hold the counts (config 4: the left
+    extractors; the right ones are synchronised but count nothing); default all."""
     work()
+    owners = exs if ncount is None else exs[:ncount]
     if dist is not None:
-        for s_, e in enumerate(exs):
+        for s_, e in enumerate(owners):
             copy_counts(s_, e)
     for e in exs:
         e.synchronize()
     if dist is not None:
         allgather_counts(dist, counts, world)
-        for s_, e in enumerate(exs):
+        for s_, e in enumerate(owners):
             after_gather(s_, e)
 
 
@@ -326,11 +340,12 @@ def setup_mono_init(args, env):
     fbytes = rows * cols
     grid = _lib.GridGeom()
     L.orbgpu_grid_geom_for_image(cols, rows, C_.byref(grid))
-    # F1 (Tracking::mInitialFrame) is extracted once, at set-up (src/Tracking.cc:571); with N > 1 only rank 0
-    # extracts it and the others receive it as one frame record, also once
-    if rank == 0:
-        ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
-        ex_ref.synchronize()
+    # F1 (Tracking::mInitialFrame) is extracted once, at set-up (src/Tracking.cc:571); with N > 1 rank 0's F1 is
+    # the one every rank matches against: it reaches the others as one frame record, also once.
+    # Every rank runs the set-up extraction too: it plans the reference context for the frame geometry (the record
+    # size and the buffers the record is unpacked into), and rank 0's record then replaces the result.
+    ex_ref.extract_batch_device(d_f1, 1, cols, rows, cols, f1.nbytes)
+    ex_ref.synchronize()
     if dist is not None:
         import torch
 
@@ -997,7 +1012,7 @@ def main():
         streams[s_].wait_stream(torch.cuda.current_stream())
 
     def step():
-        multi_rank_step(W["step"], exs, dist, world, counts_t, copy_counts, after_gather)
+        multi_rank_step(W["step"], exs, dist, world, counts_t, copy_counts, after_gather, len(W["counts"]))
 
     stage_acc = {}
     union_acc = {}  # stage -> total time with >= 1 launch of it running (union over the concurrent contexts)
@@ -1033,6 +1048,7 @@ def main():
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
+    dt_ranks = per_rank_values(dist, dt, device=f"cuda:{dev}")
     dt = max_over_ranks(dist, dt, device=f"cuda:{dev}")
     for e in exs:
         e.set_stage_timing(False)
@@ -1133,6 +1149,8 @@ def main():
         "stages_ms_per_launch": {k: round(v, 4) for k, v in stages.items()},
         "stages_busy_ms_per_step": {k: round(v / args.steps, 4) for k, v in union_acc.items()},
     }
+    if world > 1:  # each rank's own step time (the value above uses their maximum)
+        out["per_rank_ms_per_step"] = [round(v / args.steps * 1e3, 3) for v in dt_ranks]
     if "pcie" in out["config"]:  # --host-io: the step's transfers against the measured link peak
         pc = out["config"].pop("pcie")
         step_s = dt / args.steps
