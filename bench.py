@@ -989,9 +989,9 @@ def main():
 
     # RCCL ("nccl") is the backend; ORBGPU_BENCH_BACKEND=gloo rehearses the multi-rank path with more ranks than
     # GPUs (ranks then share devices round-robin; RCCL refuses two ranks on one GPU)
-    dist = dist_init(world, os.environ.get("ORBGPU_BENCH_BACKEND", "nccl"))
     dev = local % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(dev)
+    torch.cuda.set_device(dev)  # before the process group: RCCL binds each rank's communicator to this device
+    dist = dist_init(world, os.environ.get("ORBGPU_BENCH_BACKEND", "nccl"))
     env = dict(L=_lib.lib(), _lib=_lib, ORBextractor=ORBextractor, synthetic=synthetic, dev=dev, rank=rank,
                dist=dist, world=world)
     t = time.time()
