@@ -978,6 +978,16 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 #endif
 #define FQ_S 28     // quad-ROI row stride in qwords (>= 16 + 6 + 3 misalignment; 4 * FQ_S = 16 mod 32)
 #define FQ_ROWS 86  // ROI rows (detection <= 80 + 6)
+#ifndef OG_FASTQ_WL
+#define OG_FASTQ_WL 0  // 1: per-wave survivor lists (stage 2 follows each wave's stage 1 without a barrier, no LDS
+                       // atomic per unit): bit-exact but FAST +5 % (8 partly filled stage-2/3 chunks per block instead
+                       // of 7 full ones; profiles/sweeps/r03_ab_fast_wave_lists.txt); 0: one block list reserved per
+                       // unit with ds_add_rtn
+#endif
+// per-wave list capacity: wave w takes units w, w + 8, w + 16 (<= 20 units of 4 x 64 pixels: dh <= 80)
+#define FQ_WCAP 768
+static_assert(FB_NT / 64 * FQ_WCAP <= 80 * 80, "per-wave lists fit the block list");
+static_assert(OG_FASTQ_WL == 0 || OG_FASTQ_KB == 1, "per-wave lists: one block per workgroup");
 
 // The 17 quad samples of og_fast_quad_kernel's stage 1 (cv::FAST's circle order, then the centre) as plain
 // ds_read_b64 (2 LDS cycles each): the compiler would pair them into ds_read2_b64, which costs 8 cycles per pair.
@@ -1104,6 +1114,8 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     for (int kb = 0;; kb++) {
     const int dw = b.dw, dh = b.dh, wC = b.wC, hC = b.hC;
     const uint2* Tq = roiq + b.mis;  // Tq[r * FQ_S + x] = quad (x, x + 16, x + 32, x + 48) of ROI row r
+    int wofs = 0;                    // (OG_FASTQ_WL) survivors in this wave's list
+    (void)wofs;
     // ---- stage 1: quick test on every detection pixel, four per lane.  Unit u = (row group g = u >> 1, half
     // h = u & 1) covers ROI rows 8g + 2h + {0, 4, 1, 5} (the lane's 16-lane group picks one); wave w takes units
     // w, w + 8, ...  Column masks are per-block constants, row masks scalars; one LDS reservation per unit.
@@ -1119,6 +1131,9 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         };
         const u64 col0 = cmask(dw), col1 = cmask(dw - 16), col2 = cmask(dw - 32), col3 = cmask(dw - 48);
         const int nunits = ((dh + 7) >> 3) * 2;
+#if OG_FASTQ_WL
+        wofs = 0;
+#endif
         for (int u = wvu; u < nunits; u += FB_NW) {
             const int R = 8 * (u >> 1) + 2 * (u & 1);  // uniform
             const bool full = R + 5 < dh;
@@ -1184,6 +1199,11 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                 n += cnt[k];
             }
             if (n) {
+#if OG_FASTQ_WL
+                // the wave's own list: a wave-uniform running offset, no reservation round trip
+                const uint32_t ab = a_lst + 2u * (uint32_t)(wvu * FQ_WCAP + wofs);
+                wofs += n;
+#else
                 uint32_t old;
                 u64 sv;
                 __asm__ volatile(
@@ -1193,6 +1213,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                     : "v"(a_ns), "v"(n)
                     : "memory");
                 const uint32_t ab = a_lst + 2u * (uint32_t)__builtin_amdgcn_readfirstlane(old);
+#endif
                 const uint32_t base = e_lane + (uint32_t)(R << 7);
                 uint32_t v[4];
                 {
@@ -1219,6 +1240,32 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             }
         }
     }
+#if OG_FASTQ_WL
+    // ---- stage 2 on this wave's own survivors, right after its stage 1 (LDS operations of one wave complete in
+    // order, so its list stores are visible to its reads); only the score map needs the barrier below
+    const int nv = wofs;
+    uint16_t* const wl = lst + wvu * FQ_WCAP;
+    {
+        const uint16_t* T16 = (const uint16_t*)Tq;
+        for (int e = lane; e < nv; e += 64) {
+            const int ent = wl[e];
+            const int i = (ent >> 7) & 127, j = ent & 127;
+            const uint16_t* pc = &T16[4 * ((i + 3) * FQ_S + ((j & 15) + 3)) + (j >> 4)];
+            const bool dark = (ent & 0x4000) != 0, bright = (ent & 0x8000) != 0;
+            int M = og_fast_M1<4>(pc, 4 * FQ_S, dark ? 0 : 0xff);
+            if (dark && bright) {
+                __asm__ volatile("" ::: "memory");  // (as in og_fast_blocks_kernel)
+                M = max(M, og_fast_M1<4>(pc, 4 * FQ_S, 0xff));
+            }
+            Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)M;
+        }
+    }
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    constexpr bool has_next = false;
+    const int pn = p;
+    const OgFB bn = b;
+#else
     // prefetch (OG_FASTQ_KB > 1): the next block's record and ROI loads are issued now and land during stage 2
     const int pn = p + (int)gridDim.x;
     bool has_next = kb + 1 < OG_FASTQ_KB && pn < nb;  // block-uniform
@@ -1255,13 +1302,18 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     // roiq and sh_ns are free from here on: the next block's ROI goes in while this block finishes
     if (tid == 0) sh_ns = 0;
     if (has_next) og_fastq_roi_put(bn, tid, sroi, roiq);
+    uint16_t* const wl = lst;
+    const int nv = ns;
+#endif
+    // stages 3-4 walk the wave's own list (OG_FASTQ_WL) or every 8th chunk of the block list
+    const int e_first = OG_FASTQ_WL ? 0 : wv * 64, e_step = OG_FASTQ_WL ? 64 : FB_NT;
     // ---- stage 3: same-cell 3x3 NMS at both thresholds (og_fast_blocks_kernel)
     int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
-    for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
+    for (int e0 = e_first; e0 < nv; e0 += e_step) {
         const int e = e0 + lane;
         int ent = 0, mc = 0, nbm = 0;
-        if (e < ns) {
-            ent = lst[e] & 0x3fff;
+        if (e < nv) {
+            ent = wl[e] & 0x3fff;
             const uint8_t* q = &Ms[og_ms_idx(ent >> 7, ent & 127, wC, hC) - FB_MSW - 1];
             mc = q[FB_MSW + 1];
             nbm = max(max(max(q[0], q[1]), max(q[2], q[FB_MSW])),
@@ -1270,7 +1322,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const u64 top = og_lanes_gt(mc, nbm);
         const u64 K1 = og_lanes_gt(mc, tA) & top, K2 = og_lanes_gt(mc, tB) & top;
         const u64 ci = og_lanes_gt(ent >> 7, hC - 1), cj = og_lanes_gt(ent & 127, wC - 1);
-        if (e < ns) lst[e] = (uint16_t)(ent | (mc > tA && mc > nbm ? 0x4000 : 0) | (mc > tB && mc > nbm ? 0x8000 : 0));
+        if (e < nv) wl[e] = (uint16_t)(ent | (mc > tA && mc > nbm ? 0x4000 : 0) | (mc > tB && mc > nbm ? 0x8000 : 0));
         const u64 cm[4] = {~ci & ~cj, ~ci & cj, ci & ~cj, ci & cj};
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) {
@@ -1311,9 +1363,12 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     // ---- stage 4: one reservation per block; each wave writes its kept entries at its offset.  Every entry's
     // score-map cell goes back to zero (the next block of this workgroup starts from a clean map).
     int sb = 0;
+#ifndef OG_EXP_FAST_NOATOMIC
+#define OG_EXP_FAST_NOATOMIC 0  // timing experiments only (results wrong): 1 = no output reservation round trip
+#endif
     if (total != 0) {  // block-uniform
         if (tid == 0) {
-            const int bb = atomicAdd(&cand_count[f * nlevels + b.l], total);
+            const int bb = OG_EXP_FAST_NOATOMIC ? 0 : atomicAdd(&cand_count[f * nlevels + b.l], total);
             if (bb + total > b.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
             sh_base = bb;
         }
@@ -1323,15 +1378,15 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const bool emit = total != 0 && sb + total <= b.cand_cap && kept != 0;
     u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb + before);
     int run = 0;
-    for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
+    for (int e0 = e_first; e0 < nv; e0 += e_step) {
         const int e = e0 + lane;
         int ent = 0;
-        if (e < ns) ent = lst[e];
+        if (e < nv) ent = wl[e];
         const int i = (ent >> 7) & 127, j = ent & 127;
         const int cell = (i >= hC) * 2 + (j >= wC);
         const unsigned kbit = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
         const u64 mask = og_lanes_ne(kbit, 0u);
-        if (e < ns) {
+        if (e < nv) {
             uint8_t* mcell = &Ms[og_ms_idx(i, j, wC, hC)];
             if (emit && kbit) out[og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, *mcell - 1);
             if (OG_FASTQ_KB > 1) *mcell = 0;
