@@ -47,6 +47,13 @@ __device__ __forceinline__ int og_rank(u64 m, int base = 0)  // + base, for free
 // XCD-aware bijective remap (cdna_hip_programming.md §5.5 T1): workgroups are dealt round-robin over
 // the 8 XCDs (separate L2s); give each XCD one contiguous chunk of the logical index space so that
 // neighbouring FAST cells / keypoints, which share cache lines, hit the same L2.  Speed only.
+// LDS byte address of a __shared__ object
+template <typename T>
+__device__ __forceinline__ uint32_t og_lds_addr(T* p)
+{
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)p;
+}
+
 __device__ __forceinline__ unsigned og_xcd_remap(unsigned orig, unsigned nwg)
 {
     const unsigned q = nwg / 8, r = nwg % 8, xcd = orig % 8;
@@ -237,6 +244,63 @@ __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t*
     return packed;
 }
 
+// The same 4 outputs from dword reads: a lane's 4 source pairs (sx[k], sx[k] + 1) lie within 10 bytes of the
+// 4-byte-aligned word holding sx[0] (sx[3] - sx[0] <= ceil(3 * 1.6) = 5, scale <= 1.6 on the host), so one
+// ds_read2_b32 + one ds_read_b32 (F0..F2) replace the 8 byte reads of a row, and v_perm picks each pair out of
+// (F1:F0) or (F2:F1).  The byte reads put ~38 distinct dwords of a 32-lane group on 32 banks (2-way conflicts,
+// 40 % of the pyramid's LDS cycles); the dword reads touch ~13.  OgRzSel holds a lane's selectors for one row
+// alignment sh = (row address + sx[0]) & 3: pair k comes from the high window (F2:F1) where its offset
+// o_k = sx[k] - sx[0] + sh is >= 6 (pairs 0 and 1 never: o_1 <= 5).
+#ifndef OG_RZ_WORDS
+#define OG_RZ_WORDS 0  // 1: dword reads (bit-exact, pyramid +1.5 %: the LDS reads do not bound it;
+                       // profiles/sweeps/r03_ab_resize_words.txt); 0: 8 byte reads per row and quad (og_rz_quad)
+#endif
+struct OgRzSel {
+    uint32_t sel[4];
+    bool hi2, hi3;
+};
+__device__ __forceinline__ OgRzSel og_rz_sel(const int* sx, unsigned sh)
+{
+    OgRzSel s;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const unsigned o = (unsigned)(sx[k] - sx[0]) + sh;
+        const unsigned oo = (k >= 2 && o >= 6u) ? o - 4u : o;
+        s.sel[k] = 0x0c000c00u | oo | ((oo + 1u) << 16);
+        if (k == 2) s.hi2 = o >= 6u;
+        if (k == 3) s.hi3 = o >= 6u;
+    }
+    return s;
+}
+// horizontal sums (d of og_rz_vert) of the 4 outputs from the row at LDS byte address `row` (+ sx[0])
+__device__ __forceinline__ void og_rz_hrow(uint32_t rowaddr, int sx0, const OgRzSel& s, const og_rz_u16x2* wt,
+                                           uint32_t* d)
+{
+    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+    lds_u32* F = (lds_u32*)(uintptr_t)((rowaddr + (uint32_t)sx0) & ~3u);
+    const uint32_t F0 = F[0], F1 = F[1], F2 = F[2];
+    const uint32_t p0 = __builtin_amdgcn_perm(F1, F0, s.sel[0]);
+    const uint32_t p1 = __builtin_amdgcn_perm(F1, F0, s.sel[1]);
+    const uint32_t p2 = __builtin_amdgcn_perm(s.hi2 ? F2 : F1, s.hi2 ? F1 : F0, s.sel[2]);
+    const uint32_t p3 = __builtin_amdgcn_perm(s.hi3 ? F2 : F1, s.hi3 ? F1 : F0, s.sel[3]);
+    d[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[0], 0u, false);
+    d[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[1], 0u, false);
+    d[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p2), wt[2], 0u, false);
+    d[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p3), wt[3], 0u, false);
+}
+template <bool FX>
+__device__ __forceinline__ uint32_t og_rz_quad_w(uint32_t r0addr, uint32_t r1addr, const int* sx, const OgRzSel& s0,
+                                                 const OgRzSel& s1, const og_rz_u16x2* wt, unsigned yz, unsigned yw)
+{
+    uint32_t d0[4], d1[4];
+    og_rz_hrow(r0addr, sx[0], s0, wt, d0);
+    og_rz_hrow(r1addr, sx[0], s1, wt, d1);
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) packed |= og_rz_vert<FX>(yz, d0[k], yw, d1[k]) << (8 * k);
+    return packed;
+}
+
 __device__ __forceinline__ void og_rz_weights(const int4* xtab, int xmax, int dx, int base, int* sx, og_rz_u16x2* wt,
                                               int k)
 {
@@ -347,12 +411,31 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
         // ac0 is a multiple of 4 (host plan): every quad left of own_c1 is one aligned dword store
         const bool own_c = cA < own_c1;
         const int nown = min(4, own_c1 - cA);
+#if OG_RZ_WORDS
+        const uint32_t aS = og_lds_addr(S);
+        const bool same_mis = (upitch & 15u) == 0;  // every staged row keeps the first row's misalignment mb
+        const OgRzSel su = og_rz_sel(sxA, (mb + (unsigned)sxA[0]) & 3u);
+#endif
         for (int rr = rga; rr < nrA; rr += G) {
             const int4 yt = YA[rr];
             const int r = ar0 + rr;
             const int r0 = yt.x - sr0, r1 = yt.y - sr0;
+#if OG_RZ_WORDS
+            uint32_t packed;
+            if (same_mis) {
+                packed = og_rz_quad_w<FX>(aS + (unsigned)(r0 * g.SC) + mb, aS + (unsigned)(r1 * g.SC) + mb, sxA, su, su,
+                                          wtA, (unsigned)yt.z, (unsigned)yt.w);
+            } else {
+                const unsigned m0 = (unsigned)mis[r0], m1 = (unsigned)mis[r1];
+                packed = og_rz_quad_w<FX>(aS + (unsigned)(r0 * g.SC) + m0, aS + (unsigned)(r1 * g.SC) + m1, sxA,
+                                          og_rz_sel(sxA, (m0 + (unsigned)sxA[0]) & 3u),
+                                          og_rz_sel(sxA, (m1 + (unsigned)sxA[0]) & 3u), wtA, (unsigned)yt.z,
+                                          (unsigned)yt.w);
+            }
+#else
             const uint32_t packed = og_rz_quad<FX>(S + r0 * g.SC + mis[r0], S + r1 * g.SC + mis[r1], sxA, wtA,
                                                (unsigned)yt.z, (unsigned)yt.w);
+#endif
             *(uint32_t*)&A[rr * g.AC + 4 * qa] = packed;
             if (r < own_r1 && own_c) og_rz_store4(DA + ((unsigned)r * (unsigned)pitchA + (unsigned)cA), packed, nown);
         }
@@ -364,13 +447,22 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     for (int k = 0; k < 4; k++) og_rz_weights(g.xtabB, g.xmaxB, min(dxt + k, g.bw - 1), ac0, sxB, wtB, k);
     const int n = min(4, g.bw - dxt);
     uint8_t* DB = dstB + (long long)f * dst_fstride + dxt;
+#if OG_RZ_WORDS
+    const uint32_t aA = og_lds_addr(A);                    // 16-byte aligned, AC a multiple of 4: one alignment
+    const OgRzSel sb = og_rz_sel(sxB, (unsigned)sxB[0] & 3u);
+#endif
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int r = 4 * rg + q;
         if (r >= nyB) break;
         const int4 yt = YB[r];
+#if OG_RZ_WORDS
+        const uint32_t packed = og_rz_quad_w<FX>(aA + (unsigned)((yt.x - ar0) * g.AC), aA + (unsigned)((yt.y - ar0) * g.AC),
+                                                 sxB, sb, sb, wtB, (unsigned)yt.z, (unsigned)yt.w);
+#else
         const uint32_t packed = og_rz_quad<FX>(A + (yt.x - ar0) * g.AC, A + (yt.y - ar0) * g.AC, sxB, wtB, (unsigned)yt.z,
                                            (unsigned)yt.w);
+#endif
         og_rz_store4(DB + (unsigned)(by0 + r) * (unsigned)pitchB, packed, n);
     }
 }
@@ -564,12 +656,6 @@ __device__ __forceinline__ void og_ds_write_b16_lanes(u64 mask, uint32_t lds_add
                      : "memory");
 }
 
-// LDS byte address of a __shared__ object
-template <typename T>
-__device__ __forceinline__ uint32_t og_lds_addr(T* p)
-{
-    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)p;
-}
 
 // block table reads through the constant address space: uniform, so one scalar load (through a generic pointer
 // the compiler cannot prove the table unclobbered by the kernel's own stores and falls back to vector loads).  The
