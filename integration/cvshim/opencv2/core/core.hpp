@@ -1,8 +1,11 @@
-// Compile-check shim (tests/test_integration_compile.py only): declarations of the cv:: names the integration/
-// sources and the reference's include/ORBextractor.h use -- enough for `g++ -fsyntax-only`, nothing is defined
-// or executed.  Not OpenCV, not part of the product.
+// Test shim for the drop-in binding (not OpenCV, not part of the product): declarations of the cv:: names the
+// integration/ sources and the reference's include/ORBextractor.h use.  tests/test_integration_compile.py compiles
+// the binding against them (g++ -fsyntax-only); tests/binding_run/cvmini.cc defines the subset the replacement
+// ORBextractor.cc calls, so tests/binding_run/run_binding executes the binding itself on the GPU
+// (tests/test_gpu_binding_run.py).  The private members below are that minimal implementation's storage.
 #pragma once
 #include <cstddef>
+#include <memory>
 #include <vector>
 
 #define CV_8U 0
@@ -58,6 +61,10 @@ public:
     T* ptr(int i = 0);
     template <typename T>
     const T* ptr(int i = 0) const;
+
+private:
+    int type_ = 0;
+    std::shared_ptr<unsigned char> buf_;  // owned storage (shared by copies, as OpenCV's reference count)
 };
 
 class _InputArray {
@@ -66,6 +73,9 @@ public:
     _InputArray(const Mat& m);
     bool empty() const;
     Mat getMat() const;
+
+protected:
+    const Mat* m_ = nullptr;
 };
 class _OutputArray : public _InputArray {
 public:
@@ -73,6 +83,10 @@ public:
     _OutputArray(Mat& m);
     void release() const;
     void create(int rows, int cols, int type) const;
+    Mat& getMatRef() const;
+
+private:
+    Mat* out_ = nullptr;
 };
 typedef const _InputArray& InputArray;
 // matrix expressions (OpenCV returns MatExpr, which converts to Mat) and cv::norm (default NORM_L2)

@@ -98,6 +98,33 @@ def build_host(verbose: bool = False) -> str:
     return HOST_LIB
 
 
+BINDING_RUNNER = os.path.join(ROOT, "tests", "binding_run", "run_binding")
+REFERENCE_INCLUDE = "/root/reference/include"
+
+
+def build_binding_runner(verbose: bool = False):
+    """Build tests/binding_run/run_binding: the drop-in integration/ORBextractor.cc compiled against the reference's
+    UNCHANGED include/ORBextractor.h with the test cv shim (integration/cvshim + tests/binding_run/cvmini.cc),
+    linked with liborbgpu.so.  Needs the reference headers, so it is built here (CPU container) and travels to the
+    GPU box with the tree; returns None where they are absent.  Test infrastructure (tests/test_gpu_binding_run.py)."""
+    if not os.path.exists(os.path.join(REFERENCE_INCLUDE, "ORBextractor.h")):
+        return None
+    cxx = shutil.which("g++") or "g++"
+    inc = ["-I", os.path.join(ROOT, "integration", "cvshim"), "-I", REFERENCE_INCLUDE, "-I", os.path.join(ROOT, "include"),
+           "-I", os.path.join(ROOT, "integration")]
+    srcs = [os.path.join(ROOT, "integration", "ORBextractor.cc"),
+            os.path.join(ROOT, "tests", "binding_run", "cvmini.cc"),
+            os.path.join(ROOT, "tests", "binding_run", "run_binding.cc")]
+    cmd = [cxx, "-O2", "-std=c++11", "-Wall", "-Wextra", "-Wno-unused-parameter", *inc, *srcs, "-L", HERE,
+           "-l:liborbgpu.so", "-Wl,-rpath,$ORIGIN/../../orbslam2_with_quadrics_amd", "-pthread",
+           "-o", BINDING_RUNNER + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(BINDING_RUNNER + ".tmp", BINDING_RUNNER)
+    return BINDING_RUNNER
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
     print(build_host(verbose=True))

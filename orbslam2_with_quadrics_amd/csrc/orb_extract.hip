@@ -3013,8 +3013,11 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     og_dk_sync();
     // vertical: item = (column c, 4 output rows 4m..4m+3) from row pairs 2m..2m+4; even rows take taps
     // (g0,g1)(g2,g3)(g4,g5)(g6,0), odd rows (0,g0)(g1,g2)(g3,g4)(g5,g6)
-    if (active) {
-        typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+#ifndef OG_DK_SAMPLEV
+#define OG_DK_SAMPLEV 1  // 1: the vertical pass only at the 512 rBRIEF sample points (below); 0: the whole 37x37 window
+#endif
+    typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+    if (active && !OG_DK_SAMPLEV) {
         constexpr unsigned short s0 = (unsigned short)c0, s1 = (unsigned short)c1, s2 = (unsigned short)c2,
                                  s3 = (unsigned short)c3;
         const u16x2v e0 = {s0, s1}, e1 = {s2, s3}, e2 = {s2, s1}, e3 = {s0, 0};
@@ -3094,14 +3097,42 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         }
 #endif
     }
-    og_dk_sync();
+    if (!OG_DK_SAMPLEV) og_dk_sync();
     if (!active) return;
     // ---- rBRIEF (:108-147)
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     float a, b;
     og_sincosf(angle * factorPI, &b, &a);
-    const uint8_t* ctr = Bl + 18 * BL_S + 18;
     constexpr bool nofma = NOFMA;
+#if OG_DK_SAMPLEV
+    // The tests read 512 blurred pixels of the 37x37 window; each is the vertical 7-tap sum over the row-pair
+    // horizontal sums Hp at its own column: 4 dword reads and 4 v_dot2 (even rows taps (g0,g1)(g2,g3)(g4,g5)(g6,0),
+    // odd rows (0,g0)(g1,g2)(g3,g4)(g5,g6)), rounded as the window pass rounds (same integer sum, same variant).
+    const int xsimd_s = BV == 0 ? ((lw & ~3) - (cx - 18)) : 0;
+    auto blurred = [&](int row, int col) -> int {  // window offsets from the centre, |row|, |col| <= 18
+        const int y = 18 + row, xw = 18 + col;
+        const uint32_t* h = Hp + (y >> 1) * HP_S + xw;
+        const bool odd = (y & 1) != 0;
+        const u16x2v w0 = odd ? u16x2v{0, (unsigned short)c0} : u16x2v{(unsigned short)c0, (unsigned short)c1};
+        const u16x2v w1 = odd ? u16x2v{(unsigned short)c1, (unsigned short)c2} : u16x2v{(unsigned short)c2, (unsigned short)c3};
+        const u16x2v w2 = odd ? u16x2v{(unsigned short)c3, (unsigned short)c2} : u16x2v{(unsigned short)c2, (unsigned short)c1};
+        const u16x2v w3 = odd ? u16x2v{(unsigned short)c1, (unsigned short)c0} : u16x2v{(unsigned short)c0, 0};
+        uint32_t acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, h[0]), w0, 0u, false);
+        acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, h[HP_S]), w1, acc, false);
+        acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, h[2 * HP_S]), w2, acc, false);
+        acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, h[3 * HP_S]), w3, acc, false);
+        uint32_t v;
+        if (BV == 0) {
+            const uint32_t up = xw < xsimd_s ? 0u : 1u;
+            v = (acc + 0x7fffu + (__builtin_amdgcn_ubfe(acc, 16, 1) | up)) >> 16;
+        } else {
+            v = (acc + (1u << 15)) >> 16;
+        }
+        return (int)min(v, 255u);
+    };
+#else
+    const uint8_t* ctr = Bl + 18 * BL_S + 18;
+#endif
     u64 words[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
@@ -3115,7 +3146,11 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             // build without contraction rounds both products (the kernels are compiled -ffp-contract=off)
             const int row = nofma ? og_cvround(x * b + y * a) : og_cvround(__builtin_fmaf(x, b, y * a));
             const int col = nofma ? og_cvround(x * a - y * b) : og_cvround(__builtin_fmaf(x, a, -(y * b)));
+#if OG_DK_SAMPLEV
+            val[q] = blurred(row, col);
+#else
             val[q] = ctr[__mul24(row, BL_S) + col];  // |row| <= 18: a 24-bit multiply
+#endif
         }
         words[t] = og_ballot(val[0] < val[1]);
     }
