@@ -75,6 +75,27 @@ __device__ __forceinline__ uint32_t og_rz_vert(uint32_t b0, uint32_t d0, uint32_
     return min(((__umul24(b0, d0 >> 4) >> 16) + (__umul24(b1, d1 >> 4) >> 16) + 2u) >> 2, 255u);
 }
 
+// og_resize2_kernel's form of og_rz_vert: with FX = false its horizontal weights are pre-scaled by 16
+// (og_rz_weights; <= 2048 * 16 = 32768 fits the u16 dot operand), so D = 16 d and D & ~0xff = (d >> 4) << 8, and
+// v_mul_hi_u32_u24(b << 8, (d >> 4) << 8) = (b * (d >> 4)) >> 16 exactly (operands < 2^24: b <= 2049,
+// D <= 255 * 2049 * 16): two ops per term instead of three.  FX = true is og_rz_vert.
+#ifndef OG_RZ_MULHI
+#define OG_RZ_MULHI 1
+#endif
+__device__ __forceinline__ uint32_t og_mulhi_u24(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    __asm__("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+template <bool FX>
+__device__ __forceinline__ uint32_t og_rz_vert16(uint32_t b0, uint32_t D0, uint32_t b1, uint32_t D1)
+{
+    if (FX || !OG_RZ_MULHI) return og_rz_vert<FX>(b0, D0, b1, D1);  // unscaled weights: D = d
+    return min((og_mulhi_u24(b0 << 8, D0 & ~0xffu) + og_mulhi_u24(b1 << 8, D1 & ~0xffu) + 2u) >> 2,
+               255u);
+}
+
 #define RZ_NT 256
 #define RZ_TW 256                      // output columns per workgroup (64 lanes x 4)
 #define RZ_TH 16                       // output rows per workgroup (4 waves x 4 rows)
@@ -239,7 +260,7 @@ __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t*
         const uint32_t p1 = (uint32_t)R1[sx[k]] | ((uint32_t)R1[sx[k] + 1] << 16);
         const uint32_t d0 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[k], 0u, false);
         const uint32_t d1 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[k], 0u, false);
-        packed |= og_rz_vert<FX>(yz, d0, yw, d1) << (8 * k);
+        packed |= og_rz_vert16<FX>(yz, d0, yw, d1) << (8 * k);
     }
     return packed;
 }
@@ -297,16 +318,20 @@ __device__ __forceinline__ uint32_t og_rz_quad_w(uint32_t r0addr, uint32_t r1add
     og_rz_hrow(r1addr, sx[0], s1, wt, d1);
     uint32_t packed = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) packed |= og_rz_vert<FX>(yz, d0[k], yw, d1[k]) << (8 * k);
+    for (int k = 0; k < 4; k++) packed |= og_rz_vert16<FX>(yz, d0[k], yw, d1[k]) << (8 * k);
     return packed;
 }
 
+// (og_resize2_kernel: FX = false pre-scales the weights by 16 for og_rz_vert16)
+template <bool FX>
 __device__ __forceinline__ void og_rz_weights(const int4* xtab, int xmax, int dx, int base, int* sx, og_rz_u16x2* wt,
                                               int k)
 {
     const int4 xt = xtab[dx];
     sx[k] = xt.x - base;
-    wt[k] = dx < xmax ? og_rz_u16x2{(unsigned short)xt.y, (unsigned short)xt.z} : og_rz_u16x2{2048, 0};
+    const int sh = (!FX && OG_RZ_MULHI) ? 4 : 0;
+    wt[k] = dx < xmax ? og_rz_u16x2{(unsigned short)(xt.y << sh), (unsigned short)(xt.z << sh)}
+                      : og_rz_u16x2{(unsigned short)(2048 << sh), 0};
 }
 
 #ifndef RZ2_U
@@ -366,7 +391,7 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     const int cth = tid & 63, rg = tid >> 6;
     const int dxt = bx0 + 4 * cth;
 #pragma unroll
-    for (int k = 0; k < 4; k++) og_rz_weights(g.xtabA, g.xmaxA, min(cA + k, ac1), sc0, sxA, wtA, k);
+    for (int k = 0; k < 4; k++) og_rz_weights<FX>(g.xtabA, g.xmaxA, min(cA + k, ac1), sc0, sxA, wtA, k);
     // staging addresses: the region's first row (wave-uniform, SGPRs) rounded down to 16 bytes plus a 32-bit lane
     // offset; chunk -> (row, chunk) with the exact float quotient (as in og_fast_blocks_kernel: nIt < 2^14)
     const uint8_t* rbase = src + (long long)f * src_fstride + (long long)sr0 * src_pitch + sc0;
@@ -444,7 +469,7 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     // ---- level B tile from the A region
     if (dxt >= g.bw) return;
 #pragma unroll
-    for (int k = 0; k < 4; k++) og_rz_weights(g.xtabB, g.xmaxB, min(dxt + k, g.bw - 1), ac0, sxB, wtB, k);
+    for (int k = 0; k < 4; k++) og_rz_weights<FX>(g.xtabB, g.xmaxB, min(dxt + k, g.bw - 1), ac0, sxB, wtB, k);
     const int n = min(4, g.bw - dxt);
     uint8_t* DB = dstB + (long long)f * dst_fstride + dxt;
 #if OG_RZ_WORDS
@@ -1189,7 +1214,13 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     uint32_t sroi[2][4];
     og_fastq_roi_load(b, tid, sroi);
     og_fastq_roi_put(b, tid, sroi, roiq);
-    for (int idx = tid * 16; idx < FB_MSZ; idx += FB_NT * 16) *(uint4*)&Ms[idx] = make_uint4(0u, 0u, 0u, 0u);
+#ifndef OG_FASTQ_MSZ_ROWS
+#define OG_FASTQ_MSZ_ROWS 1  // zero only the score-map rows the block reads (dh + 3: gap rows included)
+#endif
+    {
+        const int msz = (OG_FASTQ_MSZ_ROWS && OG_FASTQ_KB == 1) ? min(FB_MSZ, ((b.dh + 3) * FB_MSW + 15) & ~15) : FB_MSZ;
+        for (int idx = tid * 16; idx < msz; idx += FB_NT * 16) *(uint4*)&Ms[idx] = make_uint4(0u, 0u, 0u, 0u);
+    }
     if (tid == 0) sh_ns = 0;
     __syncthreads();
 #if OG_EXP_FAST_STOP == 1  // timing experiments only (tools/fast_variants.py): results are wrong
@@ -2795,6 +2826,9 @@ __device__ __forceinline__ int og_wave_sum(int v)
     return __builtin_amdgcn_readlane(v, 63);
 }
 
+#ifndef OG_DK_SAMPLEV
+#define OG_DK_SAMPLEV 1  // 1: the vertical pass only at the 512 rBRIEF sample points (og_describe_kernel); 0: the whole 37x37 window
+#endif
 #ifndef DK_WAVES
 #define DK_WAVES 4
 #endif
@@ -3013,9 +3047,6 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     og_dk_sync();
     // vertical: item = (column c, 4 output rows 4m..4m+3) from row pairs 2m..2m+4; even rows take taps
     // (g0,g1)(g2,g3)(g4,g5)(g6,0), odd rows (0,g0)(g1,g2)(g3,g4)(g5,g6)
-#ifndef OG_DK_SAMPLEV
-#define OG_DK_SAMPLEV 1  // 1: the vertical pass only at the 512 rBRIEF sample points (below); 0: the whole 37x37 window
-#endif
     typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
     if (active && !OG_DK_SAMPLEV) {
         constexpr unsigned short s0 = (unsigned short)c0, s1 = (unsigned short)c1, s2 = (unsigned short)c2,
