@@ -2829,6 +2829,9 @@ __device__ __forceinline__ int og_wave_sum(int v)
 #ifndef OG_DK_SAMPLEV
 #define OG_DK_SAMPLEV 1  // 1: the vertical pass only at the 512 rBRIEF sample points (og_describe_kernel); 0: the whole 37x37 window
 #endif
+#ifndef OG_DK_HSHIFTW
+#define OG_DK_HSHIFTW 1  // horizontal blur pass with shifted weights (og_describe_kernel)
+#endif
 #ifndef DK_WAVES
 #define DK_WAVES 4
 #endif
@@ -3029,12 +3032,25 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
                 const int r = min(2 * rp + h, RAW_W - 1);  // row 43 (pair 21, high half) is never read
                 const uint32_t* rr = (const uint32_t*)(Rb + r * RAW_S) + g;
                 const uint32_t d0 = rr[0], d1 = rr[1], d2 = rr[2];
+#if OG_DK_HSHIFTW
+                // output k = sum over the window bytes k .. k+6 of d0:d1:d2: the weights shift, not the data --
+                // 2, 2, 3, 3 dot4 for k = 0..3 (10 instead of 8 dot4 + 6 alignbyte + 4 and)
+                constexpr uint32_t W00 = c0 | c1 << 8 | c2 << 16 | c3 << 24, W01 = c2 | c1 << 8 | c0 << 16;
+                constexpr uint32_t W10 = c0 << 8 | c1 << 16 | c2 << 24, W11 = c3 | c2 << 8 | c1 << 16 | c0 << 24;
+                constexpr uint32_t W20 = c0 << 16 | c1 << 24, W21 = c2 | c3 << 8 | c2 << 16 | c1 << 24, W22 = c0;
+                constexpr uint32_t W30 = c0 << 24, W31 = c1 | c2 << 8 | c3 << 16 | c2 << 24, W32 = c1 | c0 << 8;
+                hv[h][0] = __builtin_amdgcn_udot4(d1, W01, __builtin_amdgcn_udot4(d0, W00, 0u, false), false);
+                hv[h][1] = __builtin_amdgcn_udot4(d1, W11, __builtin_amdgcn_udot4(d0, W10, 0u, false), false);
+                hv[h][2] = __builtin_amdgcn_udot4(d2, W22, __builtin_amdgcn_udot4(d1, W21, __builtin_amdgcn_udot4(d0, W20, 0u, false), false), false);
+                hv[h][3] = __builtin_amdgcn_udot4(d2, W32, __builtin_amdgcn_udot4(d1, W31, __builtin_amdgcn_udot4(d0, W30, 0u, false), false), false);
+#else
                 hv[h][0] = __builtin_amdgcn_udot4(d1 & 0x00ffffffu, ghi, __builtin_amdgcn_udot4(d0, glo, 0u, false), false);
 #pragma unroll
                 for (int k = 1; k < 4; k++) {
                     const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, k), w1 = __builtin_amdgcn_alignbyte(d2, d1, k);
                     hv[h][k] = __builtin_amdgcn_udot4(w1 & 0x00ffffffu, ghi, __builtin_amdgcn_udot4(w0, glo, 0u, false), false);
                 }
+#endif
             }
             uint4 o;
             o.x = hv[0][0] | (hv[1][0] << 16);
