@@ -25,6 +25,7 @@ typedef unsigned long long u64;
 
 #include "orb_pattern.inc"  // static const signed char oo_orb_pattern[1024]
 __constant__ signed char og_pattern[1024];
+__constant__ float4 og_pattern_f[256];  // the same tests as floats (x0, y0, x1, y1): one 16-byte load, no conversions
 static bool g_pattern_uploaded_dev[64] = {false};
 
 // Lane masks straight from one v_cmp each (LLVM lowers ballot(a && b) as v_cmp(v_cndmask(mask), 0): two VALU
@@ -3184,11 +3185,23 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         const int p = lane + 64 * t;
+#ifndef OG_DK_PATF
+#define OG_DK_PATF 1  // pattern from the float table (0: bytes + conversions)
+#endif
+#if OG_DK_PATF
+        const float4 pf = og_pattern_f[p];
+        const float pfx[2] = {pf.x, pf.z}, pfy[2] = {pf.y, pf.w};
+#else
         const signed char* pt = og_pattern + 4 * p;
+#endif
         int val[2];
 #pragma unroll
         for (int q = 0; q < 2; q++) {
+#if OG_DK_PATF
+            const float x = pfx[q], y = pfy[q];
+#else
             const float x = (float)pt[2 * q], y = (float)pt[2 * q + 1];
+#endif
             // GCC -O3 -march=native contracts the first product of GET_VALUE into an FMA; a
             // build without contraction rounds both products (the kernels are compiled -ffp-contract=off)
             const int row = nofma ? og_cvround(x * b + y * a) : og_cvround(__builtin_fmaf(x, b, y * a));
@@ -3337,6 +3350,11 @@ hipError_t og_upload_pattern(int device)
     if (device >= 0 && device < 64 && g_pattern_uploaded_dev[device]) return hipSuccess;
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(og_pattern), oo_orb_pattern, sizeof(oo_orb_pattern), 0,
                                      hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        float pf[1024];
+        for (int i = 0; i < 1024; i++) pf[i] = (float)oo_orb_pattern[i];
+        e = hipMemcpyToSymbol(HIP_SYMBOL(og_pattern_f), pf, sizeof(pf), 0, hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess && device >= 0 && device < 64) g_pattern_uploaded_dev[device] = true;
     return e;
 }
