@@ -412,8 +412,8 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
             const int it = it0 + u * RZ2_NT;
             v[u] = make_uint4(0u, 0u, 0u, 0u);
             if (it < nIt) {
-                const int r = (int)__builtin_fmaf((float)it, rn, hn) & 127, q = it - r * (nch & 0xfff);
-                const unsigned o = (unsigned)r * upitch + mb;      // row start relative to abase
+                const int r = (int)__builtin_fmaf((float)it, rn, hn) & 127, q = it - (int)__umul24((unsigned)r, (unsigned)nch & 0xfffu);
+                const unsigned o = __umul24((unsigned)r, upitch) + mb;  // row start relative to abase (upitch < 2^24)
                 const unsigned c16 = (o & ~15u) + 16u * (unsigned)q;  // this chunk, 16-byte aligned
                 if (c16 <= o + (unsigned)(ncS - 1)) v[u] = *(const uint4*)(abase + c16);
             }
@@ -422,9 +422,9 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
         for (int u = 0; u < RZ2_U; u++) {
             const int it = it0 + u * RZ2_NT;
             if (it < nIt) {
-                const int r = (int)__builtin_fmaf((float)it, rn, hn) & 127, q = it - r * (nch & 0xfff);
-                *(uint4*)&S[r * g.SC + 16 * q] = v[u];
-                if (q == 0) mis[r] = (int)(((unsigned)r * upitch + mb) & 15u);
+                const int r = (int)__builtin_fmaf((float)it, rn, hn) & 127, q = it - (int)__umul24((unsigned)r, (unsigned)nch & 0xfffu);
+                *(uint4*)&S[__umul24((unsigned)r, (unsigned)g.SC) + 16 * q] = v[u];
+                if (q == 0) mis[r] = (int)((__umul24((unsigned)r, upitch) + mb) & 15u);
             }
         }
     }
@@ -449,21 +449,21 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
 #if OG_RZ_WORDS
             uint32_t packed;
             if (same_mis) {
-                packed = og_rz_quad_w<FX>(aS + (unsigned)(r0 * g.SC) + mb, aS + (unsigned)(r1 * g.SC) + mb, sxA, su, su,
+                packed = og_rz_quad_w<FX>(aS + __umul24((unsigned)r0, (unsigned)g.SC) + mb, aS + __umul24((unsigned)r1, (unsigned)g.SC) + mb, sxA, su, su,
                                           wtA, (unsigned)yt.z, (unsigned)yt.w);
             } else {
                 const unsigned m0 = (unsigned)mis[r0], m1 = (unsigned)mis[r1];
-                packed = og_rz_quad_w<FX>(aS + (unsigned)(r0 * g.SC) + m0, aS + (unsigned)(r1 * g.SC) + m1, sxA,
+                packed = og_rz_quad_w<FX>(aS + __umul24((unsigned)r0, (unsigned)g.SC) + m0, aS + __umul24((unsigned)r1, (unsigned)g.SC) + m1, sxA,
                                           og_rz_sel(sxA, (m0 + (unsigned)sxA[0]) & 3u),
                                           og_rz_sel(sxA, (m1 + (unsigned)sxA[0]) & 3u), wtA, (unsigned)yt.z,
                                           (unsigned)yt.w);
             }
 #else
-            const uint32_t packed = og_rz_quad<FX>(S + r0 * g.SC + mis[r0], S + r1 * g.SC + mis[r1], sxA, wtA,
+            const uint32_t packed = og_rz_quad<FX>(S + __umul24((unsigned)r0, (unsigned)g.SC) + mis[r0], S + __umul24((unsigned)r1, (unsigned)g.SC) + mis[r1], sxA, wtA,
                                                (unsigned)yt.z, (unsigned)yt.w);
 #endif
             *(uint32_t*)&A[rr * g.AC + 4 * qa] = packed;
-            if (r < own_r1 && own_c) og_rz_store4(DA + ((unsigned)r * (unsigned)pitchA + (unsigned)cA), packed, nown);
+            if (r < own_r1 && own_c) og_rz_store4(DA + (__umul24((unsigned)r, (unsigned)pitchA) + (unsigned)cA), packed, nown);
         }
     }
     __syncthreads();
@@ -486,10 +486,10 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
         const uint32_t packed = og_rz_quad_w<FX>(aA + (unsigned)((yt.x - ar0) * g.AC), aA + (unsigned)((yt.y - ar0) * g.AC),
                                                  sxB, sb, sb, wtB, (unsigned)yt.z, (unsigned)yt.w);
 #else
-        const uint32_t packed = og_rz_quad<FX>(A + (yt.x - ar0) * g.AC, A + (yt.y - ar0) * g.AC, sxB, wtB, (unsigned)yt.z,
+        const uint32_t packed = og_rz_quad<FX>(A + __umul24((unsigned)(yt.x - ar0), (unsigned)g.AC), A + __umul24((unsigned)(yt.y - ar0), (unsigned)g.AC), sxB, wtB, (unsigned)yt.z,
                                            (unsigned)yt.w);
 #endif
-        og_rz_store4(DB + (unsigned)(by0 + r) * (unsigned)pitchB, packed, n);
+        og_rz_store4(DB + __umul24((unsigned)(by0 + r), (unsigned)pitchB), packed, n);
     }
 }
 
@@ -2968,8 +2968,14 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 #pragma unroll
             for (int k = 0; k < NIT; k++) {
                 const int idx = min(lane + 64 * k, RAW_W * 11 - 1);
-                const int r = (idx * 5958) >> 16, q = idx - r * 11;  // idx / 11, exact for idx < 473 (5958 / 2^16 ~ 1/11)
-                const unsigned off = (unsigned)r * upitch + 4u * (unsigned)q + m0;
+                const int r = (idx * 5958) >> 16;  // idx / 11, exact for idx < 473 (5958 / 2^16 ~ 1/11)
+                unsigned r11 = __umul24((unsigned)r, 11u);
+                __asm__("" : "+v"(r11));  // (else idx - 11 r becomes a quarter-rate v_mul_lo_u32 by -11)
+                const int q = idx - (int)r11;
+                unsigned off = __umul24((unsigned)r, upitch) + 4u * (unsigned)q + m0;  // upitch < 2^24
+                // keep the offset a 32-bit lane value (saddr + voffset loads): otherwise the multiply is folded
+                // into a 64-bit v_mad_u64_u32 with the base pointer
+                __asm__("" : "+v"(off));
                 const uint32_t* a = (const uint32_t*)(abase + (off & ~3u));
                 sh[k] = off & 3u;
                 lo[k] = a[0];
@@ -2979,7 +2985,10 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             for (int k = 0; k < NIT; k++) {
                 const int idx = lane + 64 * k;
                 if (idx < RAW_W * 11) {
-                    const int r = (idx * 5958) >> 16, q = idx - r * 11;
+                    const int r = (idx * 5958) >> 16;
+                    unsigned r11 = __umul24((unsigned)r, 11u);
+                    __asm__("" : "+v"(r11));
+                    const int q = idx - (int)r11;
                     *(uint32_t*)&R[r * RAW_S + 4 * q] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
                 }
             }
@@ -3159,7 +3168,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     const int xsimd_s = BV == 0 ? ((lw & ~3) - (cx - 18)) : 0;
     auto blurred = [&](int row, int col) -> int {  // window offsets from the centre, |row|, |col| <= 18
         const int y = 18 + row, xw = 18 + col;
-        const uint32_t* h = Hp + (y >> 1) * HP_S + xw;
+        const uint32_t* h = Hp + __mul24(y >> 1, HP_S) + xw;  // (a 24-bit multiply: v_mul_lo_u32 is quarter rate)
         const bool odd = (y & 1) != 0;
         const u16x2v w0 = odd ? u16x2v{0, (unsigned short)c0} : u16x2v{(unsigned short)c0, (unsigned short)c1};
         const u16x2v w1 = odd ? u16x2v{(unsigned short)c1, (unsigned short)c2} : u16x2v{(unsigned short)c2, (unsigned short)c3};
