@@ -74,12 +74,32 @@ __global__ __launch_bounds__(ST_NT) void og_stereo_rows_kernel(OgStereoDev S)
     if (tid == 0) RS[S.nRows] = carry;
     __syncthreads();
     __threadfence_block();
+#ifndef OG_ST_ROWS_WAVE
+#define OG_ST_ROWS_WAVE 1  // 1: one wave per row, 64 keypoints per ballot (0: one thread per row walks them all)
+#endif
+#if OG_ST_ROWS_WAVE
+    // each row's list in index order: the wave takes the keypoints 64 at a time, ballots the ones whose band holds
+    // the row and writes them at their rank (index order within the ballot, the ballots in index order)
+    for (int y = wv; y < S.nRows; y += ST_NT / 64) {
+        int pos = RS[y];
+        const int end = min(pos + cnt[y], S.row_cap);
+        for (int c = 0; c < Nr && pos < end; c += 64) {
+            const int iR = c + lane;
+            const bool in = iR < Nr && lo_[iR] <= y && y <= hi_[iR];
+            const u64 m = __ballot(in);
+            const int r = __popcll(m & ((1ull << lane) - 1ull));
+            if (in && pos + r < end) RI[pos + r] = iR;
+            pos += __popcll(m);
+        }
+    }
+#else
     for (int y = tid; y < S.nRows; y += ST_NT) {
         int pos = RS[y];
         const int end = min(pos + cnt[y], S.row_cap);
         for (int iR = 0; iR < Nr && pos < end; iR++)
             if (lo_[iR] <= y && y <= hi_[iR]) RI[pos++] = iR;
     }
+#endif
 }
 
 __device__ __forceinline__ int og_wave_isum(int v)
