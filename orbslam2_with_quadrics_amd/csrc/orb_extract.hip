@@ -2962,6 +2962,38 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             const unsigned m0 = (unsigned)((uintptr_t)src0 & 3);
             const uint8_t* abase = src0 - m0;
             const unsigned upitch = (unsigned)pitch & (OG_MAX_PITCH - 1);  // < 2^24 (checked on the host)
+#ifndef OG_DK_RAWROWS
+#define OG_DK_RAWROWS 1  // 1: lanes 0-54 = 5 rows x 11 dwords, stepping 5 rows per iteration (offsets advance by a
+                         // uniform 5 * pitch); 0: lane + 64 k split into (row, dword) every iteration
+#endif
+#if OG_DK_RAWROWS
+            constexpr int NIT = (RAW_W + 4) / 5;  // 9 iterations of 5 rows
+            const int lr = (lane * 5958) >> 16;  // lane / 11 (lanes 55-63: row 5, inactive)
+            unsigned l11 = __umul24((unsigned)lr, 11u);
+            __asm__("" : "+v"(l11));
+            const int q = lane - (int)l11;
+            const bool lact = lane < 55;
+            const unsigned off0 = __umul24((unsigned)min(lr, 4), upitch) + 4u * (unsigned)q + m0;  // upitch < 2^24
+            const unsigned step = __umul24(5u, upitch);
+            uint32_t lo[NIT], hi[NIT];
+            unsigned sh[NIT];
+#pragma unroll
+            for (int k = 0; k < NIT; k++) {
+                // rows past the window (lr + 5 k > 42) re-read row 42's place: the last row + the lane's column
+                const unsigned kk = (unsigned)min(k, (RAW_W - 1 - min(lr, 4)) / 5);
+                unsigned off = off0 + kk * step;
+                __asm__("" : "+v"(off));  // a 32-bit lane offset (saddr + voffset loads)
+                const uint32_t* a = (const uint32_t*)(abase + (off & ~3u));
+                sh[k] = off & 3u;
+                lo[k] = a[0];
+                hi[k] = a[1];
+            }
+#pragma unroll
+            for (int k = 0; k < NIT; k++) {
+                const int r = lr + 5 * k;
+                if (lact && r < RAW_W) *(uint32_t*)&R[r * RAW_S + 4 * q] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+            }
+#else
             constexpr int NIT = (RAW_W * 11 + 63) / 64;
             uint32_t lo[NIT], hi[NIT];
             unsigned sh[NIT];
@@ -2992,6 +3024,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
                     *(uint32_t*)&R[r * RAW_S + 4 * q] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
                 }
             }
+#endif
         } else {  // within 21 px of the border: BORDER_REFLECT_101 per pixel
             for (int idx = lane; idx < RAW_W * RAW_W; idx += 64) {
                 const int r = idx / RAW_W, c = idx - (idx / RAW_W) * RAW_W;
