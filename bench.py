@@ -60,6 +60,19 @@ def dist_init(world: int, backend: str):
     return dist
 
 
+def pick_device(local: int, local_world: int, device_count: int, backend: str) -> int:
+    """The GPU of local rank `local`: one rank per GPU.  RCCL ("nccl", the default backend) cannot run two ranks on
+    one GPU, so more ranks on a node than it has GPUs is refused here, before any device or process-group call,
+    instead of failing inside RCCL.  ORBGPU_BENCH_BACKEND=gloo rehearses the multi-rank path with more ranks than
+    GPUs: ranks then share the devices round-robin."""
+    if device_count < 1:
+        raise SystemExit("bench.py: no GPU visible (torch.cuda.device_count() == 0)")
+    if backend == "nccl" and max(local_world, local + 1) > device_count:
+        raise SystemExit(f"bench.py: {max(local_world, local + 1)} ranks on this node but {device_count} GPU(s): "
+                         f"RCCL needs one GPU per rank (use ORBGPU_BENCH_BACKEND=gloo to rehearse with shared GPUs)")
+    return local % device_count
+
+
 def max_over_ranks(dist, value: float, device=None) -> float:
     if dist is None:
         return value
@@ -987,11 +1000,10 @@ def main():
 
     from orbslam2_with_quadrics_amd import ORBextractor, _lib, synthetic
 
-    # RCCL ("nccl") is the backend; ORBGPU_BENCH_BACKEND=gloo rehearses the multi-rank path with more ranks than
-    # GPUs (ranks then share devices round-robin; RCCL refuses two ranks on one GPU)
-    dev = local % max(torch.cuda.device_count(), 1)
+    backend = os.environ.get("ORBGPU_BENCH_BACKEND", "nccl")
+    dev = pick_device(local, int(os.environ.get("LOCAL_WORLD_SIZE", world)), torch.cuda.device_count(), backend)
     torch.cuda.set_device(dev)  # before the process group: RCCL binds each rank's communicator to this device
-    dist = dist_init(world, os.environ.get("ORBGPU_BENCH_BACKEND", "nccl"))
+    dist = dist_init(world, backend)
     env = dict(L=_lib.lib(), _lib=_lib, ORBextractor=ORBextractor, synthetic=synthetic, dev=dev, rank=rank,
                dist=dist, world=world)
     t = time.time()

@@ -73,7 +73,7 @@ void orbgpu_destroy(orbgpu_ctx* ctx);
 #define ORBGPU_SEM_BLUR_BITEXACT_ED (3 << ORBGPU_SEM_BLUR_SHIFT)
 #define ORBGPU_SEM_BLUR_MASK (7 << ORBGPU_SEM_BLUR_SHIFT)
 #define ORBGPU_SEM_BRIEF_NOFMA 0x20
-/* Option, not a reference behaviour (off by default; also set at orbgpu_create by ORBGPU_SCORE_HARRIS=1):
+/* Option, not a reference behaviour (off by default; set only through orbgpu_set_semantics, never by the environment):
  * the octree ranks candidates by the Harris response of OpenCV's ORB HARRIS_SCORE (features2d orb.cpp
  * HarrisResponses: 7x7 block, 3x3 Sobel-form gradients, k = 0.04, scale (1/(4*7*255))^4) at the FAST
  * candidate's level pixel instead of by the FAST score, and the keypoint response is that float.
@@ -139,9 +139,11 @@ int orbgpu_batch_download(orbgpu_ctx* ctx, int b, orbgpu_keypoint* kps, uint8_t*
  * to the others, which unpack it as frame 0 of a one-frame batch and match their frames against it
  * (SURVEY §8(e)).  Both calls are enqueued on the context stream; unpack requires a context planned for the
  * same image size and parameters, and records the event the matchers of other contexts wait for.  The record's
- * 16-byte header holds the count, a magic word, frame_cap and the undistortion flag: unpack reads it back (a
- * synchronising 16-byte read) and returns ORBGPU_ERR_ARG when it does not match the context's plan or the count
- * exceeds frame_cap. */
+ * 16-byte header holds the count, a magic word, frame_cap and the undistortion flag.  Unpack never blocks the host:
+ * the header is checked on the device, in stream order.  A record that does not match the context's plan, or
+ * whose count exceeds frame_cap, leaves frame 0 with count 0, and the next call that checks the context's status
+ * (orbgpu_synchronize, orbgpu_batch_download, or any other call that returns results to the host) returns
+ * ORBGPU_ERR_ARG.  Without a planned context, unpack itself returns ORBGPU_ERR_ARG. */
 long long orbgpu_frame_record_bytes(const orbgpu_ctx* ctx);
 int orbgpu_frame_record_pack(orbgpu_ctx* ctx, int b, void* d_dst);
 int orbgpu_frame_record_unpack(orbgpu_ctx* ctx, const void* d_src);

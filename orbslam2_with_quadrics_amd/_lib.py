@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# ORBGPU_LIB selects an experiment build of the same library (tools/fast_variants.py); default in-tree
+# ORBGPU_LIB selects an experiment build of the same library (tools/variant_bench.py, tools/octree_profile.py); default in-tree
 LIB_PATH = os.environ.get("ORBGPU_LIB") or os.path.join(HERE, "liborbgpu.so")
 
 # Every symbol include/orbgpu.h declares (checked by tests/test_lib_abi.py).

@@ -42,7 +42,7 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None) -> str:
-    """Build liborbgpu.so (or, with `out`/`defines`, an experiment variant of it, e.g. tools/fast_variants.py)."""
+    """Build liborbgpu.so (or, with `out`/`defines`, a timing variant of it: every remaining -D switch selects a bit-exact alternative)."""
     target = out or LIB
     if not force and out is None and not _stale():
         return LIB

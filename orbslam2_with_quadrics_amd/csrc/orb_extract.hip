@@ -2,7 +2,7 @@
 //
 //   k1 og_resize_kernel    : one chained pyramid level (cv::resize INTER_LINEAR 8U; vertical form per
 //                            ORBGPU_SEM_RESIZE_*)
-//   k2 og_fast_blocks_kernel: one 512-thread workgroup per block of up to 2x2 FAST cells: ROI -> LDS,
+//   k2 og_fast_quad_kernel: one 512-thread workgroup per block of up to 2x2 FAST cells: ROI -> LDS,
 //                            threshold-free quick test, FAST-9 score, same-cell 3x3 NMS, the reference's
 //                            per-cell 20 -> 7 fallback, ballot compaction into the (frame, level) slots
 //   k3 og_octree_kernel    : one 1024-thread workgroup per (frame, level): the DistributeOctTree list
@@ -394,7 +394,7 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
 #pragma unroll
     for (int k = 0; k < 4; k++) og_rz_weights<FX>(g.xtabA, g.xmaxA, min(cA + k, ac1), sc0, sxA, wtA, k);
     // staging addresses: the region's first row (wave-uniform, SGPRs) rounded down to 16 bytes plus a 32-bit lane
-    // offset; chunk -> (row, chunk) with the exact float quotient (as in og_fast_blocks_kernel: nIt < 2^14)
+    // offset; chunk -> (row, chunk) with the exact float quotient (nIt < 2^14)
     const uint8_t* rbase = src + (long long)f * src_fstride + (long long)sr0 * src_pitch + sc0;
     const unsigned mb = (unsigned)((uintptr_t)rbase & 15);
     const uint8_t* abase = rbase - mb;
@@ -545,25 +545,15 @@ __device__ __forceinline__ int og_fast_M1(const E* p, int st, int fm)
 // threshold t if for every opposite pair one pixel is darker than v-t (resp. brighter than v+t).
 // Necessary condition => every pixel that fails it has M <= t.  Restated threshold-free:
 //   dark(t)   <=>  max_k min(c_k, c_k+8) < v - t,   bright(t) <=> min_k max(c_k, c_k+8) > v + t.
-// The same quick test for two pixels at once: each dword of the pair-interleaved ROI holds (pixel x, pixel
-// x + H) as two u16, so one LDS read gives a circle sample of both pixels and v_pk_min/max_u16 test both.
-// Returns {dark, bright} dwords whose low (high) half is nonzero iff the first (second) pixel passes that
-// polarity's test.
+// Two pixels at once: each dword holds two pixels as u16 halves 0x6400 | pixel = the f16 value 1024 + pixel
+// (exact, monotone), so the packed f16 ops of gfx950 apply and v_pk_maximum3/minimum3_f16 reduce the 8 pair
+// minima (maxima) in 4 ops.  All values are integers below 2048 (exact in f16); x - x = +0 and
+// max(negative, +0) = +0, so a half of the returned {dark, bright} dwords is nonzero iff that pixel passes
+// that polarity's test.
 typedef unsigned short og_u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ og_u16x2 og_as_u16x2(uint32_t x) { return __builtin_bit_cast(og_u16x2, x); }
-
-#ifndef OG_EXP_FAST_STOP
-#define OG_EXP_FAST_STOP 0
-#endif
-#ifndef OG_FAST_SLOT_BARRIER
-#define OG_FAST_SLOT_BARRIER 0  // 1: no scheduling across stage 1's two slots
-#endif
-#ifndef OG_FAST_F16
-#define OG_FAST_F16 1  // stage 1's quick test in packed f16 with the gfx950 3-input max/min (0: packed u16)
-#endif
 
 // ------------------------------------------------------------------------------------------------
-// k2': FAST over blocks of up to 2x2 cells.  The cells' detection areas tile a level without overlap
+// k2: FAST over blocks of up to 2x2 cells.  The cells' detection areas tile a level without overlap
 // (cell j covers [minB + j*wCell + 3, minB + (j+1)*wCell + 3); only the last row/column is clipped), so a
 // block's detection area is the union and a pixel's cell is (i >= hCell, j >= wCell).  Every per-cell rule
 // of src/ORBextractor.cc:789-829 + cv::FAST is kept: the NMS only sees corners of the same cell, and each
@@ -572,10 +562,7 @@ __device__ __forceinline__ og_u16x2 og_as_u16x2(uint32_t x) { return __builtin_b
 // ------------------------------------------------------------------------------------------------
 #define FB_NT 512
 #define FB_NW (FB_NT / 64)
-#define FB_H 32                  // pair offset: roi2 dword (r, x) = ROI pixels (r, x) and (r, x + 32)
-#define FB_S2 52                 // pair-ROI row stride in dwords (>= 32 + 6 + 3 misalignment, 4-dword multiple)
-#define FB_ROWS 86               // ROI rows (detection <= 80 + 6)
-#define FB_MW 80                 // detection height capacity of a block (2 x 40 or 1 x 64); width <= 2 * FB_H
+#define FB_MW 80                 // detection height capacity of a block (2 x 40 or 1 x 64); width <= 64
 #define FB_MSW (FB_MW + 3)       // score map stride: a zero gap column before, between and after the cells
 #define FB_MSZ ((FB_MSW * FB_MSW + 15) & ~15)  // 16-byte multiple: zeroed by 16-byte stores
 
@@ -586,16 +573,10 @@ __device__ __forceinline__ int og_ms_idx(int i, int j, int wC, int hC)
     return (i + 1 + (i >= hC)) * FB_MSW + (j + 1 + (j >= wC));
 }
 
-// The pair minima / maxima reduce as trees (depth 3 instead of a chain of 8): two slots' packed ops interleave
-// without hazard nops.
-// c[k] = circle sample k (pair dwords, cv::FAST's offsets; only the opposite pairs {k, k+8} matter), pv = centre
+// c[k] = circle sample k (f16-biased pixel pairs, cv::FAST's offsets; only the opposite pairs {k, k+8} matter),
+// pv = centre.  The pair minima / maxima reduce as trees (depth 3 instead of a chain of 8).
 __device__ __forceinline__ uint2 og_fast_quick2v(const uint32_t (&c)[16], uint32_t pv, og_u16x2 tt)
 {
-#if OG_FAST_F16
-    // The ROI halves hold 0x6400 | pixel = the f16 value 1024 + pixel (exact, monotone), so the packed f16 ops of
-    // gfx950 apply: v_pk_maximum3/minimum3_f16 reduce the 8 pair minima (maxima) in 4 ops instead of 7.  All
-    // values are integers below 2048 (exact in f16); x - x = +0 and max(negative, +0) = +0, so a half is nonzero
-    // iff its test passes, as in the integer form.
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     const h2 v = __builtin_bit_cast(h2, pv);
     const h2 t = {(_Float16)tt.x, (_Float16)tt.y}, z = {(_Float16)0, (_Float16)0};
@@ -614,54 +595,6 @@ __device__ __forceinline__ uint2 og_fast_quick2v(const uint32_t (&c)[16], uint32
     const h2 dark = __builtin_elementwise_maximum((v - t) - dmax, z);
     const h2 bright = __builtin_elementwise_maximum(bmin - (v + t), z);
     return make_uint2(__builtin_bit_cast(uint32_t, dark), __builtin_bit_cast(uint32_t, bright));
-#else
-    const og_u16x2 v = og_as_u16x2(pv);
-    og_u16x2 mn[8], mx[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        mn[k] = __builtin_elementwise_min(og_as_u16x2(c[k]), og_as_u16x2(c[k + 8]));
-        mx[k] = __builtin_elementwise_max(og_as_u16x2(c[k]), og_as_u16x2(c[k + 8]));
-    }
-#pragma unroll
-    for (int w = 4; w >= 1; w >>= 1)
-#pragma unroll
-        for (int k = 0; k < w; k++) {
-            mn[k] = __builtin_elementwise_max(mn[k], mn[k + w]);
-            mx[k] = __builtin_elementwise_min(mx[k], mx[k + w]);
-        }
-    const og_u16x2 dark = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, tt), mn[0]);
-    const og_u16x2 bright = __builtin_elementwise_sub_sat(mx[0], v + tt);
-    return make_uint2(__builtin_bit_cast(uint32_t, dark), __builtin_bit_cast(uint32_t, bright));
-#endif
-}
-
-#ifndef OG_EXP_FAST_READS
-#define OG_EXP_FAST_READS 0  // timing experiments only (results wrong): 1 = 9 of the 17 LDS reads, 2 = 34 reads
-#endif
-__device__ __forceinline__ uint2 og_fast_quick2(const uint32_t* p, int st, og_u16x2 tt)
-{
-#if OG_EXP_FAST_READS == 1
-    uint32_t c[16] = {p[3 * st], p[1 + 3 * st], p[2 + 2 * st], p[3 + 1 * st], p[3], p[3 - 1 * st], p[2 - 2 * st],
-                      p[1 - 3 * st]};
-#pragma unroll
-    for (int k = 8; k < 16; k++) c[k] = __builtin_amdgcn_alignbyte(c[k - 8], c[(k - 5) & 7], 1);
-#else
-    const uint32_t c[16] = {p[3 * st],      p[1 + 3 * st],  p[2 + 2 * st],  p[3 + 1 * st],
-                            p[3],           p[3 - 1 * st],  p[2 - 2 * st],  p[1 - 3 * st],
-                            p[-3 * st],     p[-1 - 3 * st], p[-2 - 2 * st], p[-3 - 1 * st],
-                            p[-3],          p[-3 + 1 * st], p[-2 + 2 * st], p[-1 + 3 * st]};
-#endif
-#if OG_EXP_FAST_READS == 2
-    uint32_t c2[16];
-    __asm__ volatile("" ::: "memory");
-#pragma unroll
-    for (int k = 0; k < 16; k++) c2[k] = ((volatile const uint32_t*)p)[k - 3 + ((k & 3) - 1) * st] ^ c[k];
-    uint2 r = og_fast_quick2v(c, p[0], tt);
-    r.x |= (c2[0] | c2[5] | c2[9] | c2[14]) & 0x80008000u;  // keeps the 16 extra reads live (bit 15 is 0)
-    return r;
-#else
-    return og_fast_quick2v(c, p[0], tt);
-#endif
 }
 
 // lanes whose u16 low half is nonzero (one v_cmp on the low 16 bits)
@@ -671,17 +604,6 @@ __device__ __forceinline__ u64 og_lanes_lo16_nz(uint32_t a)
     __asm__("v_cmp_ne_u16_e64 %0, 0, %1" : "=s"(m) : "v"(a));
     return m;
 }
-
-// ds_write_b16 from the lanes of `mask` only (exec = exec & mask around the store, restored after it)
-__device__ __forceinline__ void og_ds_write_b16_lanes(u64 mask, uint32_t lds_addr, uint32_t val)
-{
-    u64 sv;
-    __asm__ volatile("s_and_saveexec_b64 %0, %1\n\tds_write_b16 %2, %3\n\ts_mov_b64 exec, %0"
-                     : "=&s"(sv)
-                     : "s"(mask), "v"(lds_addr), "v"(val)
-                     : "memory");
-}
-
 
 // block table reads through the constant address space: uniform, so one scalar load (through a generic pointer
 // the compiler cannot prove the table unclobbered by the kernel's own stores and falls back to vector loads).  The
@@ -758,387 +680,21 @@ __device__ __forceinline__ OgFB og_fast_decode(const OgFastBlk* blocks, int p, u
     return b;
 }
 
-// ROI -> registers: 3 rows x (lo, hi) dwords per lane (og_fast_roi_store puts them into LDS).  The loads are
-// unconditional (no exec branches): rows past the ROI re-read its last row, columns past it read image bytes to the
-// right of the ROI (or the next row's first bytes: every ROI row has a row below it in the level); both are masked
-// to 0 / not stored.  Addresses: the block's uniform row base (SGPRs) plus a 32-bit per-lane offset (saddr + voffset
-// loads, no 64-bit lane arithmetic).
-__device__ __forceinline__ void og_fast_roi_load(const OgFB& b, int tid, uint32_t (&blo)[3], uint32_t (&bhi)[3])
-{
-    constexpr int H = FB_H;
-    const int nq = (H + 6 + b.mis + 3) >> 2;  // dword groups per row
-    const int q = tid & 15;
-    const uint8_t* rbase = b.row0 - b.mis;
-    const unsigned mb = (unsigned)((uintptr_t)rbase & 3);  // odd pitch: the rows' misalignment base
-    const uint8_t* abase = rbase - mb;                       // 4-byte aligned
-    const unsigned qq = 4u * (unsigned)min(q, nq - 1);
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const int r = min((tid >> 4) + 32 * k, b.rh - 1);
-        const unsigned off = (unsigned)r * b.upitch + qq;
-        if (b.aligned) {  // block-uniform
-            blo[k] = *(const uint32_t*)(rbase + off);
-            bhi[k] = *(const uint32_t*)(rbase + off + (unsigned)H);
-        } else {
-            // odd pitch: two aligned loads funnel-shifted by the row's offset
-            const unsigned o = off + mb, o2 = o + (unsigned)H;
-            const uint32_t* a = (const uint32_t*)(abase + (o & ~3u));
-            const uint32_t* a2 = (const uint32_t*)(abase + (o2 & ~3u));
-            blo[k] = __builtin_amdgcn_alignbyte(a[1], a[0], o & 3u);
-            bhi[k] = __builtin_amdgcn_alignbyte(a2[1], a2[0], o2 & 3u);
-        }
-    }
-}
-
-// registers -> LDS as column pairs: roi2 dword (r, x) = ROI pixel (r, x) | ROI pixel (r, x + H) << 16 (at roi2 + mis),
-// split with v_perm into four pair dwords and stored as one 16-byte write
-__device__ __forceinline__ void og_fast_roi_store(const OgFB& b, int tid, const uint32_t (&blo)[3],
-                                                  const uint32_t (&bhi)[3], uint32_t* roi2)
-{
-    constexpr int H = FB_H;
-    const int nq = (H + 6 + b.mis + 3) >> 2;
-    const int q = tid & 15;
-    const int x = 4 * q - b.mis;  // ROI column of a lane's first byte
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const int r = (tid >> 4) + 32 * k;
-        const uint32_t lo = x < b.rw ? blo[k] : 0u, hi = x + H < b.rw ? bhi[k] : 0u;
-        if (r < b.rh && q < nq) {
-            uint4 o;
-            o.x = __builtin_amdgcn_perm(hi, lo, 0x0c040c00u);
-            o.y = __builtin_amdgcn_perm(hi, lo, 0x0c050c01u);
-            o.z = __builtin_amdgcn_perm(hi, lo, 0x0c060c02u);
-            o.w = __builtin_amdgcn_perm(hi, lo, 0x0c070c03u);
-#if OG_FAST_F16
-            o.x |= 0x64006400u;  // f16 1024 + pixel per half (og_fast_quick2v); the score differences cancel it
-            o.y |= 0x64006400u;
-            o.z |= 0x64006400u;
-            o.w |= 0x64006400u;
-#endif
-            *(uint4*)&roi2[r * FB_S2 + 4 * q] = o;
-        }
-    }
-}
-
-#ifndef OG_FAST_KB
-#define OG_FAST_KB 1  // FAST blocks per workgroup; > 1 prefetches the next block's ROI during stages 2-4 (measured slower)
-#endif
-
-// k2: FAST over blocks of up to 2x2 cells, OG_FAST_KB blocks per workgroup: workgroup x of frame f takes blocks
-// x, x + G, x + 2G, ... (G = gridDim.x), so every round of the grid still covers consecutive blocks (plan order).
-// Per block: ROI (prefetched into VGPRs during the previous block) -> LDS, stage 1 quick test + survivor list,
-// stage 2 exact scores, stage 3 same-cell NMS and per-cell counts, stage 4 the reference's per-cell 20 -> 7
-// fallback and one candidate reservation per block; the score map is restored to zero entry by entry in stage 4.
-__global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_fast_blocks_kernel(
-    const OgFastBlk* __restrict__ blocks, int nb, const uint8_t* __restrict__ img0, long long pitch0, long long fstride0,
-    const uint8_t* __restrict__ pyr, long long pyr_per_frame, u64* __restrict__ cand, long long cand_per_frame,
-    int* __restrict__ cand_count, int nlevels, int thr, int* __restrict__ status)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t roi2[FB_ROWS * FB_S2];
-    __shared__ __attribute__((aligned(16))) uint8_t Ms[FB_MSZ];
-    __shared__ uint16_t lst[FB_MW * FB_MW];    // survivors (i << 7) | j; bits 14/15: dark/bright passes (stages 1-2),
-                                               // then kept at t1/t2 (stages 3-4)
-    __shared__ int sh_ns;
-    __shared__ __attribute__((aligned(16))) int wk[FB_NW][8];  // per wave: kept at t1 per cell [0..3], at t2 [4..7]
-    __shared__ int sh_base;
-    constexpr int H = FB_H;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int wvu = __builtin_amdgcn_readfirstlane(wv);
-    const unsigned f = blockIdx.y;  // grid (ceil(blocks per frame / KB), frames)
-    int p = blockIdx.x;
-    if (p >= nb) return;
-    const int t1 = thr & 255, t2 = (thr >> 8) & 255;  // clamped to [0, 255] on the host
-    const int tq = min(t1, t2);
-    const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
-    const int tA = max(t1, 1), tB = max(t2, 1);
-    const uint32_t a_ns = og_lds_addr(&sh_ns), a_lst = og_lds_addr(&lst[0]);
-    OgFB b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
-    if (b.l < 0) return;  // padding entry
-    uint32_t blo[3], bhi[3];
-    og_fast_roi_load(b, tid, blo, bhi);
-    og_fast_roi_store(b, tid, blo, bhi, roi2);
-    for (int idx = tid * 16; idx < FB_MSZ; idx += FB_NT * 16) *(uint4*)&Ms[idx] = make_uint4(0u, 0u, 0u, 0u);
-    if (tid == 0) sh_ns = 0;
-    __syncthreads();
-#pragma unroll 1
-    for (int k = 0;; k++) {
-#if OG_EXP_FAST_STOP == 1  // timing experiments only (tools/fast_variants.py): results are wrong
-        if (roi2[tid] == 255u && roi2[tid + 1] == 254u) cand_count[0] = 1;
-        return;
-#endif
-        const int dw = b.dw, dh = b.dh, wC = b.wC, hC = b.hC;
-        const uint32_t* T2 = roi2 + b.mis;  // T2[r*FB_S2 + x] = pair (x, x + H) of ROI row r
-        // ---- stage 1: quick test on every detection pixel, two per lane.  Lane L of a wave holds pair column
-        // c = L & 31 of ROI pair row r0 + (L >> 5), i.e. pixels (i, c) and (i, c + 32); wave w takes the row pairs
-        // {2w, 2w + 1} + 16k, two row pairs (slots) per iteration.  Row and column validity are wave-uniform masks
-        // (scalar), addresses are a per-lane constant plus a scalar row offset.  One LDS reservation per wave
-        // iteration appends the survivors to the block's flat list (stages 2-4 then spread the list evenly); the
-        // stores take the survivor masks as exec.
-        {
-            const int lrow = lane >> 5, lcol = lane & 31;
-            const uint32_t* Tl = &T2[(lrow + 3) * FB_S2 + (lcol + 3)];
-            const uint32_t e_lane = (uint32_t)((lrow << 7) | lcol);
-            // lanes whose column (lane & 31) is inside the detection width, for the low and the high pixel
-            const unsigned clo = dw >= 32 ? 0xffffffffu : ((1u << dw) - 1u);
-            const unsigned chi = dw >= 64 ? 0xffffffffu : (dw <= 32 ? 0u : ((1u << (dw - 32)) - 1u));
-            const u64 colLo = ((u64)clo << 32) | clo, colHi = ((u64)chi << 32) | chi;
-            // one iteration: pair rows r0, r0 + 1 (slot 0) and r0 + 16, r0 + 17 (slot 1); FULL: all inside the area
-            auto iter = [&](auto full_tag, int r0) {
-                constexpr bool FULL = decltype(full_tag)::value;
-                uint2 r[2];
-                u64 m[4];
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const int rr = r0 + 2 * FB_NW * h;  // wave-uniform pair row of lanes 0-31
-                    // (tail: rows past the area re-test row dh - 1 / dh and are masked out)
-                    r[h] = og_fast_quick2(Tl + (FULL ? rr : min(rr, dh - 1)) * FB_S2, FB_S2, tt);
-                    const uint32_t any = r[h].x | r[h].y;
-                    if (FULL) {
-                        m[2 * h] = og_lanes_lo16_nz(any) & colLo;
-                        m[2 * h + 1] = og_lanes_gt((int)any, 0xffff) & colHi;
-                    } else {
-                        const u64 rows = (rr < dh ? 0xffffffffull : 0ull) | (rr + 1 < dh ? 0xffffffff00000000ull : 0ull);
-                        m[2 * h] = og_lanes_lo16_nz(any) & rows & colLo;
-                        m[2 * h + 1] = og_lanes_gt((int)any, 0xffff) & rows & colHi;
-                    }
-                }
-                int cnt[4], n = 0;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    cnt[q] = __popcll(m[q]);
-                    n += cnt[q];
-                }
-                if (n) {
-                    // one LDS reservation per wave iteration from lane 0 (exec = lane 0 only; no atomic-optimizer code)
-                    uint32_t old;
-                    u64 sv;
-                    __asm__ volatile(
-                        "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_waitcnt lgkmcnt(0)\n\t"
-                        "s_mov_b64 exec, %1"
-                        : "=&v"(old), "=&s"(sv)
-                        : "v"(a_ns), "v"(n)
-                        : "memory");
-                    const uint32_t ab = a_lst + 2u * (uint32_t)__builtin_amdgcn_readfirstlane(old);
-                    uint32_t v[4];
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        // entry (i << 7) | j, bits 14 = dark, 15 = bright (halves of r.x / r.y nonzero, min(half, 1)
-                        // per half); only the low 16 bits are stored
-                        uint32_t d1, b1;
-                        __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r[h].x), "s"(0x00010001u));
-                        __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r[h].y), "s"(0x00020002u));
-                        const uint32_t pb = d1 | b1;
-                        const uint32_t base = e_lane + (uint32_t)((r0 + 2 * FB_NW * h) << 7);
-                        v[2 * h] = (pb << 14) | base;
-                        v[2 * h + 1] = (pb >> 2) | (base + (uint32_t)H);  // pb >> 2 holds only bits 14-15
-                    }
-                    // list slot of each survivor: the wave's reservation + the counts of the masks before + its rank
-                    const uint32_t ab1 = ab + 2u * (uint32_t)cnt[0], ab2 = ab1 + 2u * (uint32_t)cnt[1],
-                                   ab3 = ab2 + 2u * (uint32_t)cnt[2];
-                    og_ds_write_b16_x4(m[0], ab + 2u * (uint32_t)og_rank(m[0]), v[0], m[1],
-                                       ab1 + 2u * (uint32_t)og_rank(m[1]), v[1], m[2], ab2 + 2u * (uint32_t)og_rank(m[2]),
-                                       v[2], m[3], ab3 + 2u * (uint32_t)og_rank(m[3]), v[3]);
-                }
-            };
-            int r0 = 2 * wvu;
-            for (; r0 + 2 * FB_NW + 1 < dh; r0 += 4 * FB_NW) iter(std::true_type{}, r0);
-            if (r0 < dh) iter(std::false_type{}, r0);
-        }
-        // prefetch: the next block's record and ROI loads are issued now and land during stages 2-4
-        const int pn = p + (int)gridDim.x;
-        bool has_next = k + 1 < OG_FAST_KB && pn < nb;  // block-uniform
-        OgFB bn = b;
-        if (has_next) {
-            bn = og_fast_decode(blocks, pn, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
-            has_next = bn.l >= 0;  // a padding entry ends the chain (the table pads each level to 8 entries)
-            if (has_next) og_fast_roi_load(bn, tid, blo, bhi);
-        }
-        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm list stores are not tracked by the compiler
-        __syncthreads();
-        const int ns = sh_ns;
-#if OG_EXP_FAST_STOP == 2  // timing experiments only (tools/fast_variants.py): results are wrong
-        if (ns == 12345) cand_count[0] = 1;
-        return;
-#endif
-        // ---- stage 2: exact M for every survivor (eager: a lazy per-cell pass costs more than it saves, DESIGN.md
-        // §5).  Single pixels are u16 reads of the pair layout (element step 2 per column).
-        const uint16_t* T16 = (const uint16_t*)T2;
-        for (int e = tid; e < ns; e += FB_NT) {
-            const int ent = lst[e];
-            const int i = (ent >> 7) & 127, j = ent & 127;
-            const int hi = j >= H;
-            const int x = j - (hi ? H : 0);
-            const uint16_t* pc = &T16[2 * ((i + 3) * FB_S2 + (x + 3)) + hi];
-            const bool dark = (ent & 0x4000) != 0, bright = (ent & 0x8000) != 0;
-            int M = og_fast_M1<2>(pc, 2 * FB_S2, dark ? 0 : 0xff);
-            if (dark && bright) {
-                // rare: both polarities pass.  The second pass re-reads its circle (the clobber stops the loads
-                // being merged with the first pass's, which would keep those 17 values live through it)
-                __asm__ volatile("" ::: "memory");
-                M = max(M, og_fast_M1<2>(pc, 2 * FB_S2, 0xff));
-            }
-            Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)M;
-        }
-        __syncthreads();
-        // roi2 and sh_ns are free from here on: the next block's ROI goes in while this block finishes
-        if (tid == 0) sh_ns = 0;
-        if (has_next) og_fast_roi_store(bn, tid, blo, bhi, roi2);
-        // ---- stage 3: same-cell 3x3 NMS at both thresholds.  cv::FAST keeps a corner (score M-1) iff its score
-        // beats every neighbour's score, where non-corners score 0: with the gap layout and M <= t for every
-        // non-corner, that is  M > max(t, 1)  and  M > max over the 8 neighbours of M.
-        int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
-        for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
-            const int e = e0 + lane;
-            int ent = 0, mc = 0, nbm = 0;
-            if (e < ns) {
-                ent = lst[e] & 0x3fff;
-                const uint8_t* q = &Ms[og_ms_idx(ent >> 7, ent & 127, wC, hC) - FB_MSW - 1];
-                mc = q[FB_MSW + 1];
-                nbm = max(max(max(q[0], q[1]), max(q[2], q[FB_MSW])),
-                          max(max(q[FB_MSW + 2], q[2 * FB_MSW]), max(q[2 * FB_MSW + 1], q[2 * FB_MSW + 2])));
-            }
-            const u64 top = og_lanes_gt(mc, nbm);
-            const u64 K1 = og_lanes_gt(mc, tA) & top, K2 = og_lanes_gt(mc, tB) & top;
-            const u64 ci = og_lanes_gt(ent >> 7, hC - 1), cj = og_lanes_gt(ent & 127, wC - 1);
-            if (e < ns) lst[e] = (uint16_t)(ent | (mc > tA && mc > nbm ? 0x4000 : 0) | (mc > tB && mc > nbm ? 0x8000 : 0));
-            const u64 cm[4] = {~ci & ~cj, ~ci & cj, ci & ~cj, ci & cj};
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                c1[c] += __popcll(K1 & cm[c]);
-                c2[c] += __popcll(K2 & cm[c]);
-            }
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                wk[wv][c] = c1[c];
-                wk[wv][4 + c] = c2[c];
-            }
-        }
-        __syncthreads();
-        // per cell: iniThFAST unless the cell is empty at it (src/ORBextractor.cc:809-816).  Lane-parallel: lane L < 32
-        // holds wave L/4's counts of cell L%4 (every wave computes the same block-uniform result; lanes >= 32 repeat
-        // lanes L - 32 and are masked off); the per-wave sums land in lanes 0-7 and are scanned with DPP
-        const int qw = (lane >> 2) & (FB_NW - 1), qc = lane & 3;
-        const int v1 = wk[qw][qc], v2 = wk[qw][4 + qc];
-        const u64 nz1 = og_lanes_ne((unsigned)v1, 0u) & 0xffffffffull;
-        unsigned useT2 = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) useT2 |= ((nz1 & (0x11111111ull << c)) ? 0u : 1u) << c;
-        const int kw = ((useT2 >> qc) & 1u) ? v2 : v1;
-        int ks = kw + __builtin_amdgcn_mov_dpp(kw, 0xb1, 0xf, 0xf, false);
-        ks = ks + __builtin_amdgcn_mov_dpp(ks, 0x4e, 0xf, 0xf, false);  // lane 4w: wave w's kept count
-        const int kx = __shfl(ks, 4 * (lane & 7));                        // lane w (< 8): wave w's kept count
-        int sc = kx;
-        sc += __builtin_amdgcn_update_dpp(0, sc, 0x111, 0xf, 0xf, true);  // row_shr:1 (inclusive scan, lanes 0-7)
-        sc += __builtin_amdgcn_update_dpp(0, sc, 0x112, 0xf, 0xf, true);  // row_shr:2
-        sc += __builtin_amdgcn_update_dpp(0, sc, 0x114, 0xf, 0xf, true);  // row_shr:4
-        const int total = __builtin_amdgcn_readlane(sc, FB_NW - 1);
-        const int kept = __builtin_amdgcn_readlane(kx, wvu);
-        const int before = __builtin_amdgcn_readlane(sc, wvu) - kept;
-#if OG_EXP_FAST_STOP == 3
-        if (total == 12345) cand_count[0] = 1;
-        return;
-#endif
-        // ---- stage 4: one reservation per block; each wave writes its kept entries at its offset (the octree
-        // orders candidates by position, not slot).  Every entry's score-map cell goes back to zero.
-        int sb = 0;
-        if (total != 0) {  // block-uniform
-            if (tid == 0) {
-                const int bb = atomicAdd(&cand_count[f * nlevels + b.l], total);
-                if (bb + total > b.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
-                sh_base = bb;
-            }
-            __syncthreads();
-            sb = sh_base;
-        }
-        const bool emit = total != 0 && sb + total <= b.cand_cap && kept != 0;
-        u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb + before);
-        int run = 0;
-        for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
-            const int e = e0 + lane;
-            int ent = 0;
-            if (e < ns) ent = lst[e];
-            const int i = (ent >> 7) & 127, j = ent & 127;
-            const int cell = (i >= hC) * 2 + (j >= wC);
-            const unsigned kb = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
-            const u64 mask = og_lanes_ne(kb, 0u);
-            if (e < ns) {
-                uint8_t* mcell = &Ms[og_ms_idx(i, j, wC, hC)];
-                if (emit && kb) out[og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, *mcell - 1);
-                *mcell = 0;
-            }
-            run += __popcll(mask);
-        }
-        if (!has_next) break;
-        b = bn;
-        p = pn;
-        __syncthreads();  // score map back to zero, list consumed, next ROI stored
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
-// k2 (quad layout): the same block, stages and results as og_fast_blocks_kernel, with the ROI stored as u16
-// quads: qword (r, x) of roiq holds ROI pixels (r, x), (r, x + 16), (r, x + 32), (r, x + 48).  One ds_read_b64 (2
-// LDS cycles) then gives one circle sample of four pixels, where the pair layout's ds_read2_b32 gives two samples
-// of two pixels each in 4 cycles: stage 1 -- LDS-bound -- moves half the LDS cycles per pixel.
+// k2 (quad layout): the ROI is stored as u16 quads: qword (r, x) of roiq holds ROI pixels (r, x), (r, x + 16),
+// (r, x + 32), (r, x + 48).  One ds_read_b64 (2 LDS cycles) then gives one circle sample of four pixels.
 // Lane L of a wave takes quad column c = L & 15 of ROI row R + {0, 4, 1, 5}[L >> 4]: the two 16-lane row groups of
 // each 32-lane LDS access are 4 rows = 112 qwords = 16 (mod 32) apart, so every b64 access is bank-conflict free.
 // ------------------------------------------------------------------------------------------------
-#ifndef OG_FASTQ_KB
-#define OG_FASTQ_KB 1  // FAST blocks per quad-kernel workgroup; > 1 prefetches the next block's ROI during stage 2
-#endif
 #define FQ_S 28     // quad-ROI row stride in qwords (>= 16 + 6 + 3 misalignment; 4 * FQ_S = 16 mod 32)
 #define FQ_ROWS 86  // ROI rows (detection <= 80 + 6)
-#ifndef OG_FASTQ_WL
-#define OG_FASTQ_WL 0  // 1: per-wave survivor lists (stage 2 follows each wave's stage 1 without a barrier, no LDS
-                       // atomic per unit): bit-exact but FAST +5 % (8 partly filled stage-2/3 chunks per block instead
-                       // of 7 full ones; profiles/sweeps/r03_ab_fast_wave_lists.txt); 0: one block list reserved per
-                       // unit with ds_add_rtn
-#endif
-// per-wave list capacity: wave w takes units w, w + 8, w + 16 (<= 20 units of 4 x 64 pixels: dh <= 80)
-#define FQ_WCAP 768
-static_assert(FB_NT / 64 * FQ_WCAP <= 80 * 80, "per-wave lists fit the block list");
-static_assert(OG_FASTQ_WL == 0 || OG_FASTQ_KB == 1, "per-wave lists: one block per workgroup");
-
-// The 17 quad samples of og_fast_quad_kernel's stage 1 (cv::FAST's circle order, then the centre) as plain
-// ds_read_b64 (2 LDS cycles each): the compiler would pair them into ds_read2_b64, which costs 8 cycles per pair.
-// base = LDS byte address of the quad 3 rows up and 3 columns left of the centre.  The reads and their wait are one
-// asm statement, so no output is used before it has landed.
-static_assert(FQ_S == 28, "og_fastq_circle's offsets assume FQ_S == 28");
-__device__ __forceinline__ void og_fastq_circle(uint32_t base, unsigned long long (&w)[17])
-{
-    __asm__ volatile(
-        "ds_read_b64 %0, %17 offset:1368\n\t"
-        "ds_read_b64 %1, %17 offset:1376\n\t"
-        "ds_read_b64 %2, %17 offset:1160\n\t"
-        "ds_read_b64 %3, %17 offset:944\n\t"
-        "ds_read_b64 %4, %17 offset:720\n\t"
-        "ds_read_b64 %5, %17 offset:496\n\t"
-        "ds_read_b64 %6, %17 offset:264\n\t"
-        "ds_read_b64 %7, %17 offset:32\n\t"
-        "ds_read_b64 %8, %17 offset:24\n\t"
-        "ds_read_b64 %9, %17 offset:16\n\t"
-        "ds_read_b64 %10, %17 offset:232\n\t"
-        "ds_read_b64 %11, %17 offset:448\n\t"
-        "ds_read_b64 %12, %17 offset:672\n\t"
-        "ds_read_b64 %13, %17 offset:896\n\t"
-        "ds_read_b64 %14, %17 offset:1128\n\t"
-        "ds_read_b64 %15, %17 offset:1360\n\t"
-        "ds_read_b64 %16, %17 offset:696\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5]), "=&v"(w[6]), "=&v"(w[7]),
-          "=&v"(w[8]), "=&v"(w[9]), "=&v"(w[10]), "=&v"(w[11]), "=&v"(w[12]), "=&v"(w[13]), "=&v"(w[14]), "=&v"(w[15]),
-          "=&v"(w[16])
-        : "v"(base)
-        : "memory");
-}
 
 __device__ __forceinline__ void og_fastq_roi_load(const OgFB& b, int tid, uint32_t (&s)[2][4])
 {
     // item (row, group of 4 qwords): 4 dword loads (one per 16-column segment), 8 v_perm into 4 quads, two 16-byte
     // LDS stores.  Columns past the ROI hold image bytes to its right (never read by a detection pixel); rows past it
-    // are not stored.  Loads as in og_fast_roi_load (unconditional, saddr + 32-bit lane offset).
+    // are not stored.  The loads are unconditional (no exec branches): rows past the ROI re-read its last row.
+    // Addresses: the block's uniform row base (SGPRs) plus a 32-bit per-lane offset (saddr + voffset loads).
     const int nq4 = (16 + 6 + b.mis + 3) >> 2;  // groups of 4 qwords per row (<= 7)
     const int q4 = min(tid & 7, nq4 - 1);
     const uint8_t* rbase = b.row0 - b.mis;
@@ -1148,16 +704,12 @@ __device__ __forceinline__ void og_fastq_roi_load(const OgFB& b, int tid, uint32
     for (int k = 0; k < 2; k++) {
         const int r = min((tid >> 3) + 64 * k, b.rh - 1);
         const unsigned off = (unsigned)r * b.upitch + 4u * (unsigned)q4;
-#ifndef OG_EXP_FAST_NOMEM
-#define OG_EXP_FAST_NOMEM 0  // timing experiments only: 1 = a synthetic ROI instead of the global loads (results wrong)
-#endif
 #pragma unroll
         for (int g = 0; g < 4; g++) {
-            if (OG_EXP_FAST_NOMEM) {
-                s[k][g] = (off + 16u * g) * 0x9e3779b1u;
-            } else if (b.aligned) {
+            if (b.aligned) {
                 s[k][g] = *(const uint32_t*)(rbase + off + 16u * g);
             } else {
+                // odd pitch: two aligned loads funnel-shifted by the row's offset
                 const unsigned o = off + 16u * g + mb;
                 const uint32_t* a = (const uint32_t*)(abase + (o & ~3u));
                 s[k][g] = __builtin_amdgcn_alignbyte(a[1], a[0], o & 3u);
@@ -1188,6 +740,9 @@ __device__ __forceinline__ void og_fastq_roi_put(const OgFB& b, int tid, const u
     }
 }
 
+// One block per workgroup.  Stage 1: quick test of every detection pixel and a survivor list; stage 2: exact scores
+// into the score map; stage 3: same-cell NMS at both thresholds and per-cell counts; stage 4: the reference's
+// per-cell 20 -> 7 fallback, one global reservation per block and the candidate stores.
 __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_fast_quad_kernel(
     const OgFastBlk* __restrict__ blocks, int nb, const uint8_t* __restrict__ img0, long long pitch0, long long fstride0,
     const uint8_t* __restrict__ pyr, long long pyr_per_frame, u64* __restrict__ cand, long long cand_per_frame,
@@ -1203,37 +758,29 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);
     const unsigned f = blockIdx.y;  // grid (blocks per frame, frames), plan order
-    int p = blockIdx.x;
+    const int p = blockIdx.x;
     if (p >= nb) return;
     const int t1 = thr & 255, t2 = (thr >> 8) & 255;  // clamped to [0, 255] on the host
     const int tq = min(t1, t2);
     const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
     const int tA = max(t1, 1), tB = max(t2, 1);
     const uint32_t a_ns = og_lds_addr(&sh_ns), a_lst = og_lds_addr(&lst[0]);
-    OgFB b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
+    const OgFB b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
     if (b.l < 0) return;
-    uint32_t sroi[2][4];
-    og_fastq_roi_load(b, tid, sroi);
-    og_fastq_roi_put(b, tid, sroi, roiq);
-#ifndef OG_FASTQ_MSZ_ROWS
-#define OG_FASTQ_MSZ_ROWS 1  // zero only the score-map rows the block reads (dh + 3: gap rows included)
-#endif
     {
-        const int msz = (OG_FASTQ_MSZ_ROWS && OG_FASTQ_KB == 1) ? min(FB_MSZ, ((b.dh + 3) * FB_MSW + 15) & ~15) : FB_MSZ;
+        uint32_t sroi[2][4];
+        og_fastq_roi_load(b, tid, sroi);
+        og_fastq_roi_put(b, tid, sroi, roiq);
+    }
+    {
+        // zero only the score-map rows the block reads (dh + 3: gap rows included)
+        const int msz = min(FB_MSZ, ((b.dh + 3) * FB_MSW + 15) & ~15);
         for (int idx = tid * 16; idx < msz; idx += FB_NT * 16) *(uint4*)&Ms[idx] = make_uint4(0u, 0u, 0u, 0u);
     }
     if (tid == 0) sh_ns = 0;
     __syncthreads();
-#if OG_EXP_FAST_STOP == 1  // timing experiments only (tools/fast_variants.py): results are wrong
-    if (roiq[tid].x == 255u && roiq[tid + 1].x == 254u) cand_count[0] = 1;
-    return;
-#endif
-#pragma unroll 1
-    for (int kb = 0;; kb++) {
     const int dw = b.dw, dh = b.dh, wC = b.wC, hC = b.hC;
     const uint2* Tq = roiq + b.mis;  // Tq[r * FQ_S + x] = quad (x, x + 16, x + 32, x + 48) of ROI row r
-    int wofs = 0;                    // (OG_FASTQ_WL) survivors in this wave's list
-    (void)wofs;
     // ---- stage 1: quick test on every detection pixel, four per lane.  Unit u = (row group g = u >> 1, half
     // h = u & 1) covers ROI rows 8g + 2h + {0, 4, 1, 5} (the lane's 16-lane group picks one); wave w takes units
     // w, w + 8, ...  Column masks are per-block constants, row masks scalars; one LDS reservation per unit.
@@ -1249,9 +796,6 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         };
         const u64 col0 = cmask(dw), col1 = cmask(dw - 16), col2 = cmask(dw - 32), col3 = cmask(dw - 48);
         const int nunits = ((dh + 7) >> 3) * 2;
-#if OG_FASTQ_WL
-        wofs = 0;
-#endif
         for (int u = wvu; u < nunits; u += FB_NW) {
             const int R = 8 * (u >> 1) + 2 * (u & 1);  // uniform
             const bool full = R + 5 < dh;
@@ -1260,14 +804,10 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             const uint2* q = Tl + R * FQ_S;
             uint32_t c0[16], c1[16];
             unsigned long long w[17];
-#ifndef OG_FASTQ_READ2
-#define OG_FASTQ_READ2 2  // circle loads: 2 volatile ds_read_b64 in pair order, partial waits (kept, -2.5 %); 0 asm
-                          // ds_read_b64 + one full wait; 1 compiler-paired ds_read2_b64 (profiles/sweeps/r03_ab_*)
-#endif
-#if OG_FASTQ_READ2 == 2
             {
-                // volatile 64-bit loads: never paired into ds_read2_b64, issued in order (opposite samples k, k + 8
-                // adjacent, centre first), each waited for only where it is used (partial lgkmcnt waits)
+                // volatile 64-bit loads: never paired into ds_read2_b64 (8 cycles per pair instead of 2 per read),
+                // issued in order (opposite samples k, k + 8 adjacent, centre first), each waited for only where it
+                // is used (partial lgkmcnt waits)
                 const int st = FQ_S;
                 const int off[17] = {3 * st,      1 + 3 * st,  2 + 2 * st,  3 + 1 * st, 3,          3 - 1 * st,
                                      2 - 2 * st,  1 - 3 * st,  -3 * st,     -1 - 3 * st, -2 - 2 * st, -3 - 1 * st,
@@ -1281,19 +821,6 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                     w[k + 8] = q64[off[k + 8]];
                 }
             }
-#elif OG_FASTQ_READ2
-            {
-                const int st = FQ_S;
-                const int off[17] = {3 * st,      1 + 3 * st,  2 + 2 * st,  3 + 1 * st, 3,          3 - 1 * st,
-                                     2 - 2 * st,  1 - 3 * st,  -3 * st,     -1 - 3 * st, -2 - 2 * st, -3 - 1 * st,
-                                     -3,          -3 + 1 * st, -2 + 2 * st, -1 + 3 * st, 0};
-                const unsigned long long* q64 = (const unsigned long long*)__builtin_assume_aligned(q, 8);
-#pragma unroll
-                for (int k = 0; k < 17; k++) w[k] = q64[off[k]];
-            }
-#else
-            og_fastq_circle(og_lds_addr(q) - 8u * (3u * FQ_S + 3u), w);
-#endif
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 c0[k] = (uint32_t)w[k];
@@ -1317,11 +844,6 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                 n += cnt[k];
             }
             if (n) {
-#if OG_FASTQ_WL
-                // the wave's own list: a wave-uniform running offset, no reservation round trip
-                const uint32_t ab = a_lst + 2u * (uint32_t)(wvu * FQ_WCAP + wofs);
-                wofs += n;
-#else
                 uint32_t old;
                 u64 sv;
                 __asm__ volatile(
@@ -1331,7 +853,6 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                     : "v"(a_ns), "v"(n)
                     : "memory");
                 const uint32_t ab = a_lst + 2u * (uint32_t)__builtin_amdgcn_readfirstlane(old);
-#endif
                 const uint32_t base = e_lane + (uint32_t)(R << 7);
                 uint32_t v[4];
                 {
@@ -1358,50 +879,9 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             }
         }
     }
-#if OG_FASTQ_WL
-    // ---- stage 2 on this wave's own survivors, right after its stage 1 (LDS operations of one wave complete in
-    // order, so its list stores are visible to its reads); only the score map needs the barrier below
-    const int nv = wofs;
-    uint16_t* const wl = lst + wvu * FQ_WCAP;
-    {
-        const uint16_t* T16 = (const uint16_t*)Tq;
-        for (int e = lane; e < nv; e += 64) {
-            const int ent = wl[e];
-            const int i = (ent >> 7) & 127, j = ent & 127;
-            const uint16_t* pc = &T16[4 * ((i + 3) * FQ_S + ((j & 15) + 3)) + (j >> 4)];
-            const bool dark = (ent & 0x4000) != 0, bright = (ent & 0x8000) != 0;
-            int M = og_fast_M1<4>(pc, 4 * FQ_S, dark ? 0 : 0xff);
-            if (dark && bright) {
-                __asm__ volatile("" ::: "memory");  // (as in og_fast_blocks_kernel)
-                M = max(M, og_fast_M1<4>(pc, 4 * FQ_S, 0xff));
-            }
-            Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)M;
-        }
-    }
-    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    constexpr bool has_next = false;
-    const int pn = p;
-    const OgFB bn = b;
-#else
-    // prefetch (OG_FASTQ_KB > 1): the next block's record and ROI loads are issued now and land during stage 2
-    const int pn = p + (int)gridDim.x;
-    bool has_next = kb + 1 < OG_FASTQ_KB && pn < nb;  // block-uniform
-    OgFB bn = b;
-    __builtin_amdgcn_sched_barrier(0);
-    if (has_next) {
-        bn = og_fast_decode(blocks, pn, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
-        has_next = bn.l >= 0;  // a padding entry ends the chain (the table pads each level to 8 entries)
-        if (has_next) og_fastq_roi_load(bn, tid, sroi);
-    }
-    __builtin_amdgcn_sched_barrier(0);
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm list stores are not tracked by the compiler
     __syncthreads();
     const int ns = sh_ns;
-#if OG_EXP_FAST_STOP == 2  // timing experiments only (tools/fast_variants.py): results are wrong
-    if (ns == 12345) cand_count[0] = 1;
-    return;
-#endif
     // ---- stage 2: exact M for every survivor; single pixels are u16 reads of the quad layout (element step 4)
     const uint16_t* T16 = (const uint16_t*)Tq;
     for (int e = tid; e < ns; e += FB_NT) {
@@ -1411,27 +891,19 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const bool dark = (ent & 0x4000) != 0, bright = (ent & 0x8000) != 0;
         int M = og_fast_M1<4>(pc, 4 * FQ_S, dark ? 0 : 0xff);
         if (dark && bright) {
-            __asm__ volatile("" ::: "memory");  // (as in og_fast_blocks_kernel)
+            __asm__ volatile("" ::: "memory");  // keeps the second polarity's reads behind the branch
             M = max(M, og_fast_M1<4>(pc, 4 * FQ_S, 0xff));
         }
         Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)M;
     }
     __syncthreads();
-    // roiq and sh_ns are free from here on: the next block's ROI goes in while this block finishes
-    if (tid == 0) sh_ns = 0;
-    if (has_next) og_fastq_roi_put(bn, tid, sroi, roiq);
-    uint16_t* const wl = lst;
-    const int nv = ns;
-#endif
-    // stages 3-4 walk the wave's own list (OG_FASTQ_WL) or every 8th chunk of the block list
-    const int e_first = OG_FASTQ_WL ? 0 : wv * 64, e_step = OG_FASTQ_WL ? 64 : FB_NT;
-    // ---- stage 3: same-cell 3x3 NMS at both thresholds (og_fast_blocks_kernel)
+    // ---- stage 3: same-cell 3x3 NMS at both thresholds; each wave walks every 8th 64-entry chunk of the list
     int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
-    for (int e0 = e_first; e0 < nv; e0 += e_step) {
+    for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
         const int e = e0 + lane;
         int ent = 0, mc = 0, nbm = 0;
-        if (e < nv) {
-            ent = wl[e] & 0x3fff;
+        if (e < ns) {
+            ent = lst[e] & 0x3fff;
             const uint8_t* q = &Ms[og_ms_idx(ent >> 7, ent & 127, wC, hC) - FB_MSW - 1];
             mc = q[FB_MSW + 1];
             nbm = max(max(max(q[0], q[1]), max(q[2], q[FB_MSW])),
@@ -1440,7 +912,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const u64 top = og_lanes_gt(mc, nbm);
         const u64 K1 = og_lanes_gt(mc, tA) & top, K2 = og_lanes_gt(mc, tB) & top;
         const u64 ci = og_lanes_gt(ent >> 7, hC - 1), cj = og_lanes_gt(ent & 127, wC - 1);
-        if (e < nv) wl[e] = (uint16_t)(ent | (mc > tA && mc > nbm ? 0x4000 : 0) | (mc > tB && mc > nbm ? 0x8000 : 0));
+        if (e < ns) lst[e] = (uint16_t)(ent | (mc > tA && mc > nbm ? 0x4000 : 0) | (mc > tB && mc > nbm ? 0x8000 : 0));
         const u64 cm[4] = {~ci & ~cj, ~ci & cj, ci & ~cj, ci & cj};
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) {
@@ -1456,7 +928,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
     }
     __syncthreads();
-    // per cell: iniThFAST unless the cell is empty at it (src/ORBextractor.cc:809-816), as og_fast_blocks_kernel
+    // per cell: iniThFAST unless the cell is empty at it (src/ORBextractor.cc:809-816)
     const int qw = (lane >> 2) & (FB_NW - 1), qc = lane & 3;
     const int v1 = wk[qw][qc], v2 = wk[qw][4 + qc];
     const u64 nz1 = og_lanes_ne((unsigned)v1, 0u) & 0xffffffffull;
@@ -1474,19 +946,11 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const int total = __builtin_amdgcn_readlane(sc, FB_NW - 1);
     const int kept = __builtin_amdgcn_readlane(kx, wvu);
     const int before = __builtin_amdgcn_readlane(sc, wvu) - kept;
-#if OG_EXP_FAST_STOP == 3
-    if (total == 12345) cand_count[0] = 1;
-    return;
-#endif
-    // ---- stage 4: one reservation per block; each wave writes its kept entries at its offset.  Every entry's
-    // score-map cell goes back to zero (the next block of this workgroup starts from a clean map).
+    // ---- stage 4: one reservation per block; each wave writes its kept entries at its offset
     int sb = 0;
-#ifndef OG_EXP_FAST_NOATOMIC
-#define OG_EXP_FAST_NOATOMIC 0  // timing experiments only (results wrong): 1 = no output reservation round trip
-#endif
     if (total != 0) {  // block-uniform
         if (tid == 0) {
-            const int bb = OG_EXP_FAST_NOATOMIC ? 0 : atomicAdd(&cand_count[f * nlevels + b.l], total);
+            const int bb = atomicAdd(&cand_count[f * nlevels + b.l], total);
             if (bb + total > b.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
             sh_base = bb;
         }
@@ -1496,25 +960,16 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const bool emit = total != 0 && sb + total <= b.cand_cap && kept != 0;
     u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb + before);
     int run = 0;
-    for (int e0 = e_first; e0 < nv; e0 += e_step) {
+    for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
         const int e = e0 + lane;
         int ent = 0;
-        if (e < nv) ent = wl[e];
+        if (e < ns) ent = lst[e];
         const int i = (ent >> 7) & 127, j = ent & 127;
         const int cell = (i >= hC) * 2 + (j >= wC);
         const unsigned kbit = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
         const u64 mask = og_lanes_ne(kbit, 0u);
-        if (e < nv) {
-            uint8_t* mcell = &Ms[og_ms_idx(i, j, wC, hC)];
-            if (emit && kbit) out[og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, *mcell - 1);
-            if (OG_FASTQ_KB > 1) *mcell = 0;
-        }
+        if (e < ns && emit && kbit) out[og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, Ms[og_ms_idx(i, j, wC, hC)] - 1);
         run += __popcll(mask);
-    }
-    if (!has_next) break;
-    b = bn;
-    p = pn;
-    __syncthreads();  // score map back to zero, list consumed, next ROI stored
     }
 }
 
@@ -2277,15 +1732,6 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                     if (!done) NO[k] = (uint16_t)n2;
                     if (done) {
                         const unsigned resp = (unsigned)(kv[u] >> 32);
-#ifndef OG_EXP_OCT_FINAL
-#define OG_EXP_OCT_FINAL 0  // timing experiments only (tools/octree_profile.py --variant): 1 no atomic, 2 no order
-#endif
-#if OG_EXP_OCT_FINAL == 1
-                        const u64 kk = ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order_m(x, y, L, mW, mH));
-                        if (kk == 0x123456789abcull) best[n2] = kk;
-#elif OG_EXP_OCT_FINAL == 2
-                        atomicMax(&best[n2], ((u64)resp << 32) | (u64)(unsigned)(x ^ y));
-#else
                         if (k32) {
                             key32 = (resp << 24) | (0xffffffu - og_cand_order_m(x, y, L, mW, mH));
                             a = n2;
@@ -2293,7 +1739,6 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                             atomicMax(&best[n2],
                                       ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order_m(x, y, L, mW, mH)));
                         }
-#endif
                     } else {
                         const int rc = splitRank[n2];
                         cnt = (rc >> 30) & 1;
@@ -2301,7 +1746,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                     }
                 }
                 if (!done) og_wave_count(NCC, a, cnt);  // `done`, k32 are workgroup-uniform
-                else if (k32 && !OG_EXP_OCT_FINAL) og_wave_max32(best32, a, key32, k < C);
+                else if (k32) og_wave_max32(best32, a, key32, k < C);
             }
         }
         __syncthreads();
@@ -3459,17 +2904,8 @@ void og_launch_fast(hipStream_t s, const OgPlan& P, const OgFastBlk* blocks, int
 {
     if (nblocks <= 0 || B <= 0) return;
     const int thr = std::min(std::max(P.iniTh, 0), 255) | (std::min(std::max(P.minTh, 0), 255) << 8);
-#ifndef OG_FAST_QUAD
-#define OG_FAST_QUAD 1  // 1: og_fast_quad_kernel (quad layout); 0: og_fast_blocks_kernel (pair layout)
-#endif
-    if (OG_FAST_QUAD)
-        hipLaunchKernelGGL(og_fast_quad_kernel, dim3((nblocks + OG_FASTQ_KB - 1) / OG_FASTQ_KB, B), dim3(FB_NT), 0, s,
-                           blocks, nblocks, img0, pitch0,
-                           fstride0, pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels, thr, status);
-    else
-        hipLaunchKernelGGL(og_fast_blocks_kernel, dim3((nblocks + OG_FAST_KB - 1) / OG_FAST_KB, B), dim3(FB_NT), 0, s,
-                           blocks, nblocks, img0, pitch0, fstride0, pyr, P.pyr_per_frame, cand, P.cand_per_frame,
-                           cand_count, P.nlevels, thr, status);
+    hipLaunchKernelGGL(og_fast_quad_kernel, dim3(nblocks, B), dim3(FB_NT), 0, s, blocks, nblocks, img0, pitch0, fstride0,
+                       pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels, thr, status);
 }
 
 void og_launch_harris(hipStream_t s, const OgPlan& P, int lb, int le, const uint8_t* img0, long long pitch0,

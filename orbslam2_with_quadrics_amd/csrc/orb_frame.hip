@@ -192,3 +192,43 @@ void og_launch_pack_host(hipStream_t s, const int* status, const int* counts, co
     hipLaunchKernelGGL(og_pack_host_kernel, dim3(16), dim3(256), 0, s, status, counts, (const uint32_t*)kps,
                        (const uint32_t*)desc, frame_cap, (uint32_t*)host_dev);
 }
+
+// ------------------------------------------------------------------------------------------------
+// Frame-record unpack (orbgpu_frame_record_unpack, the F1 broadcast of bench.py / SURVEY §8(e)), validated on the
+// device so the call stays stream-ordered: every block checks the 16-byte header {count, magic, frame_cap,
+// undistortion} against the receiving plan.  A matching record's `count` keypoints, descriptors (and undistorted
+// keypoints) are copied into frame 0; a mismatch writes count 0 and raises status bit 128, which the next status
+// check reports as ORBGPU_ERR_ARG.
+// ------------------------------------------------------------------------------------------------
+#define OG_RECORD_MAGIC 0x5246474fu
+__global__ __launch_bounds__(256) void og_record_unpack_kernel(const uint32_t* __restrict__ rec, int frame_cap, int undist,
+                                                              int* __restrict__ counts, uint32_t* __restrict__ kps,
+                                                              uint32_t* __restrict__ desc, uint32_t* __restrict__ kps_un,
+                                                              int* __restrict__ status)
+{
+    const int n = (int)rec[0];
+    const bool ok = rec[1] == OG_RECORD_MAGIC && rec[2] == (uint32_t)frame_cap && rec[3] == (undist ? 1u : 0u) &&
+                    n >= 0 && n <= frame_cap;
+    const int i0 = blockIdx.x * 256 + threadIdx.x;
+    if (i0 == 0) {
+        counts[0] = ok ? n : 0;
+        if (!ok) atomicOr(status, 128);
+    }
+    if (!ok) return;
+    const uint32_t* rk = rec + 4;
+    const uint32_t* rd = rk + 7 * frame_cap;
+    const uint32_t* ru = rd + 8 * frame_cap;
+    const int nk = 7 * n, nd = 8 * n, nu = undist ? 7 * n : 0;
+    for (int i = i0; i < nk + nd + nu; i += gridDim.x * 256) {
+        if (i < nk) kps[i] = rk[i];
+        else if (i < nk + nd) desc[i - nk] = rd[i - nk];
+        else kps_un[i - nk - nd] = ru[i - nk - nd];
+    }
+}
+
+void og_launch_record_unpack(hipStream_t s, const void* rec, int frame_cap, int undist, int* counts,
+                             orbgpu_kp_dev* kps, uint8_t* desc, orbgpu_kp_dev* kps_un, int* status)
+{
+    hipLaunchKernelGGL(og_record_unpack_kernel, dim3(16), dim3(256), 0, s, (const uint32_t*)rec, frame_cap, undist,
+                       counts, (uint32_t*)kps, (uint32_t*)desc, (uint32_t*)kps_un, status);
+}

@@ -2,9 +2,9 @@
 //
 //   og_stereo_rows_kernel   : vRowIndices (:476-493) as a CSR over image rows, right keypoints of each
 //                             row in index order (one workgroup per frame pair)
-//   og_stereo_match_kernel  : one wave per left keypoint: row-band Hamming search (levels +-1, u-range,
+//   og_stereo_match16_kernel: 16 lanes per left keypoint: row-band Hamming search (levels +-1, u-range,
 //                             strict-< first minimum, :504-549), 11x121 SAD sliding window on both
-//                             pyramids with wave reductions (exact integers), parabola sub-pixel fit,
+//                             pyramids with DPP row reductions (exact integers), parabola sub-pixel fit,
 //                             disparity / depth (:552-622)
 //   og_stereo_filter_kernel : median of the SAD distances by two-pass radix select, 2.1 x median
 //                             rejection (:626-639)
@@ -102,154 +102,9 @@ __global__ __launch_bounds__(ST_NT) void og_stereo_rows_kernel(OgStereoDev S)
 #endif
 }
 
-__device__ __forceinline__ int og_wave_isum(int v)
-{
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-__global__ __launch_bounds__(256) void og_stereo_match_kernel(OgStereoDev S)
-{
-    const int b = blockIdx.y, lane = threadIdx.x & 63;
-    const int iL = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int N = S.L.counts[b];
-    if (iL >= N) return;
-    float* UR = S.uright + (long long)b * S.L.frame_cap;
-    float* DE = S.depth + (long long)b * S.L.frame_cap;
-    int* SAD = S.sad + (long long)b * S.L.frame_cap;
-    if (lane == 0) {
-        UR[iL] = -1.0f;
-        DE[iL] = -1.0f;
-        SAD[iL] = -1;
-    }
-    const orbgpu_kp_dev kpL = S.L.kps[(long long)b * S.L.frame_cap + iL];
-    const orbgpu_kp_dev* KR = S.R.kps + (long long)b * S.R.frame_cap;
-    const int levelL = kpL.octave;
-    const float vL = kpL.y, uL = kpL.x;
-    const int row = (int)vL;
-    if (row < 0 || row >= S.nRows) return;
-    const int* RS = S.row_start + (long long)b * (S.nRows + 1);
-    const int* RI = S.row_items + (long long)b * S.row_cap;
-    const int cb = RS[row], ce = min(RS[row + 1], S.row_cap);
-    if (cb == ce) return;
-    const float minZ = S.mb, minD = 0;
-    const float maxD = S.mbf / minZ;
-    const float minU = uL - maxD, maxU = uL - minD;
-    if (maxU < 0) return;
-    // ---- row-band Hamming search: first strict minimum below TH_HIGH in candidate order
-    uint4 da, db;
-    {
-        const uint4* q = (const uint4*)(S.L.desc + ((long long)b * S.L.frame_cap + iL) * 32);
-        da = q[0];
-        db = q[1];
-    }
-    u64 best = ~0ull;
-    for (int c = cb + lane; c - lane < ce; c += 64) {
-        u64 key = ~0ull;
-        if (c < ce) {
-            const int iR = RI[c];
-            const orbgpu_kp_dev kpR = KR[iR];
-            if (!(kpR.octave < levelL - 1 || kpR.octave > levelL + 1)) {
-                const float uR = kpR.x;
-                if (uR >= minU && uR <= maxU) {
-                    const uint4* q = (const uint4*)(S.R.desc + ((long long)b * S.R.frame_cap + iR) * 32);
-                    const int dist = og_hamming(da, db, q[0], q[1]);
-                    if (dist < ST_TH_HIGH) key = ((u64)dist << 32) | ((u64)(c - cb) << 16) | (u64)iR;
-                }
-            }
-        }
-        best = key < best ? key : best;
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const u64 w = __shfl_xor(best, o);
-        best = w < best ? w : best;
-    }
-    const int thOrbDist = (ST_TH_HIGH + ST_TH_LOW) / 2;
-    if (best == ~0ull || (int)(best >> 32) >= thOrbDist) return;
-    const int bestIdxR = (int)(best & 0xffff);
-    // ---- SAD sliding window on the keypoint's pyramid level (:552-592)
-    const float uR0 = KR[bestIdxR].x;
-    const float scaleFactor = S.isf[levelL];
-    const float scaleduL = roundf(kpL.x * scaleFactor);
-    const float scaledvL = roundf(kpL.y * scaleFactor);
-    const float scaleduR0 = roundf(uR0 * scaleFactor);
-    const int w = 5, Lw = 5;
-    const float iniu = scaleduR0 + Lw - w;
-    const float endu = scaleduR0 + Lw + w + 1;
-    const int rcols = S.lvl_w[levelL];
-    if (iniu < 0 || endu >= rcols) return;
-    const uint8_t* IL;
-    const uint8_t* IR;
-    long long pl, pr;
-    if (levelL == 0) {
-        IL = S.L0 + (long long)b * S.L0_fstride;
-        pl = S.L0_pitch;
-        IR = S.R0 + (long long)b * S.R0_fstride;
-        pr = S.R0_pitch;
-    } else {
-        IL = S.Lpyr + (long long)b * S.pyr_fstride + S.lvl_off[levelL];
-        IR = S.Rpyr + (long long)b * S.pyr_fstride + S.lvl_off[levelL];
-        pl = pr = S.lvl_pitch[levelL];
-    }
-    const int ivL = (int)scaledvL, iuL = (int)scaleduL, iuR0 = (int)scaleduR0;
-    const int cL = IL[(long long)ivL * pl + iuL];
-    // lane p (< 61) owns window pixels 2p and 2p+1 of the 11x11 patch (121 pixels)
-    int lv[2] = {0, 0}, px[2] = {0, 0}, py[2] = {0, 0};
-    bool has[2] = {false, false};
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const int pidx = 2 * lane + k;
-        if (pidx < 121) {
-            has[k] = true;
-            py[k] = pidx / 11 - w;
-            px[k] = pidx % 11 - w;
-            lv[k] = (int)IL[(long long)(ivL + py[k]) * pl + iuL + px[k]] - cL;
-        }
-    }
-    int bestD = INT_MAX, bestincR = 0;
-    float vDists[11];
-#pragma unroll
-    for (int incR = -Lw; incR <= Lw; incR++) {
-        const int cR = IR[(long long)ivL * pr + iuR0 + incR];
-        int part = 0;
-#pragma unroll
-        for (int k = 0; k < 2; k++)
-            if (has[k]) {
-                const int rv = (int)IR[(long long)(ivL + py[k]) * pr + iuR0 + incR + px[k]] - cR;
-                part += abs(lv[k] - rv);
-            }
-        const float dist = (float)og_wave_isum(part);  // cv::norm(IL, IR, NORM_L1): exact integer
-        if (dist < bestD) {
-            bestD = (int)dist;
-            bestincR = incR;
-        }
-        vDists[Lw + incR] = dist;
-    }
-    if (bestincR == -Lw || bestincR == Lw) return;
-    const float dist1 = vDists[Lw + bestincR - 1];
-    const float dist2 = vDists[Lw + bestincR];
-    const float dist3 = vDists[Lw + bestincR + 1];
-    const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
-    if (deltaR < -1 || deltaR > 1) return;
-    float bestuR = S.sf[levelL] * ((float)scaleduR0 + (float)bestincR + deltaR);
-    float disparity = (uL - bestuR);
-    if (disparity >= minD && disparity < maxD) {
-        if (disparity <= 0) {
-            disparity = 0.01f;
-            bestuR = (float)((double)uL - 0.01);
-        }
-        if (lane == 0) {
-            DE[iL] = S.mbf / disparity;
-            UR[iL] = bestuR;
-            SAD[iL] = bestD;
-        }
-    }
-}
-
-// ---- og_stereo_match16_kernel: the same per-keypoint computation with 16 lanes per left keypoint (4 keypoints per
-// wave, 16 per 256-thread workgroup).  Every cross-lane step stays inside a 16-lane DPP row (row_ror / quad_perm
+// ---- og_stereo_match16_kernel: one left keypoint per 16 lanes (4 keypoints per wave, 16 per 256-thread workgroup):
+// row-band Hamming search (levels +-1, u-range, strict-< first minimum, src/Frame.cc:504-549), 11x121 SAD sliding
+// window on both pyramids (exact integers), parabola sub-pixel fit, disparity / depth (:552-622).  Every cross-lane step stays inside a 16-lane DPP row (row_ror / quad_perm
 // min and add reductions: VALU, no LDS round trips), and the SAD is computed from registers: lane r < 11 loads row
 // r - 5 of the 11-pixel left window and of the 21-pixel right band (all 11 window positions), then forms its 11 row
 // sums with v_sad_u32.
@@ -305,7 +160,10 @@ __global__ __launch_bounds__(256) void og_stereo_match16_kernel(OgStereoDev S)
         da = q[0];
         db = q[1];
     }
-    unsigned best = 0xffffffffu;  // (dist << 16) | (candidate position): smallest distance, then first in order
+    // (dist << 16) | (candidate position): smallest distance, then first in order.  The position is the index in one
+    // row list, which holds at most ST_MAXR right keypoints, so it fits the low 16 bits.
+    static_assert(ST_MAXR <= 65535, "row-list positions are packed into 16 bits");
+    unsigned best = 0xffffffffu;
     for (int c = cb + l; c < ce; c += 16) {
         const int iR = RI[c];
         const orbgpu_kp_dev kpR = KR[iR];
@@ -488,12 +346,6 @@ __global__ __launch_bounds__(256) void og_stereo_filter_kernel(OgStereoDev S)
 void og_launch_stereo(hipStream_t s, const OgStereoDev& S, int B)
 {
     hipLaunchKernelGGL(og_stereo_rows_kernel, dim3(B), dim3(ST_NT), 0, s, S);
-#ifndef OG_STEREO16
-#define OG_STEREO16 1  // 1: og_stereo_match16_kernel (16 lanes per keypoint); 0: og_stereo_match_kernel (a wave each)
-#endif
-    if (OG_STEREO16)
-        hipLaunchKernelGGL(og_stereo_match16_kernel, dim3((S.L.frame_cap + 15) / 16, B), dim3(256), 0, s, S);
-    else
-        hipLaunchKernelGGL(og_stereo_match_kernel, dim3((S.L.frame_cap + 3) / 4, B), dim3(256), 0, s, S);
+    hipLaunchKernelGGL(og_stereo_match16_kernel, dim3((S.L.frame_cap + 15) / 16, B), dim3(256), 0, s, S);
     hipLaunchKernelGGL(og_stereo_filter_kernel, dim3(B), dim3(256), 0, s, S);
 }

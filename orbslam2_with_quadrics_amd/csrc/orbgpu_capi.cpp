@@ -249,7 +249,7 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
                 cap += (long long)((dw + 1) / 2) * ((dh + 1) / 2);  // NMS keeps an independent set
             }
         }
-        // FAST blocks of up to 2x2 valid cells (og_fast_blocks_kernel); the valid cells form a rectangle
+        // FAST blocks of up to 2x2 valid cells (og_fast_quad_kernel); the valid cells form a rectangle
         // (the skip tests depend on the row or the column only)
         {
             std::vector<OgCell> lc(cells.begin() + L.cell_base, cells.end());
@@ -263,7 +263,7 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
                 c->err = "FAST cells do not form a rectangle";
                 return ORBGPU_ERR_INTERNAL;
             }
-            // the kernel's pair layout holds detection widths <= 2 * 32 and heights <= 80 (FB_H, FB_MW)
+            // the kernel's quad layout holds detection widths <= 4 * 16 and heights <= 80 (FQ_S, FB_MW)
             const int bsj = (2 * L.wCell <= 64) ? 2 : 1, bsi = (L.hCell <= 40) ? 2 : 1;
             for (int bi = 0; bi < nr; bi += bsi)
                 for (int bj = 0; bj < ncl; bj += bsj) {
@@ -693,6 +693,10 @@ static int check_status(orbgpu_ctx* c)
     if (st[0]) {  // read and clear: the flags of every launch since the last check
         HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(st), c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
+        if (st[0] == 128) {  // og_record_unpack_kernel: a refused frame record (a caller error, not a device guard)
+            c->err = "frame record does not match this context's plan (frame_cap / undistortion) or has a bad count";
+            return ORBGPU_ERR_ARG;
+        }
         c->err = "device capacity guard tripped (status " + std::to_string(st[0]) + ")";
         return ORBGPU_ERR_INTERNAL;
     }
@@ -728,8 +732,6 @@ orbgpu_ctx* orbgpu_create(int device, int nfeatures, float scaleFactor, int nlev
     c->iniTh = iniThFAST;
     c->minTh = minThFAST;
     c->scaleFactor = (double)scaleFactor;
-    if (const char* e = std::getenv("ORBGPU_SCORE_HARRIS"))  // option, off by default (include/orbgpu.h)
-        if (e[0] == '1') c->sem |= ORBGPU_SEM_SCORE_HARRIS;
     // src/ORBextractor.cc:415-446
     c->sf.assign(nlevels, 0.f);
     c->sig2.assign(nlevels, 0.f);
@@ -961,24 +963,14 @@ int orbgpu_frame_record_unpack(orbgpu_ctx* c, const void* d_src)
     if (!c || !c->planned || !d_src) return ORBGPU_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     if (int r = ensure_batch(c, 1)) return r;
-    const size_t cap = (size_t)c->plan.frame_cap;
-    const uint8_t* d = (const uint8_t*)d_src;
-    hipStream_t s = c->stream;
     // the header must describe this context's plan (frame_cap, undistortion) and a count within it; a record from
     // a differently planned context would otherwise be misread, and a larger count would send the matchers past
-    // the frame
-    uint32_t hdr[4];
-    HIP_TRY(c, hipMemcpyAsync(hdr, d, 16, hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipStreamSynchronize(s));
-    if (hdr[1] != 0x5246474fu || hdr[2] != (uint32_t)c->plan.frame_cap || hdr[3] != (c->undist ? 1u : 0u) ||
-        (int)hdr[0] < 0 || (int)hdr[0] > c->plan.frame_cap) {
-        c->err = "frame record does not match this context's plan (frame_cap / undistortion) or has a bad count";
-        return ORBGPU_ERR_ARG;
-    }
-    HIP_TRY(c, hipMemcpyAsync(c->counts.p, d, 4, hipMemcpyDeviceToDevice, s));
-    HIP_TRY(c, hipMemcpyAsync(c->kps.p, d + 16, cap * 28, hipMemcpyDeviceToDevice, s));
-    HIP_TRY(c, hipMemcpyAsync(c->desc.p, d + 16 + cap * 28, cap * 32, hipMemcpyDeviceToDevice, s));
-    if (c->undist) HIP_TRY(c, hipMemcpyAsync(c->kps_un.p, d + 16 + cap * 60, cap * 28, hipMemcpyDeviceToDevice, s));
+    // the frame.  Checked on the device, so the call stays stream-ordered (no host synchronisation): a mismatch
+    // leaves count 0 and is reported as ORBGPU_ERR_ARG by the next status check.
+    hipStream_t s = c->stream;
+    og_launch_record_unpack(s, d_src, c->plan.frame_cap, c->undist ? 1 : 0, c->counts.p, c->kps.p, c->desc.p,
+                            c->undist ? c->kps_un.p : nullptr, c->status.p);
+    HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(c->done, s));  // matchers on other contexts wait for this record
     c->last_B = std::max(c->last_B, 1);
     return ORBGPU_OK;
@@ -1026,6 +1018,10 @@ static int download_single(orbgpu_ctx* c, orbgpu_keypoint* kps, uint8_t* desc, i
         HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(int) * 4, c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         c->err = "device capacity guard tripped (status " + std::to_string(hdr[0]) + ")";
+        return ORBGPU_ERR_INTERNAL;
+    }
+    if (hdr[1] < 0 || hdr[1] > (int)fc) {  // og_pack_host_kernel copies at most frame_cap entries
+        c->err = "keypoint count " + std::to_string(hdr[1]) + " outside [0, frame_cap]";
         return ORBGPU_ERR_INTERNAL;
     }
     *n = hdr[1];

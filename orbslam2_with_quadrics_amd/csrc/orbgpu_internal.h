@@ -61,7 +61,7 @@ struct OgCell {            // one FAST block of up to 2x2 cells (ROI union), src
     short x0, y0, x1, y1;  // ROI [x0,x1) x [y0,y1) in level pixels
 };
 
-// One FAST block as the kernel reads it (og_fast_blocks_kernel): everything it needs from the block, its level and
+// One FAST block as the kernel reads it (og_fast_quad_kernel): everything it needs from the block, its level and
 // the plan, precomputed on the host and read with one 32-byte scalar load (no per-wave level-table lookups).
 struct OgFastBlk {
     int src_off;           // levels >= 1: byte offset of ROI pixel (0, 0) inside the frame's pyramid block;

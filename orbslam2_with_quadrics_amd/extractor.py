@@ -31,7 +31,7 @@ class ORBextractor:
         if not self._ctx:
             raise RuntimeError("orbgpu_create failed (no HIP device visible, or invalid parameters)")
         self.nfeatures, self.nlevels = nfeatures, nlevels
-        # None: the context's own choice (SEM_DEFAULT, plus SEM_SCORE_HARRIS when ORBGPU_SCORE_HARRIS=1)
+        # None: the context's own choice (SEM_DEFAULT)
         self.set_semantics(self._L.orbgpu_get_semantics(self._ctx) if semantics is None else semantics)
 
     def set_semantics(self, flags: int):

@@ -249,6 +249,23 @@ def test_shard_range_partitions():
             assert all(got[i][0] + got[i][1] == got[i + 1][0] for i in range(w - 1))
 
 
+def test_rccl_refuses_more_ranks_than_gpus():
+    """Under RCCL (the default backend) every rank needs its own GPU: more ranks on a node than GPUs is refused before
+    any device call, with a message; gloo keeps the round-robin rehearsal."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert [bench.pick_device(r, 8, 8, "nccl") for r in range(8)] == list(range(8))
+    assert bench.pick_device(0, 1, 1, "nccl") == 0
+    for local, lw, n in ((1, 2, 1), (0, 2, 1), (4, 8, 4), (8, 8, 8)):
+        with pytest.raises(SystemExit, match="one GPU per rank"):
+            bench.pick_device(local, lw, n, "nccl")
+    assert [bench.pick_device(r, 4, 1, "gloo") for r in range(4)] == [0, 0, 0, 0]
+    assert [bench.pick_device(r, 4, 2, "gloo") for r in range(4)] == [0, 1, 0, 1]
+    with pytest.raises(SystemExit, match="no GPU"):
+        bench.pick_device(0, 1, 0, "gloo")
+
+
 def test_single_rank_is_collective_free():
     sys.path.insert(0, ROOT)
     import bench

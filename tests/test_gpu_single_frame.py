@@ -1,8 +1,10 @@
 """The single-frame path (Frame::ExtractORB's one-frame-at-a-time call, src/Frame.cc:247-253):
 
-* batches of up to 4 frames fork level 0's FAST + octree onto the context stream and the pyramid + levels >= 1
-  onto a second stream (orbgpu_capi.cpp run_batch); with stage timing on the same batch runs serially.  Both
-  orders must give identical keypoints, descriptors and grids;
+* batches of up to 4 frames of at least ORBGPU_FORK_MIN_PIXELS (default 2^20, so the 1080p cases here; the
+  640x480 case runs serially in both orders) fork level 0's FAST + octree (and, with the Harris option, level 0's
+  Harris pass) onto the context stream and the pyramid + levels >= 1 onto a second stream (orbgpu_capi.cpp
+  run_batch); with stage timing on the same batch runs serially.  Both orders must give identical keypoints,
+  descriptors and grids;
 * orbgpu_extract downloads through one packing kernel into a pinned block (og_pack_host_kernel) and copies a
   contiguous image with its own pitch: it must equal the batch download, for contiguous and strided images, and
   report ORBGPU_ERR_CAPACITY with the needed count when the caller's capacity is short.
@@ -29,17 +31,18 @@ def _grid(ex, B):
     return CS, CI
 
 
-@pytest.mark.parametrize("shape,nf", [((480, 640), 1000), ((1080, 1920), 2000), ((1080, 1920), 4000)])
-def test_forked_small_batches_equal_serial(gpu, oracle, shape, nf):
+@pytest.mark.parametrize("shape,nf,sem", [((480, 640), 1000, 0), ((1080, 1920), 2000, 0), ((1080, 1920), 4000, 0),
+                                          ((1080, 1920), 2000, _lib.SEM_SCORE_HARRIS)])
+def test_forked_small_batches_equal_serial(gpu, oracle, shape, nf, sem):
     rows, cols = shape
-    ex = gpu.ORBextractor(nf, 1.2, 8, 20, 7)
+    ex = gpu.ORBextractor(nf, 1.2, 8, 20, 7, semantics=sem)
     frames = np.stack([synthetic.frame(40 + b, rows, cols) for b in range(5)]).astype(np.uint8)
     d = ex.device_alloc(frames.nbytes)
     try:
         ex.h2d(d, frames)
         for B in (1, 2, 4, 5):
             outs = []
-            for timing in (True, False):  # serial (stage marks) / forked (B <= 4)
+            for timing in (True, False):  # serial (stage marks) / forked (B <= 4, frames >= 2^20 px)
                 ex.set_stage_timing(timing)
                 ex.extract_batch_device(d, B, cols, rows, cols, rows * cols)
                 ex.synchronize()
@@ -51,7 +54,7 @@ def test_forked_small_batches_equal_serial(gpu, oracle, shape, nf):
             assert np.array_equal(ga[0], gb[0]) and np.array_equal(ga[1], gb[1]), B
         # and the forked single frame against the oracle
         k, dsc = ex(frames[0])
-        ko, do = oracle.OracleExtractor(nf)(frames[0])
+        ko, do = oracle.OracleExtractor(nf, semantics=sem)(frames[0])
         assert k.tobytes() == ko.tobytes() and np.array_equal(dsc, do)
     finally:
         ex.device_free(d)

@@ -552,10 +552,10 @@ print(O.LIB_PATH, hashlib.sha256(k1.tobytes() + d1.tobytes() + k2.tobytes() + d2
 
 
 def test_fast_slot_division_exact():
-    """og_fast_blocks_kernel maps a pair slot p to (row, column) with trunc(fma(p, 1/H, 0.5/H)) in float32
-    (csrc/orb_extract.hip, stage 1).  (p + 1/2)/H is at least 1/(2H) from an integer, far beyond the rounding of
+    """The quotient trick trunc(fma(p, 1/H, 0.5/H)) in float32 (og_resize2_kernel's staging maps a chunk index to
+    (row, chunk) this way, csrc/orb_extract.hip).  (p + 1/2)/H is at least 1/(2H) from an integer, far beyond the rounding of
     the correctly rounded 1/H and of the fma, so the quotient is exact: checked for every p < 2^14 and H <= 128
-    (the kernel needs p < 80 * 44 and H <= 44).  The fma is evaluated exactly in float64 (a 24 x 24-bit product
+    (the kernels need p < 2^14).  The fma is evaluated exactly in float64 (a 24 x 24-bit product
     is exact there) and rounded once to float32, as the hardware fma rounds."""
     p = np.arange(0, 1 << 14, dtype=np.int64)
     for H in range(1, 129):

@@ -10,17 +10,14 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-# --variant NAME: timing experiments of the final key pass (results wrong): noatom (no atomicMax), noorder
-VARIANTS = {"": [], "noatom": ["OG_EXP_OCT_FINAL=1"], "noorder": ["OG_EXP_OCT_FINAL=2"]}
-VAR = sys.argv[sys.argv.index("--variant") + 1] if "--variant" in sys.argv else ""
-VLIB = os.path.join(ROOT, "orbslam2_with_quadrics_amd", "variants", f"liborbgpu_octprof{VAR}.so")
+VLIB = os.path.join(ROOT, "orbslam2_with_quadrics_amd", "variants", "liborbgpu_octprof.so")
 
 
 def build():
     from orbslam2_with_quadrics_amd import build_ext
 
     os.makedirs(os.path.dirname(VLIB), exist_ok=True)
-    print(build_ext.build(force=True, defines=["OG_OCT_PROFILE=1", *VARIANTS[VAR]], out=VLIB))
+    print(build_ext.build(force=True, defines=["OG_OCT_PROFILE=1"], out=VLIB))
 
 
 def run():

@@ -24,16 +24,16 @@ def short(n):
 
 
 # kernel -> bench stage (orbgpu_set_stage_timing's names, bench.py "stages_ms_per_launch")
-STAGE = {"og_fast_blocks_kernel": "fast", "og_fast_quad_kernel": "fast", "og_octree_kernel": "octree",
+STAGE = {"og_fast_quad_kernel": "fast", "og_octree_kernel": "octree",
          "og_octree_big_kernel": "octree", "og_describe_kernel": "describe", "og_grid_kernel": "grid",
          "og_resize_kernel": "pyramid", "og_resize2_kernel": "pyramid",
          "og_init_cand_kernel": "search_init", "og_init_resolve_kernel": "search_init",
-         "og_stereo_rows_kernel": "stereo", "og_stereo_match_kernel": "stereo", "og_stereo_match16_kernel": "stereo",
+         "og_stereo_rows_kernel": "stereo", "og_stereo_match16_kernel": "stereo",
          "og_stereo_filter_kernel": "stereo",
          "og_projb_count_kernel": "search_proj", "og_projb_scan_kernel": "search_proj",
          "og_projb_fill_kernel": "search_proj", "og_projb_resolve_kernel": "search_proj",
          "og_frustum_batch_kernel": "frustum"}
-FAST = ("og_fast_blocks_kernel", "og_fast_quad_kernel")
+FAST = ("og_fast_quad_kernel",)
 
 
 def main():
