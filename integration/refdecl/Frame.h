@@ -33,6 +33,7 @@ public:
     cv::Mat mTcw;  // ref: include/Frame.h:172
     int mnScaleLevels;  // ref: include/Frame.h:182
     float mfScaleFactor;  // ref: include/Frame.h:183
+    float mfLogScaleFactor;  // ref: include/Frame.h:184
     vector<float> mvScaleFactors;  // ref: include/Frame.h:185
     static float mnMinX;  // ref: include/Frame.h:191
     static float mnMaxX;  // ref: include/Frame.h:192

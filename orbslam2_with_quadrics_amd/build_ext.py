@@ -99,29 +99,44 @@ def build_host(verbose: bool = False) -> str:
 
 
 BINDING_RUNNER = os.path.join(ROOT, "tests", "binding_run", "run_binding")
+MATCHER_RUNNER = os.path.join(ROOT, "tests", "binding_run", "run_matchers")
 REFERENCE_INCLUDE = "/root/reference/include"
 
 
 def build_binding_runner(verbose: bool = False):
-    """Build tests/binding_run/run_binding: the drop-in integration/ORBextractor.cc compiled against the reference's
-    UNCHANGED include/ORBextractor.h with the test cv shim (integration/cvshim + tests/binding_run/cvmini.cc),
-    linked with liborbgpu.so.  Needs the reference headers, so it is built here (CPU container) and travels to the
-    GPU box with the tree; returns None where they are absent.  Test infrastructure (tests/test_gpu_binding_run.py)."""
+    """Build the drop-in binding runners (test infrastructure), linked with liborbgpu.so:
+    * tests/binding_run/run_binding: integration/ORBextractor.cc compiled against the reference's UNCHANGED
+      include/ORBextractor.h with the test cv shim (integration/cvshim + tests/binding_run/cvmini.cc)
+      (tests/test_gpu_binding_run.py);
+    * tests/binding_run/run_matchers: the same extractor binding plus integration/ORBmatcher_perframe.cc and
+      integration/Frame_stereo.cc, compiled against integration/refdecl (the reference declarations they use,
+      checked line by line against the reference headers) with the test-only member definitions of
+      tests/binding_run/refstubs.cc (tests/test_gpu_binding_matchers.py).
+    Both need the reference headers, so they are built here (CPU container) and travel to the GPU box with the tree;
+    returns None where the headers are absent."""
     if not os.path.exists(os.path.join(REFERENCE_INCLUDE, "ORBextractor.h")):
         return None
     cxx = shutil.which("g++") or "g++"
+    flags = ["-O2", "-std=c++11", "-ffp-contract=off", "-Wall", "-Wextra", "-Wno-unused-parameter"]
     inc = ["-I", os.path.join(ROOT, "integration", "cvshim"), "-I", REFERENCE_INCLUDE, "-I", os.path.join(ROOT, "include"),
            "-I", os.path.join(ROOT, "integration")]
-    srcs = [os.path.join(ROOT, "integration", "ORBextractor.cc"),
-            os.path.join(ROOT, "tests", "binding_run", "cvmini.cc"),
-            os.path.join(ROOT, "tests", "binding_run", "run_binding.cc")]
-    cmd = [cxx, "-O2", "-std=c++11", "-Wall", "-Wextra", "-Wno-unused-parameter", *inc, *srcs, "-L", HERE,
-           "-l:liborbgpu.so", "-Wl,-rpath,$ORIGIN/../../orbslam2_with_quadrics_amd", "-pthread",
-           "-o", BINDING_RUNNER + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
-    os.replace(BINDING_RUNNER + ".tmp", BINDING_RUNNER)
+    link = ["-L", HERE, "-l:liborbgpu.so", "-Wl,-rpath,$ORIGIN/../../orbslam2_with_quadrics_amd", "-pthread"]
+    br = os.path.join(ROOT, "tests", "binding_run")
+    jobs = [
+        (BINDING_RUNNER, inc, [os.path.join(ROOT, "integration", "ORBextractor.cc"), os.path.join(br, "cvmini.cc"),
+                               os.path.join(br, "run_binding.cc")]),
+        # refdecl first: its Frame.h / MapPoint.h / KeyFrame.h / ORBmatcher.h stand for the reference's (which need
+        # Eigen / g2o); ORBextractor.h still comes from the reference
+        (MATCHER_RUNNER, ["-I", os.path.join(ROOT, "integration", "refdecl"), "-I", br] + inc,
+         [os.path.join(ROOT, "integration", f) for f in ("ORBextractor.cc", "ORBmatcher_perframe.cc", "Frame_stereo.cc")]
+         + [os.path.join(br, f) for f in ("cvmini.cc", "refstubs.cc", "run_matchers.cc")]),
+    ]
+    for out, incs, srcs in jobs:
+        cmd = [cxx, *flags, *incs, *srcs, *link, "-o", out + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        os.replace(out + ".tmp", out)
     return BINDING_RUNNER
 
 

@@ -541,6 +541,76 @@ __device__ __forceinline__ int og_fast_M1(const E* p, int st, int fm)
 }
 
 
+// The same score on the f16-biased quad ROI (0x6400 | pixel = the f16 value 1024 + pixel) with packed f16 ops: the
+// opposite samples (c_k, c_k+8) share a dword, so one v_pk_maximum3_f16 forms two 3-arc maxima (k and k + 8) and
+// the arcs that wrap past c_15 take the swapped halves (op_sel).  The polarity is a per-lane sign: the bright score
+// B - v = max_k min_arc(c) - v is the dark form v' - min_k max_arc(c') on c' = -c, v' = -v, so both polarities run
+// the same instructions.  All values are integers of magnitude < 2048 (exact in f16): bit-exact with og_fast_M1.
+// p = the centre's u16 in the quad ROI; SX = element step of one column, st = of one row.
+typedef _Float16 og_h2 __attribute__((ext_vector_type(2)));
+// The quad ROI is read by u16 loads straight into the halves (ds_read_u16_d16 / _d16_hi): P_k = (c_k, c_k+8) with
+// no packing instructions.  base = LDS byte address of the sample 3 rows up and 3 columns left of the centre, so
+// every offset is positive; FQ_S = row stride in qwords (the element of one pixel column is 4 u16 = 8 bytes apart).
+#define OG_MPK_OFF(dy, dx) (8 * ((3 + (dy)) * FQ_S_ + 3 + (dx)))
+template <int FQ_S_>
+__device__ __forceinline__ int og_fast_Mpk(uint32_t base, _Float16 sgn)
+{
+    uint32_t w[8];
+    uint32_t vc;
+    __asm__ volatile(
+        "ds_read_u16_d16 %0, %9 offset:%10\n\t"
+        "ds_read_u16_d16_hi %0, %9 offset:%11\n\t"
+        "ds_read_u16_d16 %1, %9 offset:%12\n\t"
+        "ds_read_u16_d16_hi %1, %9 offset:%13\n\t"
+        "ds_read_u16_d16 %2, %9 offset:%14\n\t"
+        "ds_read_u16_d16_hi %2, %9 offset:%15\n\t"
+        "ds_read_u16_d16 %3, %9 offset:%16\n\t"
+        "ds_read_u16_d16_hi %3, %9 offset:%17\n\t"
+        "ds_read_u16_d16 %4, %9 offset:%18\n\t"
+        "ds_read_u16_d16_hi %4, %9 offset:%19\n\t"
+        "ds_read_u16_d16 %5, %9 offset:%20\n\t"
+        "ds_read_u16_d16_hi %5, %9 offset:%21\n\t"
+        "ds_read_u16_d16 %6, %9 offset:%22\n\t"
+        "ds_read_u16_d16_hi %6, %9 offset:%23\n\t"
+        "ds_read_u16_d16 %7, %9 offset:%24\n\t"
+        "ds_read_u16_d16_hi %7, %9 offset:%25\n\t"
+        "ds_read_u16 %8, %9 offset:%26\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5]), "=&v"(w[6]), "=&v"(w[7]),
+          "=&v"(vc)
+        : "v"(base), "i"(OG_MPK_OFF(3, 0)), "i"(OG_MPK_OFF(-3, 0)), "i"(OG_MPK_OFF(3, 1)), "i"(OG_MPK_OFF(-3, -1)),
+          "i"(OG_MPK_OFF(2, 2)), "i"(OG_MPK_OFF(-2, -2)), "i"(OG_MPK_OFF(1, 3)), "i"(OG_MPK_OFF(-1, -3)),
+          "i"(OG_MPK_OFF(0, 3)), "i"(OG_MPK_OFF(0, -3)), "i"(OG_MPK_OFF(-1, 3)), "i"(OG_MPK_OFF(1, -3)),
+          "i"(OG_MPK_OFF(-2, 2)), "i"(OG_MPK_OFF(2, -2)), "i"(OG_MPK_OFF(-3, 1)), "i"(OG_MPK_OFF(3, -1)),
+          "i"(OG_MPK_OFF(0, 0))
+        : "memory");
+    const og_h2 sg = {sgn, sgn};
+    og_h2 P[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) P[k] = __builtin_bit_cast(og_h2, w[k]) * sg;
+    const _Float16 v = __builtin_bit_cast(og_h2, vc).x * sgn;
+#define OG_SW(a) __builtin_shufflevector(a, a, 1, 0)
+#define OG_MX3(a, b, c) __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c)
+#define OG_MN3(a, b, c) __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c)
+    // X_k = (max c_k..c_k+2, max c_k+8..c_k+10)
+    const og_h2 X0 = OG_MX3(P[0], P[1], P[2]), X1 = OG_MX3(P[1], P[2], P[3]), X2 = OG_MX3(P[2], P[3], P[4]);
+    const og_h2 X3 = OG_MX3(P[3], P[4], P[5]), X4 = OG_MX3(P[4], P[5], P[6]), X5 = OG_MX3(P[5], P[6], P[7]);
+    const og_h2 X6 = OG_MX3(P[6], P[7], OG_SW(P[0])), X7 = OG_MX3(P[7], OG_SW(P[0]), OG_SW(P[1]));
+    // Y_k = (max of the 9-arc at k, at k + 8) = max(X_k, X_k+3, X_k+6)
+    const og_h2 Y0 = OG_MX3(X0, X3, X6), Y1 = OG_MX3(X1, X4, X7), Y2 = OG_MX3(X2, X5, OG_SW(X0));
+    const og_h2 Y3 = OG_MX3(X3, X6, OG_SW(X1)), Y4 = OG_MX3(X4, X7, OG_SW(X2));
+    const og_h2 Y5 = OG_MX3(X5, OG_SW(X0), OG_SW(X3)), Y6 = OG_MX3(X6, OG_SW(X1), OG_SW(X4));
+    const og_h2 Y7 = OG_MX3(X7, OG_SW(X2), OG_SW(X5));
+    const og_h2 Z = OG_MN3(OG_MN3(Y0, Y1, Y2), OG_MN3(Y3, Y4, Y5), __builtin_elementwise_minimum(Y6, Y7));
+#undef OG_SW
+#undef OG_MX3
+#undef OG_MN3
+    const _Float16 A = __builtin_elementwise_minimum(Z.x, Z.y);
+    const int M = (int)(short)(v - A);  // an integer in [-255, 255]
+    return M > 0 ? M : 0;
+}
+#undef OG_MPK_OFF
+
 // OpenCV FAST_t quick rejection (src: cv::FAST, pairs {k, k+8}): a pixel can only be a corner at
 // threshold t if for every opposite pair one pixel is darker than v-t (resp. brighter than v+t).
 // Necessary condition => every pixel that fails it has M <= t.  Restated threshold-free:
@@ -889,11 +959,20 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const int i = (ent >> 7) & 127, j = ent & 127;
         const uint16_t* pc = &T16[4 * ((i + 3) * FQ_S + ((j & 15) + 3)) + (j >> 4)];
         const bool dark = (ent & 0x4000) != 0, bright = (ent & 0x8000) != 0;
+#ifndef OG_FASTQ_PK
+#define OG_FASTQ_PK 1  // 1: exact score with packed f16 pair ops (og_fast_Mpk); 0: scalar integer form (og_fast_M1)
+#endif
+#if OG_FASTQ_PK
+        const uint32_t pb = og_lds_addr(pc) - 8u * (3u * FQ_S + 3u);
+        int M = og_fast_Mpk<FQ_S>(pb, dark ? (_Float16)1 : (_Float16)-1);
+        if (dark && bright) M = max(M, og_fast_Mpk<FQ_S>(pb, (_Float16)-1));
+#else
         int M = og_fast_M1<4>(pc, 4 * FQ_S, dark ? 0 : 0xff);
         if (dark && bright) {
             __asm__ volatile("" ::: "memory");  // keeps the second polarity's reads behind the branch
             M = max(M, og_fast_M1<4>(pc, 4 * FQ_S, 0xff));
         }
+#endif
         Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)M;
     }
     __syncthreads();

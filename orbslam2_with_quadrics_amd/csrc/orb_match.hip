@@ -5,10 +5,10 @@
 //       vnMatches21 state couples them, :444, :463-470); the candidates of one query are scored in
 //       parallel (XOR + popcount over 8 u32) and reduced to (best, second) with a lexicographic
 //       (distance, candidate position) wave min -- exactly the reference's strict-< update order.
-//   og_projb_count/scan/fill/resolve : ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th)
-//       (src/ORBmatcher.cc:45-137) for B frames.  Candidate lists + distances are built in parallel (one
-//       thread per map point); the order-dependent claims (:87-89, :123) are resolved by a parallel
-//       fixed-point iteration of the triangular claim system (og_projb_resolve_kernel).
+//   og_projb_fill/resolve : ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th)
+//       (src/ORBmatcher.cc:45-137) for B frames.  Candidate lists + distances are built in one parallel pass
+//       (one thread per map point); the order-dependent claims (:87-89, :123) are resolved by a parallel
+//       fixed-point iteration of the triangular claim system over LDS-staged lists (og_projb_resolve_kernel).
 #include <hip/hip_runtime.h>
 #include <limits.h>
 
@@ -497,61 +497,58 @@ void og_launch_prev_from_frame(hipStream_t s, OgFrameDev F1, int ref, float* pre
 // ------------------------------------------------------------------------------------------------
 // SearchByProjection(Frame&, const vector<MapPoint*>&, th)
 // ------------------------------------------------------------------------------------------------
-struct OgProjCand {
-    int idx;
-    short dist;
-    short octave;
-};
-
-// Enumerate (or count) the candidates of map point m in GetFeaturesInArea order, applying the static
-// filters (levels, window, stereo check); claims are dynamic and applied in the ordered pass.
-template <bool FILL>
-__device__ int og_proj_enum(const OgFrameDev& F, const OgGridGeom& G, const float* sf, const OgMapPointsDev& mp,
-                            int m, float th, OgProjCand* out, int dkeep = 256)
+// Candidates of map point m in GetFeaturesInArea order (src/Frame.cc:327-380: cells ix-major, then iy, then cell
+// order) after the static filters of SearchByProjection (levels, window, stereo check, src/ORBmatcher.cc:53-104),
+// with their Hamming distances; the dynamic filter (claims, :87-89) is applied by the caller.  visit(idx, dist,
+// octave) is called in order for every candidate with dist <= dkeep (og_proj_keep_bound).
+template <class Visit>
+__device__ __forceinline__ void og_proj_visit(const OgFrameDev& F, const OgGridGeom& G, const float* sf,
+                                              const OgMapPointsDev& mp, int m, float th, int dkeep, Visit visit)
 {
-    if (!mp.track_in_view[m] || mp.is_bad[m]) return 0;
+    if (!mp.track_in_view[m] || mp.is_bad[m]) return;
     const int lvl = mp.level[m];
     float r = mp.view_cos[m] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos, :131-137
     if (th != 1.0) r *= th;
     const float R = r * sf[lvl];
     const float x = mp.proj_x[m], y = mp.proj_y[m];
     const OgCellRange cr = og_cell_range(G, x, y, R);
-    if (cr.x0 > cr.x1) return 0;
+    if (cr.x0 > cr.x1) return;
     const int minLevel = lvl - 1, maxLevel = lvl;
     const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
     uint4 da, db;
-    if (FILL) og_load_desc(mp.desc + (long long)m * 32, da, db);
-    int n = 0;
+    og_load_desc(mp.desc + (long long)m * 32, da, db);
     for (int ix = cr.x0; ix <= cr.x1; ix++)
         for (int iy = cr.y0; iy <= cr.y1; iy++) {
             const int cell = ix * OG_GRID_ROWS + iy;
             for (int j = F.cell_start[cell]; j < F.cell_start[cell + 1]; j++) {
                 const int idx = F.cell_items[j];
-                const orbgpu_kp_dev kp = F.kps[idx];
+                const orbgpu_kp_dev* kp = F.kps + idx;
+                const float kx = kp->x, ky = kp->y;
+                const int oct = kp->octave;
                 if (bCheckLevels) {
-                    if (kp.octave < minLevel) continue;
-                    if (maxLevel >= 0 && kp.octave > maxLevel) continue;
+                    if (oct < minLevel) continue;
+                    if (maxLevel >= 0 && oct > maxLevel) continue;
                 }
-                const float distx = kp.x - x, disty = kp.y - y;
+                const float distx = kx - x, disty = ky - y;
                 if (!(fabsf(distx) < R && fabsf(disty) < R)) continue;
                 if (F.uright && F.uright[idx] > 0) {
                     const float er = fabsf(mp.proj_xr[m] - F.uright[idx]);
                     if (er > r * sf[lvl]) continue;
                 }
-                if (FILL) {
-                    uint4 ea, eb;
-                    og_load_desc(F.desc + (long long)idx * 32, ea, eb);
-                    OgProjCand c;
-                    c.idx = idx;
-                    c.dist = (short)og_hamming(da, db, ea, eb);
-                    c.octave = (short)kp.octave;
-                    if (c.dist > dkeep) continue;  // og_proj_keep_bound
-                    out[n] = c;
-                }
-                n++;
+                uint4 ea, eb;
+                og_load_desc(F.desc + (long long)idx * 32, ea, eb);
+                const int dist = og_hamming(da, db, ea, eb);
+                if (dist > dkeep) continue;  // og_proj_keep_bound
+                visit(idx, dist, oct);
             }
         }
-    return n;
+}
+
+// a kept candidate as one dword: keypoint index (15 bits: the claim table of a frame holds < 2^15 keypoints,
+// orbgpu_search_by_projection checks it), distance (9 bits, <= 256), octave (8 bits)
+__device__ __forceinline__ uint32_t og_pj_pack(int idx, int dist, int oct)
+{
+    return (uint32_t)idx | ((uint32_t)dist << 15) | ((uint32_t)oct << 24);
 }
 
 __global__ __launch_bounds__(1024) void og_scan_kernel(const int* cnt, int n, int* off)
@@ -590,7 +587,6 @@ __global__ __launch_bounds__(1024) void og_scan_kernel(const int* cnt, int n, in
     if (threadIdx.x == 0) off[n] = carry;
 }
 
-// ---- batched SearchByProjection(F, vpMapPoints, th): frame b of a batch against its own map-point snapshot ----
 // Largest candidate distance that can change the outcome: a candidate at d > TH_HIGH is never the accepted
 // best, and if TH_HIGH <= nnratio * (float)d then no acceptable best b <= TH_HIGH satisfies b > nnratio * d, so as
 // a second-best it never triggers the ratio rejection (src/ORBmatcher.cc:115-121); the same holds for every
@@ -632,80 +628,22 @@ __device__ __forceinline__ OgMapPointsDev og_mp_of(const OgMapPointsDev& mp, int
     return q;
 }
 
-// candidates per (frame, point) before the distance bound (an upper bound for the fill pass)
-__global__ __launch_bounds__(256) void og_projb_count_kernel(OgFrameDev F, OgGridGeom G, const float* sf,
-                                                             OgMapPointsDev mp, int stride, float th, int* cnt)
-{
-    const int b = blockIdx.y, m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= mp.m) return;
-    cnt[(long long)b * stride + m] = og_proj_enum<false>(og_frame_of(F, b), G, sf, og_mp_of(mp, b, stride), m, th,
-                                                         nullptr);
-}
-
-// per-frame exclusive scan of the counts (one workgroup per frame); tot[b] = the frame's total
-__global__ __launch_bounds__(1024) void og_projb_scan_kernel(const int* cnt, int stride, int n, int* off, int* tot)
-{
-    __shared__ int wsum[16];
-    __shared__ int carry;
-    const int b = blockIdx.x;
-    const int* C = cnt + (long long)b * stride;
-    int* O = off + (long long)b * stride;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int base = 0; base < n; base += 1024) {
-        const int i = base + threadIdx.x;
-        const int v = i < n ? C[i] : 0;
-        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-        int x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) wsum[w] = x;
-        __syncthreads();
-        int before = carry;
-        for (int q = 0; q < w; q++) before += wsum[q];
-        if (i < n) O[i] = before + x - v;
-        int t = 0;
-        for (int q = 0; q < 16; q++) t += wsum[q];
-        __syncthreads();
-        if (threadIdx.x == 0) carry += t;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) tot[b] = carry;
-}
-
-// frame bases of the candidate buffer (exclusive scan over B frame totals, one workgroup); base[B] = total
-__global__ __launch_bounds__(1024) void og_projb_base_kernel(const int* tot, int B, long long* base)
-{
-    __shared__ long long carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int b0 = 0; b0 < B; b0 += 1024) {
-        if (threadIdx.x == 0) {
-            long long c = carry;
-            for (int b = b0; b < min(B, b0 + 1024); b++) {
-                base[b] = c;
-                c += tot[b];
-            }
-            carry = c;
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) base[B] = carry;
-}
-
+// ---- one enumeration pass: thread per (frame, point).  The first OG_PJ_K kept candidates go to the point's slots,
+// stored k-major (slot k of points m, m + 1, ... adjacent: the threads of a wave write neighbouring dwords);
+// kept[] = the point's full kept count (> OG_PJ_K: the resolve re-enumerates that point itself).
 __global__ __launch_bounds__(256) void og_projb_fill_kernel(OgFrameDev F, OgGridGeom G, const float* sf,
                                                             OgMapPointsDev mp, int stride, float th, int dkeep,
-                                                            const int* off, const long long* base, OgProjCand* cands,
-                                                            int* kept)
+                                                            uint32_t* __restrict__ slots, int* __restrict__ kept)
 {
     const int b = blockIdx.y, m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= mp.m) return;
-    const long long o = (long long)b * stride + m;
-    kept[o] = og_proj_enum<true>(og_frame_of(F, b), G, sf, og_mp_of(mp, b, stride), m, th, cands + base[b] + off[o],
-                                 dkeep);
+    uint32_t* S = slots + (long long)b * OG_PJ_K * stride + m;
+    int n = 0;
+    og_proj_visit(og_frame_of(F, b), G, sf, og_mp_of(mp, b, stride), m, th, dkeep, [&](int idx, int dist, int oct) {
+        if (n < OG_PJ_K) S[(long long)n * stride] = og_pj_pack(idx, dist, oct);
+        n++;
+    });
+    kept[(long long)b * stride + m] = n;
 }
 
 // The reference's ordered loop over map points (src/ORBmatcher.cc:53-129) couples points only through the
@@ -718,55 +656,135 @@ __global__ __launch_bounds__(256) void og_projb_fill_kernel(OgFrameDev F, OgGrid
 // result -- after at most (longest dependency chain + 1) rounds, and a round that leaves FO unchanged is that
 // fixed point.  One workgroup per frame; every point's decision within a round is independent.
 // Final ownership: keypoint i belongs to the LAST accepted claimant (assignment order), else keeps its holder.
+//
+// The candidate lists are staged once into LDS (compacted by a block scan of the kept counts), so the rounds read
+// no global memory; a frame whose lists exceed the LDS budget reads its slots instead, and a point with more than
+// OG_PJ_K kept candidates re-enumerates them (og_proj_visit) in every round.
 #define PJ_NT 1024
-__global__ __launch_bounds__(PJ_NT) void og_projb_resolve_kernel(OgMapPointsDev mp, int stride, const int* off,
-                                                                 const long long* base, const int* kept,
-                                                                 const OgProjCand* cands, const int* counts,
-                                                                 int frame_cap, float nnratio, int* owner,
-                                                                 int* owner_obs, int* nmatches, int* res, int* status)
+__device__ __forceinline__ int og_block_exclusive_scan(int v, int* wsum, int& total)
+{
+    // PJ_NT threads; wsum: PJ_NT / 64 + 1 ints of LDS
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int q = 0; q < PJ_NT / 64; q++) {
+            const int t = wsum[q];
+            wsum[q] = acc;
+            acc += t;
+        }
+        wsum[PJ_NT / 64] = acc;
+    }
+    __syncthreads();
+    total = wsum[PJ_NT / 64];
+    const int r = wsum[w] + x - v;
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(PJ_NT) void og_projb_resolve_kernel(OgFrameDev Fb, OgGridGeom G, const float* sf,
+                                                                 OgMapPointsDev mp, int stride, float th, int dkeep,
+                                                                 const uint32_t* __restrict__ slots,
+                                                                 const int* __restrict__ kept, float nnratio,
+                                                                 int lds_bytes, int* owner, int* owner_obs,
+                                                                 int* nmatches, int* res, int* status)
 {
     extern __shared__ int pj_lds[];
+    const int frame_cap = Fb.frame_cap;
     int* FO = pj_lds;               // [frame_cap] current round
     int* NF = pj_lds + frame_cap;   // [frame_cap] next round / final owner
+    int* PO = NF + frame_cap;       // [M + 1] list offsets (staged mode)
     __shared__ int sh_changed, sh_nm;
+    __shared__ int wsum[PJ_NT / 64 + 1];
     const int b = blockIdx.x, tid = threadIdx.x;
-    const int n = counts[b];
+    const OgFrameDev F = og_frame_of(Fb, b);
+    const int n = F.counts[0];
     const OgMapPointsDev q = og_mp_of(mp, b, stride);
-    const int* OFF = off + (long long)b * stride;
+    const int M = q.m;
     const int* KEPT = kept + (long long)b * stride;
-    const OgProjCand* CB = cands + base[b];
+    const uint32_t* SL = slots + (long long)b * OG_PJ_K * stride;
     int* OWN = owner + (long long)b * frame_cap;
     int* OBS = owner_obs + (long long)b * frame_cap;
     int* RES = res + (long long)b * stride;
+    // ---- stage the lists: per-point counts (0 for overflowed points: they re-enumerate), block scan, copy
+    const int ppt = (M + PJ_NT - 1) / PJ_NT;  // points per thread, contiguous: m in [tid * ppt, tid * ppt + ppt)
+    int my = 0;
+    for (int k = 0; k < ppt; k++) {
+        const int m = tid * ppt + k;
+        if (m < M) {
+            const int c = KEPT[m];
+            my += c <= OG_PJ_K ? c : 0;
+        }
+    }
+    int T = 0;
+    const int base = og_block_exclusive_scan(my, wsum, T);
+    uint32_t* LST = (uint32_t*)(PO + M + 1);
+    const int cap_entries = (lds_bytes - (int)sizeof(int) * (2 * frame_cap + M + 1)) / 4;
+    const bool staged = M > 0 && T <= cap_entries && (2 * frame_cap + M + 1) * (int)sizeof(int) <= lds_bytes;  // uniform
+    if (staged) {
+        int o = base;
+        for (int k = 0; k < ppt; k++) {
+            const int m = tid * ppt + k;
+            if (m < M) {
+                PO[m] = o;
+                const int c = KEPT[m];
+                o += c <= OG_PJ_K ? c : 0;
+            }
+        }
+        if (tid == 0) PO[M] = T;
+    }
     for (int i = tid; i < n; i += PJ_NT) {
-        const int pre = (OWN[i] >= 0 && OBS[i]) ? -1 : INT_MAX;
-        FO[i] = INT_MAX;  // round 0: no claims yet (pre-claims enter through NF below)
-        NF[i] = pre;
+        FO[i] = (OWN[i] >= 0 && OBS[i]) ? -1 : INT_MAX;  // round 0 starts from the pre-call claims only
+        NF[i] = FO[i];
     }
     if (tid == 0) sh_changed = 1;
     __syncthreads();
-    // round 0 starts from the pre-call claims only
-    for (int i = tid; i < n; i += PJ_NT) FO[i] = NF[i];
+    if (staged) {  // copy slot k of every point with more than k staged entries (k-major: coalesced reads)
+        for (int k = 0; k < OG_PJ_K; k++) {
+            for (int m = tid; m < M; m += PJ_NT) {
+                const int c = KEPT[m];
+                if (c <= OG_PJ_K && k < c) LST[PO[m] + k] = SL[(long long)k * stride + m];
+            }
+        }
+    }
     __syncthreads();
     int rounds = 0;
     for (;;) {
-        for (int m = tid; m < q.m; m += PJ_NT) {
-            const int nc = KEPT[m];
-            const OgProjCand* L = CB + OFF[m];
+        for (int m = tid; m < M; m += PJ_NT) {
             int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
-            for (int c = 0; c < nc; c++) {
-                const OgProjCand cc = L[c];
-                if (FO[cc.idx] < m) continue;  // :87-89
-                const int dist = cc.dist;
+            auto take = [&](int idx, int dist, int oct) {
+                if (FO[idx] < m) return;  // :87-89
                 if (dist < bestDist) {
                     bestDist2 = bestDist;
                     bestDist = dist;
                     bestLevel2 = bestLevel;
-                    bestLevel = cc.octave;
-                    bestIdx = cc.idx;
+                    bestLevel = oct;
+                    bestIdx = idx;
                 } else if (dist < bestDist2) {
-                    bestLevel2 = cc.octave;
+                    bestLevel2 = oct;
                     bestDist2 = dist;
+                }
+            };
+            const int nc = KEPT[m];
+            if (nc > OG_PJ_K) {
+                og_proj_visit(F, G, sf, q, m, th, dkeep, take);
+            } else if (staged) {
+                const uint32_t* L = LST + PO[m];
+                for (int c = 0; c < nc; c++) {
+                    const uint32_t e = L[c];
+                    take((int)(e & 0x7fff), (int)((e >> 15) & 0x1ff), (int)(e >> 24));
+                }
+            } else {
+                for (int c = 0; c < nc; c++) {
+                    const uint32_t e = SL[(long long)c * stride + m];
+                    take((int)(e & 0x7fff), (int)((e >> 15) & 0x1ff), (int)(e >> 24));
                 }
             }
             int r = -1;
@@ -789,7 +807,7 @@ __global__ __launch_bounds__(PJ_NT) void og_projb_resolve_kernel(OgMapPointsDev 
         const bool again = sh_changed != 0;
         __syncthreads();
         if (!again) break;
-        if (++rounds > q.m + 1) {  // cannot happen (triangular system); reported, never silent
+        if (++rounds > M + 1) {  // cannot happen (triangular system); reported, never silent
             if (tid == 0) atomicOr(status, 32);
             break;
         }
@@ -799,7 +817,7 @@ __global__ __launch_bounds__(PJ_NT) void og_projb_resolve_kernel(OgMapPointsDev 
     if (tid == 0) sh_nm = 0;
     __syncthreads();
     int cnt = 0;
-    for (int m = tid; m < q.m; m += PJ_NT) {
+    for (int m = tid; m < M; m += PJ_NT) {
         const int r = RES[m];
         if (r >= 0) {
             atomicMax(&NF[r], m);
@@ -819,33 +837,18 @@ __global__ __launch_bounds__(PJ_NT) void og_projb_resolve_kernel(OgMapPointsDev 
     if (tid == 0) nmatches[b] = sh_nm;
 }
 
-void og_launch_projb_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, int stride,
-                           float th, int B, int* cnt, int* off, int* tot, long long* base)
-{
-    if (mp.m > 0 && B > 0) {
-        hipLaunchKernelGGL(og_projb_count_kernel, dim3((mp.m + 255) / 256, B), dim3(256), 0, s, F, G, sf, mp, stride,
-                           th, cnt);
-        hipLaunchKernelGGL(og_projb_scan_kernel, dim3(B), dim3(1024), 0, s, cnt, stride, mp.m, off, tot);
-    } else if (B > 0) {
-        (void)hipMemsetAsync(tot, 0, sizeof(int) * (size_t)B, s);
-    }
-    hipLaunchKernelGGL(og_projb_base_kernel, dim3(1), dim3(1024), 0, s, tot, B, base);
-}
-
-void og_launch_projb_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, int stride,
-                             float nnratio, float th, int B, const int* off, const long long* base, OgProjCand* cands,
-                             int* kept, int* res, int* owner, int* owner_obs, int* nmatches, int* status)
+void og_launch_projb(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, int stride,
+                     float nnratio, float th, int B, uint32_t* slots, int* kept, int* res, int* owner, int* owner_obs,
+                     int* nmatches, int* status)
 {
     if (B <= 0) return;
+    const int dkeep = og_proj_keep_bound(nnratio);
     if (mp.m > 0)
         hipLaunchKernelGGL(og_projb_fill_kernel, dim3((mp.m + 255) / 256, B), dim3(256), 0, s, F, G, sf, mp, stride, th,
-                           og_proj_keep_bound(nnratio), off, base, cands, kept);
-    const size_t shm = 2 * sizeof(int) * (size_t)F.frame_cap;
-    hipLaunchKernelGGL(og_projb_resolve_kernel, dim3(B), dim3(PJ_NT), shm, s, mp, stride, off, base, kept, cands,
-                       F.counts, F.frame_cap, nnratio, owner, owner_obs, nmatches, res, status);
+                           dkeep, slots, kept);
+    hipLaunchKernelGGL(og_projb_resolve_kernel, dim3(B), dim3(PJ_NT), OG_PJ_LDS, s, F, G, sf, mp, stride, th, dkeep,
+                       slots, kept, nnratio, (int)OG_PJ_LDS, owner, owner_obs, nmatches, res, status);
 }
-
-size_t og_proj_cand_size() { return sizeof(OgProjCand); }
 
 // ------------------------------------------------------------------------------------------------
 // Frame::isInFrustum + MapPoint::PredictScale (src/Frame.cc:269-325, src/MapPoint.cc:402-417), one thread
@@ -1258,5 +1261,5 @@ hipError_t og_prepare_device_match()
                                        OG_INIT_LDS_MAX);
     if (e != hipSuccess) return e;
     return hipFuncSetAttribute((const void*)og_projb_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               OG_INIT_LDS_MAX);
+                               OG_PJ_LDS);
 }

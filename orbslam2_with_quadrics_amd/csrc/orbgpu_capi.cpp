@@ -95,8 +95,7 @@ struct orbgpu_ctx {
     DevBuf<uint32_t> mlists;  // SearchForInitialization candidate lists {dist:16|i2:16}
     DevBuf<int> mlist_n;
     DevBuf<uint8_t> mcands;   // projection-matcher candidate lists (grown on demand, kept)
-    DevBuf<int> pj_int;       // projection matcher: counts, offsets, kept counts, decisions, frame totals
-    DevBuf<long long> pj_base;
+    DevBuf<int> pj_int;       // projection matcher: kept counts, decisions
     DevBuf<float> sf_dev;     // mvScaleFactors on the device
     // Frame::UndistortKeyPoints on the device (set by orbgpu_set_undistortion): batches then also hold
     // mvKeysUn, and the grid and the matchers use it with the undistorted image bounds
@@ -819,7 +818,6 @@ void orbgpu_destroy(orbgpu_ctx* c)
     release(c->mlist_n);
     release(c->mcands);
     release(c->pj_int);
-    release(c->pj_base);
     release(c->sf_dev);
     release(c->kps_un);
     release(c->bow_word);
@@ -1730,27 +1728,19 @@ int orbgpu_compute_stereo_matches(orbgpu_ctx* left, orbgpu_ctx* right, float mbf
     return ORBGPU_OK;
 }
 
-// The candidate lists of the batched projection matcher: count + per-frame scan, one int read back to size the
-// list buffer exactly, then fill + the fixed-point resolve (og_projb_*, orb_match.hip).
+// The batched projection matcher: one enumeration pass into fixed per-point slots, then the fixed-point resolve
+// (og_launch_projb, orb_match.hip); stream-ordered, no host synchronisation.
 static int run_projection(orbgpu_ctx* c, hipStream_t s, const OgFrameDev& fd, const OgGridGeom& G, const float* sfd,
                           const OgMapPointsDev& mpd, int stride, int B, float nnratio, float th, int* own, int* obs,
                           int* nm)
 {
     const size_t pts = (size_t)B * (size_t)std::max(stride, 1);
-    HIP_TRY(c, ensure(c->pj_int, 4 * pts + (size_t)B));
-    HIP_TRY(c, ensure(c->pj_base, (size_t)B + 1));
-    int* cnt = c->pj_int.p;
-    int* off = cnt + pts;
-    int* kept = off + pts;
+    HIP_TRY(c, ensure(c->pj_int, 2 * pts));
+    HIP_TRY(c, ensure(c->mcands, pts * OG_PJ_K * sizeof(uint32_t)));
+    int* kept = c->pj_int.p;
     int* res = kept + pts;
-    int* tot = res + pts;
-    og_launch_projb_count(s, fd, G, sfd, mpd, stride, th, B, cnt, off, tot, c->pj_base.p);
-    long long total = 0;
-    HIP_TRY(c, hipMemcpyAsync(&total, c->pj_base.p + B, sizeof(total), hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipStreamSynchronize(s));
-    HIP_TRY(c, ensure(c->mcands, (size_t)std::max<long long>(total, 1) * og_proj_cand_size()));
-    og_launch_projb_resolve(s, fd, G, sfd, mpd, stride, nnratio, th, B, off, c->pj_base.p, (OgProjCand*)c->mcands.p,
-                            kept, res, own, obs, nm, c->status.p);
+    og_launch_projb(s, fd, G, sfd, mpd, stride, nnratio, th, B, (uint32_t*)c->mcands.p, kept, res, own, obs, nm,
+                    c->status.p);
     HIP_TRY(c, hipGetLastError());
     return ORBGPU_OK;
 }

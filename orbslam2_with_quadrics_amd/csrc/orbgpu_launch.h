@@ -106,17 +106,16 @@ struct OgMapPointsDev {
     int shared_map = 0;  // batched forms: 1 = is_bad / n_obs / desc are one map shared by every frame (stride 0)
 };
 
-struct OgProjCand;
-size_t og_proj_cand_size();
-// batched form (B frames, map point j of frame b at b*stride + j of every mp array; mp.m points per frame):
-// count + per-frame scan + frame bases (base[B] = the candidate total, read by the host to size `cands`), then
-// fill + the parallel fixed-point resolve (one workgroup per frame; LDS 2 * frame_cap ints)
+// batched SearchByProjection (B frames, map point j of frame b at b*stride + j of every mp array; mp.m points per
+// frame): one enumeration pass writes each point's first OG_PJ_K kept candidates (dword entries, k-major slots of
+// B * OG_PJ_K * stride) and its kept count (B * stride ints); then one workgroup per frame stages the lists in LDS
+// and runs the parallel fixed-point resolve.  No host synchronisation.
+#define OG_PJ_K 16
+#define OG_PJ_LDS (159 * 1024)  // dynamic LDS of the resolve (its static LDS is < 1 KB)
 int og_proj_keep_bound(float nnratio);
-void og_launch_projb_count(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, int stride,
-                           float th, int B, int* cnt, int* off, int* tot, long long* base);
-void og_launch_projb_resolve(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, int stride,
-                             float nnratio, float th, int B, const int* off, const long long* base, OgProjCand* cands,
-                             int* kept, int* res, int* owner, int* owner_obs, int* nmatches, int* status);
+void og_launch_projb(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, int stride,
+                     float nnratio, float th, int B, uint32_t* slots, int* kept, int* res, int* owner, int* owner_obs,
+                     int* nmatches, int* status);
 
 // stereo (orb_stereo.hip): Frame::ComputeStereoMatches over frame pairs b of two extractor batches
 struct OgStereoDev {

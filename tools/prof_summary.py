@@ -27,13 +27,14 @@ def main():
         # frames per launch: z for the pyramid kernel, x/8 for the octree, x for the matchers, y for the others
         if k.startswith("og_resize"):
             batch = gz // max(wz, 1)
-        elif k.startswith("og_octree"):  # level-major 1-D grid: 8 levels x B frames
-            batch = gx // max(wx, 1) // 8
+        elif k.startswith("og_octree"):  # level-major 1-D grid: 8 levels x B frames (the single-frame fork splits
+            batch = max(1, round(gx // max(wx, 1) / 8))  # level 0 from levels 1-7: 1 and 7 workgroups, one frame)
         elif k.startswith(("og_search_init", "og_grid", "og_init_resolve")):
             batch = gx // max(wx, 1)
         else:
             batch = gy // max(wy, 1)
-        key = (k, batch)
+        # the pyramid's fused launches ((1,2), (3,4), (5,6)) differ in their tile grid: one row each
+        key = (k + (f" [{gx // max(wx, 1)}x{gy // max(wy, 1)}]" if k.startswith("og_resize") else ""), batch)
         a = agg[key]
         a[0] += 1
         a[1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6

@@ -28,7 +28,7 @@ def main():
     res = {}
     for name in names:
         env = dict(os.environ, ORBGPU_LIB=os.path.join(VDIR, f"liborbgpu_{name}.so"))
-        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "10", "--warmup", "2", "--streams", streams,
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--warmup", "2", "--streams", streams,
                "--no-cpu-baseline", *extra]
         out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
         try:
