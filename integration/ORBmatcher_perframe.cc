@@ -135,11 +135,12 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
         cv::Mat d(1, 32, CV_8U, &desc[32 * (size_t)i]);
         p->GetDescriptor().copyTo(d);
     }
-    for (int i = 0; i < CurrentFrame.N; ++i)  // claims made before the call
+    for (int i = 0; i < CurrentFrame.N; ++i)  // claims made before the call: L + i keeps the holder recoverable
         if (MapPoint* q = CurrentFrame.mvpMapPoints[i]) {
-            owner[i] = L;
+            owner[i] = L + i;
             ownerObs[i] = q->Observations() > 0;
         }
+    const std::vector<MapPoint*> before = CurrentFrame.mvpMapPoints;
     orbgpu_last_frame_view lf{L, reinterpret_cast<const orbgpu_keypoint*>(LastFrame.mvKeysUn.data()), has.data(),
                               outl.data(), pos.data(), nobs.data(), desc.data()};
     orbgpu_frame_view v = view_of(CurrentFrame);
@@ -149,8 +150,12 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
                                                mbCheckOrientation, owner.data(), ownerObs.data(),
                                                &nmatches) != ORBGPU_OK)
         throw std::runtime_error("orbgpu_search_by_projection_last_frame");
-    for (int i = 0; i < CurrentFrame.N; ++i)
-        if (owner[i] >= 0 && owner[i] < L) CurrentFrame.mvpMapPoints[i] = LastFrame.mvpMapPoints[owner[i]];
+    // an owner of -1 is a keypoint the rotation check cleared (:1448-1467, mvpMapPoints[..] = NULL), even one that was
+    // held before the call and taken over by a point with no observations
+    for (int i = 0; i < CurrentFrame.N; ++i) {
+        const int o = owner[i];
+        CurrentFrame.mvpMapPoints[i] = o < 0 ? nullptr : (o < L ? LastFrame.mvpMapPoints[o] : before[o - L]);
+    }
     return nmatches;
 }
 
@@ -185,8 +190,9 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std
         if (dist3D < minDistance || dist3D > maxDistance) continue;  // level stays -1
         level[i] = pMP->PredictScale(dist3D, &CurrentFrame);
     }
-    for (int i = 0; i < CurrentFrame.N; ++i)  // any claim blocks the keypoint (:1532-1533)
-        if (CurrentFrame.mvpMapPoints[i]) owner[i] = L;
+    for (int i = 0; i < CurrentFrame.N; ++i)  // any claim blocks the keypoint (:1532-1533); L + i keeps the holder
+        if (CurrentFrame.mvpMapPoints[i]) owner[i] = L + i;
+    const std::vector<MapPoint*> before = CurrentFrame.mvpMapPoints;
     orbgpu_keyframe_view kf{L, reinterpret_cast<const orbgpu_keypoint*>(pKF->mvKeysUn.data()), valid.data(),
                             pos.data(), nullptr, nullptr, desc.data()};
     orbgpu_frame_view v = view_of(CurrentFrame);
@@ -195,8 +201,11 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std
     if (orbgpu_search_by_projection_keyframe_levels(ctx_of(CurrentFrame), &v, &cur, &kf, level.data(), th, ORBdist,
                                                     mbCheckOrientation, owner.data(), &nmatches) != ORBGPU_OK)
         throw std::runtime_error("orbgpu_search_by_projection_keyframe_levels");
-    for (int i = 0; i < CurrentFrame.N; ++i)
-        if (owner[i] >= 0 && owner[i] < L) CurrentFrame.mvpMapPoints[i] = vpMPs[owner[i]];
+    // -1: cleared by the rotation check (:1577-1596) or never matched
+    for (int i = 0; i < CurrentFrame.N; ++i) {
+        const int o = owner[i];
+        CurrentFrame.mvpMapPoints[i] = o < 0 ? nullptr : (o < L ? vpMPs[o] : before[o - L]);
+    }
     return nmatches;
 }
 

@@ -350,6 +350,123 @@ __device__ __forceinline__ void og_rz_store4(uint8_t* Dr, uint32_t packed, int n
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k1s: one pyramid level as a row stream, no LDS.  A wave owns a strip of 256 output columns (4 per lane) and a run
+// of RS_ROWS output rows.  It walks the source rows the run reads in order: each source row is loaded once (three
+// dwords per lane, the 4-byte-aligned window around the lane's source bytes, prefetched RS_PF rows ahead), its
+// horizontal sums are formed once (v_perm pairs + v_dot2), and an output row is emitted as soon as its second
+// source row is in (ytab[y].y == r), from the current and the previous row's sums.  The arithmetic is
+// og_resize_kernel's (cv::resize INTER_LINEAR fixed point, og_rz_vert16 / og_rz_vert).
+// ------------------------------------------------------------------------------------------------
+#define RS_ROWS 32  // output rows per wave
+#define RS_PF 4     // source rows in flight per wave
+#define RS_NT 256   // 4 independent waves per workgroup (4 row runs of one strip)
+
+// Source-row loads are issued by inline asm so that the compiler does not wait for them at the loop back-edge: the
+// loop waits explicitly (vmcnt counts every vector-memory op in issue order; the stores issued in between only make a
+// wait stronger).  A lane reads the three dwords of the row that hold its source bytes; a dword index past the row's
+// last dword is clamped to it (its bytes only meet zero weights: the pair (sw - 1, sw) at the right border), so every
+// load stays inside the row.
+__device__ __forceinline__ void og_rs_issue(const uint8_t* rb, unsigned q, unsigned qlast, uint32_t& d0, uint32_t& d1,
+                                            uint32_t& d2)
+{
+    const unsigned o0 = 4u * min(q, qlast), o1 = 4u * min(q + 1u, qlast), o2 = 4u * min(q + 2u, qlast);
+    __asm__ volatile("global_load_dword %0, %3, %6\n\t"
+                     "global_load_dword %1, %4, %6\n\t"
+                     "global_load_dword %2, %5, %6"
+                     : "=&v"(d0), "=&v"(d1), "=&v"(d2)
+                     : "v"(o0), "v"(o1), "v"(o2), "s"(rb)
+                     : "memory");
+}
+
+template <bool FX>
+__global__ __launch_bounds__(RS_NT) void og_resize_rows_kernel(const uint8_t* __restrict__ src, long long src_pitch,
+                                                               long long src_fstride, uint8_t* __restrict__ dst,
+                                                               long long dst_pitch, long long dst_fstride, int sw,
+                                                               int sh, int dw, int dh, const int4* __restrict__ xtab,
+                                                               const int4* __restrict__ ytab, int xmax)
+{
+    const int f = blockIdx.z, lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int y0 = (blockIdx.y * (RS_NT / 64) + w) * RS_ROWS;
+    if (y0 >= dh) return;
+    const int y1 = min(y0 + RS_ROWS, dh);
+    const int dxt = blockIdx.x * 256 + 4 * lane;
+    // the lane's 4 output columns: source offsets from its first source byte, weights (x16 for og_rz_vert16)
+    int sx0 = 0;
+    uint32_t sel[4];
+    og_rz_u16x2 wt[4];
+    {
+        int sxk[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) og_rz_weights<FX>(xtab, xmax, min(dxt + k, dw - 1), 0, sxk, wt, k);
+        sx0 = sxk[0];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const unsigned o = (unsigned)(sxk[k] - sx0);  // <= ceil(3 * 1.6) + 1 < 7: the pair stays in 8 bytes
+            sel[k] = 0x0c000c00u | o | ((o + 1u) << 16);
+        }
+    }
+    const uint8_t* fbase = src + (long long)f * src_fstride;
+    const int rs0 = ytab[y0].x, rs1 = ytab[y1 - 1].y;  // source rows of the run (monotone table)
+    const int nsrc = rs1 - rs0 + 1;
+    // row r: 4-byte-aligned base (SGPRs) and the lane's byte offset t from it; last = the row's last byte
+    auto issue = [&](int r, uint32_t& d0, uint32_t& d1, uint32_t& d2) {
+        const uint8_t* row = fbase + (long long)r * src_pitch;
+        const uint8_t* rb = (const uint8_t*)((uintptr_t)row & ~(uintptr_t)3);
+        const unsigned mr = (unsigned)((uintptr_t)row & 3);
+        og_rs_issue(rb, (mr + (unsigned)sx0) >> 2, (mr + (unsigned)(sw - 1)) >> 2, d0, d1, d2);
+    };
+    auto shift = [&](int r) { return ((unsigned)((uintptr_t)(fbase + (long long)r * src_pitch) & 3) + (unsigned)sx0) & 3u; };
+    uint8_t* D = dst + (long long)f * dst_fstride + dxt;
+    const int nout = min(4, dw - dxt);  // <= 0: an idle lane of the last strip
+    uint32_t ra[RS_PF], rb_[RS_PF], rc[RS_PF];
+#pragma unroll
+    for (int i = 0; i < RS_PF; i++) issue(min(rs0 + i, rs1), ra[i], rb_[i], rc[i]);
+    uint32_t hp[4] = {0u, 0u, 0u, 0u}, hc[4];
+    int y = y0;
+    int4 yt = ytab[y];
+    for (int j0 = 0; j0 < nsrc; j0 += RS_PF) {
+#pragma unroll
+        for (int i = 0; i < RS_PF; i++) {
+            const int r = rs0 + j0 + i;
+            if (j0 + i >= nsrc) break;  // uniform
+            // row r's three loads are done once at most the 3 (RS_PF - 1) issued after them are outstanding
+            __asm__ volatile("s_waitcnt vmcnt(%3)" : "+v"(ra[i]), "+v"(rb_[i]), "+v"(rc[i]) : "n"(3 * (RS_PF - 1)));
+            const unsigned m = shift(r);
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(rb_[i], ra[i], m), w1 = __builtin_amdgcn_alignbyte(rc[i], rb_[i], m);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t pr = __builtin_amdgcn_perm(w1, w0, sel[k]);
+                const uint32_t d = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, pr), wt[k], 0u, false);
+                hc[k] = (FX || !OG_RZ_MULHI) ? d : (d & ~0xffu);
+            }
+            issue(min(r + RS_PF, rs1), ra[i], rb_[i], rc[i]);  // the ring slot's next row (clamped: the count stays regular)
+            while (y < y1 && yt.y == r) {  // uniform; at most one row per source row when downscaling
+                const bool same = yt.x == r;  // clamped at the border: both taps on this row
+                uint32_t packed = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t h0 = same ? hc[k] : hp[k];
+                    uint32_t v;
+                    if (FX || !OG_RZ_MULHI)
+                        v = og_rz_vert<FX>((unsigned)yt.z, h0, (unsigned)yt.w, hc[k]);
+                    else
+                        v = min((og_mulhi_u24((unsigned)yt.z << 8, h0) + og_mulhi_u24((unsigned)yt.w << 8, hc[k]) + 2u) >> 2,
+                                255u);
+                    packed |= v << (8 * k);
+                }
+                if (nout > 0) og_rz_store4(D + (long long)y * dst_pitch, packed, nout);
+                y++;
+                if (y < y1) yt = ytab[y];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) hp[k] = hc[k];
+        }
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail loads land before the wave ends
+}
+
 template <bool FX>
 __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __restrict__ src, long long src_pitch,
                                                            long long src_fstride, uint8_t* __restrict__ dstA,
@@ -548,42 +665,27 @@ __device__ __forceinline__ int og_fast_M1(const E* p, int st, int fm)
 // the same instructions.  All values are integers of magnitude < 2048 (exact in f16): bit-exact with og_fast_M1.
 // p = the centre's u16 in the quad ROI; SX = element step of one column, st = of one row.
 typedef _Float16 og_h2 __attribute__((ext_vector_type(2)));
-// The quad ROI is read by u16 loads straight into the halves (ds_read_u16_d16 / _d16_hi): P_k = (c_k, c_k+8) with
-// no packing instructions.  base = LDS byte address of the sample 3 rows up and 3 columns left of the centre, so
-// every offset is positive; FQ_S = row stride in qwords (the element of one pixel column is 4 u16 = 8 bytes apart).
+// base = LDS byte address of the sample 3 rows up and 3 columns left of the centre; FQ_S_ = row stride in qwords
+// (one pixel column of the quad ROI is 4 u16 = 8 bytes).  The compiler packs each pair (c_k, c_k+8) with one v_perm
+// (D16 loads cannot do it here: with SRAMECC, gfx950's ds_read_u16_d16[_hi] clear the other half).
 #define OG_MPK_OFF(dy, dx) (8 * ((3 + (dy)) * FQ_S_ + 3 + (dx)))
 template <int FQ_S_>
 __device__ __forceinline__ int og_fast_Mpk(uint32_t base, _Float16 sgn)
 {
     uint32_t w[8];
     uint32_t vc;
-    __asm__ volatile(
-        "ds_read_u16_d16 %0, %9 offset:%10\n\t"
-        "ds_read_u16_d16_hi %0, %9 offset:%11\n\t"
-        "ds_read_u16_d16 %1, %9 offset:%12\n\t"
-        "ds_read_u16_d16_hi %1, %9 offset:%13\n\t"
-        "ds_read_u16_d16 %2, %9 offset:%14\n\t"
-        "ds_read_u16_d16_hi %2, %9 offset:%15\n\t"
-        "ds_read_u16_d16 %3, %9 offset:%16\n\t"
-        "ds_read_u16_d16_hi %3, %9 offset:%17\n\t"
-        "ds_read_u16_d16 %4, %9 offset:%18\n\t"
-        "ds_read_u16_d16_hi %4, %9 offset:%19\n\t"
-        "ds_read_u16_d16 %5, %9 offset:%20\n\t"
-        "ds_read_u16_d16_hi %5, %9 offset:%21\n\t"
-        "ds_read_u16_d16 %6, %9 offset:%22\n\t"
-        "ds_read_u16_d16_hi %6, %9 offset:%23\n\t"
-        "ds_read_u16_d16 %7, %9 offset:%24\n\t"
-        "ds_read_u16_d16_hi %7, %9 offset:%25\n\t"
-        "ds_read_u16 %8, %9 offset:%26\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5]), "=&v"(w[6]), "=&v"(w[7]),
-          "=&v"(vc)
-        : "v"(base), "i"(OG_MPK_OFF(3, 0)), "i"(OG_MPK_OFF(-3, 0)), "i"(OG_MPK_OFF(3, 1)), "i"(OG_MPK_OFF(-3, -1)),
-          "i"(OG_MPK_OFF(2, 2)), "i"(OG_MPK_OFF(-2, -2)), "i"(OG_MPK_OFF(1, 3)), "i"(OG_MPK_OFF(-1, -3)),
-          "i"(OG_MPK_OFF(0, 3)), "i"(OG_MPK_OFF(0, -3)), "i"(OG_MPK_OFF(-1, 3)), "i"(OG_MPK_OFF(1, -3)),
-          "i"(OG_MPK_OFF(-2, 2)), "i"(OG_MPK_OFF(2, -2)), "i"(OG_MPK_OFF(-3, 1)), "i"(OG_MPK_OFF(3, -1)),
-          "i"(OG_MPK_OFF(0, 0))
-        : "memory");
+    {
+        typedef const __attribute__((address_space(3))) _Float16 lds_h;
+        lds_h* q = (lds_h*)(uintptr_t)(base + OG_MPK_OFF(0, 0));
+        constexpr int st = 4 * FQ_S_, SX = 4;
+        const _Float16 c[16] = {q[3 * st],      q[1 * SX + 3 * st], q[2 * SX + 2 * st],  q[3 * SX + 1 * st],
+                                q[3 * SX],      q[3 * SX - 1 * st], q[2 * SX - 2 * st],  q[1 * SX - 3 * st],
+                                q[-3 * st],     q[-1 * SX - 3 * st], q[-2 * SX - 2 * st], q[-3 * SX - 1 * st],
+                                q[-3 * SX],     q[-3 * SX + 1 * st], q[-2 * SX + 2 * st], q[-1 * SX + 3 * st]};
+#pragma unroll
+        for (int k = 0; k < 8; k++) w[k] = __builtin_bit_cast(uint32_t, og_h2{c[k], c[k + 8]});
+        vc = __builtin_bit_cast(uint16_t, q[0]);
+    }
     const og_h2 sg = {sgn, sgn};
     og_h2 P[8];
 #pragma unroll
@@ -2934,6 +3036,20 @@ hipError_t og_read_oct_prof(unsigned long long* out, int n)
     (void)n;
     return hipErrorNotSupported;
 #endif
+}
+
+void og_launch_resize_rows(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,
+                           long long dst_pitch, long long dst_fstride, int sw, int sh, int dw, int dh, const int4* xtab,
+                           const int4* ytab, int xmax, int B, int sem)
+{
+    const int runs = (dh + RS_ROWS - 1) / RS_ROWS;
+    dim3 grid((dw + 255) / 256, (runs + RS_NT / 64 - 1) / (RS_NT / 64), B);
+    if (sem & ORBGPU_SEM_RESIZE_FIXEDPT)
+        hipLaunchKernelGGL(og_resize_rows_kernel<true>, grid, dim3(RS_NT), 0, s, src, src_pitch, src_fstride, dst,
+                           dst_pitch, dst_fstride, sw, sh, dw, dh, xtab, ytab, xmax);
+    else
+        hipLaunchKernelGGL(og_resize_rows_kernel<false>, grid, dim3(RS_NT), 0, s, src, src_pitch, src_fstride, dst,
+                           dst_pitch, dst_fstride, sw, sh, dw, dh, xtab, ytab, xmax);
 }
 
 void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,

@@ -571,6 +571,22 @@ static const orbgpu_kp_dev* kps_match(const orbgpu_ctx* c) { return c->undist ? 
 static void launch_pyramid(orbgpu_ctx* c, hipStream_t s, const uint8_t* d_imgs, int B, long long pitch, long long fstride)
 {
     const OgPlan& P = c->plan;
+    static const int rows_mode = [] {  // ORBGPU_PYR_ROWS=1: every level by the row-stream kernel (A/B switch)
+        const char* e = std::getenv("ORBGPU_PYR_ROWS");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (rows_mode) {
+        for (int l = 1; l < P.nlevels; l++) {
+            const OgLevel& L = P.lv[l];
+            const OgLevel& Lp = P.lv[l - 1];
+            const uint8_t* src = l == 1 ? d_imgs : c->pyr.p + Lp.pyr_off;
+            const long long sp = l == 1 ? pitch : Lp.pitch;
+            const long long sfs = l == 1 ? fstride : P.pyr_per_frame;
+            og_launch_resize_rows(s, src, sp, sfs, c->pyr.p + L.pyr_off, L.pitch, P.pyr_per_frame, Lp.w, Lp.h, L.w, L.h,
+                                  c->tabs.p + L.xtab_off, c->tabs.p + L.ytab_off, L.xmax, B, P.sem);
+        }
+        return;
+    }
     for (int l = 1; l < P.nlevels;) {
         const OgLevel& L = P.lv[l];
         const OgLevel& Lp = P.lv[l - 1];

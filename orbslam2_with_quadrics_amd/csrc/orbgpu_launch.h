@@ -19,6 +19,10 @@ hipError_t og_upload_pattern(int device);
 hipError_t og_math_hash(int fn, unsigned long long begin, unsigned long long end, int chunk_log2,
                         unsigned long long* d_out, hipStream_t s);
 
+// one level as a row stream (og_resize_rows_kernel): strips of 256 columns x runs of 32 rows, no LDS
+void og_launch_resize_rows(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,
+                           long long dst_pitch, long long dst_fstride, int sw, int sh, int dw, int dh, const int4* xtab,
+                           const int4* ytab, int xmax, int B, int sem);
 // two chained levels per launch (og_resize2_kernel): A = level l from S = level l-1, B = level l+1 from A
 struct OgRz2Geom {
     int sw, sh, aw, ah, bw, bh;
