@@ -382,6 +382,10 @@ int orbgpu_compute_stereo_matches_batch(orbgpu_ctx* left, orbgpu_ctx* right, flo
  * sizes of the octree workgroup of (frame 0, level 0) of the last batch.  ORBGPU_ERR_UNSUPPORTED in the
  * product build. */
 int orbgpu_debug_octree_profile(orbgpu_ctx* ctx, unsigned long long* out, int n);
+/* Diagnostic builds only (OG_FAST_PROFILE=1, tools/fast_profile.py): per-phase s_memtime clocks of every FAST block
+ * of the middle frame of the last launch, 8 per block (ROI, stage 1-3, counts, reservation, end, survivors | level
+ * << 32).  ORBGPU_ERR_UNSUPPORTED in product builds. */
+int orbgpu_debug_fast_profile(orbgpu_ctx* ctx, unsigned long long* out, int n);
 /* Exhaustive pin of the device restatements of glibc sincosf (fn 0; src/ORBextractor.cc:113) and logf (fn 1;
  * src/MapPoint.cc:410): every float bit pattern u in [begin, end) is evaluated on `device` and folded into
  * out[(u >> chunk_log2) - (begin >> chunk_log2)] (nchunks entries) as the order-free hash of

@@ -912,6 +912,21 @@ __device__ __forceinline__ void og_fastq_roi_put(const OgFB& b, int tid, const u
     }
 }
 
+#ifndef OG_FAST_PROFILE
+#define OG_FAST_PROFILE 0
+#endif
+#if OG_FAST_PROFILE  // diagnostic builds only (tools/fast_profile.py): per-phase clocks of every block of the middle frame
+__device__ unsigned long long og_fast_prof[4096 * 8];
+#define FAST_PROF(slot)                                                                                         \
+    do {                                                                                                        \
+        if (tid == 0 && f == gridDim.y / 2 && p < 4096) og_fast_prof[p * 8 + (slot)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define FAST_PROF(slot) \
+    do {                \
+    } while (0)
+#endif
+
 // One block per workgroup.  Stage 1: quick test of every detection pixel and a survivor list; stage 2: exact scores
 // into the score map; stage 3: same-cell NMS at both thresholds and per-cell counts; stage 4: the reference's
 // per-cell 20 -> 7 fallback, one global reservation per block and the candidate stores.
@@ -939,6 +954,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const uint32_t a_ns = og_lds_addr(&sh_ns), a_lst = og_lds_addr(&lst[0]);
     const OgFB b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
     if (b.l < 0) return;
+    FAST_PROF(0);
     {
         uint32_t sroi[2][4];
         og_fastq_roi_load(b, tid, sroi);
@@ -951,6 +967,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     }
     if (tid == 0) sh_ns = 0;
     __syncthreads();
+    FAST_PROF(1);
     const int dw = b.dw, dh = b.dh, wC = b.wC, hC = b.hC;
     const uint2* Tq = roiq + b.mis;  // Tq[r * FQ_S + x] = quad (x, x + 16, x + 32, x + 48) of ROI row r
     // ---- stage 1: quick test on every detection pixel, four per lane.  Unit u = (row group g = u >> 1, half
@@ -1053,6 +1070,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     }
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm list stores are not tracked by the compiler
     __syncthreads();
+    FAST_PROF(2);
     const int ns = sh_ns;
     // ---- stage 2: exact M for every survivor; single pixels are u16 reads of the quad layout (element step 4)
     const uint16_t* T16 = (const uint16_t*)Tq;
@@ -1078,6 +1096,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)M;
     }
     __syncthreads();
+    FAST_PROF(3);
     // ---- stage 3: same-cell 3x3 NMS at both thresholds; each wave walks every 8th 64-entry chunk of the list
     int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
     for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
@@ -1109,6 +1128,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
     }
     __syncthreads();
+    FAST_PROF(4);
     // per cell: iniThFAST unless the cell is empty at it (src/ORBextractor.cc:809-816)
     const int qw = (lane >> 2) & (FB_NW - 1), qc = lane & 3;
     const int v1 = wk[qw][qc], v2 = wk[qw][4 + qc];
@@ -1138,6 +1158,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         __syncthreads();
         sb = sh_base;
     }
+    FAST_PROF(5);
     const bool emit = total != 0 && sb + total <= b.cand_cap && kept != 0;
     u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb + before);
     int run = 0;
@@ -1152,6 +1173,22 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         if (e < ns && emit && kbit) out[og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, Ms[og_ms_idx(i, j, wC, hC)] - 1);
         run += __popcll(mask);
     }
+#if OG_FAST_PROFILE
+    __builtin_amdgcn_s_waitcnt(0);  // the candidate stores issued
+    FAST_PROF(6);
+    if (tid == 0 && f == gridDim.y / 2 && p < 4096) og_fast_prof[p * 8 + 7] = (unsigned long long)ns | ((unsigned long long)b.l << 32);
+#endif
+}
+
+hipError_t og_read_fast_prof(unsigned long long* out, int n)
+{
+#if OG_FAST_PROFILE
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(og_fast_prof), sizeof(unsigned long long) * (size_t)std::min(n, 4096 * 8));
+#else
+    (void)out;
+    (void)n;
+    return hipErrorNotSupported;
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -2229,6 +2229,17 @@ int orbgpu_debug_octree_profile(orbgpu_ctx* c, unsigned long long* out, int n)
     return ORBGPU_OK;
 }
 
+int orbgpu_debug_fast_profile(orbgpu_ctx* c, unsigned long long* out, int n)
+{
+    if (!c || !out || n <= 0) return ORBGPU_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const hipError_t e = og_read_fast_prof(out, n);
+    if (e == hipErrorNotSupported) return ORBGPU_ERR_UNSUPPORTED;
+    HIP_TRY(c, e);
+    return ORBGPU_OK;
+}
+
 void* orbgpu_stream(orbgpu_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int orbgpu_synchronize(orbgpu_ctx* c)

@@ -59,6 +59,7 @@ hipError_t og_prepare_device_bow();
 void og_launch_fast(hipStream_t s, const OgPlan& P, const OgFastBlk* blocks, int nblocks, const uint8_t* img0,
                     long long pitch0, long long fstride0, const uint8_t* pyr, unsigned long long* cand, int* cand_count,
                     int* status, int B);
+hipError_t og_read_fast_prof(unsigned long long* out, int n);  // OG_FAST_PROFILE builds only
 hipError_t og_read_oct_prof(unsigned long long* out, int n);  // OG_OCT_PROFILE builds only
 // ORBGPU_SEM_SCORE_HARRIS option: rewrite the response key of each candidate of levels [lb, le) with its Harris key
 void og_launch_harris(hipStream_t s, const OgPlan& P, int lb, int le, const uint8_t* img0, long long pitch0,
