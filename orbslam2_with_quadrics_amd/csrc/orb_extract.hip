@@ -912,6 +912,66 @@ __device__ __forceinline__ void og_fastq_roi_put(const OgFB& b, int tid, const u
     }
 }
 
+// KB > 1 with OG_FASTQ_DMA: the next block's ROI goes HBM -> LDS by LDS-DMA (global_load_lds_dword, no VGPR
+// destination) into roiq, free from the end of stage 2: wave w stages the rows it converts itself (ROI rows 8w .. 8w + 7
+// and 64 + 8w .. 64 + 8w + 7), FQ_RS dwords per row from the row's 4-byte-aligned start, lane-linear (local row lr at
+// dword lr * FQ_RS of the wave's 16 * FQ_RS-dword slice).  Before the emission the wave waits for its own DMA and reads
+// its rows into the registers og_fastq_roi_put converts (og_fastq_raw_get); the raw slices are 10 KB of roiq's 19 KB.
+#ifndef OG_FASTQ_DMA
+#define OG_FASTQ_DMA 0
+#endif
+#define FQ_RS 20  // dwords per staged row: the quads read bytes <= 4 * 6 + 48 + 3 (+ 3 misalignment) of a row
+__device__ __forceinline__ void og_fastq_roi_dma(const OgFB& b, int wv, int lane, uint32_t* raw)
+{
+    typedef __attribute__((address_space(3))) void lds_void;
+    typedef __attribute__((address_space(1))) const void glb_void;
+    const uint8_t* rbase = b.row0 - b.mis;
+    // (the lane's row/dword split is recomputed here, not hoisted out of the block loop into spilled registers)
+    __asm__ volatile("" : "+v"(lane));
+#pragma unroll
+    for (int j = 0; j < 16 * FQ_RS / 64; j++) {
+        const int lr0 = (64 * j) / FQ_RS;  // the instruction's first local row (uniform)
+        if ((lr0 < 8 ? 8 * wv + lr0 : 56 + 8 * wv + lr0) >= b.rh) continue;
+        const int t = 64 * j + lane;
+        const int lr = (t * 3277) >> 16;  // t / 20 for t < 320
+        const int d = t - FQ_RS * lr;
+        const int r = min(lr < 8 ? 8 * wv + lr : 56 + 8 * wv + lr, b.rh - 1);  // rows past the ROI re-read its last row
+        const uintptr_t ra = (uintptr_t)rbase + (unsigned)r * b.upitch;
+        const uint8_t* a = (const uint8_t*)((ra & ~(uintptr_t)3) + 4u * (unsigned)d);
+        __builtin_amdgcn_global_load_lds((glb_void*)a, (lds_void*)(raw + wv * 16 * FQ_RS + 64 * j), 4, 0, 0);
+    }
+}
+// the wave's own staged rows -> og_fastq_roi_load's registers (the caller has waited for the wave's DMA)
+__device__ __forceinline__ void og_fastq_raw_get(const OgFB& b, int wv, int lane, const uint32_t* raw, uint32_t (&s)[2][4])
+{
+    const int nq4 = (16 + 6 + b.mis + 3) >> 2;
+    const int q4 = min(lane & 7, nq4 - 1);
+    const uint8_t* rbase = b.row0 - b.mis;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int lr = (lane >> 3) + 8 * k;
+        const int r = min(8 * wv + (lane >> 3) + 64 * k, b.rh - 1);
+        const uint32_t* R = raw + wv * 16 * FQ_RS + lr * FQ_RS + q4;
+        if (b.aligned) {
+#pragma unroll
+            for (int g = 0; g < 4; g++) s[k][g] = R[4 * g];
+        } else {
+            const unsigned sh = (unsigned)(((uintptr_t)rbase + (unsigned)r * b.upitch) & 3u);
+#pragma unroll
+            for (int g = 0; g < 4; g++) s[k][g] = __builtin_amdgcn_alignbyte(R[4 * g + 1], R[4 * g], sh);
+        }
+    }
+}
+// a workgroup barrier for LDS data only: with an LDS-DMA in flight __syncthreads() would wait for it (vmcnt(0))
+__device__ __forceinline__ void og_fastq_sync()
+{
+#if OG_FASTQ_DMA
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+    __syncthreads();
+#endif
+}
+
 #ifndef OG_FAST_PROFILE
 #define OG_FAST_PROFILE 0
 #endif
@@ -930,6 +990,7 @@ __device__ unsigned long long og_fast_prof[4096 * 8];
 // One block per workgroup.  Stage 1: quick test of every detection pixel and a survivor list; stage 2: exact scores
 // into the score map; stage 3: same-cell NMS at both thresholds and per-cell counts; stage 4: the reference's
 // per-cell 20 -> 7 fallback, one global reservation per block and the candidate stores.
+template <int KB>
 __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_fast_quad_kernel(
     const OgFastBlk* __restrict__ blocks, int nb, const uint8_t* __restrict__ img0, long long pitch0, long long fstride0,
     const uint8_t* __restrict__ pyr, long long pyr_per_frame, u64* __restrict__ cand, long long cand_per_frame,
@@ -944,30 +1005,39 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     __shared__ int sh_base;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);
-    const unsigned f = blockIdx.y;  // grid (blocks per frame, frames), plan order
-    const int p = blockIdx.x;
-    if (p >= nb) return;
+    const unsigned f = blockIdx.y;  // grid (workgroups per frame, frames)
     const int t1 = thr & 255, t2 = (thr >> 8) & 255;  // clamped to [0, 255] on the host
     const int tq = min(t1, t2);
     const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
     const int tA = max(t1, 1), tB = max(t2, 1);
     const uint32_t a_ns = og_lds_addr(&sh_ns), a_lst = og_lds_addr(&lst[0]);
-    const OgFB b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
-    if (b.l < 0) return;
-    FAST_PROF(0);
-    {
-        uint32_t sroi[2][4];
-        og_fastq_roi_load(b, tid, sroi);
-        og_fastq_roi_put(b, tid, sroi, roiq);
+    // KB > 1: workgroup x takes the valid blocks among x, x + G, ..., x + (KB - 1) G (G = gridDim.x, a multiple of 8:
+    // every block keeps the XCD of block x, og_launch_fast); the next block's ROI is loaded into registers during
+    // stage 2 and stored once stage 2 is done with roiq, so only the first block of a workgroup waits for its ROI
+    int j = 0, p = 0;
+    OgFB b;
+    for (;; j++) {  // uniform: the first valid block of the chain (the table pads each level to 8 entries)
+        if (j >= KB) return;
+        p = (int)blockIdx.x + j * (int)gridDim.x;
+        if (p >= nb) return;
+        b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
+        if (b.l >= 0) break;
     }
+    FAST_PROF(0);
+    uint32_t sroi[2][4];
+    og_fastq_roi_load(b, tid, sroi);
+    og_fastq_roi_put(b, tid, sroi, roiq);
     {
-        // zero only the score-map rows the block reads (dh + 3: gap rows included)
-        const int msz = min(FB_MSZ, ((b.dh + 3) * FB_MSW + 15) & ~15);
+        // zero only the score-map rows the block reads (dh + 3: gap rows included); later blocks of the workgroup find
+        // it zero again (the emission clears every cell stage 2 wrote), so they zero nothing
+        const int msz = KB == 1 ? min(FB_MSZ, ((b.dh + 3) * FB_MSW + 15) & ~15) : FB_MSZ;
         for (int idx = tid * 16; idx < msz; idx += FB_NT * 16) *(uint4*)&Ms[idx] = make_uint4(0u, 0u, 0u, 0u);
     }
     if (tid == 0) sh_ns = 0;
     __syncthreads();
     FAST_PROF(1);
+#pragma unroll 1
+    for (;;) {
     const int dw = b.dw, dh = b.dh, wC = b.wC, hC = b.hC;
     const uint2* Tq = roiq + b.mis;  // Tq[r * FQ_S + x] = quad (x, x + 16, x + 32, x + 48) of ROI row r
     // ---- stage 1: quick test on every detection pixel, four per lane.  Unit u = (row group g = u >> 1, half
@@ -1097,6 +1167,28 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     }
     __syncthreads();
     FAST_PROF(3);
+    // the next valid block of the chain: its ROI loads are in flight during stages 3-4 and land in roiq (free since
+    // stage 2) at the end of the emission
+    OgFB bn = b;
+    int pn = p;
+    bool has_next = false;
+    if (KB > 1) {
+        for (j++; j < KB; j++) {  // uniform
+            pn = (int)blockIdx.x + j * (int)gridDim.x;
+            if (pn >= nb) break;
+            bn = og_fast_decode(blocks, pn, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
+            if (bn.l >= 0) {
+                has_next = true;
+                break;
+            }
+        }
+        if (has_next) {
+            if (OG_FASTQ_DMA)
+                og_fastq_roi_dma(bn, wvu, lane, (uint32_t*)roiq);
+            else
+                og_fastq_roi_load(bn, tid, sroi);
+        }
+    }
     // ---- stage 3: same-cell 3x3 NMS at both thresholds; each wave walks every 8th 64-entry chunk of the list
     int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
     for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
@@ -1127,7 +1219,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             wk[wv][4 + cc] = c2[cc];
         }
     }
-    __syncthreads();
+    og_fastq_sync();
     FAST_PROF(4);
     // per cell: iniThFAST unless the cell is empty at it (src/ORBextractor.cc:809-816)
     const int qw = (lane >> 2) & (FB_NW - 1), qc = lane & 3;
@@ -1155,10 +1247,14 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             if (bb + total > b.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
             sh_base = bb;
         }
-        __syncthreads();
+        og_fastq_sync();
         sb = sh_base;
     }
     FAST_PROF(5);
+    if (OG_FASTQ_DMA && has_next) {  // the wave's own staged rows of the next block, landed during stages 3-4
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        og_fastq_raw_get(bn, wvu, lane, (const uint32_t*)roiq, sroi);
+    }
     const bool emit = total != 0 && sb + total <= b.cand_cap && kept != 0;
     u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb + before);
     int run = 0;
@@ -1170,7 +1266,11 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const int cell = (i >= hC) * 2 + (j >= wC);
         const unsigned kbit = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
         const u64 mask = og_lanes_ne(kbit, 0u);
-        if (e < ns && emit && kbit) out[og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, Ms[og_ms_idx(i, j, wC, hC)] - 1);
+        if (e < ns) {
+            uint8_t* mcell = &Ms[og_ms_idx(i, j, wC, hC)];
+            if (emit && kbit) out[og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, *mcell - 1);
+            if (KB > 1) *mcell = 0;  // the next block of this workgroup starts from a clean score map
+        }
         run += __popcll(mask);
     }
 #if OG_FAST_PROFILE
@@ -1178,6 +1278,15 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     FAST_PROF(6);
     if (tid == 0 && f == gridDim.y / 2 && p < 4096) og_fast_prof[p * 8 + 7] = (unsigned long long)ns | ((unsigned long long)b.l << 32);
 #endif
+    if (!has_next) break;
+    if (tid == 0) sh_ns = 0;
+    if (OG_FASTQ_DMA) og_fastq_sync();  // every wave has read its staged rows before the quads overwrite them
+    og_fastq_roi_put(bn, tid, sroi, roiq);
+    b = bn;
+    p = pn;
+    __syncthreads();  // score map back to zero, list consumed, next ROI stored
+    FAST_PROF(1);
+    }
 }
 
 hipError_t og_read_fast_prof(unsigned long long* out, int n)
@@ -3136,8 +3245,13 @@ void og_launch_fast(hipStream_t s, const OgPlan& P, const OgFastBlk* blocks, int
 {
     if (nblocks <= 0 || B <= 0) return;
     const int thr = std::min(std::max(P.iniTh, 0), 255) | (std::min(std::max(P.minTh, 0), 255) << 8);
-    hipLaunchKernelGGL(og_fast_quad_kernel, dim3(nblocks, B), dim3(FB_NT), 0, s, blocks, nblocks, img0, pitch0, fstride0,
-                       pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels, thr, status);
+#ifndef OG_FASTQ_KB
+#define OG_FASTQ_KB 1
+#endif
+    // KB blocks per workgroup (og_fast_quad_kernel): G workgroups per frame, a multiple of 8
+    const int G = OG_FASTQ_KB == 1 ? nblocks : ((nblocks + OG_FASTQ_KB - 1) / OG_FASTQ_KB + 7) & ~7;
+    hipLaunchKernelGGL(og_fast_quad_kernel<OG_FASTQ_KB>, dim3(G, B), dim3(FB_NT), 0, s, blocks, nblocks, img0, pitch0,
+                       fstride0, pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels, thr, status);
 }
 
 void og_launch_harris(hipStream_t s, const OgPlan& P, int lb, int le, const uint8_t* img0, long long pitch0,

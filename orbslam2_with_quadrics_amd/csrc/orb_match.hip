@@ -501,8 +501,39 @@ void og_launch_prev_from_frame(hipStream_t s, OgFrameDev F1, int ref, float* pre
 // order) after the static filters of SearchByProjection (levels, window, stereo check, src/ORBmatcher.cc:53-104),
 // with their Hamming distances; the dynamic filter (claims, :87-89) is applied by the caller.  visit(idx, dist,
 // octave) is called in order for every candidate with dist <= dkeep (og_proj_keep_bound).
-template <class Visit>
-__device__ __forceinline__ void og_proj_visit(const OgFrameDev& F, const OgGridGeom& G, const float* sf,
+// Keypoint geometry as the enumeration reads it: straight from the frame's arrays in HBM ...
+struct OgGeomGlobal {
+    const OgFrameDev& F;
+    __device__ int cs(int c) const { return F.cell_start[c]; }
+    __device__ int item(int j) const { return F.cell_items[j]; }
+    __device__ float x(int i) const { return F.kps[i].x; }
+    __device__ float y(int i) const { return F.kps[i].y; }
+    __device__ int oct(int i) const { return F.kps[i].octave; }
+    __device__ bool has_ur() const { return F.uright != nullptr; }
+    __device__ float ur(int i) const { return F.uright[i]; }
+};
+// ... or from the frame's copy in LDS (og_projb_fill_kernel)
+struct OgGeomLds {
+    const int* CS;
+    const uint16_t* CI;
+    const float2* XY;
+    const uint8_t* OC;
+    const float* UR;  // nullptr without mvuRight
+    __device__ int cs(int c) const { return CS[c]; }
+    __device__ int item(int j) const { return CI[j]; }
+    __device__ float x(int i) const { return XY[i].x; }
+    __device__ float y(int i) const { return XY[i].y; }
+    __device__ int oct(int i) const { return OC[i]; }
+    __device__ bool has_ur() const { return UR != nullptr; }
+    __device__ float ur(int i) const { return UR[i]; }
+};
+
+// Candidates of map point m in GetFeaturesInArea order (src/Frame.cc:327-380: cells ix-major, then iy, then cell
+// order) after the static filters of SearchByProjection (levels, window, stereo check, src/ORBmatcher.cc:53-104),
+// with their Hamming distances (descriptors from HBM); the dynamic filter (claims, :87-89) is applied by the caller.
+// visit(idx, dist, octave) is called in order for every candidate with dist <= dkeep (og_proj_keep_bound).
+template <class Geom, class Visit>
+__device__ __forceinline__ void og_proj_visit(const Geom& K, const uint8_t* fdesc, const OgGridGeom& G, const float* sf,
                                               const OgMapPointsDev& mp, int m, float th, int dkeep, Visit visit)
 {
     if (!mp.track_in_view[m] || mp.is_bad[m]) return;
@@ -520,23 +551,22 @@ __device__ __forceinline__ void og_proj_visit(const OgFrameDev& F, const OgGridG
     for (int ix = cr.x0; ix <= cr.x1; ix++)
         for (int iy = cr.y0; iy <= cr.y1; iy++) {
             const int cell = ix * OG_GRID_ROWS + iy;
-            for (int j = F.cell_start[cell]; j < F.cell_start[cell + 1]; j++) {
-                const int idx = F.cell_items[j];
-                const orbgpu_kp_dev* kp = F.kps + idx;
-                const float kx = kp->x, ky = kp->y;
-                const int oct = kp->octave;
+            const int je = K.cs(cell + 1);
+            for (int j = K.cs(cell); j < je; j++) {
+                const int idx = K.item(j);
+                const int oct = K.oct(idx);
                 if (bCheckLevels) {
                     if (oct < minLevel) continue;
                     if (maxLevel >= 0 && oct > maxLevel) continue;
                 }
-                const float distx = kx - x, disty = ky - y;
+                const float distx = K.x(idx) - x, disty = K.y(idx) - y;
                 if (!(fabsf(distx) < R && fabsf(disty) < R)) continue;
-                if (F.uright && F.uright[idx] > 0) {
-                    const float er = fabsf(mp.proj_xr[m] - F.uright[idx]);
+                if (K.has_ur() && K.ur(idx) > 0) {
+                    const float er = fabsf(mp.proj_xr[m] - K.ur(idx));
                     if (er > r * sf[lvl]) continue;
                 }
                 uint4 ea, eb;
-                og_load_desc(F.desc + (long long)idx * 32, ea, eb);
+                og_load_desc(fdesc + (long long)idx * 32, ea, eb);
                 const int dist = og_hamming(da, db, ea, eb);
                 if (dist > dkeep) continue;  // og_proj_keep_bound
                 visit(idx, dist, oct);
@@ -628,22 +658,60 @@ __device__ __forceinline__ OgMapPointsDev og_mp_of(const OgMapPointsDev& mp, int
     return q;
 }
 
-// ---- one enumeration pass: thread per (frame, point).  The first OG_PJ_K kept candidates go to the point's slots,
-// stored k-major (slot k of points m, m + 1, ... adjacent: the threads of a wave write neighbouring dwords);
-// kept[] = the point's full kept count (> OG_PJ_K: the resolve re-enumerates that point itself).
-__global__ __launch_bounds__(256) void og_projb_fill_kernel(OgFrameDev F, OgGridGeom G, const float* sf,
-                                                            OgMapPointsDev mp, int stride, float th, int dkeep,
-                                                            uint32_t* __restrict__ slots, int* __restrict__ kept)
+// ---- one enumeration pass.  A workgroup of PF_NT threads takes every PF_WG-th block of PF_NT map points of one
+// frame; it first copies the frame's keypoint geometry (x, y, octave, mvuRight) and grid into LDS with coalesced
+// loads, so the window enumeration reads LDS and only the candidates' descriptors come from HBM.  The first OG_PJ_K
+// kept candidates of a point go to its slots, stored k-major (slot k of points m, m + 1, ... adjacent); kept[] = the
+// point's full kept count (> OG_PJ_K: the resolve re-enumerates that point itself).  Frames whose geometry does not
+// fit the LDS take the same enumeration from HBM.
+#define PF_NT 512
+#define PF_WG 4  // workgroups per frame
+__host__ __device__ inline size_t og_projb_fill_lds(int frame_cap, bool ur)
 {
-    const int b = blockIdx.y, m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= mp.m) return;
-    uint32_t* S = slots + (long long)b * OG_PJ_K * stride + m;
-    int n = 0;
-    og_proj_visit(og_frame_of(F, b), G, sf, og_mp_of(mp, b, stride), m, th, dkeep, [&](int idx, int dist, int oct) {
-        if (n < OG_PJ_K) S[(long long)n * stride] = og_pj_pack(idx, dist, oct);
-        n++;
-    });
-    kept[(long long)b * stride + m] = n;
+    return (size_t)(OG_GRID_CELLS + 1) * 4 + (size_t)frame_cap * (8 + 1 + 2 + (ur ? 4 : 0)) + 16;
+}
+
+__global__ __launch_bounds__(PF_NT) void og_projb_fill_kernel(OgFrameDev Fb, OgGridGeom G, const float* sf,
+                                                              OgMapPointsDev mp, int stride, float th, int dkeep,
+                                                              int use_lds, uint32_t* __restrict__ slots,
+                                                              int* __restrict__ kept)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t pf_lds[];
+    const int b = blockIdx.y, tid = threadIdx.x;
+    const OgFrameDev F = og_frame_of(Fb, b);
+    const OgMapPointsDev q = og_mp_of(mp, b, stride);
+    uint32_t* S = slots + (long long)b * OG_PJ_K * stride;
+    int* KEPT = kept + (long long)b * stride;
+    auto run = [&](const auto& K) {
+        for (int m = blockIdx.x * PF_NT + tid; m < q.m; m += PF_WG * PF_NT) {
+            int n = 0;
+            og_proj_visit(K, F.desc, G, sf, q, m, th, dkeep, [&](int idx, int dist, int oct) {
+                if (n < OG_PJ_K) S[(long long)n * stride + m] = og_pj_pack(idx, dist, oct);
+                n++;
+            });
+            KEPT[m] = n;
+        }
+    };
+    if (!use_lds) {  // uniform (host decision from frame_cap)
+        run(OgGeomGlobal{F});
+        return;
+    }
+    const int n = min(F.counts[0], F.frame_cap);
+    int* CS = (int*)pf_lds;
+    float2* XY = (float2*)(CS + OG_GRID_CELLS + 1);
+    float* UR = (float*)(XY + F.frame_cap);
+    uint16_t* CI = (uint16_t*)(UR + (F.uright ? F.frame_cap : 0));
+    uint8_t* OC = (uint8_t*)(CI + F.frame_cap);
+    for (int c = tid; c <= OG_GRID_CELLS; c += PF_NT) CS[c] = F.cell_start[c];
+    for (int i = tid; i < n; i += PF_NT) {
+        const orbgpu_kp_dev* kp = F.kps + i;
+        XY[i] = make_float2(kp->x, kp->y);
+        OC[i] = (uint8_t)kp->octave;
+        CI[i] = (uint16_t)F.cell_items[i];
+        if (F.uright) UR[i] = F.uright[i];
+    }
+    __syncthreads();
+    run(OgGeomLds{CS, CI, XY, OC, F.uright ? UR : nullptr});
 }
 
 // The reference's ordered loop over map points (src/ORBmatcher.cc:53-129) couples points only through the
@@ -774,7 +842,7 @@ __global__ __launch_bounds__(PJ_NT) void og_projb_resolve_kernel(OgFrameDev Fb, 
             };
             const int nc = KEPT[m];
             if (nc > OG_PJ_K) {
-                og_proj_visit(F, G, sf, q, m, th, dkeep, take);
+                og_proj_visit(OgGeomGlobal{F}, F.desc, G, sf, q, m, th, dkeep, take);
             } else if (staged) {
                 const uint32_t* L = LST + PO[m];
                 for (int c = 0; c < nc; c++) {
@@ -843,9 +911,13 @@ void og_launch_projb(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf,
 {
     if (B <= 0) return;
     const int dkeep = og_proj_keep_bound(nnratio);
-    if (mp.m > 0)
-        hipLaunchKernelGGL(og_projb_fill_kernel, dim3((mp.m + 255) / 256, B), dim3(256), 0, s, F, G, sf, mp, stride, th,
-                           dkeep, slots, kept);
+    if (mp.m > 0) {
+        // cell items are u16 in LDS: frames of at most 65535 keypoints (the host form checks far less)
+        const size_t lds = og_projb_fill_lds(F.frame_cap, F.uright != nullptr);
+        const int use_lds = lds <= OG_PJ_LDS && F.frame_cap <= 65535;
+        hipLaunchKernelGGL(og_projb_fill_kernel, dim3(PF_WG, B), dim3(PF_NT), use_lds ? lds : 0, s, F, G, sf, mp, stride,
+                           th, dkeep, use_lds, slots, kept);
+    }
     hipLaunchKernelGGL(og_projb_resolve_kernel, dim3(B), dim3(PJ_NT), OG_PJ_LDS, s, F, G, sf, mp, stride, th, dkeep,
                        slots, kept, nnratio, (int)OG_PJ_LDS, owner, owner_obs, nmatches, res, status);
 }
@@ -1260,6 +1332,7 @@ hipError_t og_prepare_device_match()
     hipError_t e = hipFuncSetAttribute((const void*)og_init_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        OG_INIT_LDS_MAX);
     if (e != hipSuccess) return e;
-    return hipFuncSetAttribute((const void*)og_projb_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               OG_PJ_LDS);
+    e = hipFuncSetAttribute((const void*)og_projb_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, OG_PJ_LDS);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)og_projb_fill_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, OG_PJ_LDS);
 }

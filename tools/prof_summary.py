@@ -29,7 +29,8 @@ def main():
             batch = gz // max(wz, 1)
         elif k.startswith("og_octree"):  # level-major 1-D grid: 8 levels x B frames (the single-frame fork splits
             batch = max(1, round(gx // max(wx, 1) / 8))  # level 0 from levels 1-7: 1 and 7 workgroups, one frame)
-        elif k.startswith(("og_search_init", "og_grid", "og_init_resolve")):
+        elif k.startswith(("og_search_init", "og_grid", "og_init_resolve", "og_projb_resolve", "og_stereo_rows",
+                            "og_stereo_filter")):
             batch = gx // max(wx, 1)
         else:
             batch = gy // max(wy, 1)
