@@ -1093,6 +1093,20 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                 rows = (R < dh ? 0xffffull : 0ull) | (R + 4 < dh ? 0xffff0000ull : 0ull) |
                        (R + 1 < dh ? 0xffff00000000ull : 0ull) | (R + 5 < dh ? 0xffff000000000000ull : 0ull);
             }
+#if defined(OG_PROBE_SALU) && OG_PROBE_SALU > 0  // sensitivity probe (measurement builds only): dead SALU work
+            {
+                unsigned pz = (unsigned)u;
+#pragma unroll
+                for (int z = 0; z < OG_PROBE_SALU; z++) __asm__ volatile("s_add_u32 %0, %0, 1" : "+s"(pz) : : "scc");
+            }
+#endif
+#if defined(OG_PROBE_VALU) && OG_PROBE_VALU > 0  // sensitivity probe (measurement builds only): dead VALU work
+            {
+                unsigned pz = (unsigned)lane;
+#pragma unroll
+                for (int z = 0; z < OG_PROBE_VALU; z++) __asm__ volatile("v_add_u32 %0, %0, 1" : "+v"(pz));
+            }
+#endif
             const uint32_t a0 = r0.x | r0.y, a1 = r1.x | r1.y;
             const u64 m[4] = {og_lanes_lo16_nz(a0) & rows & col0, og_lanes_gt((int)a0, 0xffff) & rows & col1,
                               og_lanes_lo16_nz(a1) & rows & col2, og_lanes_gt((int)a1, 0xffff) & rows & col3};
@@ -1241,6 +1255,48 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const int before = __builtin_amdgcn_readlane(sc, wvu) - kept;
     // ---- stage 4: one reservation per block; each wave writes its kept entries at its offset
     int sb = 0;
+#ifndef OG_FASTQ_LDSOUT
+#define OG_FASTQ_LDSOUT 0  // 1: emission into LDS while the reservation atomic is in flight, then one coalesced copy
+                           // (bit-exact, FAST +1.5 %: profiles/sweeps/r04_ab_fast_lds_emission.txt)
+#endif
+    // (block-uniform) the kept entries fit roiq, free since stage 2 (the DMA prefetch variant keeps it busy)
+    const bool lds_out = OG_FASTQ_LDSOUT && !OG_FASTQ_DMA && total <= FQ_ROWS * FQ_S;
+    if (lds_out) {
+        // the device-scope atomic's round trip (~10 % of a block's time when waited for at once) overlaps the
+        // emission: entries go to LDS at the wave's offset + rank, the base is read after the emission, and the block's
+        // candidates leave in one coalesced copy
+        int bb = 0;
+        if (total != 0 && tid == 0) bb = atomicAdd(&cand_count[f * nlevels + b.l], total);
+        u64* st = (u64*)roiq;
+        int run = 0;
+        for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
+            const int e = e0 + lane;
+            int ent = 0;
+            if (e < ns) ent = lst[e];
+            const int i = (ent >> 7) & 127, j = ent & 127;
+            const int cell = (i >= hC) * 2 + (j >= wC);
+            const unsigned kbit = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
+            const u64 mask = og_lanes_ne(kbit, 0u);
+            if (e < ns) {
+                uint8_t* mcell = &Ms[og_ms_idx(i, j, wC, hC)];
+                if (kbit) st[before + og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, *mcell - 1);
+                if (KB > 1) *mcell = 0;  // the next block of this workgroup starts from a clean score map
+            }
+            run += __popcll(mask);
+        }
+        if (tid == 0) {
+            if (total != 0 && bb + total > b.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
+            sh_base = bb;
+        }
+        __syncthreads();
+        FAST_PROF(5);
+        sb = sh_base;
+        if (total != 0 && sb + total <= b.cand_cap) {
+            u64* o = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb);
+            for (int k = tid; k < total; k += FB_NT) o[k] = st[k];
+        }
+        if (KB > 1) __syncthreads();  // the staged entries are read before the next ROI overwrites roiq
+    } else {
     if (total != 0) {  // block-uniform
         if (tid == 0) {
             const int bb = atomicAdd(&cand_count[f * nlevels + b.l], total);
@@ -1272,6 +1328,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             if (KB > 1) *mcell = 0;  // the next block of this workgroup starts from a clean score map
         }
         run += __popcll(mask);
+    }
     }
 #if OG_FAST_PROFILE
     __builtin_amdgcn_s_waitcnt(0);  // the candidate stores issued
@@ -1576,6 +1633,7 @@ __device__ unsigned long long og_oct_prof[256];
 __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_octree_kernel(OgPlan P, int l0, const u64* __restrict__ cand,
                                                            const int* __restrict__ cand_count,
                                                            uint16_t* __restrict__ node_of,
+                                                           unsigned* __restrict__ oct_best,
                                                            uint32_t* __restrict__ oct_xy,
                                                            uint32_t* __restrict__ oct_resp,
                                                            int* __restrict__ oct_count, int* __restrict__ status,
@@ -1649,8 +1707,46 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const bool k32 = !(P.sem & ORBGPU_SEM_SCORE_HARRIS) &&
                      (unsigned)(L.nRows * L.hCell) * (unsigned)(L.nCols * L.wCell) <= 0xffffffu;
     unsigned* best32 = (unsigned*)childCnt;
+    // cell-best table (table mode, 32-bit keys): the counting pass also keeps every depth-D cell's best key (in the
+    // node buffers' LDS, free until the roots are listed) and parks the table in HBM (OG_OCT_BEST_CELLS u32 per frame
+    // and level); the final phase then takes each listed node's best from its cells through the position table -- no
+    // second pass over the keys.  Used when the keys outweigh the table (workgroup-uniform).
+#ifndef OG_OCT_BESTTAB
+#define OG_OCT_BESTTAB 1
+#endif
+    const int bD0 = tbase(D), cellsD = Ttot - bD0;
+    const bool btab = OG_OCT_BESTTAB && tmode && k32 && C >= cellsD;
+    unsigned* cellbest = (unsigned*)&nodes[0][0];
+    static_assert(sizeof(nodes) >= 3 * OG_OCT_MAXL * sizeof(unsigned), "depth-D cells fit the node buffers");
+    unsigned* BT = oct_best + (long long)(f * P.nlevels + l) * OG_OCT_BEST_CELLS;
+    // one pass over the cells: every cell's best goes to the list node that holds it (position table in childPos)
+    auto cell_pass = [&]() {
+        for (int c0 = 0; c0 < cellsD; c0 += OCT_NT) {  // uniform trip count: og_wave_max32 wants whole waves
+            const int c = c0 + tid;
+            const unsigned key = c < cellsD ? BT[c] : 0u;
+            og_wave_max32(best32, c < cellsD ? (int)childPos[bD0 + c] : 0, key, key != 0u);
+        }
+    };
+    // a key's depth-D path (og_quadrant / og_child from its root): the leave pass's form when NO[] was not written
+    auto dpath = [&](int x, int y) {
+        const int r = min((int)((float)x / L.hX), nIni - 1);
+        int x0 = (int)(L.hX * (float)r), x1 = (int)(L.hX * (float)(r + 1)), y0 = 0, y1 = H;
+        int pth = r;
+        for (int d = 0; d < D; d++) {
+            const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
+            const int qx = x >= mx, qy = y >= my;
+            x0 = qx ? mx : x0;
+            x1 = qx ? x1 : mx;
+            y0 = qy ? my : y0;
+            y1 = qy ? y1 : my;
+            pth = 4 * pth + qx + 2 * qy;
+        }
+        return pth;
+    };
     if (tmode) {
         for (int q = tid; q < Ttot; q += OCT_NT) childCnt[q] = 0;
+        if (btab)
+            for (int q = tid; q < cellsD; q += OCT_NT) cellbest[q] = 0u;
         // the depth-D path is separable: x alone picks the root and the x halves, y alone the y halves.  Per-column
         // and per-row tables (in childPos, free until the position table) hold them with the quadrant bits already
         // spread (x at even bit positions with the root above them, y at odd): path = XT[x] | YT[y]
@@ -1684,18 +1780,27 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         __syncthreads();
         const int bD = tbase(D);
         for (int base = tid; base < C; base += OCT_NT * OCT_U) {
-            uint32_t kv[OCT_U];
+            uint32_t kv[OCT_U], kr[OCT_U];
 #pragma unroll
             for (int u = 0; u < OCT_U; u++) {
                 const int k = base + u * OCT_NT;
-                kv[u] = k < C ? K32[2 * k] : 0u;
+                if (btab) {  // the whole key: the response joins the cell's best (same lines as the xy half)
+                    const u64 kk = k < C ? K[k] : 0ull;
+                    kv[u] = (uint32_t)kk;
+                    kr[u] = (uint32_t)(kk >> 32);
+                } else {
+                    kv[u] = k < C ? K32[2 * k] : 0u;
+                    kr[u] = 0u;
+                }
             }
 #pragma unroll
             for (int u = 0; u < OCT_U; u++) {
                 const int k = base + u * OCT_NT;
                 int a = 0;
+                unsigned key32 = 0;
                 if (k < C) {
                     const int x = (int)(kv[u] & 0xffff), y = (int)(kv[u] >> 16);
+                    if (btab) key32 = (kr[u] << 24) | (0xffffffu - og_cand_order_m(x, y, L, mW, mH));
                     int pth;
                     if (xyt) {
                         pth = XT[x] | YT[y];
@@ -1714,12 +1819,15 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                         }
                     }
                     a = bD + pth;
-                    NO[k] = (uint16_t)a;
+                    if (!btab) NO[k] = (uint16_t)a;  // (with the cell table only a leave pass needs it: recomputed)
                 }
                 og_wave_count(childCnt, a, k < C);
+                if (btab) og_wave_max32(cellbest, a - bD, key32, k < C);
             }
         }
         __syncthreads();
+        if (btab)  // (before the roots overwrite the node buffers; read back by cell_pass after barriers)
+            for (int q = tid; q < cellsD; q += OCT_NT) BT[q] = cellbest[q];
         for (int d = D - 1; d >= 0; d--) {  // counts of shallower depths: sums of the four children
             const int b0 = tbase(d), b1 = tbase(d + 1), n = b1 - b0;
             for (int e = tid; e < n; e += OCT_NT)
@@ -2026,6 +2134,21 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             continue;
         }
         if (tmode) pos_table(cur ^ 1, Lnew);  // NO[k] (depth-D index) -> new list position
+        if (btab && tmode && done) {  // the last round in table mode: bests from the cell table, no key pass
+            cell_pass();
+            __syncthreads();
+            tmode = false;
+            if (tid == 0) {
+                sv[0] = Lnew;
+                sv[1] = nextMode;
+                sv[2] += T;
+                sv[3] = 1;
+                sv[4] = cur ^ 1;
+                sv[8] = 1;
+            }
+            __syncthreads();
+            break;
+        }
         // ---- one pass over the keys: move to the new list position, and either count the children of
         // the next round's split candidates or (last round) keep the best key per node (:744-760)
         for (int base = tid; base < C; base += OCT_NT * OCT_U) {
@@ -2035,7 +2158,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             for (int u = 0; u < OCT_U; u++) {
                 const int k = base + u * OCT_NT;
                 kv[u] = k < C ? K[k] : 0ull;
-                no[u] = k < C ? NO[k] : 0;
+                no[u] = k < C && !(tmode && btab) ? NO[k] : 0;
             }
 #pragma unroll
             for (int u = 0; u < OCT_U; u++) {
@@ -2047,7 +2170,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                     const int x = (int)(kv[u] & 0xffff), y = (int)((kv[u] >> 16) & 0xffff);
                     int n2;
                     if (tmode) {
-                        n2 = childPos[no[u]];
+                        n2 = childPos[btab ? bD0 + dpath(x, y) : no[u]];
                     } else {
                         const int n = noRoot ? aux[no[u]] : no[u];
                         // remap record: the node's split point (newPos) and its four target positions (childPos)
@@ -2092,7 +2215,13 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     __syncthreads();
     OCT_PROF(3, clock64());
     const int Ln = sv[0];
-    if (!sv[8]) {  // finished without a final key pass (empty split set): one pass for the best key
+    if (!sv[8] && btab && tmode) {  // finished in table mode without a final round: bests from the cell table
+        pos_table(sv[4], Ln);
+        for (int n = tid; n < Ln; n += OCT_NT) best[n] = 0ull;
+        __syncthreads();
+        cell_pass();
+        __syncthreads();
+    } else if (!sv[8]) {  // finished without a final key pass (empty split set): one pass for the best key
         if (tmode) pos_table(sv[4], Ln);  // (childPos: dead after the plan)
         for (int n = tid; n < Ln; n += OCT_NT) best[n] = 0ull;
         __syncthreads();
@@ -2971,7 +3100,12 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     // horizontal sums Hp at its own column: 4 dword reads and 4 v_dot2 (even rows taps (g0,g1)(g2,g3)(g4,g5)(g6,0),
     // odd rows (0,g0)(g1,g2)(g3,g4)(g5,g6)), rounded as the window pass rounds (same integer sum, same variant).
     const int xsimd_s = BV == 0 ? ((lw & ~3) - (cx - 18)) : 0;
-    auto blurred = [&](int row, int col) -> int {  // window offsets from the centre, |row|, |col| <= 18
+#ifndef OG_DK_UPU
+#define OG_DK_UPU 1  // 1: a keypoint whose 37 window columns all lie in the SSE2 body rounds every sample half-to-even
+                     // without the per-sample column test (wave-uniform branch); 0: the per-sample test only
+#endif
+    // ALLEVEN: every window column is < xsimd_s (the usual case away from the level's right edge)
+    auto blurred = [&](int row, int col, auto alleven) -> int {  // window offsets from the centre, |row|, |col| <= 18
         const int y = 18 + row, xw = 18 + col;
         const uint32_t* h = Hp + __mul24(y >> 1, HP_S) + xw;  // (a 24-bit multiply: v_mul_lo_u32 is quarter rate)
         const bool odd = (y & 1) != 0;
@@ -2985,7 +3119,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, h[3 * HP_S]), w3, acc, false);
         uint32_t v;
         if (BV == 0) {
-            const uint32_t up = xw < xsimd_s ? 0u : 1u;
+            const uint32_t up = decltype(alleven)::value ? 0u : (xw < xsimd_s ? 0u : 1u);
             v = (acc + 0x7fffu + (__builtin_amdgcn_ubfe(acc, 16, 1) | up)) >> 16;
         } else {
             v = (acc + (1u << 15)) >> 16;
@@ -2995,39 +3129,73 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 #else
     const uint8_t* ctr = Bl + 18 * BL_S + 18;
 #endif
-    u64 words[4];
+#ifndef OG_DK_PK
+#define OG_DK_PK 1  // 1: a sample's (row, col) by packed f32 ops (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32): same
+                    // roundings as the scalar form; 0: four scalar ops
+#endif
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v ab = {a, b}, ba = {b, a};
+    auto brief_words = [&](auto alleven, u64 (&words)[4]) {
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const int p = lane + 64 * t;
+        for (int t = 0; t < 4; t++) {
+            const int p = lane + 64 * t;
 #ifndef OG_DK_PATF
 #define OG_DK_PATF 1  // pattern from the float table (0: bytes + conversions)
 #endif
 #if OG_DK_PATF
-        const float4 pf = og_pattern_f[p];
-        const float pfx[2] = {pf.x, pf.z}, pfy[2] = {pf.y, pf.w};
+            const float4 pf = og_pattern_f[p];
+            const float pfx[2] = {pf.x, pf.z}, pfy[2] = {pf.y, pf.w};
 #else
-        const signed char* pt = og_pattern + 4 * p;
+            const signed char* pt = og_pattern + 4 * p;
 #endif
-        int val[2];
+            const f2v xy[2] = {f2v{pf.x, pf.y}, f2v{pf.z, pf.w}};
+            int val[2];
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
+            for (int q = 0; q < 2; q++) {
 #if OG_DK_PATF
-            const float x = pfx[q], y = pfy[q];
+                const float x = pfx[q], y = pfy[q];
 #else
-            const float x = (float)pt[2 * q], y = (float)pt[2 * q + 1];
+                const float x = (float)pt[2 * q], y = (float)pt[2 * q + 1];
 #endif
-            // GCC -O3 -march=native contracts the first product of GET_VALUE into an FMA; a
-            // build without contraction rounds both products (the kernels are compiled -ffp-contract=off)
-            const int row = nofma ? og_cvround(x * b + y * a) : og_cvround(__builtin_fmaf(x, b, y * a));
-            const int col = nofma ? og_cvround(x * a - y * b) : og_cvround(__builtin_fmaf(x, a, -(y * b)));
+                // GCC -O3 -march=native contracts the first product of GET_VALUE into an FMA; a
+                // build without contraction rounds both products (the kernels are compiled -ffp-contract=off)
+                int row, col;
+                if (OG_DK_PK && OG_DK_PATF) {
+                    // (row, col) = (x b + y a, x a - y b) as one pair: the products, the sums and the FMAs round
+                    // exactly as the scalar statements below.  op_sel picks x or y out of the (x, y) pair for both
+                    // halves, neg_hi negates y b in the high half only.
+                    f2v yab, rc;
+                    __asm__("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(yab) : "v"(xy[q]), "v"(ab));
+                    if (nofma) {
+                        f2v xba;
+                        __asm__("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1]" : "=v"(xba) : "v"(xy[q]), "v"(ba));
+                        __asm__("v_pk_add_f32 %0, %1, %2 neg_lo:[0,0] neg_hi:[0,1]" : "=v"(rc) : "v"(xba), "v"(yab));
+                    } else {
+                        __asm__("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_lo:[0,0,0] neg_hi:[0,0,1]"
+                                : "=v"(rc)
+                                : "v"(xy[q]), "v"(ba), "v"(yab));
+                    }
+                    row = og_cvround(rc.x);
+                    col = og_cvround(rc.y);
+                } else {
+                    row = nofma ? og_cvround(x * b + y * a) : og_cvround(__builtin_fmaf(x, b, y * a));
+                    col = nofma ? og_cvround(x * a - y * b) : og_cvround(__builtin_fmaf(x, a, -(y * b)));
+                }
 #if OG_DK_SAMPLEV
-            val[q] = blurred(row, col);
+                val[q] = blurred(row, col, alleven);
 #else
-            val[q] = ctr[__mul24(row, BL_S) + col];  // |row| <= 18: a 24-bit multiply
+                (void)alleven;
+                val[q] = ctr[__mul24(row, BL_S) + col];  // |row| <= 18: a 24-bit multiply
 #endif
+            }
+            words[t] = og_ballot(val[0] < val[1]);
         }
-        words[t] = og_ballot(val[0] < val[1]);
-    }
+    };
+    u64 words[4];
+    if (OG_DK_UPU && OG_DK_SAMPLEV && BV == 0 && xsimd_s >= BL_W)  // wave-uniform
+        brief_words(std::integral_constant<bool, true>{}, words);
+    else
+        brief_words(std::integral_constant<bool, false>{}, words);
     const long long o = (long long)f * P.frame_cap + g;
     if (lane < 4) {
         u64 v = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
@@ -3266,7 +3434,8 @@ void og_launch_harris(hipStream_t s, const OgPlan& P, int lb, int le, const uint
 }
 
 void og_launch_octree(hipStream_t s, const OgPlan& P, int lb, int le, const u64* cand, const int* cand_count,
-                      uint16_t* node_of, uint32_t* oct_xy, uint32_t* oct_resp, int* oct_count, int* status, int B)
+                      uint16_t* node_of, unsigned* oct_best, uint32_t* oct_xy, uint32_t* oct_resp, int* oct_count,
+                      int* status, int B)
 {
     // levels whose list may exceed OG_OCT_MAXL (more than ~1000 features: the finest levels, P.oct_big of them)
     // take the 2-nodes-per-thread kernel; the rest the 1-node-per-thread one
@@ -3277,7 +3446,7 @@ void og_launch_octree(hipStream_t s, const OgPlan& P, int lb, int le, const u64*
                            cand_count, node_of, oct_xy, oct_resp, oct_count, status, b1 - b0);
     if (s1 > s0)
         hipLaunchKernelGGL(og_octree_kernel, dim3((s1 - s0) * B), dim3(OCT_NT), 0, s, P, s0, cand,
-                           cand_count, node_of, oct_xy, oct_resp, oct_count, status, s1 - s0);
+                           cand_count, node_of, oct_best, oct_xy, oct_resp, oct_count, status, s1 - s0);
 }
 
 void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, long long pitch0, long long fstride0,

@@ -71,6 +71,7 @@ struct orbgpu_ctx {
     DevBuf<unsigned long long> cand;
     DevBuf<int> cand_count;
     DevBuf<uint16_t> node_of;
+    DevBuf<unsigned> oct_best;
     DevBuf<uint32_t> oct_xy;
     DevBuf<uint32_t> oct_resp;  // response keys (FAST score, or the Harris key under ORBGPU_SEM_SCORE_HARRIS)
     DevBuf<int> oct_count;
@@ -512,6 +513,7 @@ static int ensure_batch(orbgpu_ctx* c, int B)
     HIP_TRY(c, ensure(c->cand, Bn * (size_t)P.cand_per_frame));
     HIP_TRY(c, ensure(c->cand_count, Bn * (size_t)P.nlevels));
     HIP_TRY(c, ensure(c->node_of, Bn * (size_t)P.cand_per_frame));
+    HIP_TRY(c, ensure(c->oct_best, Bn * (size_t)P.nlevels * OG_OCT_BEST_CELLS));
     HIP_TRY(c, ensure(c->oct_xy, Bn * (size_t)P.kcap_total));
     HIP_TRY(c, ensure(c->oct_resp, Bn * (size_t)P.kcap_total));
     HIP_TRY(c, ensure(c->oct_count, Bn * (size_t)P.nlevels));
@@ -623,7 +625,7 @@ static void launch_levels(orbgpu_ctx* c, hipStream_t s, int lb, int le, const ui
         og_launch_harris(s, P, lb, le, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p, B);
         if (marks) timer_mark(c, "harris");
     }
-    og_launch_octree(s, P, lb, le, c->cand.p, c->cand_count.p, c->node_of.p, c->oct_xy.p, c->oct_resp.p,
+    og_launch_octree(s, P, lb, le, c->cand.p, c->cand_count.p, c->node_of.p, c->oct_best.p, c->oct_xy.p, c->oct_resp.p,
                      c->oct_count.p, c->status.p, B);
 }
 
@@ -816,6 +818,7 @@ void orbgpu_destroy(orbgpu_ctx* c)
     release(c->cand);
     release(c->cand_count);
     release(c->node_of);
+    release(c->oct_best);
     release(c->oct_xy);
     release(c->oct_resp);
     release(c->oct_count);

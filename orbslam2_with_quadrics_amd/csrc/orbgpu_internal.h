@@ -7,6 +7,7 @@
 //   cand      : per (frame, level) FAST candidate slots, one u64 {x_rel:16, y_rel:16, response:8};
 //               slot capacity = the exact NMS bound of that level (no overflow possible).
 //   node_of   : per candidate u16 node index (octree scratch).
+//   oct_best  : per (frame, level) OG_OCT_BEST_CELLS u32: the octree's depth-D cell-best table (scratch).
 //   octree out: per (frame, level) up to kcap u32 {x:16, y:16} + u8 response, list order.
 //   kps/desc  : per frame `frame_cap` orbgpu_keypoint (28 B AoS, cv::KeyPoint layout) + 32-B rows.
 #pragma once
@@ -25,6 +26,7 @@
 #define OG_GRID_ROWS 48
 #define OG_GRID_CELLS (OG_GRID_COLS * OG_GRID_ROWS)
 #define OG_OCT_MAXL 1024   // max octree list length handled in LDS (N_l + 3 + slack), one node per thread
+#define OG_OCT_BEST_CELLS (4 * OG_OCT_MAXL)  // octree cell-best table entries per (frame, level): >= depth-D cells
 #define OG_OCT_MAXL_BIG 2048  // the same with two list nodes per thread (~143 KB of LDS): levels of up to ~2040 features
 #define OG_MAX_CELL_W 64   // wCell <= 59 for any width (nCols = floor(w/30))
 #define OG_MAX_PITCH (1u << 24)  // row pitches (bytes) below this: 24-bit row-offset products in the kernels

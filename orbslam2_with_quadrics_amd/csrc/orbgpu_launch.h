@@ -64,10 +64,10 @@ hipError_t og_read_oct_prof(unsigned long long* out, int n);  // OG_OCT_PROFILE 
 // ORBGPU_SEM_SCORE_HARRIS option: rewrite the response key of each candidate of levels [lb, le) with its Harris key
 void og_launch_harris(hipStream_t s, const OgPlan& P, int lb, int le, const uint8_t* img0, long long pitch0,
                       long long fstride0, const uint8_t* pyr, unsigned long long* cand, const int* cand_count, int B);
-// octree of levels [lb, le)
+// octree of levels [lb, le); oct_best: OG_OCT_BEST_CELLS u32 per (frame, level) of scratch (the cell-best table)
 void og_launch_octree(hipStream_t s, const OgPlan& P, int lb, int le, const unsigned long long* cand,
-                      const int* cand_count, uint16_t* node_of, uint32_t* oct_xy, uint32_t* oct_resp, int* oct_count,
-                      int* status, int B);
+                      const int* cand_count, uint16_t* node_of, unsigned* oct_best, uint32_t* oct_xy, uint32_t* oct_resp,
+                      int* oct_count, int* status, int B);
 void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, long long pitch0, long long fstride0,
                         const uint8_t* pyr, const uint32_t* oct_xy, const uint32_t* oct_resp, const int* oct_count,
                         orbgpu_kp_dev* kps, uint8_t* desc, int* counts, int B);

@@ -1,7 +1,8 @@
 """Per-phase timeline of the FAST workgroups under full load (diagnostic, test infrastructure).
 
 python tools/fast_profile.py --build          # here: variant library with OG_FAST_PROFILE=1
-python tools/fast_profile.py --run [--batch B] # GPU box: B 1080p frames (default 256); prints the mean cycles of each
+python tools/fast_profile.py --run [--batch B] [--name N] # GPU box (--name: variants/liborbgpu_<N>.so)
+                                               #: B 1080p frames (default 256); prints the mean cycles of each
                                                # phase over the middle frame's blocks (s_memtime, shader clock)
 """
 import os
@@ -11,7 +12,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VLIB = os.path.join(ROOT, "orbslam2_with_quadrics_amd", "variants", "liborbgpu_fastprof.so")
+VNAME = sys.argv[sys.argv.index("--name") + 1] if "--name" in sys.argv else "fastprof"
+VLIB = os.path.join(ROOT, "orbslam2_with_quadrics_amd", "variants", f"liborbgpu_{VNAME}.so")
 PHASES = ["roi+zero", "stage1 quick", "stage2 score", "stage3 nms+counts", "reservation", "emission"]
 
 
@@ -42,12 +44,12 @@ def run():
     t = buf.reshape(-1, 8).astype(np.int64)
     t = t[t[:, 0] > 0]
     ns, lev = t[:, 7] & 0xffffffff, t[:, 7] >> 32
-    d = np.diff(t[:, :7], axis=1)
+    dt = np.diff(t[:, :7], axis=1)
     life = t[:, 6] - t[:, 0]
     print(f"blocks {len(t)}  mean lifetime {life.mean():.0f} cycles (median {np.median(life):.0f})")
     for i, name in enumerate(PHASES):
-        print(f"  {name:20s} mean {d[:, i].mean():8.0f}  median {np.median(d[:, i]):8.0f}  "
-              f"share {d[:, i].sum() / life.sum():.3f}")
+        print(f"  {name:20s} mean {dt[:, i].mean():8.0f}  median {np.median(dt[:, i]):8.0f}  "
+              f"share {dt[:, i].sum() / life.sum():.3f}")
     for l in range(8):
         m = lev == l
         if m.any():
