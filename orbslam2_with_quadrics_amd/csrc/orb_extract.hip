@@ -785,7 +785,7 @@ __device__ __forceinline__ og_u32x8 og_fast_block(const OgFastBlk* blocks, int b
 {
     static_assert(sizeof(OgFastBlk) == 32, "OgFastBlk is read as one dwordx8");
     static_assert(offsetof(OgFastBlk, y0) == 8 && offsetof(OgFastBlk, rw) == 12 && offsetof(OgFastBlk, cand_off) == 16 &&
-                      offsetof(OgFastBlk, ox) == 24,
+                      offsetof(OgFastBlk, ox) == 24 && offsetof(OgFastBlk, colw) == 28,
                   "OgFastBlk field offsets");
 #if defined(__HIP_DEVICE_COMPILE__)
     return ((const __attribute__((address_space(4))) og_u32x8*)blocks)[b];
@@ -817,6 +817,7 @@ __device__ __forceinline__ void og_ds_write_b16_x4(u64 m0, uint32_t a0, uint32_t
 // One FAST block as the kernel works on it, decoded from its OgFastBlk record (scalar registers)
 struct OgFB {
     int l, rw, rh, dw, dh, wC, hC, cand_off, cand_cap, ox, oy, mis;
+    unsigned colw;       // OgFastBlk::colw
     unsigned upitch;     // < 2^24 (checked on the host)
     bool aligned;        // row pitch a multiple of 4
     const uint8_t* row0; // ROI pixel (0, 0) of frame f
@@ -839,6 +840,7 @@ __device__ __forceinline__ OgFB og_fast_decode(const OgFastBlk* blocks, int p, u
     b.cand_cap = (int)bk[5];
     b.ox = (int)(short)(bk[6] & 0xffffu);
     b.oy = (int)bk[6] >> 16;
+    b.colw = bk[7];
     if (b.l == 0) {
         b.upitch = (unsigned)pitch0 & (OG_MAX_PITCH - 1);
         b.row0 = img0 + (unsigned long long)f * (unsigned long long)fstride0 +
@@ -866,27 +868,42 @@ __device__ __forceinline__ void og_fastq_roi_load(const OgFB& b, int tid, uint32
     // item (row, group of 4 qwords): 4 dword loads (one per 16-column segment), 8 v_perm into 4 quads, two 16-byte
     // LDS stores.  Columns past the ROI hold image bytes to its right (never read by a detection pixel); rows past it
     // are not stored.  The loads are unconditional (no exec branches): rows past the ROI re-read its last row.
-    // Addresses: the block's uniform row base (SGPRs) plus a 32-bit per-lane offset (saddr + voffset loads).
+    // Addresses: the block's uniform row base (SGPRs) plus a 32-bit per-lane offset (saddr + voffset loads).  The
+    // pitch test is one uniform branch around all the loads (not one per load), and every load of a path is issued
+    // before the first use.
     const int nq4 = (16 + 6 + b.mis + 3) >> 2;  // groups of 4 qwords per row (<= 7)
     const int q4 = min(tid & 7, nq4 - 1);
     const uint8_t* rbase = b.row0 - b.mis;
-    const unsigned mb = (unsigned)((uintptr_t)rbase & 3);
-    const uint8_t* abase = rbase - mb;
+    unsigned off[2];
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         const int r = min((tid >> 3) + 64 * k, b.rh - 1);
-        const unsigned off = (unsigned)r * b.upitch + 4u * (unsigned)q4;
+        off[k] = __umul24((unsigned)r, b.upitch) + 4u * (unsigned)q4;  // upitch < 2^24, r < 128
+        __asm__("" : "+v"(off[k]));  // a 32-bit lane offset (saddr + voffset loads)
+    }
+    if (b.aligned) {
 #pragma unroll
-        for (int g = 0; g < 4; g++) {
-            if (b.aligned) {
-                s[k][g] = *(const uint32_t*)(rbase + off + 16u * g);
-            } else {
-                // odd pitch: two aligned loads funnel-shifted by the row's offset
-                const unsigned o = off + 16u * g + mb;
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) s[k][g] = *(const uint32_t*)(rbase + off[k] + 16u * g);
+    } else {
+        // odd pitch: two aligned loads funnel-shifted by the row's offset
+        const unsigned mb = (unsigned)((uintptr_t)rbase & 3);
+        const uint8_t* abase = rbase - mb;
+        uint32_t lo[2][4], hi[2][4];
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const unsigned o = off[k] + 16u * g + mb;
                 const uint32_t* a = (const uint32_t*)(abase + (o & ~3u));
-                s[k][g] = __builtin_amdgcn_alignbyte(a[1], a[0], o & 3u);
+                lo[k][g] = a[0];
+                hi[k][g] = a[1];
             }
-        }
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) s[k][g] = __builtin_amdgcn_alignbyte(hi[k][g], lo[k][g], (off[k] + mb) & 3u);
     }
 }
 
@@ -1048,12 +1065,14 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const int lrow = ((lg & 1) << 2) | (lg >> 1);  // 0, 4, 1, 5
         const uint2* Tl = &Tq[(lrow + 3) * FQ_S + (c + 3)];
         const uint32_t e_lane = (uint32_t)((lrow << 7) | c);
-        auto cmask = [](int n) -> u64 {  // lanes whose column c (lane & 15) is below n, in all four 16-lane groups
-            const unsigned m16 = n >= 16 ? 0xffffu : (n <= 0 ? 0u : ((1u << n) - 1u));
-            const unsigned m32 = m16 | (m16 << 16);
+        // lanes whose column c (lane & 15) is below segment k's column count (the block record's byte k, in [0, 16]),
+        // in all four 16-lane groups
+        auto cmask = [&](int k) -> u64 {
+            const unsigned m16 = (1u << ((b.colw >> (8 * k)) & 31u)) - 1u;
+            const unsigned m32 = m16 * 0x10001u;
             return ((u64)m32 << 32) | m32;
         };
-        const u64 col0 = cmask(dw), col1 = cmask(dw - 16), col2 = cmask(dw - 32), col3 = cmask(dw - 48);
+        const u64 col0 = cmask(0), col1 = cmask(1), col2 = cmask(2), col3 = cmask(3);
         const int nunits = ((dh + 7) >> 3) * 2;
         for (int u = wvu; u < nunits; u += FB_NW) {
             const int R = 8 * (u >> 1) + 2 * (u & 1);  // uniform
@@ -1088,10 +1107,15 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             const uint2 ctr = make_uint2((uint32_t)w[16], (uint32_t)(w[16] >> 32));
             const uint2 r0 = og_fast_quick2v(c0, ctr.x, tt);  // pixels c, c + 16
             const uint2 r1 = og_fast_quick2v(c1, ctr.y, tt);  // pixels c + 32, c + 48
-            u64 rows = ~0ull;
+            // the column masks, restricted in a tail unit to its rows inside the area
+            u64 cm0 = col0, cm1 = col1, cm2 = col2, cm3 = col3;
             if (!full) {
-                rows = (R < dh ? 0xffffull : 0ull) | (R + 4 < dh ? 0xffff0000ull : 0ull) |
-                       (R + 1 < dh ? 0xffff00000000ull : 0ull) | (R + 5 < dh ? 0xffff000000000000ull : 0ull);
+                const u64 rows = (R < dh ? 0xffffull : 0ull) | (R + 4 < dh ? 0xffff0000ull : 0ull) |
+                                 (R + 1 < dh ? 0xffff00000000ull : 0ull) | (R + 5 < dh ? 0xffff000000000000ull : 0ull);
+                cm0 &= rows;
+                cm1 &= rows;
+                cm2 &= rows;
+                cm3 &= rows;
             }
 #if defined(OG_PROBE_SALU) && OG_PROBE_SALU > 0  // sensitivity probe (measurement builds only): dead SALU work
             {
@@ -1108,8 +1132,8 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             }
 #endif
             const uint32_t a0 = r0.x | r0.y, a1 = r1.x | r1.y;
-            const u64 m[4] = {og_lanes_lo16_nz(a0) & rows & col0, og_lanes_gt((int)a0, 0xffff) & rows & col1,
-                              og_lanes_lo16_nz(a1) & rows & col2, og_lanes_gt((int)a1, 0xffff) & rows & col3};
+            const u64 m[4] = {og_lanes_lo16_nz(a0) & cm0, og_lanes_gt((int)a0, 0xffff) & cm1, og_lanes_lo16_nz(a1) & cm2,
+                              og_lanes_gt((int)a1, 0xffff) & cm3};
             int cnt[4], n = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -1205,7 +1229,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     }
     // ---- stage 3: same-cell 3x3 NMS at both thresholds; each wave walks every 8th 64-entry chunk of the list
     int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
-    for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
+    for (int e0 = wvu * 64; e0 < ns; e0 += FB_NT) {
         const int e = e0 + lane;
         int ent = 0, mc = 0, nbm = 0;
         if (e < ns) {
@@ -1269,7 +1293,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         if (total != 0 && tid == 0) bb = atomicAdd(&cand_count[f * nlevels + b.l], total);
         u64* st = (u64*)roiq;
         int run = 0;
-        for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
+        for (int e0 = wvu * 64; e0 < ns; e0 += FB_NT) {
             const int e = e0 + lane;
             int ent = 0;
             if (e < ns) ent = lst[e];
@@ -1314,7 +1338,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const bool emit = total != 0 && sb + total <= b.cand_cap && kept != 0;
     u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb + before);
     int run = 0;
-    for (int e0 = wv * 64; e0 < ns; e0 += FB_NT) {
+    for (int e0 = wvu * 64; e0 < ns; e0 += FB_NT) {
         const int e = e0 + lane;
         int ent = 0;
         if (e < ns) ent = lst[e];
@@ -2802,7 +2826,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
                                                                     const int* __restrict__ oct_count,
                                                                     orbgpu_kp_dev* __restrict__ kps,
                                                                     uint8_t* __restrict__ desc,
-                                                                    int* __restrict__ counts)
+                                                                    int* __restrict__ counts, unsigned dmagic)
 {
     __shared__ __attribute__((aligned(16))) uint8_t raw[DK_WAVES][RAW_W * RAW_S];
     __shared__ __attribute__((aligned(16))) uint32_t hp[DK_WAVES][HP_ROWS * HP_S];
@@ -2813,17 +2837,29 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 #endif
     const unsigned lin = OG_DESC_XCD_REMAP ? og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y)
                                            : blockIdx.y * gridDim.x + blockIdx.x;
-    const int f = (int)(lin / gridDim.x);
-    const int g = (int)(lin % gridDim.x) * DK_WAVES + w;
-    // which level does keypoint g belong to (levels concatenated 0..L-1, :1076-1104)
+    // frame = lin / gridDim.x by the host's multiply-high constant (exact for every lin of the launch, checked on the
+    // host; 0: the division)
+    const unsigned fq = dmagic ? __umulhi(lin, dmagic) : lin / gridDim.x;
+    const int f = (int)fq;
+    const int g = (int)(lin - fq * gridDim.x) * DK_WAVES + w;
+    // which level does keypoint g belong to (levels concatenated 0..L-1, :1076-1104); with 8 levels the frame's
+    // counts are one 32-byte scalar load and the search is unrolled (per keypoint wave: the scalar unit is shared)
     int l = -1, li = 0, total = 0;
-    for (int q = 0; q < P.nlevels; q++) {
-        const int c = oct_count[f * P.nlevels + q];
+    auto visit = [&](int q, int c) {
         if (l < 0 && g < total + c) {
             l = q;
             li = g - total;
         }
         total += c;
+    };
+    if (P.nlevels == 8) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const og_u32x8 c8 = ((const __attribute__((address_space(4))) og_u32x8*)(oct_count + 8 * f))[0];
+#pragma unroll
+        for (int q = 0; q < 8; q++) visit(q, (int)c8[q]);
+#endif
+    } else {
+        for (int q = 0; q < P.nlevels; q++) visit(q, oct_count[f * P.nlevels + q]);
     }
     if (g == 0 && lane == 0) counts[f] = total;
     const bool active = l >= 0;
@@ -3458,12 +3494,15 @@ void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, lon
     const bool nofma = (P.sem & ORBGPU_SEM_BRIEF_NOFMA) != 0;
     // the 8 (blur variant, rotation form) instantiations
     using K = void (*)(OgPlan, const uint8_t*, long long, long long, const uint8_t*, const uint32_t*, const uint32_t*,
-                       const int*, orbgpu_kp_dev*, uint8_t*, int*);
+                       const int*, orbgpu_kp_dev*, uint8_t*, int*, unsigned);
     static const K table[8] = {og_describe_kernel<0, false>, og_describe_kernel<1, false>, og_describe_kernel<2, false>,
                                og_describe_kernel<3, false>, og_describe_kernel<0, true>,  og_describe_kernel<1, true>,
                                og_describe_kernel<2, true>,  og_describe_kernel<3, true>};
+    // lin / blocks == mulhi(lin, floor(2^32 / blocks) + 1) for every lin < blocks * B when blocks^2 * B < 2^32
+    const unsigned long long d = (unsigned long long)blocks;
+    const unsigned dmagic = (d > 1 && d * d * (unsigned long long)B < (1ull << 32)) ? (unsigned)((1ull << 32) / d + 1) : 0u;
     hipLaunchKernelGGL(table[bv + 4 * nofma], dim3(blocks, B), dim3(64 * DK_WAVES), 0, s, P, img0, pitch0, fstride0,
-                       pyr, oct_xy, oct_resp, oct_count, kps, desc, counts);
+                       pyr, oct_xy, oct_resp, oct_count, kps, desc, counts, dmagic);
 }
 
 void og_launch_grid(hipStream_t s, const orbgpu_kp_dev* kps, const int* counts, int frame_cap, OgGridGeom G,

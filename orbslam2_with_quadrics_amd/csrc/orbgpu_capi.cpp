@@ -453,6 +453,7 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
             r.cand_cap = L.cand_cap;
             r.ox = (short)(cd.x0 - L.minB + 3);
             r.oy = (short)(cd.y0 - L.minB + 3);
+            for (int k = 0; k < 4; k++) r.colw |= (unsigned)std::min(std::max(rw - 6 - 16 * k, 0), 16) << (8 * k);
         }
         P.fast_blocks = n;
         if (cand_off >= (1LL << 31) || std::max<long long>(pyr_off, 256) >= (1LL << 31)) {

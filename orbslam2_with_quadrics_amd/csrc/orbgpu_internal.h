@@ -75,7 +75,7 @@ struct OgFastBlk {
     int cand_off;          // the level's candidate slots inside a frame (entries)
     int cand_cap;          // ... and their number (the exact NMS bound)
     short ox, oy;          // candidate coordinates of detection pixel (0, 0): x0 - minB + 3, y0 - minB + 3
-    int pad;
+    unsigned colw;         // byte k: detection columns of the block in 16-column segment k, clamp(dw - 16 k, 0, 16)
 };
 
 struct OgPlan {
