@@ -1,0 +1,55 @@
+"""Host-side integer identities the kernels rely on (CPU only).
+
+* describe's frame index: og_launch_describe passes dmagic = floor(2^32 / blocks) + 1 and the kernel takes
+  lin / blocks as mulhi(lin, dmagic) whenever blocks^2 * B < 2^32 (orb_extract.hip, og_launch_describe).
+* FAST's stage-1 unit walk: units u = w, w + 8, ... of a wave start at rows R = 8 (u >> 1) + 2 (u & 1), walked as
+  R += 32 up to 8 (nunits >> 1) + 2 (w & 1) (og_fast_quad_kernel).
+* FAST's column counts: OgFastBlk::colw byte k = clamp(dw - 16 k, 0, 16), mask (0x10001 << n) - 0x10001 per 16-lane
+  group.
+"""
+import random
+
+
+def mulhi32(a, b):
+    return (a * b) >> 32
+
+
+def test_describe_frame_magic_exact():
+    rng = random.Random(7)
+    cases = [(d, b) for d in (2, 3, 7, 250, 500, 512, 1000, 1001, 1023, 2047, 4095) for b in (1, 2, 64, 256, 512, 1024)]
+    cases += [(rng.randrange(2, 5000), rng.randrange(1, 2049)) for _ in range(60)]
+    checked = 0
+    for d, b in cases:
+        if d * d * b >= 1 << 32:
+            continue
+        m = (1 << 32) // d + 1
+        assert m < 1 << 32
+        n = d * b
+        pts = set(range(0, min(n, 4096))) | set(range(max(0, n - 4096), n)) | {rng.randrange(n) for _ in range(2000)}
+        # every multiple of d and its predecessor: where a wrong quotient would first show
+        pts |= {q * d for q in range(b)} | {q * d - 1 for q in range(1, b + 1)}
+        for x in pts:
+            assert mulhi32(x, m) == x // d, (d, b, x)
+        checked += 1
+    assert checked > 40
+
+
+def test_fast_unit_rows_walk():
+    for dh in range(1, 81):
+        nunits = ((dh + 7) >> 3) * 2
+        for w in range(8):
+            want = [8 * (u >> 1) + 2 * (u & 1) for u in range(w, nunits, 8)]
+            got = list(range(8 * (w >> 1) + 2 * (w & 1), 8 * (nunits >> 1) + 2 * (w & 1), 32))
+            assert got == want, (dh, w)
+
+
+def test_fast_column_masks():
+    for dw in range(1, 65):
+        colw = 0
+        for k in range(4):
+            colw |= min(max(dw - 16 * k, 0), 16) << (8 * k)
+        for k in range(4):
+            n = (colw >> (8 * k)) & 31
+            m32 = ((0x10001 << n) - 0x10001) & 0xFFFFFFFF
+            lanes = [lane for lane in range(32) if (m32 >> lane) & 1]
+            assert lanes == [lane for lane in range(32) if (lane & 15) + 16 * k < dw], (dw, k)
