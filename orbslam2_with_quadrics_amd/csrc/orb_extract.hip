@@ -250,6 +250,13 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
 
 // 4 horizontally adjacent outputs of one row from two LDS source rows: sx = byte offsets in the rows, weights
 // (a0, a1) per column (a1 = 0 at the right border), vertical weights (yz, yw)
+#ifndef OG_RZ_BREUSE
+#define OG_RZ_BREUSE 1  // og_resize2_kernel's B pass forms each distinct A row's horizontal sums once per wave
+#endif
+#ifndef OG_RZ_SDWA
+#define OG_RZ_SDWA 1  // 1: each output byte's final min(., 255) writes its byte of the packed dword (SDWA dst_sel), no
+                      // shift-or per byte; 0: shift and or
+#endif
 template <bool FX>
 __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t* R1, const int* sx,
                                                const og_rz_u16x2* wt, unsigned yz, unsigned yw)
@@ -261,7 +268,24 @@ __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t*
         const uint32_t p1 = (uint32_t)R1[sx[k]] | ((uint32_t)R1[sx[k] + 1] << 16);
         const uint32_t d0 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[k], 0u, false);
         const uint32_t d1 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[k], 0u, false);
-        packed |= og_rz_vert16<FX>(yz, d0, yw, d1) << (8 * k);
+        if (!FX && OG_RZ_MULHI && OG_RZ_SDWA) {
+            // og_rz_vert16 up to its final min, which writes byte k of `packed` (the other bytes preserved)
+            const uint32_t t = (og_mulhi_u24(yz << 8, d0 & ~0xffu) + og_mulhi_u24(yw << 8, d1 & ~0xffu) + 2u) >> 2;
+            if (k == 0)
+                __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                        : "+v"(packed) : "v"(t), "s"(255u));
+            else if (k == 1)
+                __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                        : "+v"(packed) : "v"(t), "s"(255u));
+            else if (k == 2)
+                __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                        : "+v"(packed) : "v"(t), "s"(255u));
+            else
+                __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                        : "+v"(packed) : "v"(t), "s"(255u));
+        } else {
+            packed |= og_rz_vert16<FX>(yz, d0, yw, d1) << (8 * k);
+        }
     }
     return packed;
 }
@@ -576,7 +600,9 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
                                           (unsigned)yt.w);
             }
 #else
-            const uint32_t packed = og_rz_quad<FX>(S + __umul24((unsigned)r0, (unsigned)g.SC) + mis[r0], S + __umul24((unsigned)r1, (unsigned)g.SC) + mis[r1], sxA, wtA,
+            // a 16-byte multiple pitch gives every staged row the first row's misalignment mb: no per-row lookups
+            const unsigned m0 = (upitch & 15u) == 0 ? mb : (unsigned)mis[r0], m1 = (upitch & 15u) == 0 ? mb : (unsigned)mis[r1];
+            const uint32_t packed = og_rz_quad<FX>(S + __umul24((unsigned)r0, (unsigned)g.SC) + m0, S + __umul24((unsigned)r1, (unsigned)g.SC) + m1, sxA, wtA,
                                                (unsigned)yt.z, (unsigned)yt.w);
 #endif
             *(uint32_t*)&A[rr * g.AC + 4 * qa] = packed;
@@ -594,6 +620,66 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     const uint32_t aA = og_lds_addr(A);                    // 16-byte aligned, AC a multiple of 4: one alignment
     const OgRzSel sb = og_rz_sel(sxB, (unsigned)sxB[0] & 3u);
 #endif
+#if !OG_RZ_WORDS && OG_RZ_BREUSE
+    // the wave's 4 output rows read nondecreasing A rows, and consecutive outputs share one (a 1.2 downscale: ~5
+    // distinct rows for 4 outputs): each distinct row's 4 horizontal sums are formed once and kept for the next
+    // output (the rows are wave-uniform, so every reuse test is a scalar branch)
+    const int rgu = __builtin_amdgcn_readfirstlane(rg);
+    constexpr bool MH = !FX && OG_RZ_MULHI;  // sums kept as (d >> 4) << 8 for the multiply-high vertical form
+    auto hsum = [&](int row, uint32_t (&h)[4]) {
+        const uint8_t* R = A + __umul24((unsigned)(row - ar0), (unsigned)g.AC);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t pr = (uint32_t)R[sxB[k]] | ((uint32_t)R[sxB[k] + 1] << 16);
+            const uint32_t d = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, pr), wtB[k], 0u, false);
+            h[k] = MH ? (d & ~0xffu) : d;
+        }
+    };
+    uint32_t hx[4] = {0u, 0u, 0u, 0u}, hy[4] = {0u, 0u, 0u, 0u};  // sums of rows rx < ry, the last output's two rows
+    int rx = -1, ry = -1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int r = 4 * rgu + q;
+        if (r >= nyB) break;
+        const int4 yt = YB[r];
+        uint32_t h0[4], h1[4];
+        if (yt.x == ry) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) h0[k] = hy[k];
+        } else if (yt.x == rx) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) h0[k] = hx[k];
+        } else {
+            hsum(yt.x, h0);
+        }
+        if (yt.y == yt.x) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) h1[k] = h0[k];
+        } else if (yt.y == ry) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) h1[k] = hy[k];
+        } else {
+            hsum(yt.y, h1);
+        }
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (MH)
+                packed |= min((og_mulhi_u24((unsigned)yt.z << 8, h0[k]) + og_mulhi_u24((unsigned)yt.w << 8, h1[k]) + 2u) >> 2,
+                              255u) << (8 * k);
+            else
+                packed |= og_rz_vert<FX>((unsigned)yt.z, h0[k], (unsigned)yt.w, h1[k]) << (8 * k);
+        }
+        og_rz_store4(DB + __umul24((unsigned)(by0 + r), (unsigned)pitchB), packed, n);
+        rx = yt.x;
+        ry = yt.y;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            hx[k] = h0[k];
+            hy[k] = h1[k];
+        }
+    }
+#else
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int r = 4 * rg + q;
@@ -608,6 +694,7 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
 #endif
         og_rz_store4(DB + __umul24((unsigned)(by0 + r), (unsigned)pitchB), packed, n);
     }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1074,8 +1161,9 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         };
         const u64 col0 = cmask(0), col1 = cmask(1), col2 = cmask(2), col3 = cmask(3);
         const int nunits = ((dh + 7) >> 3) * 2;
-        for (int u = wvu; u < nunits; u += FB_NW) {
-            const int R = 8 * (u >> 1) + 2 * (u & 1);  // uniform
+        // wave w takes units u = w, w + 8, ...: their first rows R = 8 (u >> 1) + 2 (u & 1) step by 32 (uniform)
+        const int Rlim = 8 * (nunits >> 1) + 2 * (wvu & 1);
+        for (int R = 8 * (wvu >> 1) + 2 * (wvu & 1); R < Rlim; R += 4 * FB_NW) {
             const bool full = R + 5 < dh;
             // (tail: lanes whose row is past the area read rows below the ROI -- inside the LDS allocation, at most
             // 11 rows past row 80 -- and are masked out)
@@ -1119,7 +1207,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             }
 #if defined(OG_PROBE_SALU) && OG_PROBE_SALU > 0  // sensitivity probe (measurement builds only): dead SALU work
             {
-                unsigned pz = (unsigned)u;
+                unsigned pz = (unsigned)R;
 #pragma unroll
                 for (int z = 0; z < OG_PROBE_SALU; z++) __asm__ volatile("s_add_u32 %0, %0, 1" : "+s"(pz) : : "scc");
             }
@@ -2845,21 +2933,30 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     // which level does keypoint g belong to (levels concatenated 0..L-1, :1076-1104); with 8 levels the frame's
     // counts are one 32-byte scalar load and the search is unrolled (per keypoint wave: the scalar unit is shared)
     int l = -1, li = 0, total = 0;
-    auto visit = [&](int q, int c) {
-        if (l < 0 && g < total + c) {
-            l = q;
-            li = g - total;
-        }
-        total += c;
-    };
     if (P.nlevels == 8) {
 #if defined(__HIP_DEVICE_COMPILE__)
+        // one 32-byte scalar load of the frame's 8 level counts and an unrolled search (a DPP scan over a per-lane
+        // vector load was 3 % slower: the vector load's round trip at the kernel's start)
         const og_u32x8 c8 = ((const __attribute__((address_space(4))) og_u32x8*)(oct_count + 8 * f))[0];
 #pragma unroll
-        for (int q = 0; q < 8; q++) visit(q, (int)c8[q]);
+        for (int q = 0; q < 8; q++) {
+            const int c = (int)c8[q];
+            if (l < 0 && g < total + c) {
+                l = q;
+                li = g - total;
+            }
+            total += c;
+        }
 #endif
     } else {
-        for (int q = 0; q < P.nlevels; q++) visit(q, oct_count[f * P.nlevels + q]);
+        for (int q = 0; q < P.nlevels; q++) {
+            const int c = oct_count[f * P.nlevels + q];
+            if (l < 0 && g < total + c) {
+                l = q;
+                li = g - total;
+            }
+            total += c;
+        }
     }
     if (g == 0 && lane == 0) counts[f] = total;
     const bool active = l >= 0;

@@ -140,13 +140,15 @@ __global__ __launch_bounds__(256) void og_init_cand_kernel(OgFrameDev F1, int re
             cell = (cr.x0 + c / ncy) * OG_GRID_ROWS + (cr.y0 + c % ncy);
             cnt = CS[cell + 1] - CS[cell];
         }
+        // inclusive scan of the cell counts with DPP (row_shr 1/2/4/8, then row_bcast 15/31), no LDS round trips
         int incl = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(incl, o);
-            if (lane >= o) incl += t;
-        }
-        const int T = __shfl(incl, 63);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xf, 0xf, false);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xf, 0xf, false);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xf, 0xf, false);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xf, 0xf, false);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xa, 0xf, false);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xc, 0xf, false);
+        const int T = __builtin_amdgcn_readlane(incl, 63);
         const int cellStart = c < ncells ? CS[cell] : 0;
         for (int e = lane; e - lane < T; e += 64) {
             const int ee = min(e, T - 1);

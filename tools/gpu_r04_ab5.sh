@@ -1,9 +1,9 @@
 set -e
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/tests.log 2>&1 || { tail -30 gpurun_out/tests.log; exit 1; }
 tail -1 gpurun_out/tests.log
-for i in 1 2 3; do timeout -k 10 300 python tools/variant_bench.py --streams 2 --names s2,s3,s4,s5 -- --steps 30; done > gpurun_out/s2ab.log 2>&1
+for i in 1 2 3; do timeout -k 10 300 python tools/variant_bench.py --streams 2 --names s2,s4,s5,s6 -- --steps 30; done > gpurun_out/s2ab.log 2>&1
 for i in 1 2; do timeout -k 10 300 python tools/variant_bench.py --streams 2 --names s2,s5 -- --workload stereo --steps 30; done >> gpurun_out/s2ab.log 2>&1
 cat gpurun_out/s2ab.log | python3 -c "
 import sys, json
 for l in sys.stdin:
-    n, j = l.split(' ', 1); d = json.loads(j); print(n, d['value'], d['stages']['fast'], d['stages']['describe'], d['stages']['pyramid'], d['parity']['mismatches'])"
+    n, j = l.split(' ', 1); d = json.loads(j); print(n, d['value'], d['stages']['fast'], d['stages']['describe'], d['stages']['pyramid'], d['stages']['search_init'] if 'search_init' in d['stages'] else '-', d['parity']['mismatches'])"
