@@ -3060,11 +3060,35 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             }
 #endif
         } else {  // within 21 px of the border: BORDER_REFLECT_101 per pixel
+#ifndef OG_DK_BORDER_BATCH
+#define OG_DK_BORDER_BATCH 1  // 1: lane = window column, OG_DK_BORDER_RB rows' byte loads in flight per batch; 0: 29 dependent rounds
+#endif
+#if OG_DK_BORDER_BATCH
+            // lane c < 43 owns window column c (its reflected image column, once); each row's reflected image row is
+            // wave-uniform.  The loads of a batch of rows are issued before their stores: 2 memory round trips instead of the
+            // 29 of a pixel-per-lane loop that waits for each load (a keypoint near the edge cost ~20 interior ones)
+#ifndef OG_DK_BORDER_RB
+#define OG_DK_BORDER_RB 22  // rows per batch of loads in flight
+#endif
+            const int xx = og_reflect101(cx - 21 + min(lane, RAW_W - 1), lw);
+            for (int r0 = 0; r0 < RAW_W; r0 += OG_DK_BORDER_RB) {
+                uint32_t v[OG_DK_BORDER_RB];
+#pragma unroll
+                for (int k = 0; k < OG_DK_BORDER_RB; k++) {
+                    const int yy = og_reflect101(cy - 21 + min(r0 + k, RAW_W - 1), lh);
+                    v[k] = img[(long long)yy * pitch + xx];
+                }
+#pragma unroll
+                for (int k = 0; k < OG_DK_BORDER_RB; k++)
+                    if (lane < RAW_W && r0 + k < RAW_W) R[(r0 + k) * RAW_S + lane] = (uint8_t)v[k];
+            }
+#else
             for (int idx = lane; idx < RAW_W * RAW_W; idx += 64) {
                 const int r = idx / RAW_W, c = idx - (idx / RAW_W) * RAW_W;
                 const int yy = og_reflect101(cy - 21 + r, lh), xx = og_reflect101(cx - 21 + c, lw);
                 R[r * RAW_S + c] = img[(long long)yy * pitch + xx];
             }
+#endif
         }
     }
     og_dk_sync();
