@@ -164,15 +164,44 @@ __global__ __launch_bounds__(256) void og_stereo_match16_kernel(OgStereoDev S)
     // row list, which holds at most ST_MAXR right keypoints, so it fits the low 16 bits.
     static_assert(ST_MAXR <= 65535, "row-list positions are packed into 16 bits");
     unsigned best = 0xffffffffu;
-    for (int c = cb + l; c < ce; c += 16) {
-        const int iR = RI[c];
-        const orbgpu_kp_dev kpR = KR[iR];
-        if (!(kpR.octave < levelL - 1 || kpR.octave > levelL + 1)) {
-            const float uR = kpR.x;
-            if (uR >= minU && uR <= maxU) {
-                const uint4* q = (const uint4*)(S.R.desc + ((long long)b * S.R.frame_cap + iR) * 32);
-                const int dist = og_hamming(da, db, q[0], q[1]);
-                if (dist < ST_TH_HIGH) best = min(best, ((unsigned)dist << 16) | (unsigned)(c - cb));
+#ifndef OG_ST_BAND_U
+#define OG_ST_BAND_U 4  // band candidates per lane whose dependent loads (list entry, keypoint, descriptor) are batched
+#endif
+    // each stage's loads for OG_ST_BAND_U candidates are issued together: 3 memory round trips per batch instead of 3
+    // per candidate (the candidate order only enters through the packed position, so the batching is exact)
+    for (int c0 = cb + l; c0 < ce; c0 += 16 * OG_ST_BAND_U) {
+        int iR[OG_ST_BAND_U];
+#pragma unroll
+        for (int u = 0; u < OG_ST_BAND_U; u++) {
+            const int c = c0 + 16 * u;
+            iR[u] = c < ce ? RI[c] : -1;
+        }
+        bool pass[OG_ST_BAND_U];
+#pragma unroll
+        for (int u = 0; u < OG_ST_BAND_U; u++) {
+            pass[u] = false;
+            if (iR[u] >= 0) {
+                const orbgpu_kp_dev* kr = KR + iR[u];
+                const int oct = kr->octave;
+                const float uR = kr->x;
+                pass[u] = !(oct < levelL - 1 || oct > levelL + 1) && uR >= minU && uR <= maxU;
+            }
+        }
+        uint4 qa[OG_ST_BAND_U], qb[OG_ST_BAND_U];
+#pragma unroll
+        for (int u = 0; u < OG_ST_BAND_U; u++) {
+            qa[u] = qb[u] = make_uint4(0u, 0u, 0u, 0u);
+            if (pass[u]) {
+                const uint4* q = (const uint4*)(S.R.desc + ((long long)b * S.R.frame_cap + iR[u]) * 32);
+                qa[u] = q[0];
+                qb[u] = q[1];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < OG_ST_BAND_U; u++) {
+            if (pass[u]) {
+                const int dist = og_hamming(da, db, qa[u], qb[u]);
+                if (dist < ST_TH_HIGH) best = min(best, ((unsigned)dist << 16) | (unsigned)(c0 + 16 * u - cb));
             }
         }
     }
