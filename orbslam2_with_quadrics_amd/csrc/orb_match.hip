@@ -576,6 +576,89 @@ __device__ __forceinline__ void og_proj_visit(const Geom& K, const uint8_t* fdes
         }
 }
 
+// og_proj_visit with the candidates' descriptor loads batched: up to 4 candidates that pass the geometric filters are
+// queued (in order) and their descriptors loaded together, so a point's window costs one memory round trip per 4
+// candidates instead of one per candidate.  Same candidates, same order, same visits.
+#ifndef OG_PJ_BATCH
+#define OG_PJ_BATCH 1
+#endif
+template <class Geom, class Visit>
+__device__ __forceinline__ void og_proj_visit_b(const Geom& K, const uint8_t* fdesc, const OgGridGeom& G, const float* sf,
+                                                const OgMapPointsDev& mp, int m, float th, int dkeep, Visit visit)
+{
+    if (!mp.track_in_view[m] || mp.is_bad[m]) return;
+    const int lvl = mp.level[m];
+    float r = mp.view_cos[m] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos, :131-137
+    if (th != 1.0) r *= th;
+    const float R = r * sf[lvl];
+    const float x = mp.proj_x[m], y = mp.proj_y[m];
+    const OgCellRange cr = og_cell_range(G, x, y, R);
+    if (cr.x0 > cr.x1) return;
+    const int minLevel = lvl - 1, maxLevel = lvl;
+    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    uint4 da, db;
+    og_load_desc(mp.desc + (long long)m * 32, da, db);
+    int q0 = 0, q1 = 0, q2 = 0, q3 = 0, o0 = 0, o1 = 0, o2 = 0, o3 = 0, nq = 0;
+    auto flush = [&]() {
+        uint4 a0 = {}, b0 = {}, a1 = {}, b1 = {}, a2 = {}, b2 = {}, a3 = {}, b3 = {};
+        if (nq > 0) og_load_desc(fdesc + (long long)q0 * 32, a0, b0);
+        if (nq > 1) og_load_desc(fdesc + (long long)q1 * 32, a1, b1);
+        if (nq > 2) og_load_desc(fdesc + (long long)q2 * 32, a2, b2);
+        if (nq > 3) og_load_desc(fdesc + (long long)q3 * 32, a3, b3);
+        if (nq > 0) {
+            const int d = og_hamming(da, db, a0, b0);
+            if (d <= dkeep) visit(q0, d, o0);  // og_proj_keep_bound
+        }
+        if (nq > 1) {
+            const int d = og_hamming(da, db, a1, b1);
+            if (d <= dkeep) visit(q1, d, o1);
+        }
+        if (nq > 2) {
+            const int d = og_hamming(da, db, a2, b2);
+            if (d <= dkeep) visit(q2, d, o2);
+        }
+        if (nq > 3) {
+            const int d = og_hamming(da, db, a3, b3);
+            if (d <= dkeep) visit(q3, d, o3);
+        }
+        nq = 0;
+    };
+    for (int ix = cr.x0; ix <= cr.x1; ix++)
+        for (int iy = cr.y0; iy <= cr.y1; iy++) {
+            const int cell = ix * OG_GRID_ROWS + iy;
+            const int je = K.cs(cell + 1);
+            for (int j = K.cs(cell); j < je; j++) {
+                const int idx = K.item(j);
+                const int oct = K.oct(idx);
+                if (bCheckLevels) {
+                    if (oct < minLevel) continue;
+                    if (maxLevel >= 0 && oct > maxLevel) continue;
+                }
+                const float distx = K.x(idx) - x, disty = K.y(idx) - y;
+                if (!(fabsf(distx) < R && fabsf(disty) < R)) continue;
+                if (K.has_ur() && K.ur(idx) > 0) {
+                    const float er = fabsf(mp.proj_xr[m] - K.ur(idx));
+                    if (er > r * sf[lvl]) continue;
+                }
+                if (nq == 0) {
+                    q0 = idx;
+                    o0 = oct;
+                } else if (nq == 1) {
+                    q1 = idx;
+                    o1 = oct;
+                } else if (nq == 2) {
+                    q2 = idx;
+                    o2 = oct;
+                } else {
+                    q3 = idx;
+                    o3 = oct;
+                }
+                if (++nq == 4) flush();
+            }
+        }
+    flush();
+}
+
 // a kept candidate as one dword: keypoint index (15 bits: the claim table of a frame holds < 2^15 keypoints,
 // orbgpu_search_by_projection checks it), distance (9 bits, <= 256), octave (8 bits)
 __device__ __forceinline__ uint32_t og_pj_pack(int idx, int dist, int oct)
@@ -687,10 +770,14 @@ __global__ __launch_bounds__(PF_NT) void og_projb_fill_kernel(OgFrameDev Fb, OgG
     auto run = [&](const auto& K) {
         for (int m = blockIdx.x * PF_NT + tid; m < q.m; m += PF_WG * PF_NT) {
             int n = 0;
-            og_proj_visit(K, F.desc, G, sf, q, m, th, dkeep, [&](int idx, int dist, int oct) {
+            auto put = [&](int idx, int dist, int oct) {
                 if (n < OG_PJ_K) S[(long long)n * stride + m] = og_pj_pack(idx, dist, oct);
                 n++;
-            });
+            };
+            if (OG_PJ_BATCH)
+                og_proj_visit_b(K, F.desc, G, sf, q, m, th, dkeep, put);
+            else
+                og_proj_visit(K, F.desc, G, sf, q, m, th, dkeep, put);
             KEPT[m] = n;
         }
     };
