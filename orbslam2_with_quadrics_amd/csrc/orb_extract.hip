@@ -2816,6 +2816,12 @@ __global__ __launch_bounds__(OCT_NT) void og_octree_big_kernel(OgPlan P, int l0,
 // ------------------------------------------------------------------------------------------------
 // k4: orientation + blur + rBRIEF + assembly (src/ORBextractor.cc:77-147, 851-852, 1076-1104)
 // ------------------------------------------------------------------------------------------------
+// BORDER_REFLECT_101 for an index at most n - 2 outside [0, n): one reflection (the describe window of a keypoint at
+// least 19 px inside its level overshoots by a few pixels), no loop
+__device__ __forceinline__ int og_reflect101_1(int i, int n)
+{
+    return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
+}
 __device__ __forceinline__ int og_reflect101(int i, int n)
 {
     if (n == 1) return 0;
@@ -3070,13 +3076,21 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 #ifndef OG_DK_BORDER_RB
 #define OG_DK_BORDER_RB 22  // rows per batch of loads in flight
 #endif
-            const int xx = og_reflect101(cx - 21 + min(lane, RAW_W - 1), lw);
+            // (one reflection is exact: keypoints lie in [19, size - 19) of their level, so the window spans
+            // [-2, size + 1] and a level holding a keypoint is at least 39 px)
+            unsigned xx = (unsigned)og_reflect101_1(cx - 21 + min(lane, RAW_W - 1), lw);
+            // loads from the uniform base of the lowest row the window can reflect to, plus a 32-bit lane offset
+            // (saddr + voffset loads; < 47 rows x 2^24)
+            const int y0r = max(cy - 23, 0);
+            const uint8_t* wbase = img + (long long)y0r * pitch;
             for (int r0 = 0; r0 < RAW_W; r0 += OG_DK_BORDER_RB) {
                 uint32_t v[OG_DK_BORDER_RB];
 #pragma unroll
                 for (int k = 0; k < OG_DK_BORDER_RB; k++) {
-                    const int yy = og_reflect101(cy - 21 + min(r0 + k, RAW_W - 1), lh);
-                    v[k] = img[(long long)yy * pitch + xx];
+                    const int yy = og_reflect101_1(cy - 21 + min(r0 + k, RAW_W - 1), lh);
+                    unsigned off = __umul24((unsigned)(yy - y0r), (unsigned)pitch & (OG_MAX_PITCH - 1)) + xx;
+                    __asm__("" : "+v"(off));
+                    v[k] = wbase[off];
                 }
 #pragma unroll
                 for (int k = 0; k < OG_DK_BORDER_RB; k++)
