@@ -1130,14 +1130,14 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     FAST_PROF(0);
     uint32_t sroi[2][4];
     og_fastq_roi_load(b, tid, sroi);
-    og_fastq_roi_put(b, tid, sroi, roiq);
     {
-        // zero only the score-map rows the block reads (dh + 3: gap rows included); later blocks of the workgroup find
-        // it zero again (the emission clears every cell stage 2 wrote), so they zero nothing
+        // zero only the score-map rows the block reads (dh + 3: gap rows included), while the ROI loads are in flight;
+        // later blocks of the workgroup find it zero again (the emission clears every cell stage 2 wrote)
         const int msz = KB == 1 ? min(FB_MSZ, ((b.dh + 3) * FB_MSW + 15) & ~15) : FB_MSZ;
         for (int idx = tid * 16; idx < msz; idx += FB_NT * 16) *(uint4*)&Ms[idx] = make_uint4(0u, 0u, 0u, 0u);
     }
     if (tid == 0) sh_ns = 0;
+    og_fastq_roi_put(b, tid, sroi, roiq);
     __syncthreads();
     FAST_PROF(1);
 #pragma unroll 1
@@ -2884,6 +2884,37 @@ constexpr OgDisk og_make_disk()
     return d;
 }
 __constant__ OgDisk og_disk = og_make_disk();
+
+// IC_Angle by rows with v_dot4 (OG_DK_ICDOT): item t < 279 = (disk row v = t / 9 - 15, window dword j = t % 9, which
+// holds window columns 4 + 4j .. 7 + 4j, i.e. u = 4j - 17 .. 4j - 14).  Per item: the byte mask of the columns inside
+// the disk row (|u| <= umax[|v|]), the weights u + 16 of those bytes (in [1, 31]; bytes outside the disk are masked
+// to 0 first), and the dword's LDS byte offset | v << 16.  m10 = sum (u + 16) I - 16 sum I, m01 = sum v sum I.
+#define OG_IC_ITEMS 320  // 279 items padded to 5 x 64 lanes (padding: mask 0)
+struct OgIcTab {
+    uint32_t mask[OG_IC_ITEMS], wt[OG_IC_ITEMS], ov[OG_IC_ITEMS];
+};
+constexpr OgIcTab og_make_ic()
+{
+    OgIcTab t{};
+    constexpr int umax[16] = {OG_UMAX};
+    for (int i = 0; i < 279; i++) {
+        const int v = i / 9 - 15, j = i % 9, av = v < 0 ? -v : v;
+        uint32_t m = 0, w = 0;
+        for (int k = 0; k < 4; k++) {
+            const int u = 4 * j + k - 17;
+            const int au = u < 0 ? -u : u;
+            if (au <= umax[av]) {
+                m |= 0xffu << (8 * k);
+                w |= (uint32_t)(u + 16) << (8 * k);
+            }
+        }
+        t.mask[i] = m;
+        t.wt[i] = w;
+        t.ov[i] = (uint32_t)((21 + v) * 52 + 4 + 4 * j) | ((uint32_t)(v & 0xffff) << 16);  // RAW_S = 52
+    }
+    return t;
+}
+__constant__ OgIcTab og_ic = og_make_ic();
 // GaussianBlur 7x7 sigma 2 integer kernels by ORBGPU_SEM_BLUR_* variant, c0 | c1 << 8 | c2 << 16 | c3 << 24 for
 // [c0,c1,c2,c3,c2,c1,c0]: cvRound(256 g) (sum 257) twice, the bit-exact kernel with centre 256 - 2 sum(sides),
 // the error-diffused bit-exact kernel
@@ -2941,17 +2972,27 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     int l = -1, li = 0, total = 0;
     if (P.nlevels == 8) {
 #if defined(__HIP_DEVICE_COMPILE__)
-        // one 32-byte scalar load of the frame's 8 level counts and an unrolled search (a DPP scan over a per-lane
-        // vector load was 3 % slower: the vector load's round trip at the kernel's start)
+        // one 32-byte scalar load of the frame's 8 level counts (a DPP scan over a per-lane vector load was 3 % slower:
+        // the vector load's round trip at the kernel's start).  The level is the number of prefix sums <= g (they are
+        // nondecreasing) and its first keypoint the last such prefix sum: 4 scalar instructions per level, the compare's
+        // SCC feeding both the select and the add-with-carry
         const og_u32x8 c8 = ((const __attribute__((address_space(4))) og_u32x8*)(oct_count + 8 * f))[0];
+        int nl = 0, st = 0;
+        const int gu = __builtin_amdgcn_readfirstlane(g);
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             const int c = (int)c8[q];
-            if (l < 0 && g < total + c) {
-                l = q;
-                li = g - total;
-            }
-            total += c;
+            __asm__("s_add_i32 %0, %0, %3\n\t"
+                    "s_cmp_ge_i32 %4, %0\n\t"
+                    "s_cselect_b32 %2, %0, %2\n\t"
+                    "s_addc_u32 %1, %1, 0"
+                    : "+s"(total), "+s"(nl), "+s"(st)
+                    : "s"(c), "s"(gu)
+                    : "scc");
+        }
+        if (nl < 8) {
+            l = nl;
+            li = g - st;
         }
 #endif
     } else {
@@ -2975,7 +3016,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     unsigned resp = 0;  // response key (og_harris_key under ORBGPU_SEM_SCORE_HARRIS, else the FAST score)
     if (active) {
         const OgLevel& L = P.lv[l];
-        const long long o = (long long)f * P.kcap_total + L.koff + li;
+        const unsigned o = (unsigned)f * (unsigned)P.kcap_total + (unsigned)(L.koff + li);  // < 2^31 (host plan)
         const uint32_t xy = oct_xy[o];
         cx = (int)(xy & 0xffff);
         cy = (int)(xy >> 16);
@@ -3109,7 +3150,26 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     const uint8_t* Rb = R;  // Rb[r * RAW_S + c] = window pixel (r, c)
     // ---- IC_Angle on the unblurred level (:77-104); integer moments are order-independent
     int m01 = 0, m10 = 0;
-    if (active) {
+#ifndef OG_DK_ICDOT
+#define OG_DK_ICDOT 1  // 1: disk rows by v_dot4 over masked window dwords (og_ic); 0: (u, v) point pairs (og_disk)
+#endif
+    if (active && OG_DK_ICDOT) {
+        static_assert(RAW_S == 52, "og_make_ic's row stride");
+        const uint32_t rb = og_lds_addr(Rb);
+        int a10 = 0, a01 = 0;
+#pragma unroll
+        for (int it = 0; it < OG_IC_ITEMS / 64; it++) {
+            const int t = lane + 64 * it;
+            const uint32_t msk = og_ic.mask[t], wt = og_ic.wt[t], ov = og_ic.ov[t];
+            typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+            const uint32_t d = *(lds_u32*)(uintptr_t)(rb + (ov & 0xffffu)) & msk;
+            const int s0 = (int)__builtin_amdgcn_udot4(d, 0x01010101u, 0u, false);
+            a10 += (int)__builtin_amdgcn_udot4(d, wt, 0u, false) - 16 * s0;
+            a01 += ((int)ov >> 16) * s0;
+        }
+        m01 = og_wave_sum(a01);
+        m10 = og_wave_sum(a10);
+    } else if (active) {
         const uint8_t* ctr = Rb + 21 * RAW_S + 21;
         if (lane < 31) m10 += (lane - 15) * ctr[lane - 15];
         short e[OG_DISK_ITEMS / 64];
@@ -3367,10 +3427,10 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         brief_words(std::integral_constant<bool, true>{}, words);
     else
         brief_words(std::integral_constant<bool, false>{}, words);
-    const long long o = (long long)f * P.frame_cap + g;
+    const unsigned o = (unsigned)f * (unsigned)P.frame_cap + (unsigned)g;  // < 2^31 (host plan)
     if (lane < 4) {
         u64 v = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
-        ((u64*)(desc + o * 32))[lane] = v;
+        ((u64*)(desc + (size_t)o * 32))[lane] = v;
     }
     if (lane == 0) {
         const OgLevel& L = P.lv[l];

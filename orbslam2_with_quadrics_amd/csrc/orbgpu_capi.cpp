@@ -510,6 +510,11 @@ static int ensure_batch(orbgpu_ctx* c, int B)
     if (c->Bcap >= B) return ORBGPU_OK;
     const OgPlan& P = c->plan;
     const size_t Bn = (size_t)B;
+    // the describe kernel indexes keypoint slots of a batch with 32-bit offsets (frame x frame_cap + slot)
+    if ((long long)B * (long long)P.frame_cap >= (1LL << 31)) {
+        c->err = "batch x keypoint capacity of 2^31 or more";
+        return ORBGPU_ERR_UNSUPPORTED;
+    }
     HIP_TRY(c, ensure(c->pyr, Bn * (size_t)P.pyr_per_frame));
     HIP_TRY(c, ensure(c->cand, Bn * (size_t)P.cand_per_frame));
     HIP_TRY(c, ensure(c->cand_count, Bn * (size_t)P.nlevels));
