@@ -3197,6 +3197,15 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     // (row 2rp, row 2rp+1) u16 pairs Hp[rp][col]
     constexpr uint32_t gc = og_blur_coefs[BV];  // c0 | c1 << 8 | c2 << 16 | c3 << 24
     constexpr uint32_t c0 = gc & 0xff, c1 = (gc >> 8) & 0xff, c2 = (gc >> 16) & 0xff, c3 = gc >> 24;
+#ifndef OG_DK_PATPRE
+#define OG_DK_PATPRE 1  // 1: the lane's four rBRIEF test pairs are loaded here, in flight over the blur passes
+                        // (0: at their first use, one round trip on every wave's path)
+#endif
+    float4 pfs[4];
+    if (OG_DK_PATPRE) {
+#pragma unroll
+        for (int t = 0; t < 4; t++) pfs[t] = og_pattern_f[lane + 64 * t];
+    }
     if (active) {
         constexpr uint32_t glo = gc, ghi = c2 | (c1 << 8) | (c0 << 16);
         for (int it = lane; it < HP_ROWS * 10; it += 64) {
@@ -3374,7 +3383,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 #define OG_DK_PATF 1  // pattern from the float table (0: bytes + conversions)
 #endif
 #if OG_DK_PATF
-            const float4 pf = og_pattern_f[p];
+            const float4 pf = OG_DK_PATPRE ? pfs[t] : og_pattern_f[p];
             const float pfx[2] = {pf.x, pf.z}, pfy[2] = {pf.y, pf.w};
 #else
             const signed char* pt = og_pattern + 4 * p;
