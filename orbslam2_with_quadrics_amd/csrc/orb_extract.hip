@@ -2915,6 +2915,27 @@ constexpr OgIcTab og_make_ic()
     return t;
 }
 __constant__ OgIcTab og_ic = og_make_ic();
+#ifndef OG_DK_ICDOT
+#define OG_DK_ICDOT 1  // 1: disk rows by v_dot4 over masked window dwords (og_ic); 0: (u, v) point pairs (og_disk)
+#endif
+// the same table lane-major (OG_DK_ICPRE): lane i's items i, i + 64, .. i + 256 as (mask, wt, ov) triples in 16 words,
+// four 16-byte loads from one base
+struct OgIcLane {
+    uint32_t w[64][16];
+};
+constexpr OgIcLane og_make_icl()
+{
+    const OgIcTab t = og_make_ic();
+    OgIcLane l{};
+    for (int i = 0; i < 64; i++)
+        for (int it = 0; it < OG_IC_ITEMS / 64; it++) {
+            l.w[i][3 * it] = t.mask[i + 64 * it];
+            l.w[i][3 * it + 1] = t.wt[i + 64 * it];
+            l.w[i][3 * it + 2] = t.ov[i + 64 * it];
+        }
+    return l;
+}
+__constant__ OgIcLane og_icl = og_make_icl();
 // GaussianBlur 7x7 sigma 2 integer kernels by ORBGPU_SEM_BLUR_* variant, c0 | c1 << 8 | c2 << 16 | c3 << 24 for
 // [c0,c1,c2,c3,c2,c1,c0]: cvRound(256 g) (sum 257) twice, the bit-exact kernel with centre 256 - 2 sum(sides),
 // the error-diffused bit-exact kernel
@@ -2957,6 +2978,20 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     __shared__ __attribute__((aligned(16))) uint32_t hp[DK_WAVES][HP_ROWS * HP_S];
     // w is wave-uniform: made explicit, so the keypoint index, its level and its window origin live in SGPRs
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+#ifndef OG_DK_ICPRE
+#define OG_DK_ICPRE 1  // 1: the lane's IC_Angle items (og_icl) are loaded first, in flight over the level search and the
+                       // window load (0: og_ic after the window barrier, one round trip on every wave's path)
+#endif
+    uint4 icq[4] = {};
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (OG_DK_ICDOT && OG_DK_ICPRE) {
+        typedef const __attribute__((address_space(1))) uint4 g_u4;
+        g_u4* ib = (g_u4*)&og_icl.w[0][0];
+        __asm__("" : "+s"(ib));  // one SGPR base: a lane offset and 16-byte immediate steps
+#pragma unroll
+        for (int k = 0; k < 4; k++) icq[k] = ib[4 * lane + k];
+    }
+#endif
 #ifndef OG_DESC_XCD_REMAP
 #define OG_DESC_XCD_REMAP 1  // experiment switch: 0 = plain dispatch order
 #endif
@@ -3150,9 +3185,6 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     const uint8_t* Rb = R;  // Rb[r * RAW_S + c] = window pixel (r, c)
     // ---- IC_Angle on the unblurred level (:77-104); integer moments are order-independent
     int m01 = 0, m10 = 0;
-#ifndef OG_DK_ICDOT
-#define OG_DK_ICDOT 1  // 1: disk rows by v_dot4 over masked window dwords (og_ic); 0: (u, v) point pairs (og_disk)
-#endif
     if (active && OG_DK_ICDOT) {
         static_assert(RAW_S == 52, "og_make_ic's row stride");
         const uint32_t rb = og_lds_addr(Rb);
@@ -3160,7 +3192,20 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 #pragma unroll
         for (int it = 0; it < OG_IC_ITEMS / 64; it++) {
             const int t = lane + 64 * it;
-            const uint32_t msk = og_ic.mask[t], wt = og_ic.wt[t], ov = og_ic.ov[t];
+            uint32_t msk, wt, ov;
+            if (OG_DK_ICPRE) {
+                auto word = [&](int i) -> uint32_t {
+                    const uint4 q = icq[i >> 2];
+                    return (i & 3) == 0 ? q.x : (i & 3) == 1 ? q.y : (i & 3) == 2 ? q.z : q.w;
+                };
+                msk = word(3 * it);
+                wt = word(3 * it + 1);
+                ov = word(3 * it + 2);
+            } else {
+                msk = og_ic.mask[t];
+                wt = og_ic.wt[t];
+                ov = og_ic.ov[t];
+            }
             typedef const __attribute__((address_space(3))) uint32_t lds_u32;
             const uint32_t d = *(lds_u32*)(uintptr_t)(rb + (ov & 0xffffu)) & msk;
             const int s0 = (int)__builtin_amdgcn_udot4(d, 0x01010101u, 0u, false);
@@ -3201,11 +3246,16 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 #define OG_DK_PATPRE 1  // 1: the lane's four rBRIEF test pairs are loaded here, in flight over the blur passes
                         // (0: at their first use, one round trip on every wave's path)
 #endif
-    float4 pfs[4];
+    float4 pfs[4] = {};
+#if defined(__HIP_DEVICE_COMPILE__)
     if (OG_DK_PATPRE) {
+        typedef const __attribute__((address_space(1))) float4 g_f4;
+        g_f4* pb = (g_f4*)og_pattern_f;
+        __asm__("" : "+s"(pb));  // one SGPR base: a lane offset and 1 KB immediate steps
 #pragma unroll
-        for (int t = 0; t < 4; t++) pfs[t] = og_pattern_f[lane + 64 * t];
+        for (int t = 0; t < 4; t++) pfs[t] = pb[lane + 64 * t];
     }
+#endif
     if (active) {
         constexpr uint32_t glo = gc, ghi = c2 | (c1 << 8) | (c0 << 16);
         for (int it = lane; it < HP_ROWS * 10; it += 64) {
