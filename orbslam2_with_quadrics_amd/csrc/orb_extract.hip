@@ -534,6 +534,14 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     const int dxt = bx0 + 4 * cth;
 #pragma unroll
     for (int k = 0; k < 4; k++) og_rz_weights<FX>(g.xtabA, g.xmaxA, min(cA + k, ac1), sc0, sxA, wtA, k);
+#ifndef OG_RZ_BPRE
+#define OG_RZ_BPRE 0  // 1: the B pass's x weights are loaded here too, in flight over the staging and the A pass (72
+                      // VGPRs instead of 54, no gain: profiles/sweeps/r04_ab_rzbpre.txt); 0: after the A pass's barrier
+#endif
+    if (OG_RZ_BPRE) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) og_rz_weights<FX>(g.xtabB, g.xmaxB, min(dxt + k, g.bw - 1), ac0, sxB, wtB, k);
+    }
     // staging addresses: the region's first row (wave-uniform, SGPRs) rounded down to 16 bytes plus a 32-bit lane
     // offset; chunk -> (row, chunk) with the exact float quotient (nIt < 2^14)
     const uint8_t* rbase = src + (long long)f * src_fstride + (long long)sr0 * src_pitch + sc0;
@@ -612,8 +620,10 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     __syncthreads();
     // ---- level B tile from the A region
     if (dxt >= g.bw) return;
+    if (!OG_RZ_BPRE) {
 #pragma unroll
-    for (int k = 0; k < 4; k++) og_rz_weights<FX>(g.xtabB, g.xmaxB, min(dxt + k, g.bw - 1), ac0, sxB, wtB, k);
+        for (int k = 0; k < 4; k++) og_rz_weights<FX>(g.xtabB, g.xmaxB, min(dxt + k, g.bw - 1), ac0, sxB, wtB, k);
+    }
     const int n = min(4, g.bw - dxt);
     uint8_t* DB = dstB + (long long)f * dst_fstride + dxt;
 #if OG_RZ_WORDS
