@@ -3005,23 +3005,35 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 #ifndef OG_DESC_XCD_REMAP
 #define OG_DESC_XCD_REMAP 1  // experiment switch: 0 = plain dispatch order
 #endif
-    const unsigned lin = OG_DESC_XCD_REMAP ? og_xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y)
-                                           : blockIdx.y * gridDim.x + blockIdx.x;
+#ifndef OG_DK_ARGS1
+#define OG_DK_ARGS1 0  // 1: the prologue's kernel arguments are fetched together behind an asm barrier, one scalar-cache
+                       // round trip instead of four, yet describe +3.5 % (profiles/sweeps/r04_ab_dkargs.txt); 0: the
+                       // compiler's order
+#endif
+    unsigned gx = gridDim.x, gy = gridDim.y, dm = dmagic;
+    int nlv = P.nlevels, kct = P.kcap_total;
+    long long p0 = pitch0, fs0 = fstride0, ppf = P.pyr_per_frame;
+    const int* occ = oct_count;
+    if (OG_DK_ARGS1)
+        __asm__ volatile("" : "+s"(gx), "+s"(gy), "+s"(dm), "+s"(nlv), "+s"(kct), "+s"(p0), "+s"(fs0), "+s"(ppf), "+s"(occ)
+                            : "s"(img0), "s"(pyr), "s"(oct_xy), "s"(oct_resp));  // (the pointers: fetched, not opaque)
+    const unsigned lin = OG_DESC_XCD_REMAP ? og_xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy)
+                                           : blockIdx.y * gx + blockIdx.x;
     // frame = lin / gridDim.x by the host's multiply-high constant (exact for every lin of the launch, checked on the
     // host; 0: the division)
-    const unsigned fq = dmagic ? __umulhi(lin, dmagic) : lin / gridDim.x;
+    const unsigned fq = dm ? __umulhi(lin, dm) : lin / gx;
     const int f = (int)fq;
-    const int g = (int)(lin - fq * gridDim.x) * DK_WAVES + w;
+    const int g = (int)(lin - fq * gx) * DK_WAVES + w;
     // which level does keypoint g belong to (levels concatenated 0..L-1, :1076-1104); with 8 levels the frame's
     // counts are one 32-byte scalar load and the search is unrolled (per keypoint wave: the scalar unit is shared)
     int l = -1, li = 0, total = 0;
-    if (P.nlevels == 8) {
+    if (nlv == 8) {
 #if defined(__HIP_DEVICE_COMPILE__)
         // one 32-byte scalar load of the frame's 8 level counts (a DPP scan over a per-lane vector load was 3 % slower:
         // the vector load's round trip at the kernel's start).  The level is the number of prefix sums <= g (they are
         // nondecreasing) and its first keypoint the last such prefix sum: 4 scalar instructions per level, the compare's
         // SCC feeding both the select and the add-with-carry
-        const og_u32x8 c8 = ((const __attribute__((address_space(4))) og_u32x8*)(oct_count + 8 * f))[0];
+        const og_u32x8 c8 = ((const __attribute__((address_space(4))) og_u32x8*)(occ + 8 * f))[0];
         int nl = 0, st = 0;
         const int gu = __builtin_amdgcn_readfirstlane(g);
 #pragma unroll
@@ -3041,8 +3053,8 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         }
 #endif
     } else {
-        for (int q = 0; q < P.nlevels; q++) {
-            const int c = oct_count[f * P.nlevels + q];
+        for (int q = 0; q < nlv; q++) {
+            const int c = occ[f * nlv + q];
             if (l < 0 && g < total + c) {
                 l = q;
                 li = g - total;
@@ -3050,6 +3062,11 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
             total += c;
         }
     }
+    // wave-uniform by construction: SGPRs, so that P.lv[l] below is a scalar load, not a vector load from the kernarg
+    // segment (the generic branch's loop would otherwise make them VGPRs)
+    l = __builtin_amdgcn_readfirstlane(l);
+    li = __builtin_amdgcn_readfirstlane(li);
+    total = __builtin_amdgcn_readfirstlane(total);
     if (g == 0 && lane == 0) counts[f] = total;
     const bool active = l >= 0;
     uint8_t* R = raw[w];
@@ -3061,22 +3078,20 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     unsigned resp = 0;  // response key (og_harris_key under ORBGPU_SEM_SCORE_HARRIS, else the FAST score)
     if (active) {
         const OgLevel& L = P.lv[l];
-        const unsigned o = (unsigned)f * (unsigned)P.kcap_total + (unsigned)(L.koff + li);  // < 2^31 (host plan)
+        // the level's fields and the frame's image origin fetched together (one scalar round trip before the
+        // keypoint's position; the image origin by selects, not a branch)
+        int koff = L.koff, Lp = L.pitch;
+        long long Lpo = L.pyr_off;
+        lw = L.w;
+        lh = L.h;
+        if (OG_DK_ARGS1) __asm__ volatile("" : "+s"(koff), "+s"(Lp), "+s"(Lpo), "+s"(lw), "+s"(lh));
+        const unsigned o = (unsigned)f * (unsigned)kct + (unsigned)(koff + li);  // < 2^31 (host plan)
         const uint32_t xy = oct_xy[o];
         cx = (int)(xy & 0xffff);
         cy = (int)(xy >> 16);
         resp = oct_resp[o];
-        lw = L.w;
-        lh = L.h;
-        const uint8_t* img;
-        long long pitch;
-        if (l == 0) {
-            img = img0 + (long long)f * fstride0;
-            pitch = pitch0;
-        } else {
-            img = pyr + (long long)f * P.pyr_per_frame + L.pyr_off;
-            pitch = L.pitch;
-        }
+        const uint8_t* img = l == 0 ? img0 + (long long)f * fs0 : pyr + ((long long)f * ppf + Lpo);
+        const long long pitch = l == 0 ? p0 : (long long)Lp;
         if (cx >= 21 && cy >= 21 && cx + 28 < lw && cy + 21 < lh) {
             // interior (almost every keypoint): 43 rows x 11 dwords.  Each dword comes from two aligned loads
             // funnel-shifted by the row's own misalignment (any pitch, e.g. a contiguous 1241-px KITTI image);
