@@ -1130,6 +1130,12 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     // stage 2 and stored once stage 2 is done with roiq, so only the first block of a workgroup waits for its ROI
     int j = 0, p = 0;
     OgFB b;
+#ifndef OG_FASTQ_ARGS1
+#define OG_FASTQ_ARGS1 1  // 1: every kernel argument the block decode reads is fetched before the first of them is used,
+                          // one scalar-cache round trip (0: the compiler's order, three round trips before the block record)
+#endif
+    if (OG_FASTQ_ARGS1)
+        __asm__ volatile("" ::"s"(blocks), "s"(nb), "s"(img0), "s"(pitch0), "s"(fstride0), "s"(pyr), "s"(pyr_per_frame));
     for (;; j++) {  // uniform: the first valid block of the chain (the table pads each level to 8 entries)
         if (j >= KB) return;
         p = (int)blockIdx.x + j * (int)gridDim.x;
