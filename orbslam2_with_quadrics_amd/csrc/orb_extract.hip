@@ -1158,7 +1158,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     FAST_PROF(1);
 #pragma unroll 1
     for (;;) {
-    const int dw = b.dw, dh = b.dh, wC = b.wC, hC = b.hC;
+    const int dh = b.dh, wC = b.wC, hC = b.hC;  // (the block's width enters through its column masks, b.colw)
     const uint2* Tq = roiq + b.mis;  // Tq[r * FQ_S + x] = quad (x, x + 16, x + 32, x + 48) of ROI row r
     // ---- stage 1: quick test on every detection pixel, four per lane.  Unit u = (row group g = u >> 1, half
     // h = u & 1) covers ROI rows 8g + 2h + {0, 4, 1, 5} (the lane's 16-lane group picks one); wave w takes units
@@ -3288,7 +3288,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     }
 #endif
     if (active) {
-        constexpr uint32_t glo = gc, ghi = c2 | (c1 << 8) | (c0 << 16);
+        [[maybe_unused]] constexpr uint32_t glo = gc, ghi = c2 | (c1 << 8) | (c0 << 16);  // (OG_DK_HSHIFTW 0)
         for (int it = lane; it < HP_ROWS * 10; it += 64) {
             const int rp = it / 10, g = it - rp * 10;
             uint32_t hv[2][4];
