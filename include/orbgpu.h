@@ -386,6 +386,13 @@ int orbgpu_debug_octree_profile(orbgpu_ctx* ctx, unsigned long long* out, int n)
  * of the middle frame of the last launch, 8 per block (ROI, stage 1-3, counts, reservation, end, survivors | level
  * << 32).  ORBGPU_ERR_UNSUPPORTED in product builds. */
 int orbgpu_debug_fast_profile(orbgpu_ctx* ctx, unsigned long long* out, int n);
+/* Test hook: make the context's SearchByProjection launches (host and batch forms) take the paths of frames too large
+ * for the LDS, so tests can pin them against the oracle on ordinary frames.  flags: ORBGPU_DEBUG_PROJ_FILL_HBM =
+ * enumerate windows from the frame geometry in HBM instead of the LDS copy; ORBGPU_DEBUG_PROJ_RESOLVE_HBM = run the
+ * claim rounds on the candidate slots in HBM instead of LDS-staged lists.  0 restores the default. */
+#define ORBGPU_DEBUG_PROJ_FILL_HBM 1
+#define ORBGPU_DEBUG_PROJ_RESOLVE_HBM 2
+int orbgpu_debug_set_projection_paths(orbgpu_ctx* ctx, int flags);
 /* Exhaustive pin of the device restatements of glibc sincosf (fn 0; src/ORBextractor.cc:113) and logf (fn 1;
  * src/MapPoint.cc:410): every float bit pattern u in [begin, end) is evaluated on `device` and folded into
  * out[(u >> chunk_log2) - (begin >> chunk_log2)] (nchunks entries) as the order-free hash of

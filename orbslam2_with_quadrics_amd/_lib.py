@@ -27,7 +27,7 @@ EXPORTS = [
     "orbgpu_memset_d", "orbgpu_prev_matched_from_frame", "orbgpu_memcpy_d2d_async",
     "orbgpu_batch_candidate_total", "orbgpu_compute_stereo_matches", "orbgpu_compute_stereo_matches_batch",
     "orbgpu_is_in_frustum", "orbgpu_search_by_projection_last_frame", "orbgpu_debug_octree_profile",
-    "orbgpu_debug_fast_profile",
+    "orbgpu_debug_fast_profile", "orbgpu_debug_set_projection_paths",
     "orbgpu_stage_marks", "orbgpu_undistort_keypoints", "orbgpu_compute_image_bounds", "orbgpu_set_undistortion",
     "orbgpu_batch_outputs_undistorted", "orbgpu_search_by_projection_keyframe",
     "orbgpu_search_by_projection_keyframe_levels",
@@ -174,6 +174,7 @@ def _declare(L):
     L.orbgpu_batch_candidate_total.restype = C.c_longlong
     L.orbgpu_debug_octree_profile.argtypes = [vp, vp, i32]
     L.orbgpu_debug_fast_profile.argtypes = [vp, vp, i32]
+    L.orbgpu_debug_set_projection_paths.argtypes = [vp, i32]
     L.orbgpu_search_by_projection_keyframe.argtypes = [vp, C.POINTER(FrameView), C.POINTER(Camera),
                                                        C.POINTER(KeyFrameView), f32, i32, i32, vp, C.POINTER(i32)]
     L.orbgpu_search_by_projection_keyframe_levels.argtypes = [vp, C.POINTER(FrameView), C.POINTER(Camera),

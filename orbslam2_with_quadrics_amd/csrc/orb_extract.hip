@@ -80,9 +80,6 @@ __device__ __forceinline__ uint32_t og_rz_vert(uint32_t b0, uint32_t d0, uint32_
 // (og_rz_weights; <= 2048 * 16 = 32768 fits the u16 dot operand), so D = 16 d and D & ~0xff = (d >> 4) << 8, and
 // v_mul_hi_u32_u24(b << 8, (d >> 4) << 8) = (b * (d >> 4)) >> 16 exactly (operands < 2^24: b <= 2049,
 // D <= 255 * 2049 * 16): two ops per term instead of three.  FX = true is og_rz_vert.
-#ifndef OG_RZ_MULHI
-#define OG_RZ_MULHI 1
-#endif
 __device__ __forceinline__ uint32_t og_mulhi_u24(uint32_t a, uint32_t b)
 {
     uint32_t r;
@@ -92,7 +89,7 @@ __device__ __forceinline__ uint32_t og_mulhi_u24(uint32_t a, uint32_t b)
 template <bool FX>
 __device__ __forceinline__ uint32_t og_rz_vert16(uint32_t b0, uint32_t D0, uint32_t b1, uint32_t D1)
 {
-    if (FX || !OG_RZ_MULHI) return og_rz_vert<FX>(b0, D0, b1, D1);  // unscaled weights: D = d
+    if (FX) return og_rz_vert<FX>(b0, D0, b1, D1);  // unscaled weights: D = d
     return min((og_mulhi_u24(b0 << 8, D0 & ~0xffu) + og_mulhi_u24(b1 << 8, D1 & ~0xffu) + 2u) >> 2,
                255u);
 }
@@ -250,13 +247,6 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
 
 // 4 horizontally adjacent outputs of one row from two LDS source rows: sx = byte offsets in the rows, weights
 // (a0, a1) per column (a1 = 0 at the right border), vertical weights (yz, yw)
-#ifndef OG_RZ_BREUSE
-#define OG_RZ_BREUSE 1  // og_resize2_kernel's B pass forms each distinct A row's horizontal sums once per wave
-#endif
-#ifndef OG_RZ_SDWA
-#define OG_RZ_SDWA 1  // 1: each output byte's final min(., 255) writes its byte of the packed dword (SDWA dst_sel), no
-                      // shift-or per byte; 0: shift and or
-#endif
 template <bool FX>
 __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t* R1, const int* sx,
                                                const og_rz_u16x2* wt, unsigned yz, unsigned yw)
@@ -268,8 +258,9 @@ __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t*
         const uint32_t p1 = (uint32_t)R1[sx[k]] | ((uint32_t)R1[sx[k] + 1] << 16);
         const uint32_t d0 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[k], 0u, false);
         const uint32_t d1 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[k], 0u, false);
-        if (!FX && OG_RZ_MULHI && OG_RZ_SDWA) {
-            // og_rz_vert16 up to its final min, which writes byte k of `packed` (the other bytes preserved)
+        if (!FX) {
+            // og_rz_vert16 up to its final min, which writes byte k of `packed` (the other bytes preserved: SDWA
+            // dst_sel, no shift-or per byte)
             const uint32_t t = (og_mulhi_u24(yz << 8, d0 & ~0xffu) + og_mulhi_u24(yw << 8, d1 & ~0xffu) + 2u) >> 2;
             if (k == 0)
                 __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
@@ -290,63 +281,6 @@ __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t*
     return packed;
 }
 
-// The same 4 outputs from dword reads: a lane's 4 source pairs (sx[k], sx[k] + 1) lie within 10 bytes of the
-// 4-byte-aligned word holding sx[0] (sx[3] - sx[0] <= ceil(3 * 1.6) = 5, scale <= 1.6 on the host), so one
-// ds_read2_b32 + one ds_read_b32 (F0..F2) replace the 8 byte reads of a row, and v_perm picks each pair out of
-// (F1:F0) or (F2:F1).  The byte reads put ~38 distinct dwords of a 32-lane group on 32 banks (2-way conflicts,
-// 40 % of the pyramid's LDS cycles); the dword reads touch ~13.  OgRzSel holds a lane's selectors for one row
-// alignment sh = (row address + sx[0]) & 3: pair k comes from the high window (F2:F1) where its offset
-// o_k = sx[k] - sx[0] + sh is >= 6 (pairs 0 and 1 never: o_1 <= 5).
-#ifndef OG_RZ_WORDS
-#define OG_RZ_WORDS 0  // 1: dword reads (bit-exact, pyramid +1.5 %: the LDS reads do not bound it;
-                       // profiles/sweeps/r03_ab_resize_words.txt); 0: 8 byte reads per row and quad (og_rz_quad)
-#endif
-struct OgRzSel {
-    uint32_t sel[4];
-    bool hi2, hi3;
-};
-__device__ __forceinline__ OgRzSel og_rz_sel(const int* sx, unsigned sh)
-{
-    OgRzSel s;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const unsigned o = (unsigned)(sx[k] - sx[0]) + sh;
-        const unsigned oo = (k >= 2 && o >= 6u) ? o - 4u : o;
-        s.sel[k] = 0x0c000c00u | oo | ((oo + 1u) << 16);
-        if (k == 2) s.hi2 = o >= 6u;
-        if (k == 3) s.hi3 = o >= 6u;
-    }
-    return s;
-}
-// horizontal sums (d of og_rz_vert) of the 4 outputs from the row at LDS byte address `row` (+ sx[0])
-__device__ __forceinline__ void og_rz_hrow(uint32_t rowaddr, int sx0, const OgRzSel& s, const og_rz_u16x2* wt,
-                                           uint32_t* d)
-{
-    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
-    lds_u32* F = (lds_u32*)(uintptr_t)((rowaddr + (uint32_t)sx0) & ~3u);
-    const uint32_t F0 = F[0], F1 = F[1], F2 = F[2];
-    const uint32_t p0 = __builtin_amdgcn_perm(F1, F0, s.sel[0]);
-    const uint32_t p1 = __builtin_amdgcn_perm(F1, F0, s.sel[1]);
-    const uint32_t p2 = __builtin_amdgcn_perm(s.hi2 ? F2 : F1, s.hi2 ? F1 : F0, s.sel[2]);
-    const uint32_t p3 = __builtin_amdgcn_perm(s.hi3 ? F2 : F1, s.hi3 ? F1 : F0, s.sel[3]);
-    d[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[0], 0u, false);
-    d[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[1], 0u, false);
-    d[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p2), wt[2], 0u, false);
-    d[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p3), wt[3], 0u, false);
-}
-template <bool FX>
-__device__ __forceinline__ uint32_t og_rz_quad_w(uint32_t r0addr, uint32_t r1addr, const int* sx, const OgRzSel& s0,
-                                                 const OgRzSel& s1, const og_rz_u16x2* wt, unsigned yz, unsigned yw)
-{
-    uint32_t d0[4], d1[4];
-    og_rz_hrow(r0addr, sx[0], s0, wt, d0);
-    og_rz_hrow(r1addr, sx[0], s1, wt, d1);
-    uint32_t packed = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) packed |= og_rz_vert16<FX>(yz, d0[k], yw, d1[k]) << (8 * k);
-    return packed;
-}
-
 // (og_resize2_kernel: FX = false pre-scales the weights by 16 for og_rz_vert16)
 template <bool FX>
 __device__ __forceinline__ void og_rz_weights(const int4* xtab, int xmax, int dx, int base, int* sx, og_rz_u16x2* wt,
@@ -354,7 +288,7 @@ __device__ __forceinline__ void og_rz_weights(const int4* xtab, int xmax, int dx
 {
     const int4 xt = xtab[dx];
     sx[k] = xt.x - base;
-    const int sh = (!FX && OG_RZ_MULHI) ? 4 : 0;
+    const int sh = FX ? 0 : 4;
     wt[k] = dx < xmax ? og_rz_u16x2{(unsigned short)(xt.y << sh), (unsigned short)(xt.z << sh)}
                       : og_rz_u16x2{(unsigned short)(2048 << sh), 0};
 }
@@ -372,123 +306,6 @@ __device__ __forceinline__ void og_rz_store4(uint8_t* Dr, uint32_t packed, int n
         for (int k = 0; k < 4; k++)
             if (k < n) Dr[k] = (uint8_t)(packed >> (8 * k));
     }
-}
-
-// ------------------------------------------------------------------------------------------------
-// k1s: one pyramid level as a row stream, no LDS.  A wave owns a strip of 256 output columns (4 per lane) and a run
-// of RS_ROWS output rows.  It walks the source rows the run reads in order: each source row is loaded once (three
-// dwords per lane, the 4-byte-aligned window around the lane's source bytes, prefetched RS_PF rows ahead), its
-// horizontal sums are formed once (v_perm pairs + v_dot2), and an output row is emitted as soon as its second
-// source row is in (ytab[y].y == r), from the current and the previous row's sums.  The arithmetic is
-// og_resize_kernel's (cv::resize INTER_LINEAR fixed point, og_rz_vert16 / og_rz_vert).
-// ------------------------------------------------------------------------------------------------
-#define RS_ROWS 32  // output rows per wave
-#define RS_PF 4     // source rows in flight per wave
-#define RS_NT 256   // 4 independent waves per workgroup (4 row runs of one strip)
-
-// Source-row loads are issued by inline asm so that the compiler does not wait for them at the loop back-edge: the
-// loop waits explicitly (vmcnt counts every vector-memory op in issue order; the stores issued in between only make a
-// wait stronger).  A lane reads the three dwords of the row that hold its source bytes; a dword index past the row's
-// last dword is clamped to it (its bytes only meet zero weights: the pair (sw - 1, sw) at the right border), so every
-// load stays inside the row.
-__device__ __forceinline__ void og_rs_issue(const uint8_t* rb, unsigned q, unsigned qlast, uint32_t& d0, uint32_t& d1,
-                                            uint32_t& d2)
-{
-    const unsigned o0 = 4u * min(q, qlast), o1 = 4u * min(q + 1u, qlast), o2 = 4u * min(q + 2u, qlast);
-    __asm__ volatile("global_load_dword %0, %3, %6\n\t"
-                     "global_load_dword %1, %4, %6\n\t"
-                     "global_load_dword %2, %5, %6"
-                     : "=&v"(d0), "=&v"(d1), "=&v"(d2)
-                     : "v"(o0), "v"(o1), "v"(o2), "s"(rb)
-                     : "memory");
-}
-
-template <bool FX>
-__global__ __launch_bounds__(RS_NT) void og_resize_rows_kernel(const uint8_t* __restrict__ src, long long src_pitch,
-                                                               long long src_fstride, uint8_t* __restrict__ dst,
-                                                               long long dst_pitch, long long dst_fstride, int sw,
-                                                               int sh, int dw, int dh, const int4* __restrict__ xtab,
-                                                               const int4* __restrict__ ytab, int xmax)
-{
-    const int f = blockIdx.z, lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int y0 = (blockIdx.y * (RS_NT / 64) + w) * RS_ROWS;
-    if (y0 >= dh) return;
-    const int y1 = min(y0 + RS_ROWS, dh);
-    const int dxt = blockIdx.x * 256 + 4 * lane;
-    // the lane's 4 output columns: source offsets from its first source byte, weights (x16 for og_rz_vert16)
-    int sx0 = 0;
-    uint32_t sel[4];
-    og_rz_u16x2 wt[4];
-    {
-        int sxk[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) og_rz_weights<FX>(xtab, xmax, min(dxt + k, dw - 1), 0, sxk, wt, k);
-        sx0 = sxk[0];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const unsigned o = (unsigned)(sxk[k] - sx0);  // <= ceil(3 * 1.6) + 1 < 7: the pair stays in 8 bytes
-            sel[k] = 0x0c000c00u | o | ((o + 1u) << 16);
-        }
-    }
-    const uint8_t* fbase = src + (long long)f * src_fstride;
-    const int rs0 = ytab[y0].x, rs1 = ytab[y1 - 1].y;  // source rows of the run (monotone table)
-    const int nsrc = rs1 - rs0 + 1;
-    // row r: 4-byte-aligned base (SGPRs) and the lane's byte offset t from it; last = the row's last byte
-    auto issue = [&](int r, uint32_t& d0, uint32_t& d1, uint32_t& d2) {
-        const uint8_t* row = fbase + (long long)r * src_pitch;
-        const uint8_t* rb = (const uint8_t*)((uintptr_t)row & ~(uintptr_t)3);
-        const unsigned mr = (unsigned)((uintptr_t)row & 3);
-        og_rs_issue(rb, (mr + (unsigned)sx0) >> 2, (mr + (unsigned)(sw - 1)) >> 2, d0, d1, d2);
-    };
-    auto shift = [&](int r) { return ((unsigned)((uintptr_t)(fbase + (long long)r * src_pitch) & 3) + (unsigned)sx0) & 3u; };
-    uint8_t* D = dst + (long long)f * dst_fstride + dxt;
-    const int nout = min(4, dw - dxt);  // <= 0: an idle lane of the last strip
-    uint32_t ra[RS_PF], rb_[RS_PF], rc[RS_PF];
-#pragma unroll
-    for (int i = 0; i < RS_PF; i++) issue(min(rs0 + i, rs1), ra[i], rb_[i], rc[i]);
-    uint32_t hp[4] = {0u, 0u, 0u, 0u}, hc[4];
-    int y = y0;
-    int4 yt = ytab[y];
-    for (int j0 = 0; j0 < nsrc; j0 += RS_PF) {
-#pragma unroll
-        for (int i = 0; i < RS_PF; i++) {
-            const int r = rs0 + j0 + i;
-            if (j0 + i >= nsrc) break;  // uniform
-            // row r's three loads are done once at most the 3 (RS_PF - 1) issued after them are outstanding
-            __asm__ volatile("s_waitcnt vmcnt(%3)" : "+v"(ra[i]), "+v"(rb_[i]), "+v"(rc[i]) : "n"(3 * (RS_PF - 1)));
-            const unsigned m = shift(r);
-            const uint32_t w0 = __builtin_amdgcn_alignbyte(rb_[i], ra[i], m), w1 = __builtin_amdgcn_alignbyte(rc[i], rb_[i], m);
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t pr = __builtin_amdgcn_perm(w1, w0, sel[k]);
-                const uint32_t d = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, pr), wt[k], 0u, false);
-                hc[k] = (FX || !OG_RZ_MULHI) ? d : (d & ~0xffu);
-            }
-            issue(min(r + RS_PF, rs1), ra[i], rb_[i], rc[i]);  // the ring slot's next row (clamped: the count stays regular)
-            while (y < y1 && yt.y == r) {  // uniform; at most one row per source row when downscaling
-                const bool same = yt.x == r;  // clamped at the border: both taps on this row
-                uint32_t packed = 0;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t h0 = same ? hc[k] : hp[k];
-                    uint32_t v;
-                    if (FX || !OG_RZ_MULHI)
-                        v = og_rz_vert<FX>((unsigned)yt.z, h0, (unsigned)yt.w, hc[k]);
-                    else
-                        v = min((og_mulhi_u24((unsigned)yt.z << 8, h0) + og_mulhi_u24((unsigned)yt.w << 8, hc[k]) + 2u) >> 2,
-                                255u);
-                    packed |= v << (8 * k);
-                }
-                if (nout > 0) og_rz_store4(D + (long long)y * dst_pitch, packed, nout);
-                y++;
-                if (y < y1) yt = ytab[y];
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) hp[k] = hc[k];
-        }
-    }
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail loads land before the wave ends
 }
 
 template <bool FX>
@@ -534,14 +351,6 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     const int dxt = bx0 + 4 * cth;
 #pragma unroll
     for (int k = 0; k < 4; k++) og_rz_weights<FX>(g.xtabA, g.xmaxA, min(cA + k, ac1), sc0, sxA, wtA, k);
-#ifndef OG_RZ_BPRE
-#define OG_RZ_BPRE 0  // 1: the B pass's x weights are loaded here too, in flight over the staging and the A pass (72
-                      // VGPRs instead of 54, no gain: profiles/sweeps/r04_ab_rzbpre.txt); 0: after the A pass's barrier
-#endif
-    if (OG_RZ_BPRE) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) og_rz_weights<FX>(g.xtabB, g.xmaxB, min(dxt + k, g.bw - 1), ac0, sxB, wtB, k);
-    }
     // staging addresses: the region's first row (wave-uniform, SGPRs) rounded down to 16 bytes plus a 32-bit lane
     // offset; chunk -> (row, chunk) with the exact float quotient (nIt < 2^14)
     const uint8_t* rbase = src + (long long)f * src_fstride + (long long)sr0 * src_pitch + sc0;
@@ -586,33 +395,14 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
         // ac0 is a multiple of 4 (host plan): every quad left of own_c1 is one aligned dword store
         const bool own_c = cA < own_c1;
         const int nown = min(4, own_c1 - cA);
-#if OG_RZ_WORDS
-        const uint32_t aS = og_lds_addr(S);
-        const bool same_mis = (upitch & 15u) == 0;  // every staged row keeps the first row's misalignment mb
-        const OgRzSel su = og_rz_sel(sxA, (mb + (unsigned)sxA[0]) & 3u);
-#endif
         for (int rr = rga; rr < nrA; rr += G) {
             const int4 yt = YA[rr];
             const int r = ar0 + rr;
             const int r0 = yt.x - sr0, r1 = yt.y - sr0;
-#if OG_RZ_WORDS
-            uint32_t packed;
-            if (same_mis) {
-                packed = og_rz_quad_w<FX>(aS + __umul24((unsigned)r0, (unsigned)g.SC) + mb, aS + __umul24((unsigned)r1, (unsigned)g.SC) + mb, sxA, su, su,
-                                          wtA, (unsigned)yt.z, (unsigned)yt.w);
-            } else {
-                const unsigned m0 = (unsigned)mis[r0], m1 = (unsigned)mis[r1];
-                packed = og_rz_quad_w<FX>(aS + __umul24((unsigned)r0, (unsigned)g.SC) + m0, aS + __umul24((unsigned)r1, (unsigned)g.SC) + m1, sxA,
-                                          og_rz_sel(sxA, (m0 + (unsigned)sxA[0]) & 3u),
-                                          og_rz_sel(sxA, (m1 + (unsigned)sxA[0]) & 3u), wtA, (unsigned)yt.z,
-                                          (unsigned)yt.w);
-            }
-#else
             // a 16-byte multiple pitch gives every staged row the first row's misalignment mb: no per-row lookups
             const unsigned m0 = (upitch & 15u) == 0 ? mb : (unsigned)mis[r0], m1 = (upitch & 15u) == 0 ? mb : (unsigned)mis[r1];
             const uint32_t packed = og_rz_quad<FX>(S + __umul24((unsigned)r0, (unsigned)g.SC) + m0, S + __umul24((unsigned)r1, (unsigned)g.SC) + m1, sxA, wtA,
                                                (unsigned)yt.z, (unsigned)yt.w);
-#endif
             *(uint32_t*)&A[rr * g.AC + 4 * qa] = packed;
             if (r < own_r1 && own_c) og_rz_store4(DA + (__umul24((unsigned)r, (unsigned)pitchA) + (unsigned)cA), packed, nown);
         }
@@ -620,22 +410,15 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     __syncthreads();
     // ---- level B tile from the A region
     if (dxt >= g.bw) return;
-    if (!OG_RZ_BPRE) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) og_rz_weights<FX>(g.xtabB, g.xmaxB, min(dxt + k, g.bw - 1), ac0, sxB, wtB, k);
-    }
+    for (int k = 0; k < 4; k++) og_rz_weights<FX>(g.xtabB, g.xmaxB, min(dxt + k, g.bw - 1), ac0, sxB, wtB, k);
     const int n = min(4, g.bw - dxt);
     uint8_t* DB = dstB + (long long)f * dst_fstride + dxt;
-#if OG_RZ_WORDS
-    const uint32_t aA = og_lds_addr(A);                    // 16-byte aligned, AC a multiple of 4: one alignment
-    const OgRzSel sb = og_rz_sel(sxB, (unsigned)sxB[0] & 3u);
-#endif
-#if !OG_RZ_WORDS && OG_RZ_BREUSE
     // the wave's 4 output rows read nondecreasing A rows, and consecutive outputs share one (a 1.2 downscale: ~5
     // distinct rows for 4 outputs): each distinct row's 4 horizontal sums are formed once and kept for the next
     // output (the rows are wave-uniform, so every reuse test is a scalar branch)
     const int rgu = __builtin_amdgcn_readfirstlane(rg);
-    constexpr bool MH = !FX && OG_RZ_MULHI;  // sums kept as (d >> 4) << 8 for the multiply-high vertical form
+    constexpr bool MH = !FX;  // sums kept as (d >> 4) << 8 for the multiply-high vertical form
     auto hsum = [&](int row, uint32_t (&h)[4]) {
         const uint8_t* R = A + __umul24((unsigned)(row - ar0), (unsigned)g.AC);
 #pragma unroll
@@ -689,22 +472,6 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
             hy[k] = h1[k];
         }
     }
-#else
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int r = 4 * rg + q;
-        if (r >= nyB) break;
-        const int4 yt = YB[r];
-#if OG_RZ_WORDS
-        const uint32_t packed = og_rz_quad_w<FX>(aA + (unsigned)((yt.x - ar0) * g.AC), aA + (unsigned)((yt.y - ar0) * g.AC),
-                                                 sxB, sb, sb, wtB, (unsigned)yt.z, (unsigned)yt.w);
-#else
-        const uint32_t packed = og_rz_quad<FX>(A + __umul24((unsigned)(yt.x - ar0), (unsigned)g.AC), A + __umul24((unsigned)(yt.y - ar0), (unsigned)g.AC), sxB, wtB, (unsigned)yt.z,
-                                           (unsigned)yt.w);
-#endif
-        og_rz_store4(DB + __umul24((unsigned)(by0 + r), (unsigned)pitchB), packed, n);
-    }
-#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1471,6 +1238,270 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     p = pn;
     __syncthreads();  // score map back to zero, list consumed, next ROI stored
     FAST_PROF(1);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k2c: FAST with one wave per cell, for the levels whose cells are at most FC_MAXC x FC_MAXC detection pixels (every
+// level of a 1080p or KITTI-width frame but the coarsest few).  The cell is the reference's unit of work: one cv::FAST
+// call with its own NMS, and the 20 -> 7 fallback decided by the cell alone (src/ORBextractor.cc:789-829), so a wave
+// runs the whole chain without a workgroup barrier or an LDS atomic: ROI -> LDS, quick test into a wave-private
+// survivor list (the running offset is a scalar), exact scores into a wave-private score map, NMS, and one global
+// reservation per cell.  A workgroup is the 4 waves of one table block (2 x 2 cells, og_fast_quad_kernel's table,
+// its XCD runs included); the waves share nothing, and a wave whose cell does not exist exits at once.
+// ROI layout: qword (r, x) holds ROI row r, columns x - mis + 8k (k = 0..3) as f16-biased u16 (0x6400 | pixel), with
+// mis the ROI origin's misalignment (aligned dword loads); lane (s, x) of a stage-1 iteration takes detection columns
+// x + 8k of one row, 8 lanes a row.  The 32-lane groups hold rows r, r + 4, r + 8, r + 12: 4 * FC_S = 72 = 8 (mod 32)
+// qwords, so their 16-dword row segments cover the 64 banks once (conflict-free ds_read_b64).
+// ------------------------------------------------------------------------------------------------
+#define FC_S 18                                 // qword stride of a ROI row (>= 14 + 3 misalignment)
+#define FC_MAXC 32                              // cell detection width / height capacity
+#define FC_ROWS (FC_MAXC + 6)
+#define FC_MSW 36                               // score-map row stride (bytes): a zero border around cw x ch
+#define FC_MSZ (((FC_MSW * (FC_MAXC + 2)) + 15) & ~15)
+#define FC_NW 4                                 // waves (cells) per workgroup
+#define FC_LST (FC_MAXC * FC_MAXC)              // survivor list capacity: every detection pixel
+
+// this wave's LDS stores and loads are ordered for all of its lanes (the waves of a workgroup share no LDS)
+__device__ __forceinline__ void og_wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(64 * FC_NW) void og_fast_cell_kernel(
+    const OgFastBlk* __restrict__ blocks, int nb, const uint8_t* __restrict__ img0, long long pitch0, long long fstride0,
+    const uint8_t* __restrict__ pyr, long long pyr_per_frame, u64* __restrict__ cand, long long cand_per_frame,
+    int* __restrict__ cand_count, int nlevels, int thr, int* __restrict__ status)
+{
+    __shared__ __attribute__((aligned(16))) uint2 roiw[FC_NW][FC_ROWS * FC_S];
+    __shared__ __attribute__((aligned(16))) uint8_t msw[FC_NW][FC_MSZ];
+    __shared__ __attribute__((aligned(16))) uint16_t lstw[FC_NW][FC_LST];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const unsigned f = blockIdx.y;
+    const int p = blockIdx.x;
+    if (p >= nb) return;
+    __asm__ volatile("" ::"s"(blocks), "s"(nb), "s"(img0), "s"(pitch0), "s"(fstride0), "s"(pyr), "s"(pyr_per_frame));
+    const OgFB b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
+    if (b.l < 0) return;
+    // this wave's cell of the block
+    const int ci = wv >> 1, cj = wv & 1;
+    const int cw = min(b.wC, b.dw - cj * b.wC), ch = min(b.hC, b.dh - ci * b.hC);
+    if (cw <= 0 || ch <= 0) return;
+    const uint8_t* row0 = b.row0 + (unsigned)(ci * b.hC) * b.upitch + (unsigned)(cj * b.wC);
+    const int mis = b.aligned ? (int)((uintptr_t)row0 & 3) : 0;
+    const int rh = ch + 6;
+    uint2* roi = roiw[wv];
+    uint8_t* ms = msw[wv];
+    const uint32_t a_roi = og_lds_addr(roi), a_lst = og_lds_addr(&lstw[wv][0]);
+    // ---- ROI -> LDS.  Item (r, g) = qwords 4g .. 4g + 3 of ROI row r: the dwords at bytes 4g + 8k (k = 0..3) of the
+    // row from its aligned start, 8 v_perm into four quads, two 16-byte stores (one for g = 4, the last 2 qwords of
+    // the FC_S-qword row).  All loads are issued before the first use; rows of a 64-item round come from one
+    // multiply-high division by ng (exact below 200 items).
+    {
+        const int ng = (14 + mis + 3) >> 2;                 // 4 or 5 groups of 4 qwords
+        const int nitem = rh * ng;                         // <= 38 * 5 = 190 <= 3 * 64
+        const unsigned mg = ng == 4 ? 16384u : 13108u;     // ceil(2^16 / ng)
+        const uint8_t* abase = row0 - mis;
+        uint32_t s[3][4];
+        int rr[3], gg[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const int it = min(64 * k + lane, nitem - 1);   // lanes past the items re-read the last one
+            rr[k] = (int)(((unsigned)it * mg) >> 16);
+            gg[k] = it - rr[k] * ng;
+        }
+        if (b.aligned) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                unsigned off = __umul24((unsigned)rr[k], b.upitch) + 4u * (unsigned)gg[k];
+                __asm__("" : "+v"(off));
+#pragma unroll
+                for (int q = 0; q < 4; q++) s[k][q] = *(const uint32_t*)(abase + off + 8u * q);
+            }
+        } else {
+            // odd pitch (mis = 0): two aligned loads funnel-shifted by the row's own offset
+            const unsigned mb = (unsigned)((uintptr_t)abase & 3);
+            const uint8_t* ab = abase - mb;
+            uint32_t lo[3][4], hi[3][4];
+            unsigned sh[3];
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                unsigned o = __umul24((unsigned)rr[k], b.upitch) + 4u * (unsigned)gg[k] + mb;
+                sh[k] = o & 3u;
+                o &= ~3u;
+                __asm__("" : "+v"(o));
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    lo[k][q] = *(const uint32_t*)(ab + o + 8u * q);
+                    hi[k][q] = *(const uint32_t*)(ab + o + 8u * q + 4u);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) s[k][q] = __builtin_amdgcn_alignbyte(hi[k][q], lo[k][q], sh[k]);
+        }
+        // zero the score map (its border and every non-survivor read 0) while the loads are in flight
+        for (int idx = lane; idx < FC_MSZ / 16; idx += 64) *(uint4*)&ms[16 * idx] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            if (64 * k + lane < nitem) {
+                uint32_t w[8];
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    // quad t of the group: byte t of dwords 0..3 (pixels 4g + t + 8q) as four f16-biased u16
+                    const uint32_t sel = 0x0c000c00u | ((4u + t) << 16) | t;
+                    w[2 * t] = __builtin_amdgcn_perm(s[k][1], s[k][0], sel) | 0x64006400u;
+                    w[2 * t + 1] = __builtin_amdgcn_perm(s[k][3], s[k][2], sel) | 0x64006400u;
+                }
+                uint4* d = (uint4*)&roi[rr[k] * FC_S + 4 * gg[k]];
+                d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+                if (gg[k] < 4) d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+            }
+        }
+    }
+    og_wave_lds_sync();
+    const int t1 = thr & 255, t2 = (thr >> 8) & 255;
+    const int tq = min(t1, t2);
+    const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
+    // ---- stage 1: quick test, 4 pixels per lane (columns x + 8k of one row), survivors appended to the wave's list
+    int n = 0;  // survivors so far (uniform)
+    {
+        const int x = lane & 7, sl = lane >> 3;
+        const int srow = (sl >> 2) + 4 * (sl & 3);  // 0, 4, 8, 12 (lanes 0-31) / 1, 5, 9, 13 (lanes 32-63)
+        const uint32_t a_lane = a_roi + 8u * (uint32_t)(srow * FC_S + x + mis);  // top-left sample of the circle
+        auto cmask = [&](int k) -> u64 {
+            const int c = min(max(cw - 8 * k, 0), 8);
+            return (u64)((1u << c) - 1u) * 0x0101010101010101ull;
+        };
+        const u64 col0 = cmask(0), col1 = cmask(1), col2 = cmask(2), col3 = cmask(3);
+        const int nit = ch <= 16 ? 2 : 4;
+#pragma unroll 1
+        for (int it = 0; it < nit; it++) {
+            const int R = 16 * (it >> 1) + 2 * (it & 1);
+            u64 w[17];
+            {
+                // from the top-left sample (dy, dx) = (-3, -3): every offset is a positive immediate
+                typedef const volatile __attribute__((address_space(3))) unsigned long long lds_u64;
+                lds_u64* q64 = (lds_u64*)(uintptr_t)(a_lane + 8u * (uint32_t)(R * FC_S));
+                constexpr int st = FC_S, c0f = 3 * FC_S + 3;
+                const int off[17] = {c0f + 3 * st,     c0f + 1 + 3 * st,  c0f + 2 + 2 * st,  c0f + 3 + 1 * st,
+                                     c0f + 3,          c0f + 3 - 1 * st,  c0f + 2 - 2 * st,  c0f + 1 - 3 * st,
+                                     c0f - 3 * st,     c0f - 1 - 3 * st,  c0f - 2 - 2 * st,  c0f - 3 - 1 * st,
+                                     c0f - 3,          c0f - 3 + 1 * st,  c0f - 2 + 2 * st,  c0f - 1 + 3 * st, c0f};
+                w[16] = q64[off[16]];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    w[k] = q64[off[k]];
+                    w[k + 8] = q64[off[k + 8]];
+                }
+            }
+            uint32_t c0[16], c1[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                c0[k] = (uint32_t)w[k];
+                c1[k] = (uint32_t)(w[k] >> 32);
+            }
+            const uint2 r0 = og_fast_quick2v(c0, (uint32_t)w[16], tt);          // columns x, x + 8
+            const uint2 r1 = og_fast_quick2v(c1, (uint32_t)(w[16] >> 32), tt);  // columns x + 16, x + 24
+            const u64 rows = R + 13 < ch ? ~0ull : og_lanes_lt(R + srow, ch);
+            const uint32_t a0 = r0.x | r0.y, a1 = r1.x | r1.y;
+            const u64 m[4] = {og_lanes_lo16_nz(a0) & col0 & rows, og_lanes_gt((int)a0, 0xffff) & col1 & rows,
+                              og_lanes_lo16_nz(a1) & col2 & rows, og_lanes_gt((int)a1, 0xffff) & col3 & rows};
+            const int cnt0 = __popcll(m[0]), cnt1 = __popcll(m[1]), cnt2 = __popcll(m[2]), cnt3 = __popcll(m[3]);
+            const int nn = cnt0 + cnt1 + cnt2 + cnt3;
+            if (nn) {
+                const uint32_t base = (uint32_t)(((R + srow) << 7) | x);
+                uint32_t v[4];
+                {
+                    uint32_t d1, b1;
+                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r0.x), "s"(0x00010001u));
+                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r0.y), "s"(0x00020002u));
+                    const uint32_t pb = d1 | b1;
+                    v[0] = (pb << 14) | base;
+                    v[1] = (pb >> 2) | (base + 8u);
+                }
+                {
+                    uint32_t d1, b1;
+                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r1.x), "s"(0x00010001u));
+                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r1.y), "s"(0x00020002u));
+                    const uint32_t pb = d1 | b1;
+                    v[2] = (pb << 14) | (base + 16u);
+                    v[3] = (pb >> 2) | (base + 24u);
+                }
+                const uint32_t ab0 = a_lst + 2u * (uint32_t)n, ab1 = ab0 + 2u * (uint32_t)cnt0,
+                               ab2 = ab1 + 2u * (uint32_t)cnt1, ab3 = ab2 + 2u * (uint32_t)cnt2;
+                og_ds_write_b16_x4(m[0], ab0 + 2u * (uint32_t)og_rank(m[0]), v[0], m[1], ab1 + 2u * (uint32_t)og_rank(m[1]),
+                                   v[1], m[2], ab2 + 2u * (uint32_t)og_rank(m[2]), v[2], m[3],
+                                   ab3 + 2u * (uint32_t)og_rank(m[3]), v[3]);
+                n += nn;
+            }
+        }
+    }
+    og_wave_lds_sync();
+    // ---- stage 2: exact score of every survivor into the score map (u16 reads of the quad layout)
+    const uint16_t* lst = &lstw[wv][0];
+    for (int e = lane; e < n; e += 64) {
+        const int ent = lst[e];
+        const int i = (ent >> 7) & 127, j = ent & 127;
+        const bool dark = (ent & 0x4000) != 0, bright = (ent & 0x8000) != 0;
+        const uint32_t pb = a_roi + 8u * (uint32_t)(i * FC_S + (j & 7) + mis) + 2u * (uint32_t)(j >> 3);
+        int M = og_fast_Mpk<FC_S>(pb, dark ? (_Float16)1 : (_Float16)-1);
+        if (dark && bright) M = max(M, og_fast_Mpk<FC_S>(pb, (_Float16)-1));
+        ms[(i + 1) * FC_MSW + j + 1] = (uint8_t)M;
+    }
+    og_wave_lds_sync();
+    // ---- stage 3: 3x3 NMS at both thresholds; kept flags into bits 14 / 15 of the list entries
+    const int tA = max(t1, 1), tB = max(t2, 1);
+    int k1 = 0, k2 = 0;
+    uint16_t* lstm = &lstw[wv][0];
+    for (int e0 = 0; e0 < n; e0 += 64) {
+        const int e = e0 + lane;
+        int ent = 0, mc = 0, nbm = 0;
+        if (e < n) {
+            ent = lstm[e] & 0x3fff;
+            const uint8_t* q = &ms[((ent >> 7) & 127) * FC_MSW + (ent & 127)];  // top-left neighbour
+            mc = q[FC_MSW + 1];
+            nbm = max(max(max(q[0], q[1]), max(q[2], q[FC_MSW])),
+                      max(max(q[FC_MSW + 2], q[2 * FC_MSW]), max(q[2 * FC_MSW + 1], q[2 * FC_MSW + 2])));
+        }
+        const u64 top = og_lanes_gt(mc, nbm);
+        const u64 K1 = og_lanes_gt(mc, tA) & top, K2 = og_lanes_gt(mc, tB) & top;
+        if (e < n) lstm[e] = (uint16_t)(ent | (mc > tA && mc > nbm ? 0x4000 : 0) | (mc > tB && mc > nbm ? 0x8000 : 0));
+        k1 += __popcll(K1);
+        k2 += __popcll(K2);
+    }
+    // ---- stage 4: the cell's threshold (iniThFAST unless it keeps nothing, src/ORBextractor.cc:809-816), one
+    // reservation, the kept entries in list order
+    const bool useT2 = k1 == 0;
+    const int total = useT2 ? k2 : k1;
+    if (total == 0) return;
+    int old = 0;
+    if (lane == 0) old = atomicAdd(&cand_count[f * nlevels + b.l], total);
+    og_wave_lds_sync();
+    const int sb = __builtin_amdgcn_readfirstlane(old);
+    if (sb + total > b.cand_cap) {  // cannot happen: the capacity is the exact NMS bound
+        if (lane == 0) atomicOr(status, 1);
+        return;
+    }
+    u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb);
+    const unsigned kmask = useT2 ? 0x8000u : 0x4000u;
+    const int ox = b.ox + cj * b.wC, oy = b.oy + ci * b.hC;
+    int run = 0;
+    for (int e0 = 0; e0 < n; e0 += 64) {
+        const int e = e0 + lane;
+        const int ent = e < n ? lst[e] : 0;
+        const unsigned kb = (unsigned)ent & kmask;
+        const u64 mask = og_lanes_ne(kb, 0u);
+        if (kb) {
+            const int i = (ent >> 7) & 127, j = ent & 127;
+            out[og_rank(mask, run)] = og_pack_cand(ox + j, oy + i, ms[(i + 1) * FC_MSW + j + 1] - 1);
+        }
+        run += __popcll(mask);
     }
 }
 
@@ -2838,15 +2869,6 @@ __device__ __forceinline__ int og_reflect101_1(int i, int n)
 {
     return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
 }
-__device__ __forceinline__ int og_reflect101(int i, int n)
-{
-    if (n == 1) return 0;
-    while (i < 0 || i >= n) {
-        if (i < 0) i = -i;
-        if (i >= n) i = 2 * n - 2 - i;
-    }
-    return i;
-}
 
 // sum over the 64 lanes (all active) with DPP: quad_perm [1,0,3,2] and [2,3,0,1] (quads), row_half_mirror (8),
 // row_mirror (16), row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3; lane 63 then holds the sum.
@@ -2862,49 +2884,20 @@ __device__ __forceinline__ int og_wave_sum(int v)
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-#ifndef OG_DK_SAMPLEV
-#define OG_DK_SAMPLEV 1  // 1: the vertical pass only at the 512 rBRIEF sample points (og_describe_kernel); 0: the whole 37x37 window
-#endif
-#ifndef OG_DK_HSHIFTW
-#define OG_DK_HSHIFTW 1  // horizontal blur pass with shifted weights (og_describe_kernel)
-#endif
-#ifndef DK_WAVES
-#define DK_WAVES 4
-#endif
+#define DK_WAVES 4  // keypoint waves per workgroup (1 and 2 measured: profiles/sweeps/r04_ab_dk_waves.txt)
 #define RAW_W 43
 #define RAW_S 52  // 43 + 3 misalignment bytes, dword multiple; 13 dwords: conflict-free lane-per-row reads
-#define BL_W 37
-#ifndef OG_DK_VDWORD
-#define OG_DK_VDWORD 1  // vertical blur pass: 2 rows x 4 columns per item, dword stores (0: 4 rows x 1 column, bytes)
-#endif
-#define BL_S (OG_DK_VDWORD ? 40 : BL_W)  // blurred-window row stride in bytes
-static_assert(BL_W * BL_S <= RAW_W * RAW_S, "the blurred window aliases the raw one");
+#define BL_W 37   // the blurred window the tests can reach (only its 512 samples are formed)
 #define HP_ROWS 22  // row pairs of the horizontal pass (43 rows -> 22 pairs)
 #define HP_S 40     // pair-row stride in dwords (10 groups of 4 columns)
+#define DK_BORDER_RB 22  // border windows: rows of byte loads in flight per batch
 
-// IC_Angle's disk (src/ORBextractor.cc:77-104) as a flat list of the (u, v) points with v >= 1: each pair of
-// points (u, +-v) is one lane's item, so a wave covers the 359 pairs in 6 full iterations instead of 15 row
-// iterations with 2 * umax[v] + 1 of 64 lanes active.  umax depends only on HALF_PATCH_SIZE = 15 (:454-469); the
-// host checks that its table equals OG_UMAX (orbgpu_create).  Padding items are (0, 0): they add nothing.
-#define OG_DISK_ITEMS 384
-struct OgDisk {
-    short e[OG_DISK_ITEMS];  // (u & 0xff) | v << 8
-};
-constexpr OgDisk og_make_disk()
-{
-    OgDisk d{};
-    constexpr int umax[16] = {OG_UMAX};
-    int k = 0;
-    for (int v = 1; v <= 15; v++)
-        for (int u = -umax[v]; u <= umax[v]; u++) d.e[k++] = (short)((u & 0xff) | (v << 8));
-    return d;
-}
-__constant__ OgDisk og_disk = og_make_disk();
-
-// IC_Angle by rows with v_dot4 (OG_DK_ICDOT): item t < 279 = (disk row v = t / 9 - 15, window dword j = t % 9, which
-// holds window columns 4 + 4j .. 7 + 4j, i.e. u = 4j - 17 .. 4j - 14).  Per item: the byte mask of the columns inside
-// the disk row (|u| <= umax[|v|]), the weights u + 16 of those bytes (in [1, 31]; bytes outside the disk are masked
-// to 0 first), and the dword's LDS byte offset | v << 16.  m10 = sum (u + 16) I - 16 sum I, m01 = sum v sum I.
+// IC_Angle (src/ORBextractor.cc:77-104) by disk rows with v_dot4: item t < 279 = (disk row v = t / 9 - 15, window
+// dword j = t % 9, which holds window columns 4 + 4j .. 7 + 4j, i.e. u = 4j - 17 .. 4j - 14).  Per item: the byte mask
+// of the columns inside the disk row (|u| <= umax[|v|]; umax depends only on HALF_PATCH_SIZE = 15, :454-469, and the
+// host checks that its table equals OG_UMAX), the weights u + 16 of those bytes (in [1, 31]; bytes outside the disk
+// are masked to 0 first), and the dword's LDS byte offset | v << 16.  m10 = sum (u + 16) I - 16 sum I, m01 = sum v
+// sum I.
 #define OG_IC_ITEMS 320  // 279 items padded to 5 x 64 lanes (padding: mask 0)
 struct OgIcTab {
     uint32_t mask[OG_IC_ITEMS], wt[OG_IC_ITEMS], ov[OG_IC_ITEMS];
@@ -2930,12 +2923,8 @@ constexpr OgIcTab og_make_ic()
     }
     return t;
 }
-__constant__ OgIcTab og_ic = og_make_ic();
-#ifndef OG_DK_ICDOT
-#define OG_DK_ICDOT 1  // 1: disk rows by v_dot4 over masked window dwords (og_ic); 0: (u, v) point pairs (og_disk)
-#endif
-// the same table lane-major (OG_DK_ICPRE): lane i's items i, i + 64, .. i + 256 as (mask, wt, ov) triples in 16 words,
-// four 16-byte loads from one base
+// the table lane-major: lane i's items i, i + 64, .. i + 256 as (mask, wt, ov) triples in 16 words, loaded at kernel
+// start with four 16-byte loads from one base (in flight over the level search and the window load)
 struct OgIcLane {
     uint32_t w[64][16];
 };
@@ -2958,23 +2947,16 @@ __constant__ OgIcLane og_icl = og_make_icl();
 constexpr uint32_t og_blur_coefs[4] = {18u | 34u << 8 | 49u << 16 | 55u << 24, 18u | 34u << 8 | 49u << 16 | 55u << 24,
                                           18u | 34u << 8 | 49u << 16 | 54u << 24, 18u | 34u << 8 | 48u << 16 | 56u << 24};
 
-#ifndef OG_DK_BLOCKSYNC
-#define OG_DK_BLOCKSYNC 0
-#endif
-// The describe kernel's waves share no LDS: each wave owns its raw/blurred windows.  A wave only has to see
-// its own LDS writes before it reads them back, so it synchronises with itself (LDS counter drained, no
-// reordering across the point) instead of with the other waves of the workgroup; a wave that finished its
-// loads does not wait for a neighbour's global loads.
+// The describe kernel's waves share no LDS: each wave owns its raw window and horizontal sums.  A wave only has to
+// see its own LDS writes before it reads them back, so it synchronises with itself (LDS counter drained, no
+// reordering across the point) instead of with the other waves of the workgroup; a wave that finished its loads does
+// not wait for a neighbour's global loads (-2 % describe time against workgroup barriers).
 __device__ __forceinline__ void og_dk_sync()
 {
-#if OG_DK_BLOCKSYNC
-    __syncthreads();
-#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores have landed
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
 }
 
 // BV = ORBGPU_SEM_BLUR_* variant >> ORBGPU_SEM_BLUR_SHIFT, NOFMA = ORBGPU_SEM_BRIEF_NOFMA: compile-time, so every
@@ -2994,13 +2976,10 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     __shared__ __attribute__((aligned(16))) uint32_t hp[DK_WAVES][HP_ROWS * HP_S];
     // w is wave-uniform: made explicit, so the keypoint index, its level and its window origin live in SGPRs
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-#ifndef OG_DK_ICPRE
-#define OG_DK_ICPRE 1  // 1: the lane's IC_Angle items (og_icl) are loaded first, in flight over the level search and the
-                       // window load (0: og_ic after the window barrier, one round trip on every wave's path)
-#endif
+    // the lane's IC_Angle items, loaded first: in flight over the level search and the window load
     uint4 icq[4] = {};
 #if defined(__HIP_DEVICE_COMPILE__)
-    if (OG_DK_ICDOT && OG_DK_ICPRE) {
+    {
         typedef const __attribute__((address_space(1))) uint4 g_u4;
         g_u4* ib = (g_u4*)&og_icl.w[0][0];
         __asm__("" : "+s"(ib));  // one SGPR base: a lane offset and 16-byte immediate steps
@@ -3008,26 +2987,12 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         for (int k = 0; k < 4; k++) icq[k] = ib[4 * lane + k];
     }
 #endif
-#ifndef OG_DESC_XCD_REMAP
-#define OG_DESC_XCD_REMAP 1  // experiment switch: 0 = plain dispatch order
-#endif
-#ifndef OG_DK_ARGS1
-#define OG_DK_ARGS1 0  // 1: the prologue's kernel arguments are fetched together behind an asm barrier, one scalar-cache
-                       // round trip instead of four, yet describe +3.5 % (profiles/sweeps/r04_ab_dkargs.txt); 0: the
-                       // compiler's order
-#endif
-    unsigned gx = gridDim.x, gy = gridDim.y, dm = dmagic;
-    int nlv = P.nlevels, kct = P.kcap_total;
-    long long p0 = pitch0, fs0 = fstride0, ppf = P.pyr_per_frame;
-    const int* occ = oct_count;
-    if (OG_DK_ARGS1)
-        __asm__ volatile("" : "+s"(gx), "+s"(gy), "+s"(dm), "+s"(nlv), "+s"(kct), "+s"(p0), "+s"(fs0), "+s"(ppf), "+s"(occ)
-                            : "s"(img0), "s"(pyr), "s"(oct_xy), "s"(oct_resp));  // (the pointers: fetched, not opaque)
-    const unsigned lin = OG_DESC_XCD_REMAP ? og_xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy)
-                                           : blockIdx.y * gx + blockIdx.x;
+    const unsigned gx = gridDim.x, gy = gridDim.y;
+    const int nlv = P.nlevels, kct = P.kcap_total;
+    const unsigned lin = og_xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
     // frame = lin / gridDim.x by the host's multiply-high constant (exact for every lin of the launch, checked on the
     // host; 0: the division)
-    const unsigned fq = dm ? __umulhi(lin, dm) : lin / gx;
+    const unsigned fq = dmagic ? __umulhi(lin, dmagic) : lin / gx;
     const int f = (int)fq;
     const int g = (int)(lin - fq * gx) * DK_WAVES + w;
     // which level does keypoint g belong to (levels concatenated 0..L-1, :1076-1104); with 8 levels the frame's
@@ -3039,7 +3004,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         // the vector load's round trip at the kernel's start).  The level is the number of prefix sums <= g (they are
         // nondecreasing) and its first keypoint the last such prefix sum: 4 scalar instructions per level, the compare's
         // SCC feeding both the select and the add-with-carry
-        const og_u32x8 c8 = ((const __attribute__((address_space(4))) og_u32x8*)(occ + 8 * f))[0];
+        const og_u32x8 c8 = ((const __attribute__((address_space(4))) og_u32x8*)(oct_count + 8 * f))[0];
         int nl = 0, st = 0;
         const int gu = __builtin_amdgcn_readfirstlane(g);
 #pragma unroll
@@ -3060,7 +3025,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
 #endif
     } else {
         for (int q = 0; q < nlv; q++) {
-            const int c = occ[f * nlv + q];
+            const int c = oct_count[f * nlv + q];
             if (l < 0 && g < total + c) {
                 l = q;
                 li = g - total;
@@ -3077,43 +3042,33 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     const bool active = l >= 0;
     uint8_t* R = raw[w];
     uint32_t* Hp = hp[w];
-    // the blurred window reuses the raw window's bytes: the raw window's last readers (IC angle, horizontal
-    // pass) are done before the vertical pass writes Bl; 5.8 KB of LDS per wave keeps ~27 waves per CU resident
-    uint8_t* Bl = raw[w];
     int cx = 0, cy = 0, lw = 1, lh = 1;
     unsigned resp = 0;  // response key (og_harris_key under ORBGPU_SEM_SCORE_HARRIS, else the FAST score)
     if (active) {
         const OgLevel& L = P.lv[l];
-        // the level's fields and the frame's image origin fetched together (one scalar round trip before the
-        // keypoint's position; the image origin by selects, not a branch)
-        int koff = L.koff, Lp = L.pitch;
-        long long Lpo = L.pyr_off;
+        const int koff = L.koff, Lp = L.pitch;
+        const long long Lpo = L.pyr_off;
         lw = L.w;
         lh = L.h;
-        if (OG_DK_ARGS1) __asm__ volatile("" : "+s"(koff), "+s"(Lp), "+s"(Lpo), "+s"(lw), "+s"(lh));
         const unsigned o = (unsigned)f * (unsigned)kct + (unsigned)(koff + li);  // < 2^31 (host plan)
         const uint32_t xy = oct_xy[o];
         cx = (int)(xy & 0xffff);
         cy = (int)(xy >> 16);
         resp = oct_resp[o];
-        const uint8_t* img = l == 0 ? img0 + (long long)f * fs0 : pyr + ((long long)f * ppf + Lpo);
-        const long long pitch = l == 0 ? p0 : (long long)Lp;
+        // the image origin by selects, not a branch
+        const uint8_t* img = l == 0 ? img0 + (long long)f * fstride0 : pyr + ((long long)f * P.pyr_per_frame + Lpo);
+        const long long pitch = l == 0 ? pitch0 : (long long)Lp;
         if (cx >= 21 && cy >= 21 && cx + 28 < lw && cy + 21 < lh) {
-            // interior (almost every keypoint): 43 rows x 11 dwords.  Each dword comes from two aligned loads
-            // funnel-shifted by the row's own misalignment (any pitch, e.g. a contiguous 1241-px KITTI image);
-            // the farthest byte read is x = cx + 26, inside the row (level starts are 256-B aligned, so the
-            // rounded-down first load never precedes the image)
-            // All 2 x 8 loads of a lane are issued before the first use (one memory round trip, not eight).
-            // Addresses: the window origin rounded down to 4 bytes (wave-uniform, SGPRs) plus a 32-bit lane offset.
+            // interior (almost every keypoint): 43 rows x 11 dwords, lanes 0-54 = 5 rows x 11 dwords stepping 5 rows
+            // per iteration (offsets advance by a uniform 5 * pitch).  Each dword comes from two aligned loads
+            // funnel-shifted by the row's own misalignment (any pitch, e.g. a contiguous 1241-px KITTI image); the
+            // farthest byte read is x = cx + 26, inside the row (level starts are 256-B aligned, so the rounded-down
+            // first load never precedes the image).  All loads of a lane are issued before the first use; addresses
+            // are the window origin rounded down to 4 bytes (wave-uniform, SGPRs) plus a 32-bit lane offset.
             const uint8_t* src0 = img + (long long)(cy - 21) * pitch + (cx - 21);
             const unsigned m0 = (unsigned)((uintptr_t)src0 & 3);
             const uint8_t* abase = src0 - m0;
             const unsigned upitch = (unsigned)pitch & (OG_MAX_PITCH - 1);  // < 2^24 (checked on the host)
-#ifndef OG_DK_RAWROWS
-#define OG_DK_RAWROWS 1  // 1: lanes 0-54 = 5 rows x 11 dwords, stepping 5 rows per iteration (offsets advance by a
-                         // uniform 5 * pitch); 0: lane + 64 k split into (row, dword) every iteration
-#endif
-#if OG_DK_RAWROWS
             constexpr int NIT = (RAW_W + 4) / 5;  // 9 iterations of 5 rows
             const int lr = (lane * 5958) >> 16;  // lane / 11 (lanes 55-63: row 5, inactive)
             unsigned l11 = __umul24((unsigned)lr, 11u);
@@ -3140,103 +3095,47 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
                 const int r = lr + 5 * k;
                 if (lact && r < RAW_W) *(uint32_t*)&R[r * RAW_S + 4 * q] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
             }
-#else
-            constexpr int NIT = (RAW_W * 11 + 63) / 64;
-            uint32_t lo[NIT], hi[NIT];
-            unsigned sh[NIT];
-#pragma unroll
-            for (int k = 0; k < NIT; k++) {
-                const int idx = min(lane + 64 * k, RAW_W * 11 - 1);
-                const int r = (idx * 5958) >> 16;  // idx / 11, exact for idx < 473 (5958 / 2^16 ~ 1/11)
-                unsigned r11 = __umul24((unsigned)r, 11u);
-                __asm__("" : "+v"(r11));  // (else idx - 11 r becomes a quarter-rate v_mul_lo_u32 by -11)
-                const int q = idx - (int)r11;
-                unsigned off = __umul24((unsigned)r, upitch) + 4u * (unsigned)q + m0;  // upitch < 2^24
-                // keep the offset a 32-bit lane value (saddr + voffset loads): otherwise the multiply is folded
-                // into a 64-bit v_mad_u64_u32 with the base pointer
-                __asm__("" : "+v"(off));
-                const uint32_t* a = (const uint32_t*)(abase + (off & ~3u));
-                sh[k] = off & 3u;
-                lo[k] = a[0];
-                hi[k] = a[1];
-            }
-#pragma unroll
-            for (int k = 0; k < NIT; k++) {
-                const int idx = lane + 64 * k;
-                if (idx < RAW_W * 11) {
-                    const int r = (idx * 5958) >> 16;
-                    unsigned r11 = __umul24((unsigned)r, 11u);
-                    __asm__("" : "+v"(r11));
-                    const int q = idx - (int)r11;
-                    *(uint32_t*)&R[r * RAW_S + 4 * q] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
-                }
-            }
-#endif
-        } else {  // within 21 px of the border: BORDER_REFLECT_101 per pixel
-#ifndef OG_DK_BORDER_BATCH
-#define OG_DK_BORDER_BATCH 1  // 1: lane = window column, OG_DK_BORDER_RB rows' byte loads in flight per batch; 0: 29 dependent rounds
-#endif
-#if OG_DK_BORDER_BATCH
-            // lane c < 43 owns window column c (its reflected image column, once); each row's reflected image row is
-            // wave-uniform.  The loads of a batch of rows are issued before their stores: 2 memory round trips instead of the
-            // 29 of a pixel-per-lane loop that waits for each load (a keypoint near the edge cost ~20 interior ones)
-#ifndef OG_DK_BORDER_RB
-#define OG_DK_BORDER_RB 22  // rows per batch of loads in flight
-#endif
-            // (one reflection is exact: keypoints lie in [19, size - 19) of their level, so the window spans
-            // [-2, size + 1] and a level holding a keypoint is at least 39 px)
+        } else {
+            // within 21 px of the border: BORDER_REFLECT_101.  Lane c < 43 owns window column c (its reflected image
+            // column, once); each row's reflected image row is wave-uniform.  The loads of a batch of rows are issued
+            // before their stores: 2 memory round trips instead of the 29 of a pixel-per-lane loop.  One reflection
+            // is exact: keypoints lie in [19, size - 19) of their level, so the window spans [-2, size + 1] and a
+            // level holding a keypoint is at least 39 px.
             unsigned xx = (unsigned)og_reflect101_1(cx - 21 + min(lane, RAW_W - 1), lw);
             // loads from the uniform base of the lowest row the window can reflect to, plus a 32-bit lane offset
             // (saddr + voffset loads; < 47 rows x 2^24)
             const int y0r = max(cy - 23, 0);
             const uint8_t* wbase = img + (long long)y0r * pitch;
-            for (int r0 = 0; r0 < RAW_W; r0 += OG_DK_BORDER_RB) {
-                uint32_t v[OG_DK_BORDER_RB];
+            for (int r0 = 0; r0 < RAW_W; r0 += DK_BORDER_RB) {
+                uint32_t v[DK_BORDER_RB];
 #pragma unroll
-                for (int k = 0; k < OG_DK_BORDER_RB; k++) {
+                for (int k = 0; k < DK_BORDER_RB; k++) {
                     const int yy = og_reflect101_1(cy - 21 + min(r0 + k, RAW_W - 1), lh);
                     unsigned off = __umul24((unsigned)(yy - y0r), (unsigned)pitch & (OG_MAX_PITCH - 1)) + xx;
                     __asm__("" : "+v"(off));
                     v[k] = wbase[off];
                 }
 #pragma unroll
-                for (int k = 0; k < OG_DK_BORDER_RB; k++)
+                for (int k = 0; k < DK_BORDER_RB; k++)
                     if (lane < RAW_W && r0 + k < RAW_W) R[(r0 + k) * RAW_S + lane] = (uint8_t)v[k];
             }
-#else
-            for (int idx = lane; idx < RAW_W * RAW_W; idx += 64) {
-                const int r = idx / RAW_W, c = idx - (idx / RAW_W) * RAW_W;
-                const int yy = og_reflect101(cy - 21 + r, lh), xx = og_reflect101(cx - 21 + c, lw);
-                R[r * RAW_S + c] = img[(long long)yy * pitch + xx];
-            }
-#endif
         }
     }
     og_dk_sync();
     const uint8_t* Rb = R;  // Rb[r * RAW_S + c] = window pixel (r, c)
     // ---- IC_Angle on the unblurred level (:77-104); integer moments are order-independent
     int m01 = 0, m10 = 0;
-    if (active && OG_DK_ICDOT) {
+    if (active) {
         static_assert(RAW_S == 52, "og_make_ic's row stride");
         const uint32_t rb = og_lds_addr(Rb);
         int a10 = 0, a01 = 0;
 #pragma unroll
         for (int it = 0; it < OG_IC_ITEMS / 64; it++) {
-            const int t = lane + 64 * it;
-            uint32_t msk, wt, ov;
-            if (OG_DK_ICPRE) {
-                auto word = [&](int i) -> uint32_t {
-                    const uint4 q = icq[i >> 2];
-                    return (i & 3) == 0 ? q.x : (i & 3) == 1 ? q.y : (i & 3) == 2 ? q.z : q.w;
-                };
-                msk = word(3 * it);
-                wt = word(3 * it + 1);
-                ov = word(3 * it + 2);
-            } else {
-                msk = og_ic.mask[t];
-                wt = og_ic.wt[t];
-                ov = og_ic.ov[t];
-            }
+            auto word = [&](int i) -> uint32_t {
+                const uint4 q = icq[i >> 2];
+                return (i & 3) == 0 ? q.x : (i & 3) == 1 ? q.y : (i & 3) == 2 ? q.z : q.w;
+            };
+            const uint32_t msk = word(3 * it), wt = word(3 * it + 1), ov = word(3 * it + 2);
             typedef const __attribute__((address_space(3))) uint32_t lds_u32;
             const uint32_t d = *(lds_u32*)(uintptr_t)(rb + (ov & 0xffffu)) & msk;
             const int s0 = (int)__builtin_amdgcn_udot4(d, 0x01010101u, 0u, false);
@@ -3245,41 +3144,20 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         }
         m01 = og_wave_sum(a01);
         m10 = og_wave_sum(a10);
-    } else if (active) {
-        const uint8_t* ctr = Rb + 21 * RAW_S + 21;
-        if (lane < 31) m10 += (lane - 15) * ctr[lane - 15];
-        short e[OG_DISK_ITEMS / 64];
-#pragma unroll
-        for (int it = 0; it < OG_DISK_ITEMS / 64; it++) e[it] = og_disk.e[lane + 64 * it];
-#pragma unroll
-        for (int it = 0; it < OG_DISK_ITEMS / 64; it++) {
-            const int u = (int)(signed char)(e[it] & 0xff), v = e[it] >> 8;
-            const int vp = ctr[u + v * RAW_S], vm = ctr[u - v * RAW_S];
-            m01 += v * (vp - vm);
-            m10 += u * (vp + vm);
-        }
-        m01 = og_wave_sum(m01);
-        m10 = og_wave_sum(m10);
     }
     const float angle = og_fast_atan2((float)m01, (float)m10);
-    // ---- 7x7 Gaussian (sigma 2, BORDER_REFLECT_101) of the 37x37 window the tests can reach.  Integer
-    // weights gk[i]*gk[j] summed exactly and rounded once, so any factoring is exact.  The kernel
-    // [c0,c1,c2,c3,c2,c1,c0] and the rounding follow the context's ORBGPU_SEM_BLUR_* variant:
-    // (acc + 2^15) >> 16, except that the SSE2 variant rounds ties half-to-even in columns x < 4*floor(w/4)
-    // (OpenCV 3.x SymmColumnVec_32s8u: float sums, cvtps2dq).
-    // horizontal pass with v_dot4_u32_u8 (taps 0-3 and 4-6 of a byte window), vertical pass with
-    // v_dot2_u32_u16 over row pairs of the horizontal sums (<= 257 * 255 = 65535, exact in u16).
-    // horizontal: item = (row pair rp, 4-column group g): rows 2rp, 2rp+1, outputs 4g..4g+3, stored as
-    // (row 2rp, row 2rp+1) u16 pairs Hp[rp][col]
+    // ---- 7x7 Gaussian (sigma 2, BORDER_REFLECT_101) at the rBRIEF samples.  Integer weights gk[i]*gk[j] summed
+    // exactly and rounded once, so any factoring is exact.  The kernel [c0,c1,c2,c3,c2,c1,c0] and the rounding follow
+    // the context's ORBGPU_SEM_BLUR_* variant: (acc + 2^15) >> 16, except that the SSE2 variant
+    // rounds ties half-to-even in columns x < 4*floor(w/4) (OpenCV 3.x SymmColumnVec_32s8u: float sums, cvtps2dq).
+    // Horizontal pass over the window with v_dot4_u32_u8: item = (row pair rp, 4-column group g): rows 2rp, 2rp+1,
+    // outputs 4g..4g+3, stored as (row 2rp, row 2rp+1) u16 pairs Hp[rp][col] (<= 257 * 255 = 65535, exact in u16)
     constexpr uint32_t gc = og_blur_coefs[BV];  // c0 | c1 << 8 | c2 << 16 | c3 << 24
     constexpr uint32_t c0 = gc & 0xff, c1 = (gc >> 8) & 0xff, c2 = (gc >> 16) & 0xff, c3 = gc >> 24;
-#ifndef OG_DK_PATPRE
-#define OG_DK_PATPRE 1  // 1: the lane's four rBRIEF test pairs are loaded here, in flight over the blur passes
-                        // (0: at their first use, one round trip on every wave's path)
-#endif
+    // the lane's four rBRIEF test pairs, loaded here: in flight over the blur pass
     float4 pfs[4] = {};
 #if defined(__HIP_DEVICE_COMPILE__)
-    if (OG_DK_PATPRE) {
+    {
         typedef const __attribute__((address_space(1))) float4 g_f4;
         g_f4* pb = (g_f4*)og_pattern_f;
         __asm__("" : "+s"(pb));  // one SGPR base: a lane offset and 1 KB immediate steps
@@ -3288,7 +3166,6 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     }
 #endif
     if (active) {
-        [[maybe_unused]] constexpr uint32_t glo = gc, ghi = c2 | (c1 << 8) | (c0 << 16);  // (OG_DK_HSHIFTW 0)
         for (int it = lane; it < HP_ROWS * 10; it += 64) {
             const int rp = it / 10, g = it - rp * 10;
             uint32_t hv[2][4];
@@ -3297,9 +3174,8 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
                 const int r = min(2 * rp + h, RAW_W - 1);  // row 43 (pair 21, high half) is never read
                 const uint32_t* rr = (const uint32_t*)(Rb + r * RAW_S) + g;
                 const uint32_t d0 = rr[0], d1 = rr[1], d2 = rr[2];
-#if OG_DK_HSHIFTW
                 // output k = sum over the window bytes k .. k+6 of d0:d1:d2: the weights shift, not the data --
-                // 2, 2, 3, 3 dot4 for k = 0..3 (10 instead of 8 dot4 + 6 alignbyte + 4 and)
+                // 2, 2, 3, 3 dot4 for k = 0..3
                 constexpr uint32_t W00 = c0 | c1 << 8 | c2 << 16 | c3 << 24, W01 = c2 | c1 << 8 | c0 << 16;
                 constexpr uint32_t W10 = c0 << 8 | c1 << 16 | c2 << 24, W11 = c3 | c2 << 8 | c1 << 16 | c0 << 24;
                 constexpr uint32_t W20 = c0 << 16 | c1 << 24, W21 = c2 | c3 << 8 | c2 << 16 | c1 << 24, W22 = c0;
@@ -3308,14 +3184,6 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
                 hv[h][1] = __builtin_amdgcn_udot4(d1, W11, __builtin_amdgcn_udot4(d0, W10, 0u, false), false);
                 hv[h][2] = __builtin_amdgcn_udot4(d2, W22, __builtin_amdgcn_udot4(d1, W21, __builtin_amdgcn_udot4(d0, W20, 0u, false), false), false);
                 hv[h][3] = __builtin_amdgcn_udot4(d2, W32, __builtin_amdgcn_udot4(d1, W31, __builtin_amdgcn_udot4(d0, W30, 0u, false), false), false);
-#else
-                hv[h][0] = __builtin_amdgcn_udot4(d1 & 0x00ffffffu, ghi, __builtin_amdgcn_udot4(d0, glo, 0u, false), false);
-#pragma unroll
-                for (int k = 1; k < 4; k++) {
-                    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, k), w1 = __builtin_amdgcn_alignbyte(d2, d1, k);
-                    hv[h][k] = __builtin_amdgcn_udot4(w1 & 0x00ffffffu, ghi, __builtin_amdgcn_udot4(w0, glo, 0u, false), false);
-                }
-#endif
             }
             uint4 o;
             o.x = hv[0][0] | (hv[1][0] << 16);
@@ -3326,105 +3194,17 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         }
     }
     og_dk_sync();
-    // vertical: item = (column c, 4 output rows 4m..4m+3) from row pairs 2m..2m+4; even rows take taps
-    // (g0,g1)(g2,g3)(g4,g5)(g6,0), odd rows (0,g0)(g1,g2)(g3,g4)(g5,g6)
-    typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
-    if (active && !OG_DK_SAMPLEV) {
-        constexpr unsigned short s0 = (unsigned short)c0, s1 = (unsigned short)c1, s2 = (unsigned short)c2,
-                                 s3 = (unsigned short)c3;
-        const u16x2v e0 = {s0, s1}, e1 = {s2, s3}, e2 = {s2, s1}, e3 = {s0, 0};
-        const u16x2v o0 = {0, s0}, o1 = {s1, s2}, o2 = {s3, s2}, o3 = {s1, s0};
-        // level column of window column c is cx - 18 + c (inside the level: keypoints sit >= 19 px from the edge)
-        const int xsimd = BV == 0 ? ((lw & ~3) - (cx - 18)) : 0;  // window columns c < xsimd round half-to-even
-#if OG_DK_VDWORD
-        // item = (row pair p, 4-column group g): rows 2p, 2p + 1 from pairs p .. p + 3 (one 16-byte read each),
-        // columns 4g .. 4g + 3 packed into one dword store per row (columns 37-39 are padding of the BL_S stride)
-        for (int it = lane; it < 19 * 10; it += 64) {
-            const int p = it / 10, g = it - p * 10;
-            uint4 pr4[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) pr4[k] = *(const uint4*)&Hp[(p + k) * HP_S + 4 * g];
-            uint32_t ve4 = 0, vo4 = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                u16x2v q[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t d = j == 0 ? pr4[k].x : j == 1 ? pr4[k].y : j == 2 ? pr4[k].z : pr4[k].w;
-                    q[k] = __builtin_bit_cast(u16x2v, d);
-                }
-                uint32_t ae = __builtin_amdgcn_udot2(q[0], e0, 0u, false);
-                ae = __builtin_amdgcn_udot2(q[1], e1, ae, false);
-                ae = __builtin_amdgcn_udot2(q[2], e2, ae, false);
-                ae = __builtin_amdgcn_udot2(q[3], e3, ae, false);
-                uint32_t ao = __builtin_amdgcn_udot2(q[0], o0, 0u, false);
-                ao = __builtin_amdgcn_udot2(q[1], o1, ao, false);
-                ao = __builtin_amdgcn_udot2(q[2], o2, ao, false);
-                ao = __builtin_amdgcn_udot2(q[3], o3, ao, false);
-                uint32_t ve, vo;
-                if (BV == 0) {
-                    const uint32_t up = 4 * g + j < xsimd ? 0u : 1u;
-                    ve = (ae + 0x7fffu + (__builtin_amdgcn_ubfe(ae, 16, 1) | up)) >> 16;
-                    vo = (ao + 0x7fffu + (__builtin_amdgcn_ubfe(ao, 16, 1) | up)) >> 16;
-                } else {
-                    ve = (ae + (1u << 15)) >> 16;
-                    vo = (ao + (1u << 15)) >> 16;
-                }
-                ve4 |= min(ve, 255u) << (8 * j);
-                vo4 |= min(vo, 255u) << (8 * j);
-            }
-            *(uint32_t*)&Bl[(2 * p) * BL_S + 4 * g] = ve4;
-            if (2 * p + 1 < BL_W) *(uint32_t*)&Bl[(2 * p + 1) * BL_S + 4 * g] = vo4;
-        }
-#else
-        for (int it = lane; it < BL_W * 10; it += 64) {
-            const int m = it / BL_W, c = it - m * BL_W;
-            u16x2v pr[5];
-#pragma unroll
-            for (int k = 0; k < 5; k++) pr[k] = __builtin_bit_cast(u16x2v, Hp[min(2 * m + k, HP_ROWS - 1) * HP_S + c]);
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int r0 = 4 * m + 2 * h;  // rows r0 (even) and r0 + 1 (odd) from pairs 2m+h ..
-                const u16x2v* q = pr + h;
-                uint32_t ae = __builtin_amdgcn_udot2(q[0], e0, 0u, false);
-                ae = __builtin_amdgcn_udot2(q[1], e1, ae, false);
-                ae = __builtin_amdgcn_udot2(q[2], e2, ae, false);
-                ae = __builtin_amdgcn_udot2(q[3], e3, ae, false);
-                uint32_t ao = __builtin_amdgcn_udot2(q[0], o0, 0u, false);
-                ao = __builtin_amdgcn_udot2(q[1], o1, ao, false);
-                ao = __builtin_amdgcn_udot2(q[2], o2, ao, false);
-                ao = __builtin_amdgcn_udot2(q[3], o3, ao, false);
-                uint32_t ve, vo;
-                if (BV == 0) {  // half-to-even in the SIMD columns: + 0x7fff + bit 16 (the quotient's parity)
-                    const uint32_t up = c < xsimd ? 0u : 1u;  // the scalar tail rounds half-up
-                    ve = (ae + 0x7fffu + (__builtin_amdgcn_ubfe(ae, 16, 1) | up)) >> 16;
-                    vo = (ao + 0x7fffu + (__builtin_amdgcn_ubfe(ao, 16, 1) | up)) >> 16;
-                } else {
-                    ve = (ae + (1u << 15)) >> 16;
-                    vo = (ao + (1u << 15)) >> 16;
-                }
-                if (r0 < BL_W) Bl[r0 * BL_W + c] = (uint8_t)min(ve, 255u);
-                if (r0 + 1 < BL_W) Bl[(r0 + 1) * BL_W + c] = (uint8_t)min(vo, 255u);
-            }
-        }
-#endif
-    }
-    if (!OG_DK_SAMPLEV) og_dk_sync();
     if (!active) return;
     // ---- rBRIEF (:108-147)
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     float a, b;
     og_sincosf(angle * factorPI, &b, &a);
     constexpr bool nofma = NOFMA;
-#if OG_DK_SAMPLEV
     // The tests read 512 blurred pixels of the 37x37 window; each is the vertical 7-tap sum over the row-pair
     // horizontal sums Hp at its own column: 4 dword reads and 4 v_dot2 (even rows taps (g0,g1)(g2,g3)(g4,g5)(g6,0),
-    // odd rows (0,g0)(g1,g2)(g3,g4)(g5,g6)), rounded as the window pass rounds (same integer sum, same variant).
-    const int xsimd_s = BV == 0 ? ((lw & ~3) - (cx - 18)) : 0;
-#ifndef OG_DK_UPU
-#define OG_DK_UPU 1  // 1: a keypoint whose 37 window columns all lie in the SSE2 body rounds every sample half-to-even
-                     // without the per-sample column test (wave-uniform branch); 0: the per-sample test only
-#endif
+    // odd rows (0,g0)(g1,g2)(g3,g4)(g5,g6)), rounded by the context's variant.
+    typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+    const int xsimd_s = BV == 0 ? ((lw & ~3) - (cx - 18)) : 0;  // window columns < xsimd_s round half-to-even
     // ALLEVEN: every window column is < xsimd_s (the usual case away from the level's right edge)
     auto blurred = [&](int row, int col, auto alleven) -> int {  // window offsets from the centre, |row|, |col| <= 18
         const int y = 18 + row, xw = 18 + col;
@@ -3447,73 +3227,39 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
         }
         return (int)min(v, 255u);
     };
-#else
-    const uint8_t* ctr = Bl + 18 * BL_S + 18;
-#endif
-#ifndef OG_DK_PK
-#define OG_DK_PK 1  // 1: a sample's (row, col) by packed f32 ops (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32): same
-                    // roundings as the scalar form; 0: four scalar ops
-#endif
     typedef float f2v __attribute__((ext_vector_type(2)));
     const f2v ab = {a, b}, ba = {b, a};
     auto brief_words = [&](auto alleven, u64 (&words)[4]) {
 #pragma unroll
         for (int t = 0; t < 4; t++) {
-            const int p = lane + 64 * t;
-#ifndef OG_DK_PATF
-#define OG_DK_PATF 1  // pattern from the float table (0: bytes + conversions)
-#endif
-#if OG_DK_PATF
-            const float4 pf = OG_DK_PATPRE ? pfs[t] : og_pattern_f[p];
-            const float pfx[2] = {pf.x, pf.z}, pfy[2] = {pf.y, pf.w};
-#else
-            const signed char* pt = og_pattern + 4 * p;
-#endif
+            const float4 pf = pfs[t];
             const f2v xy[2] = {f2v{pf.x, pf.y}, f2v{pf.z, pf.w}};
             int val[2];
 #pragma unroll
             for (int q = 0; q < 2; q++) {
-#if OG_DK_PATF
-                const float x = pfx[q], y = pfy[q];
-#else
-                const float x = (float)pt[2 * q], y = (float)pt[2 * q + 1];
-#endif
-                // GCC -O3 -march=native contracts the first product of GET_VALUE into an FMA; a
-                // build without contraction rounds both products (the kernels are compiled -ffp-contract=off)
-                int row, col;
-                if (OG_DK_PK && OG_DK_PATF) {
-                    // (row, col) = (x b + y a, x a - y b) as one pair: the products, the sums and the FMAs round
-                    // exactly as the scalar statements below.  op_sel picks x or y out of the (x, y) pair for both
-                    // halves, neg_hi negates y b in the high half only.
-                    f2v yab, rc;
-                    __asm__("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(yab) : "v"(xy[q]), "v"(ab));
-                    if (nofma) {
-                        f2v xba;
-                        __asm__("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1]" : "=v"(xba) : "v"(xy[q]), "v"(ba));
-                        __asm__("v_pk_add_f32 %0, %1, %2 neg_lo:[0,0] neg_hi:[0,1]" : "=v"(rc) : "v"(xba), "v"(yab));
-                    } else {
-                        __asm__("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_lo:[0,0,0] neg_hi:[0,0,1]"
-                                : "=v"(rc)
-                                : "v"(xy[q]), "v"(ba), "v"(yab));
-                    }
-                    row = og_cvround(rc.x);
-                    col = og_cvround(rc.y);
+                // GCC -O3 -march=native contracts the first product of GET_VALUE into an FMA; a build
+                // without contraction rounds both products (the kernels are compiled -ffp-contract=off).
+                // (row, col) = (x b + y a, x a - y b) as one pair of packed f32 ops: the products, the sums and the FMAs
+                // round exactly as the scalar statements of the reference.  op_sel picks x or y out of the (x, y) pair
+                // for both halves, neg_hi negates y b in the high half only.
+                f2v yab, rc;
+                __asm__("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(yab) : "v"(xy[q]), "v"(ab));
+                if (nofma) {
+                    f2v xba;
+                    __asm__("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1]" : "=v"(xba) : "v"(xy[q]), "v"(ba));
+                    __asm__("v_pk_add_f32 %0, %1, %2 neg_lo:[0,0] neg_hi:[0,1]" : "=v"(rc) : "v"(xba), "v"(yab));
                 } else {
-                    row = nofma ? og_cvround(x * b + y * a) : og_cvround(__builtin_fmaf(x, b, y * a));
-                    col = nofma ? og_cvround(x * a - y * b) : og_cvround(__builtin_fmaf(x, a, -(y * b)));
+                    __asm__("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_lo:[0,0,0] neg_hi:[0,0,1]"
+                            : "=v"(rc)
+                            : "v"(xy[q]), "v"(ba), "v"(yab));
                 }
-#if OG_DK_SAMPLEV
-                val[q] = blurred(row, col, alleven);
-#else
-                (void)alleven;
-                val[q] = ctr[__mul24(row, BL_S) + col];  // |row| <= 18: a 24-bit multiply
-#endif
+                val[q] = blurred(og_cvround(rc.x), og_cvround(rc.y), alleven);
             }
             words[t] = og_ballot(val[0] < val[1]);
         }
     };
     u64 words[4];
-    if (OG_DK_UPU && OG_DK_SAMPLEV && BV == 0 && xsimd_s >= BL_W)  // wave-uniform
+    if (BV == 0 && xsimd_s >= BL_W)  // wave-uniform: the whole window rounds half-to-even
         brief_words(std::integral_constant<bool, true>{}, words);
     else
         brief_words(std::integral_constant<bool, false>{}, words);
@@ -3673,20 +3419,6 @@ hipError_t og_read_oct_prof(unsigned long long* out, int n)
 #endif
 }
 
-void og_launch_resize_rows(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,
-                           long long dst_pitch, long long dst_fstride, int sw, int sh, int dw, int dh, const int4* xtab,
-                           const int4* ytab, int xmax, int B, int sem)
-{
-    const int runs = (dh + RS_ROWS - 1) / RS_ROWS;
-    dim3 grid((dw + 255) / 256, (runs + RS_NT / 64 - 1) / (RS_NT / 64), B);
-    if (sem & ORBGPU_SEM_RESIZE_FIXEDPT)
-        hipLaunchKernelGGL(og_resize_rows_kernel<true>, grid, dim3(RS_NT), 0, s, src, src_pitch, src_fstride, dst,
-                           dst_pitch, dst_fstride, sw, sh, dw, dh, xtab, ytab, xmax);
-    else
-        hipLaunchKernelGGL(og_resize_rows_kernel<false>, grid, dim3(RS_NT), 0, s, src, src_pitch, src_fstride, dst,
-                           dst_pitch, dst_fstride, sw, sh, dw, dh, xtab, ytab, xmax);
-}
-
 void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,
                       long long dst_pitch, long long dst_fstride, int sw, int sh, int dw, int dh, const int4* xtab,
                       const int4* ytab, int xmax, int* status, int B, int sem)
@@ -3728,19 +3460,44 @@ void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, l
                            pitchA, dstB, pitchB, dst_fstride, g, status);
 }
 
-void og_launch_fast(hipStream_t s, const OgPlan& P, const OgFastBlk* blocks, int nblocks, const uint8_t* img0,
+#ifndef OG_FAST_CELLS
+#define OG_FAST_CELLS 1  // 1: levels with cells <= FC_MAXC x FC_MAXC run og_fast_cell_kernel (one wave per cell)
+#endif
+bool og_fast_cell_level(const OgLevel& L) { return OG_FAST_CELLS && L.wCell <= FC_MAXC && L.hCell <= FC_MAXC; }
+
+void og_launch_fast(hipStream_t s, const OgPlan& P, int lb, int le, const OgFastBlk* table, const uint8_t* img0,
                     long long pitch0, long long fstride0, const uint8_t* pyr, u64* cand, int* cand_count, int* status,
                     int B)
 {
-    if (nblocks <= 0 || B <= 0) return;
+    le = std::min(le, P.nlevels);
+    if (lb >= le || B <= 0) return;
     const int thr = std::min(std::max(P.iniTh, 0), 255) | (std::min(std::max(P.minTh, 0), 255) << 8);
 #ifndef OG_FASTQ_KB
 #define OG_FASTQ_KB 1
 #endif
-    // KB blocks per workgroup (og_fast_quad_kernel): G workgroups per frame, a multiple of 8
-    const int G = OG_FASTQ_KB == 1 ? nblocks : ((nblocks + OG_FASTQ_KB - 1) / OG_FASTQ_KB + 7) & ~7;
-    hipLaunchKernelGGL(og_fast_quad_kernel<OG_FASTQ_KB>, dim3(G, B), dim3(FB_NT), 0, s, blocks, nblocks, img0, pitch0,
-                       fstride0, pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels, thr, status);
+    // runs of consecutive levels of one kernel; each level's table range starts at a multiple of 8, so workgroup w of
+    // every frame keeps XCD w % 8 (the table's XCD runs)
+    for (int l = lb; l < le;) {
+        const bool cm = og_fast_cell_level(P.lv[l]);
+        int l1 = l + 1;
+        while (l1 < le && og_fast_cell_level(P.lv[l1]) == cm) l1++;
+        const int p0 = P.lv[l].fb_off, p1 = l1 < P.nlevels ? P.lv[l1].fb_off : P.fast_blocks;
+        const int nblocks = p1 - p0;
+        const OgFastBlk* blocks = table + p0;
+        l = l1;
+        if (nblocks <= 0) continue;
+        if (cm) {
+            hipLaunchKernelGGL(og_fast_cell_kernel, dim3(nblocks, B), dim3(64 * FC_NW), 0, s, blocks, nblocks, img0,
+                               pitch0, fstride0, pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels,
+                               thr, status);
+            continue;
+        }
+        // KB blocks per workgroup (og_fast_quad_kernel): G workgroups per frame, a multiple of 8
+        const int G = OG_FASTQ_KB == 1 ? nblocks : ((nblocks + OG_FASTQ_KB - 1) / OG_FASTQ_KB + 7) & ~7;
+        hipLaunchKernelGGL(og_fast_quad_kernel<OG_FASTQ_KB>, dim3(G, B), dim3(FB_NT), 0, s, blocks, nblocks, img0,
+                           pitch0, fstride0, pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels, thr,
+                           status);
+    }
 }
 
 void og_launch_harris(hipStream_t s, const OgPlan& P, int lb, int le, const uint8_t* img0, long long pitch0,

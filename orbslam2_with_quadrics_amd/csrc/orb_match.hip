@@ -579,9 +579,6 @@ __device__ __forceinline__ void og_proj_visit(const Geom& K, const uint8_t* fdes
 // og_proj_visit with the candidates' descriptor loads batched: up to 4 candidates that pass the geometric filters are
 // queued (in order) and their descriptors loaded together, so a point's window costs one memory round trip per 4
 // candidates instead of one per candidate.  Same candidates, same order, same visits.
-#ifndef OG_PJ_BATCH
-#define OG_PJ_BATCH 1
-#endif
 template <class Geom, class Visit>
 __device__ __forceinline__ void og_proj_visit_b(const Geom& K, const uint8_t* fdesc, const OgGridGeom& G, const float* sf,
                                                 const OgMapPointsDev& mp, int m, float th, int dkeep, Visit visit)
@@ -751,9 +748,12 @@ __device__ __forceinline__ OgMapPointsDev og_mp_of(const OgMapPointsDev& mp, int
 // fit the LDS take the same enumeration from HBM.
 #define PF_NT 512
 #define PF_WG 4  // workgroups per frame
+// the cell starts (OG_GRID_CELLS + 1 ints) padded to a 16-byte multiple, so the float2 XY array after them is
+// 8-byte aligned (ds_read_b64, no split accesses)
+#define PF_CS_INTS (((OG_GRID_CELLS + 1) + 3) & ~3)
 __host__ __device__ inline size_t og_projb_fill_lds(int frame_cap, bool ur)
 {
-    return (size_t)(OG_GRID_CELLS + 1) * 4 + (size_t)frame_cap * (8 + 1 + 2 + (ur ? 4 : 0)) + 16;
+    return (size_t)PF_CS_INTS * 4 + (size_t)frame_cap * (8 + 1 + 2 + (ur ? 4 : 0)) + 16;
 }
 
 __global__ __launch_bounds__(PF_NT) void og_projb_fill_kernel(OgFrameDev Fb, OgGridGeom G, const float* sf,
@@ -774,10 +774,7 @@ __global__ __launch_bounds__(PF_NT) void og_projb_fill_kernel(OgFrameDev Fb, OgG
                 if (n < OG_PJ_K) S[(long long)n * stride + m] = og_pj_pack(idx, dist, oct);
                 n++;
             };
-            if (OG_PJ_BATCH)
-                og_proj_visit_b(K, F.desc, G, sf, q, m, th, dkeep, put);
-            else
-                og_proj_visit(K, F.desc, G, sf, q, m, th, dkeep, put);
+            og_proj_visit_b(K, F.desc, G, sf, q, m, th, dkeep, put);
             KEPT[m] = n;
         }
     };
@@ -787,7 +784,7 @@ __global__ __launch_bounds__(PF_NT) void og_projb_fill_kernel(OgFrameDev Fb, OgG
     }
     const int n = min(F.counts[0], F.frame_cap);
     int* CS = (int*)pf_lds;
-    float2* XY = (float2*)(CS + OG_GRID_CELLS + 1);
+    float2* XY = (float2*)(CS + PF_CS_INTS);
     float* UR = (float*)(XY + F.frame_cap);
     uint16_t* CI = (uint16_t*)(UR + (F.uright ? F.frame_cap : 0));
     uint8_t* OC = (uint8_t*)(CI + F.frame_cap);
@@ -850,8 +847,8 @@ __global__ __launch_bounds__(PJ_NT) void og_projb_resolve_kernel(OgFrameDev Fb, 
                                                                  OgMapPointsDev mp, int stride, float th, int dkeep,
                                                                  const uint32_t* __restrict__ slots,
                                                                  const int* __restrict__ kept, float nnratio,
-                                                                 int lds_bytes, int* owner, int* owner_obs,
-                                                                 int* nmatches, int* res, int* status)
+                                                                 int lds_bytes, int stage_ok, int* owner,
+                                                                 int* owner_obs, int* nmatches, int* res, int* status)
 {
     extern __shared__ int pj_lds[];
     const int frame_cap = Fb.frame_cap;
@@ -884,7 +881,8 @@ __global__ __launch_bounds__(PJ_NT) void og_projb_resolve_kernel(OgFrameDev Fb, 
     const int base = og_block_exclusive_scan(my, wsum, T);
     uint32_t* LST = (uint32_t*)(PO + M + 1);
     const int cap_entries = (lds_bytes - (int)sizeof(int) * (2 * frame_cap + M + 1)) / 4;
-    const bool staged = M > 0 && T <= cap_entries && (2 * frame_cap + M + 1) * (int)sizeof(int) <= lds_bytes;  // uniform
+    const bool staged = stage_ok && M > 0 && T <= cap_entries &&
+                        (2 * frame_cap + M + 1) * (int)sizeof(int) <= lds_bytes;  // uniform
     if (staged) {
         int o = base;
         for (int k = 0; k < ppt; k++) {
@@ -996,19 +994,21 @@ __global__ __launch_bounds__(PJ_NT) void og_projb_resolve_kernel(OgFrameDev Fb, 
 
 void og_launch_projb(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, int stride,
                      float nnratio, float th, int B, uint32_t* slots, int* kept, int* res, int* owner, int* owner_obs,
-                     int* nmatches, int* status)
+                     int* nmatches, int* status, int dbg)
 {
+    // dbg (orbgpu_debug_set_projection_paths, tests only): 1 = enumerate from HBM geometry, 2 = resolve from the
+    // slots in HBM (no LDS-staged lists); both are the paths of frames too large for the LDS
     if (B <= 0) return;
     const int dkeep = og_proj_keep_bound(nnratio);
     if (mp.m > 0) {
         // cell items are u16 in LDS: frames of at most 65535 keypoints (the host form checks far less)
         const size_t lds = og_projb_fill_lds(F.frame_cap, F.uright != nullptr);
-        const int use_lds = lds <= OG_PJ_LDS && F.frame_cap <= 65535;
+        const int use_lds = !(dbg & 1) && lds <= OG_PJ_LDS && F.frame_cap <= 65535;
         hipLaunchKernelGGL(og_projb_fill_kernel, dim3(PF_WG, B), dim3(PF_NT), use_lds ? lds : 0, s, F, G, sf, mp, stride,
                            th, dkeep, use_lds, slots, kept);
     }
     hipLaunchKernelGGL(og_projb_resolve_kernel, dim3(B), dim3(PJ_NT), OG_PJ_LDS, s, F, G, sf, mp, stride, th, dkeep,
-                       slots, kept, nnratio, (int)OG_PJ_LDS, owner, owner_obs, nmatches, res, status);
+                       slots, kept, nnratio, (int)OG_PJ_LDS, (dbg & 2) ? 0 : 1, owner, owner_obs, nmatches, res, status);
 }
 
 // ------------------------------------------------------------------------------------------------

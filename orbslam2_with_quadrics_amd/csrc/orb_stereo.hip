@@ -74,10 +74,6 @@ __global__ __launch_bounds__(ST_NT) void og_stereo_rows_kernel(OgStereoDev S)
     if (tid == 0) RS[S.nRows] = carry;
     __syncthreads();
     __threadfence_block();
-#ifndef OG_ST_ROWS_WAVE
-#define OG_ST_ROWS_WAVE 1  // 1: one wave per row, 64 keypoints per ballot (0: one thread per row walks them all)
-#endif
-#if OG_ST_ROWS_WAVE
     // each row's list in index order: the wave takes the keypoints 64 at a time, ballots the ones whose band holds
     // the row and writes them at their rank (index order within the ballot, the ballots in index order)
     for (int y = wv; y < S.nRows; y += ST_NT / 64) {
@@ -92,14 +88,6 @@ __global__ __launch_bounds__(ST_NT) void og_stereo_rows_kernel(OgStereoDev S)
             pos += __popcll(m);
         }
     }
-#else
-    for (int y = tid; y < S.nRows; y += ST_NT) {
-        int pos = RS[y];
-        const int end = min(pos + cnt[y], S.row_cap);
-        for (int iR = 0; iR < Nr && pos < end; iR++)
-            if (lo_[iR] <= y && y <= hi_[iR]) RI[pos++] = iR;
-    }
-#endif
 }
 
 // ---- og_stereo_match16_kernel: one left keypoint per 16 lanes (4 keypoints per wave, 16 per 256-thread workgroup):
@@ -164,9 +152,7 @@ __global__ __launch_bounds__(256) void og_stereo_match16_kernel(OgStereoDev S)
     // row list, which holds at most ST_MAXR right keypoints, so it fits the low 16 bits.
     static_assert(ST_MAXR <= 65535, "row-list positions are packed into 16 bits");
     unsigned best = 0xffffffffu;
-#ifndef OG_ST_BAND_U
 #define OG_ST_BAND_U 4  // band candidates per lane whose dependent loads (list entry, keypoint, descriptor) are batched
-#endif
     // each stage's loads for OG_ST_BAND_U candidates are issued together: 3 memory round trips per batch instead of 3
     // per candidate (the candidate order only enters through the packed position, so the batching is exact)
     for (int c0 = cb + l; c0 < ce; c0 += 16 * OG_ST_BAND_U) {

@@ -60,6 +60,7 @@ struct orbgpu_ctx {
     // plan for the current geometry
     int W = 0, H = 0;
     bool planned = false;
+    int dbg_proj = 0;  // orbgpu_debug_set_projection_paths (tests only)
     OgPlan plan{};
     std::vector<OgCell> cells_h;
     std::vector<int4> xtab_h, ytab_h;
@@ -579,22 +580,6 @@ static const orbgpu_kp_dev* kps_match(const orbgpu_ctx* c) { return c->undist ? 
 static void launch_pyramid(orbgpu_ctx* c, hipStream_t s, const uint8_t* d_imgs, int B, long long pitch, long long fstride)
 {
     const OgPlan& P = c->plan;
-    static const int rows_mode = [] {  // ORBGPU_PYR_ROWS=1: every level by the row-stream kernel (A/B switch)
-        const char* e = std::getenv("ORBGPU_PYR_ROWS");
-        return e ? std::atoi(e) : 0;
-    }();
-    if (rows_mode) {
-        for (int l = 1; l < P.nlevels; l++) {
-            const OgLevel& L = P.lv[l];
-            const OgLevel& Lp = P.lv[l - 1];
-            const uint8_t* src = l == 1 ? d_imgs : c->pyr.p + Lp.pyr_off;
-            const long long sp = l == 1 ? pitch : Lp.pitch;
-            const long long sfs = l == 1 ? fstride : P.pyr_per_frame;
-            og_launch_resize_rows(s, src, sp, sfs, c->pyr.p + L.pyr_off, L.pitch, P.pyr_per_frame, Lp.w, Lp.h, L.w, L.h,
-                                  c->tabs.p + L.xtab_off, c->tabs.p + L.ytab_off, L.xmax, B, P.sem);
-        }
-        return;
-    }
     for (int l = 1; l < P.nlevels;) {
         const OgLevel& L = P.lv[l];
         const OgLevel& Lp = P.lv[l - 1];
@@ -623,8 +608,7 @@ static void launch_levels(orbgpu_ctx* c, hipStream_t s, int lb, int le, const ui
                           long long fstride, bool marks)
 {
     const OgPlan& P = c->plan;
-    const int p0 = P.lv[lb].fb_off, p1 = le < P.nlevels ? P.lv[le].fb_off : P.fast_blocks;
-    og_launch_fast(s, P, c->cells.p + p0, p1 - p0, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p,
+    og_launch_fast(s, P, lb, le, c->cells.p, d_imgs, pitch, fstride, c->pyr.p, c->cand.p, c->cand_count.p,
                    c->status.p, B);
     if (marks) timer_mark(c, "fast");
     if (P.sem & ORBGPU_SEM_SCORE_HARRIS) {  // option: rank by the Harris response (include/orbgpu.h)
@@ -1765,7 +1749,7 @@ static int run_projection(orbgpu_ctx* c, hipStream_t s, const OgFrameDev& fd, co
     int* kept = c->pj_int.p;
     int* res = kept + pts;
     og_launch_projb(s, fd, G, sfd, mpd, stride, nnratio, th, B, (uint32_t*)c->mcands.p, kept, res, own, obs, nm,
-                    c->status.p);
+                    c->status.p, c->dbg_proj);
     HIP_TRY(c, hipGetLastError());
     return ORBGPU_OK;
 }
@@ -2235,6 +2219,13 @@ int orbgpu_debug_octree_profile(orbgpu_ctx* c, unsigned long long* out, int n)
     const hipError_t e = og_read_oct_prof(out, n);
     if (e == hipErrorNotSupported) return ORBGPU_ERR_UNSUPPORTED;
     HIP_TRY(c, e);
+    return ORBGPU_OK;
+}
+
+int orbgpu_debug_set_projection_paths(orbgpu_ctx* c, int flags)
+{
+    if (!c || (flags & ~(ORBGPU_DEBUG_PROJ_FILL_HBM | ORBGPU_DEBUG_PROJ_RESOLVE_HBM))) return ORBGPU_ERR_ARG;
+    c->dbg_proj = flags;
     return ORBGPU_OK;
 }
 

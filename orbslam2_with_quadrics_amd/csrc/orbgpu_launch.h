@@ -19,10 +19,6 @@ hipError_t og_upload_pattern(int device);
 hipError_t og_math_hash(int fn, unsigned long long begin, unsigned long long end, int chunk_log2,
                         unsigned long long* d_out, hipStream_t s);
 
-// one level as a row stream (og_resize_rows_kernel): strips of 256 columns x runs of 32 rows, no LDS
-void og_launch_resize_rows(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dst,
-                           long long dst_pitch, long long dst_fstride, int sw, int sh, int dw, int dh, const int4* xtab,
-                           const int4* ytab, int xmax, int B, int sem);
 // two chained levels per launch (og_resize2_kernel): A = level l from S = level l-1, B = level l+1 from A
 struct OgRz2Geom {
     int sw, sh, aw, ah, bw, bh;
@@ -55,8 +51,10 @@ void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, lo
 hipError_t og_prepare_device();  // per-device kernel attributes (call after hipSetDevice)
 hipError_t og_prepare_device_match();  // (called by og_prepare_device)
 hipError_t og_prepare_device_bow();
-// nblocks entries of the block table from `cells` on, for each of B frames
-void og_launch_fast(hipStream_t s, const OgPlan& P, const OgFastBlk* blocks, int nblocks, const uint8_t* img0,
+// FAST of levels [lb, le) for each of B frames (table = the whole block table; og_fast_cell_kernel for the levels
+// og_fast_cell_level accepts, og_fast_quad_kernel for the others)
+bool og_fast_cell_level(const OgLevel& L);
+void og_launch_fast(hipStream_t s, const OgPlan& P, int lb, int le, const OgFastBlk* table, const uint8_t* img0,
                     long long pitch0, long long fstride0, const uint8_t* pyr, unsigned long long* cand, int* cand_count,
                     int* status, int B);
 hipError_t og_read_fast_prof(unsigned long long* out, int n);  // OG_FAST_PROFILE builds only
@@ -120,7 +118,7 @@ struct OgMapPointsDev {
 int og_proj_keep_bound(float nnratio);
 void og_launch_projb(hipStream_t s, OgFrameDev F, OgGridGeom G, const float* sf, OgMapPointsDev mp, int stride,
                      float nnratio, float th, int B, uint32_t* slots, int* kept, int* res, int* owner, int* owner_obs,
-                     int* nmatches, int* status);
+                     int* nmatches, int* status, int dbg);
 
 // stereo (orb_stereo.hip): Frame::ComputeStereoMatches over frame pairs b of two extractor batches
 struct OgStereoDev {

@@ -91,6 +91,84 @@ def test_search_by_projection_vs_oracle(gpu, oracle, th):
     assert np.array_equal(obs, obo)
 
 
+def _dense_frame(rng, Q=48, per=40, rows=1080, cols=1920):
+    """Crafted keypoints: Q clusters of `per` level-0 keypoints within +-2 px, their descriptors 20-90 bits from the
+    cluster's base descriptor, plus scattered background keypoints.  A map point projected on a cluster sees every
+    keypoint of it inside its window with a distance <= TH_HIGH: far more than OG_PJ_K = 16 kept candidates."""
+    from orbslam2_with_quadrics_amd import extractor as gx
+
+    def at_distance(base, dist):
+        bits = np.unpackbits(base)
+        flip = rng.choice(256, dist, replace=False)
+        bits[flip] ^= 1
+        return np.packbits(bits)
+
+    cx = rng.uniform(60, cols - 60, Q)
+    cy = rng.uniform(60, rows - 60, Q)
+    base = rng.integers(0, 256, (Q, 32), dtype=np.uint8)
+    kl, dl = [], []
+    for q in range(Q):
+        for _ in range(per):
+            kl.append((cx[q] + rng.uniform(-2, 2), cy[q] + rng.uniform(-2, 2)))
+            dl.append(at_distance(base[q], int(rng.integers(20, 91))))
+    nb = 600  # background
+    for _ in range(nb):
+        kl.append((rng.uniform(20, cols - 20), rng.uniform(20, rows - 20)))
+        dl.append(rng.integers(0, 256, 32, dtype=np.uint8))
+    k = np.zeros(len(kl), gx.KP_DTYPE)
+    k["x"] = [p[0] for p in kl]
+    k["y"] = [p[1] for p in kl]
+    k["size"], k["octave"], k["class_id"], k["response"] = 31.0, 0, -1, 1.0
+    k["angle"] = rng.uniform(0, 360, len(kl))
+    return k, np.stack(dl), cx, cy, base
+
+
+@pytest.mark.parametrize("flags", [0, 1, 2, 3])
+def test_search_by_projection_dense_windows_and_forced_paths(gpu, oracle, flags):
+    """the projection matcher's paths that ordinary frames never reach, pinned against the oracle.
+    * Dense windows: every map point projected on a crafted cluster keeps ~40 candidates (> OG_PJ_K = 16), so the
+      resolve re-enumerates those points in every round (and several points contest each cluster's keypoints,
+      with and without observations, so the claim rounds iterate).
+    * flags (orbgpu_debug_set_projection_paths): 1 = window enumeration from HBM geometry instead of the LDS copy,
+      2 = claim rounds on the HBM slots instead of LDS-staged lists (the paths of frames too large for the LDS)."""
+    from orbslam2_with_quadrics_amd import _lib
+
+    rng = np.random.default_rng(55)
+    rows, cols = 1080, 1920
+    k, d, cx, cy, base = _dense_frame(rng)
+    Q = len(cx)
+    reps = 5
+    M = Q * reps
+    src = np.repeat(np.arange(Q), reps)
+    desc = base[src] ^ np.packbits(rng.random((M, 256)) < 0.04, axis=1)
+    mp = dict(track_in_view=np.ones(M, np.uint8), is_bad=np.zeros(M, np.uint8), level=np.zeros(M, np.int32),
+              view_cos=rng.choice([0.95, 0.999], M).astype(np.float32),
+              proj_x=(cx[src] + rng.normal(0, 0.3, M)).astype(np.float32),
+              proj_y=(cy[src] + rng.normal(0, 0.3, M)).astype(np.float32),
+              proj_xr=np.full(M, -1, np.float32), n_obs=np.where(rng.random(M) < 0.5, 0, 3).astype(np.int32),
+              desc=desc)
+    # plus ordinary map points on the background keypoints
+    ex = gpu.ORBextractor(2000, 1.2, 8, 20, 7)
+    sf = ex.GetScaleFactors()
+    owner0 = np.full(len(k), -1, np.int32)
+    obs0 = np.zeros(len(k), np.int32)
+    owner0[::29] = M + 3  # claims made before the call
+    obs0[::58] = 1
+    _lib.check(ex.ctx, _lib.lib().orbgpu_debug_set_projection_paths(ex.ctx, flags), "debug paths")
+    try:
+        for th in (1.0, 3.0):
+            F = gpu.Frame(k, d, cols, rows, sf)
+            n, own, obs = gpu.ORBmatcher(0.8, context=ex).SearchByProjection(F, mp, th, owner=owner0.copy(),
+                                                                             owner_obs=obs0.copy())
+            no, owo, obo = oracle.search_by_projection(oracle.OracleFrame(k, d, cols, rows, sf), mp, 0.8, th,
+                                                       owner0, obs0)
+            assert n == no and n >= Q // 2, (flags, th, n, no)
+            assert np.array_equal(own, owo), (flags, th)
+            assert np.array_equal(obs, obo), (flags, th)
+    finally:
+        _lib.lib().orbgpu_debug_set_projection_paths(ex.ctx, 0)
+
+
 def test_search_by_projection_stereo_and_preclaimed(gpu, oracle):
     rng = np.random.default_rng(3)
     img = synthetic.frame(61, 376, 1241)
