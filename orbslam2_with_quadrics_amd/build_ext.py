@@ -65,6 +65,35 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
     return target
 
 
+# ---- experiment / diagnostic builds of the same library (orbslam2_with_quadrics_amd/variants/liborbgpu_<name>.so).
+# Every compile-time switch left in csrc/ is listed here with the build that flips it; build() of __graft_entry__
+# builds them all, and tests/test_gpu_variants.py runs each one on the GPU and checks its keypoints, descriptors and
+# matches bit-exactly against the default build's.
+VARIANT_DIR = os.path.join(HERE, "variants")
+VARIANTS = {
+    "fastprof": ["OG_FAST_PROFILE=1"],        # FAST per-phase clocks (tools/fast_profile.py)
+    "octprof0": ["OG_OCT_PROFILE=1"],         # octree per-round clocks of level 0 (tools/octree_profile.py)
+    "octbt0": ["OG_OCT_BESTTAB=0"],           # octree final key pass instead of the cell-best table
+}
+# the run-time switches (environment variables read by liborbgpu.so), checked the same way with the default build
+ENV_VARIANTS = {
+    "order1": {"ORBGPU_FAST_ORDER": "1"},          # FAST blocks in plain plan order instead of XCD runs of 4
+    "order8": {"ORBGPU_FAST_ORDER": "8"},
+    "forkall": {"ORBGPU_FORK_MIN_PIXELS": "0"},    # every small batch forks level 0 onto its own stream
+    "forknone": {"ORBGPU_FORK_MIN_PIXELS": "1000000000000"},
+    "debugsync": {"ORBGPU_DEBUG_SYNC": "1"},       # synchronise after every stage (diagnostics)
+}
+
+
+def variant_path(name: str) -> str:
+    return os.path.join(VARIANT_DIR, f"liborbgpu_{name}.so")
+
+
+def build_variants(names=None) -> list:
+    os.makedirs(VARIANT_DIR, exist_ok=True)
+    return [build(force=True, defines=VARIANTS[n], out=variant_path(n)) for n in (names or VARIANTS)]
+
+
 # ---- C++ host layer (ORB_SLAM2::ORBextractor / Frame / ORBmatcher / ORBVocabulary over the C ABI) ----
 ROOT = os.path.dirname(HERE)
 HOST_SRC = os.path.join(HERE, "host")

@@ -247,6 +247,23 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
 
 // 4 horizontally adjacent outputs of one row from two LDS source rows: sx = byte offsets in the rows, weights
 // (a0, a1) per column (a1 = 0 at the right border), vertical weights (yz, yw)
+// min(t, 255) into byte k of `packed`, the other bytes preserved (SDWA dst_sel: no shift-or per byte)
+__device__ __forceinline__ void og_rz_put_byte(uint32_t& packed, uint32_t t, int k)
+{
+    if (k == 0)
+        __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                : "+v"(packed) : "v"(t), "s"(255u));
+    else if (k == 1)
+        __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                : "+v"(packed) : "v"(t), "s"(255u));
+    else if (k == 2)
+        __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                : "+v"(packed) : "v"(t), "s"(255u));
+    else
+        __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                : "+v"(packed) : "v"(t), "s"(255u));
+}
+
 template <bool FX>
 __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t* R1, const int* sx,
                                                const og_rz_u16x2* wt, unsigned yz, unsigned yw)
@@ -258,25 +275,10 @@ __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t*
         const uint32_t p1 = (uint32_t)R1[sx[k]] | ((uint32_t)R1[sx[k] + 1] << 16);
         const uint32_t d0 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[k], 0u, false);
         const uint32_t d1 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[k], 0u, false);
-        if (!FX) {
-            // og_rz_vert16 up to its final min, which writes byte k of `packed` (the other bytes preserved: SDWA
-            // dst_sel, no shift-or per byte)
-            const uint32_t t = (og_mulhi_u24(yz << 8, d0 & ~0xffu) + og_mulhi_u24(yw << 8, d1 & ~0xffu) + 2u) >> 2;
-            if (k == 0)
-                __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                        : "+v"(packed) : "v"(t), "s"(255u));
-            else if (k == 1)
-                __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                        : "+v"(packed) : "v"(t), "s"(255u));
-            else if (k == 2)
-                __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                        : "+v"(packed) : "v"(t), "s"(255u));
-            else
-                __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                        : "+v"(packed) : "v"(t), "s"(255u));
-        } else {
+        if (!FX)  // og_rz_vert16 up to its final min, which writes byte k of `packed`
+            og_rz_put_byte(packed, (og_mulhi_u24(yz << 8, d0 & ~0xffu) + og_mulhi_u24(yw << 8, d1 & ~0xffu) + 2u) >> 2, k);
+        else
             packed |= og_rz_vert16<FX>(yz, d0, yw, d1) << (8 * k);
-        }
     }
     return packed;
 }
@@ -293,9 +295,7 @@ __device__ __forceinline__ void og_rz_weights(const int4* xtab, int xmax, int dx
                       : og_rz_u16x2{(unsigned short)(2048 << sh), 0};
 }
 
-#ifndef RZ2_U
-#define RZ2_U 3
-#endif
+#define RZ2_U 3  // staging chunks per thread per round of og_resize2_kernel
 
 __device__ __forceinline__ void og_rz_store4(uint8_t* Dr, uint32_t packed, int n)
 {
@@ -793,68 +793,8 @@ __device__ __forceinline__ void og_fastq_roi_put(const OgFB& b, int tid, const u
     }
 }
 
-// KB > 1 with OG_FASTQ_DMA: the next block's ROI goes HBM -> LDS by LDS-DMA (global_load_lds_dword, no VGPR
-// destination) into roiq, free from the end of stage 2: wave w stages the rows it converts itself (ROI rows 8w .. 8w + 7
-// and 64 + 8w .. 64 + 8w + 7), FQ_RS dwords per row from the row's 4-byte-aligned start, lane-linear (local row lr at
-// dword lr * FQ_RS of the wave's 16 * FQ_RS-dword slice).  Before the emission the wave waits for its own DMA and reads
-// its rows into the registers og_fastq_roi_put converts (og_fastq_raw_get); the raw slices are 10 KB of roiq's 19 KB.
-#ifndef OG_FASTQ_DMA
-#define OG_FASTQ_DMA 0
-#endif
-#define FQ_RS 20  // dwords per staged row: the quads read bytes <= 4 * 6 + 48 + 3 (+ 3 misalignment) of a row
-__device__ __forceinline__ void og_fastq_roi_dma(const OgFB& b, int wv, int lane, uint32_t* raw)
-{
-    typedef __attribute__((address_space(3))) void lds_void;
-    typedef __attribute__((address_space(1))) const void glb_void;
-    const uint8_t* rbase = b.row0 - b.mis;
-    // (the lane's row/dword split is recomputed here, not hoisted out of the block loop into spilled registers)
-    __asm__ volatile("" : "+v"(lane));
-#pragma unroll
-    for (int j = 0; j < 16 * FQ_RS / 64; j++) {
-        const int lr0 = (64 * j) / FQ_RS;  // the instruction's first local row (uniform)
-        if ((lr0 < 8 ? 8 * wv + lr0 : 56 + 8 * wv + lr0) >= b.rh) continue;
-        const int t = 64 * j + lane;
-        const int lr = (t * 3277) >> 16;  // t / 20 for t < 320
-        const int d = t - FQ_RS * lr;
-        const int r = min(lr < 8 ? 8 * wv + lr : 56 + 8 * wv + lr, b.rh - 1);  // rows past the ROI re-read its last row
-        const uintptr_t ra = (uintptr_t)rbase + (unsigned)r * b.upitch;
-        const uint8_t* a = (const uint8_t*)((ra & ~(uintptr_t)3) + 4u * (unsigned)d);
-        __builtin_amdgcn_global_load_lds((glb_void*)a, (lds_void*)(raw + wv * 16 * FQ_RS + 64 * j), 4, 0, 0);
-    }
-}
-// the wave's own staged rows -> og_fastq_roi_load's registers (the caller has waited for the wave's DMA)
-__device__ __forceinline__ void og_fastq_raw_get(const OgFB& b, int wv, int lane, const uint32_t* raw, uint32_t (&s)[2][4])
-{
-    const int nq4 = (16 + 6 + b.mis + 3) >> 2;
-    const int q4 = min(lane & 7, nq4 - 1);
-    const uint8_t* rbase = b.row0 - b.mis;
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const int lr = (lane >> 3) + 8 * k;
-        const int r = min(8 * wv + (lane >> 3) + 64 * k, b.rh - 1);
-        const uint32_t* R = raw + wv * 16 * FQ_RS + lr * FQ_RS + q4;
-        if (b.aligned) {
-#pragma unroll
-            for (int g = 0; g < 4; g++) s[k][g] = R[4 * g];
-        } else {
-            const unsigned sh = (unsigned)(((uintptr_t)rbase + (unsigned)r * b.upitch) & 3u);
-#pragma unroll
-            for (int g = 0; g < 4; g++) s[k][g] = __builtin_amdgcn_alignbyte(R[4 * g + 1], R[4 * g], sh);
-        }
-    }
-}
-// a workgroup barrier for LDS data only: with an LDS-DMA in flight __syncthreads() would wait for it (vmcnt(0))
-__device__ __forceinline__ void og_fastq_sync()
-{
-#if OG_FASTQ_DMA
-    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
-    __syncthreads();
-#endif
-}
-
 #ifndef OG_FAST_PROFILE
-#define OG_FAST_PROFILE 0
+#define OG_FAST_PROFILE 0  // 1: diagnostic clocks (variant "fastprof", tests/test_gpu_variants.py)
 #endif
 #if OG_FAST_PROFILE  // diagnostic builds only (tools/fast_profile.py): per-phase clocks of every block of the middle frame
 __device__ unsigned long long og_fast_prof[4096 * 8];
@@ -871,7 +811,8 @@ __device__ unsigned long long og_fast_prof[4096 * 8];
 // One block per workgroup.  Stage 1: quick test of every detection pixel and a survivor list; stage 2: exact scores
 // into the score map; stage 3: same-cell NMS at both thresholds and per-cell counts; stage 4: the reference's
 // per-cell 20 -> 7 fallback, one global reservation per block and the candidate stores.
-template <int KB>
+// (8 waves per SIMD: 64 VGPRs.  Prefetching a second block's ROI under a relaxed budget of 4 waves per SIMD measured
+// 2.2x (registers) and 1.6x (LDS-DMA) the FAST time: profiles/sweeps/r05_ab_fast_cell_prefetch_describe_kp2_mono.txt)
 __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_fast_quad_kernel(
     const OgFastBlk* __restrict__ blocks, int nb, const uint8_t* __restrict__ img0, long long pitch0, long long fstride0,
     const uint8_t* __restrict__ pyr, long long pyr_per_frame, u64* __restrict__ cand, long long cand_per_frame,
@@ -892,39 +833,25 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
     const int tA = max(t1, 1), tB = max(t2, 1);
     const uint32_t a_ns = og_lds_addr(&sh_ns), a_lst = og_lds_addr(&lst[0]);
-    // KB > 1: workgroup x takes the valid blocks among x, x + G, ..., x + (KB - 1) G (G = gridDim.x, a multiple of 8:
-    // every block keeps the XCD of block x, og_launch_fast); the next block's ROI is loaded into registers during
-    // stage 2 and stored once stage 2 is done with roiq, so only the first block of a workgroup waits for its ROI
-    int j = 0, p = 0;
-    OgFB b;
-#ifndef OG_FASTQ_ARGS1
-#define OG_FASTQ_ARGS1 1  // 1: every kernel argument the block decode reads is fetched before the first of them is used,
-                          // one scalar-cache round trip (0: the compiler's order, three round trips before the block record)
-#endif
-    if (OG_FASTQ_ARGS1)
-        __asm__ volatile("" ::"s"(blocks), "s"(nb), "s"(img0), "s"(pitch0), "s"(fstride0), "s"(pyr), "s"(pyr_per_frame));
-    for (;; j++) {  // uniform: the first valid block of the chain (the table pads each level to 8 entries)
-        if (j >= KB) return;
-        p = (int)blockIdx.x + j * (int)gridDim.x;
-        if (p >= nb) return;
-        b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
-        if (b.l >= 0) break;
-    }
+    const int p = (int)blockIdx.x;
+    // every kernel argument the block decode reads is fetched before the first of them is used: one scalar-cache round
+    // trip (the compiler's order took three before the block record)
+    __asm__ volatile("" ::"s"(blocks), "s"(nb), "s"(img0), "s"(pitch0), "s"(fstride0), "s"(pyr), "s"(pyr_per_frame));
+    if (p >= nb) return;
+    const OgFB b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
+    if (b.l < 0) return;  // padding entry of the level (the table pads each level to 8 entries)
     FAST_PROF(0);
     uint32_t sroi[2][4];
     og_fastq_roi_load(b, tid, sroi);
     {
-        // zero only the score-map rows the block reads (dh + 3: gap rows included), while the ROI loads are in flight;
-        // later blocks of the workgroup find it zero again (the emission clears every cell stage 2 wrote)
-        const int msz = KB == 1 ? min(FB_MSZ, ((b.dh + 3) * FB_MSW + 15) & ~15) : FB_MSZ;
+        // zero only the score-map rows the block reads (dh + 3: gap rows included), while the ROI loads are in flight
+        const int msz = min(FB_MSZ, ((b.dh + 3) * FB_MSW + 15) & ~15);
         for (int idx = tid * 16; idx < msz; idx += FB_NT * 16) *(uint4*)&Ms[idx] = make_uint4(0u, 0u, 0u, 0u);
     }
     if (tid == 0) sh_ns = 0;
     og_fastq_roi_put(b, tid, sroi, roiq);
     __syncthreads();
     FAST_PROF(1);
-#pragma unroll 1
-    for (;;) {
     const int dh = b.dh, wC = b.wC, hC = b.hC;  // (the block's width enters through its column masks, b.colw)
     const uint2* Tq = roiq + b.mis;  // Tq[r * FQ_S + x] = quad (x, x + 16, x + 32, x + 48) of ROI row r
     // ---- stage 1: quick test on every detection pixel, four per lane.  Unit u = (row group g = u >> 1, half
@@ -988,20 +915,6 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                 cm2 &= rows;
                 cm3 &= rows;
             }
-#if defined(OG_PROBE_SALU) && OG_PROBE_SALU > 0  // sensitivity probe (measurement builds only): dead SALU work
-            {
-                unsigned pz = (unsigned)R;
-#pragma unroll
-                for (int z = 0; z < OG_PROBE_SALU; z++) __asm__ volatile("s_add_u32 %0, %0, 1" : "+s"(pz) : : "scc");
-            }
-#endif
-#if defined(OG_PROBE_VALU) && OG_PROBE_VALU > 0  // sensitivity probe (measurement builds only): dead VALU work
-            {
-                unsigned pz = (unsigned)lane;
-#pragma unroll
-                for (int z = 0; z < OG_PROBE_VALU; z++) __asm__ volatile("v_add_u32 %0, %0, 1" : "+v"(pz));
-            }
-#endif
             const uint32_t a0 = r0.x | r0.y, a1 = r1.x | r1.y;
             const u64 m[4] = {og_lanes_lo16_nz(a0) & cm0, og_lanes_gt((int)a0, 0xffff) & cm1, og_lanes_lo16_nz(a1) & cm2,
                               og_lanes_gt((int)a1, 0xffff) & cm3};
@@ -1058,46 +971,14 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const int i = (ent >> 7) & 127, j = ent & 127;
         const uint16_t* pc = &T16[4 * ((i + 3) * FQ_S + ((j & 15) + 3)) + (j >> 4)];
         const bool dark = (ent & 0x4000) != 0, bright = (ent & 0x8000) != 0;
-#ifndef OG_FASTQ_PK
-#define OG_FASTQ_PK 1  // 1: exact score with packed f16 pair ops (og_fast_Mpk); 0: scalar integer form (og_fast_M1)
-#endif
-#if OG_FASTQ_PK
+        // the exact score with packed f16 pair ops (og_fast_Mpk)
         const uint32_t pb = og_lds_addr(pc) - 8u * (3u * FQ_S + 3u);
         int M = og_fast_Mpk<FQ_S>(pb, dark ? (_Float16)1 : (_Float16)-1);
         if (dark && bright) M = max(M, og_fast_Mpk<FQ_S>(pb, (_Float16)-1));
-#else
-        int M = og_fast_M1<4>(pc, 4 * FQ_S, dark ? 0 : 0xff);
-        if (dark && bright) {
-            __asm__ volatile("" ::: "memory");  // keeps the second polarity's reads behind the branch
-            M = max(M, og_fast_M1<4>(pc, 4 * FQ_S, 0xff));
-        }
-#endif
         Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)M;
     }
     __syncthreads();
     FAST_PROF(3);
-    // the next valid block of the chain: its ROI loads are in flight during stages 3-4 and land in roiq (free since
-    // stage 2) at the end of the emission
-    OgFB bn = b;
-    int pn = p;
-    bool has_next = false;
-    if (KB > 1) {
-        for (j++; j < KB; j++) {  // uniform
-            pn = (int)blockIdx.x + j * (int)gridDim.x;
-            if (pn >= nb) break;
-            bn = og_fast_decode(blocks, pn, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
-            if (bn.l >= 0) {
-                has_next = true;
-                break;
-            }
-        }
-        if (has_next) {
-            if (OG_FASTQ_DMA)
-                og_fastq_roi_dma(bn, wvu, lane, (uint32_t*)roiq);
-            else
-                og_fastq_roi_load(bn, tid, sroi);
-        }
-    }
     // ---- stage 3: same-cell 3x3 NMS at both thresholds; each wave walks every 8th 64-entry chunk of the list
     int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
     for (int e0 = wvu * 64; e0 < ns; e0 += FB_NT) {
@@ -1128,7 +1009,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             wk[wv][4 + cc] = c2[cc];
         }
     }
-    og_fastq_sync();
+    __syncthreads();
     FAST_PROF(4);
     // per cell: iniThFAST unless the cell is empty at it (src/ORBextractor.cc:809-816)
     const int qw = (lane >> 2) & (FB_NW - 1), qc = lane & 3;
@@ -1150,62 +1031,16 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const int before = __builtin_amdgcn_readlane(sc, wvu) - kept;
     // ---- stage 4: one reservation per block; each wave writes its kept entries at its offset
     int sb = 0;
-#ifndef OG_FASTQ_LDSOUT
-#define OG_FASTQ_LDSOUT 0  // 1: emission into LDS while the reservation atomic is in flight, then one coalesced copy
-                           // (bit-exact, FAST +1.5 %: profiles/sweeps/r04_ab_fast_lds_emission.txt)
-#endif
-    // (block-uniform) the kept entries fit roiq, free since stage 2 (the DMA prefetch variant keeps it busy)
-    const bool lds_out = OG_FASTQ_LDSOUT && !OG_FASTQ_DMA && total <= FQ_ROWS * FQ_S;
-    if (lds_out) {
-        // the device-scope atomic's round trip (~10 % of a block's time when waited for at once) overlaps the
-        // emission: entries go to LDS at the wave's offset + rank, the base is read after the emission, and the block's
-        // candidates leave in one coalesced copy
-        int bb = 0;
-        if (total != 0 && tid == 0) bb = atomicAdd(&cand_count[f * nlevels + b.l], total);
-        u64* st = (u64*)roiq;
-        int run = 0;
-        for (int e0 = wvu * 64; e0 < ns; e0 += FB_NT) {
-            const int e = e0 + lane;
-            int ent = 0;
-            if (e < ns) ent = lst[e];
-            const int i = (ent >> 7) & 127, j = ent & 127;
-            const int cell = (i >= hC) * 2 + (j >= wC);
-            const unsigned kbit = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
-            const u64 mask = og_lanes_ne(kbit, 0u);
-            if (e < ns) {
-                uint8_t* mcell = &Ms[og_ms_idx(i, j, wC, hC)];
-                if (kbit) st[before + og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, *mcell - 1);
-                if (KB > 1) *mcell = 0;  // the next block of this workgroup starts from a clean score map
-            }
-            run += __popcll(mask);
-        }
-        if (tid == 0) {
-            if (total != 0 && bb + total > b.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
-            sh_base = bb;
-        }
-        __syncthreads();
-        FAST_PROF(5);
-        sb = sh_base;
-        if (total != 0 && sb + total <= b.cand_cap) {
-            u64* o = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb);
-            for (int k = tid; k < total; k += FB_NT) o[k] = st[k];
-        }
-        if (KB > 1) __syncthreads();  // the staged entries are read before the next ROI overwrites roiq
-    } else {
     if (total != 0) {  // block-uniform
         if (tid == 0) {
             const int bb = atomicAdd(&cand_count[f * nlevels + b.l], total);
             if (bb + total > b.cand_cap) atomicOr(status, 1);  // cannot happen: cap is the exact NMS bound
             sh_base = bb;
         }
-        og_fastq_sync();
+        __syncthreads();
         sb = sh_base;
     }
     FAST_PROF(5);
-    if (OG_FASTQ_DMA && has_next) {  // the wave's own staged rows of the next block, landed during stages 3-4
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        og_fastq_raw_get(bn, wvu, lane, (const uint32_t*)roiq, sroi);
-    }
     const bool emit = total != 0 && sb + total <= b.cand_cap && kept != 0;
     u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb + before);
     int run = 0;
@@ -1220,289 +1055,14 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         if (e < ns) {
             uint8_t* mcell = &Ms[og_ms_idx(i, j, wC, hC)];
             if (emit && kbit) out[og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, *mcell - 1);
-            if (KB > 1) *mcell = 0;  // the next block of this workgroup starts from a clean score map
         }
         run += __popcll(mask);
-    }
     }
 #if OG_FAST_PROFILE
     __builtin_amdgcn_s_waitcnt(0);  // the candidate stores issued
     FAST_PROF(6);
     if (tid == 0 && f == gridDim.y / 2 && p < 4096) og_fast_prof[p * 8 + 7] = (unsigned long long)ns | ((unsigned long long)b.l << 32);
 #endif
-    if (!has_next) break;
-    if (tid == 0) sh_ns = 0;
-    if (OG_FASTQ_DMA) og_fastq_sync();  // every wave has read its staged rows before the quads overwrite them
-    og_fastq_roi_put(bn, tid, sroi, roiq);
-    b = bn;
-    p = pn;
-    __syncthreads();  // score map back to zero, list consumed, next ROI stored
-    FAST_PROF(1);
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// k2c: FAST with one wave per cell, for the levels whose cells are at most FC_MAXC x FC_MAXC detection pixels (every
-// level of a 1080p or KITTI-width frame but the coarsest few).  The cell is the reference's unit of work: one cv::FAST
-// call with its own NMS, and the 20 -> 7 fallback decided by the cell alone (src/ORBextractor.cc:789-829), so a wave
-// runs the whole chain without a workgroup barrier or an LDS atomic: ROI -> LDS, quick test into a wave-private
-// survivor list (the running offset is a scalar), exact scores into a wave-private score map, NMS, and one global
-// reservation per cell.  A workgroup is the 4 waves of one table block (2 x 2 cells, og_fast_quad_kernel's table,
-// its XCD runs included); the waves share nothing, and a wave whose cell does not exist exits at once.
-// ROI layout: qword (r, x) holds ROI row r, columns x - mis + 8k (k = 0..3) as f16-biased u16 (0x6400 | pixel), with
-// mis the ROI origin's misalignment (aligned dword loads); lane (s, x) of a stage-1 iteration takes detection columns
-// x + 8k of one row, 8 lanes a row.  The 32-lane groups hold rows r, r + 4, r + 8, r + 12: 4 * FC_S = 72 = 8 (mod 32)
-// qwords, so their 16-dword row segments cover the 64 banks once (conflict-free ds_read_b64).
-// ------------------------------------------------------------------------------------------------
-#define FC_S 18                                 // qword stride of a ROI row (>= 14 + 3 misalignment)
-#define FC_MAXC 32                              // cell detection width / height capacity
-#define FC_ROWS (FC_MAXC + 6)
-#define FC_MSW 36                               // score-map row stride (bytes): a zero border around cw x ch
-#define FC_MSZ (((FC_MSW * (FC_MAXC + 2)) + 15) & ~15)
-#define FC_NW 4                                 // waves (cells) per workgroup
-#define FC_LST (FC_MAXC * FC_MAXC)              // survivor list capacity: every detection pixel
-
-// this wave's LDS stores and loads are ordered for all of its lanes (the waves of a workgroup share no LDS)
-__device__ __forceinline__ void og_wave_lds_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__global__ __launch_bounds__(64 * FC_NW) void og_fast_cell_kernel(
-    const OgFastBlk* __restrict__ blocks, int nb, const uint8_t* __restrict__ img0, long long pitch0, long long fstride0,
-    const uint8_t* __restrict__ pyr, long long pyr_per_frame, u64* __restrict__ cand, long long cand_per_frame,
-    int* __restrict__ cand_count, int nlevels, int thr, int* __restrict__ status)
-{
-    __shared__ __attribute__((aligned(16))) uint2 roiw[FC_NW][FC_ROWS * FC_S];
-    __shared__ __attribute__((aligned(16))) uint8_t msw[FC_NW][FC_MSZ];
-    __shared__ __attribute__((aligned(16))) uint16_t lstw[FC_NW][FC_LST];
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const unsigned f = blockIdx.y;
-    const int p = blockIdx.x;
-    if (p >= nb) return;
-    __asm__ volatile("" ::"s"(blocks), "s"(nb), "s"(img0), "s"(pitch0), "s"(fstride0), "s"(pyr), "s"(pyr_per_frame));
-    const OgFB b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
-    if (b.l < 0) return;
-    // this wave's cell of the block
-    const int ci = wv >> 1, cj = wv & 1;
-    const int cw = min(b.wC, b.dw - cj * b.wC), ch = min(b.hC, b.dh - ci * b.hC);
-    if (cw <= 0 || ch <= 0) return;
-    const uint8_t* row0 = b.row0 + (unsigned)(ci * b.hC) * b.upitch + (unsigned)(cj * b.wC);
-    const int mis = b.aligned ? (int)((uintptr_t)row0 & 3) : 0;
-    const int rh = ch + 6;
-    uint2* roi = roiw[wv];
-    uint8_t* ms = msw[wv];
-    const uint32_t a_roi = og_lds_addr(roi), a_lst = og_lds_addr(&lstw[wv][0]);
-    // ---- ROI -> LDS.  Item (r, g) = qwords 4g .. 4g + 3 of ROI row r: the dwords at bytes 4g + 8k (k = 0..3) of the
-    // row from its aligned start, 8 v_perm into four quads, two 16-byte stores (one for g = 4, the last 2 qwords of
-    // the FC_S-qword row).  All loads are issued before the first use; rows of a 64-item round come from one
-    // multiply-high division by ng (exact below 200 items).
-    {
-        const int ng = (14 + mis + 3) >> 2;                 // 4 or 5 groups of 4 qwords
-        const int nitem = rh * ng;                         // <= 38 * 5 = 190 <= 3 * 64
-        const unsigned mg = ng == 4 ? 16384u : 13108u;     // ceil(2^16 / ng)
-        const uint8_t* abase = row0 - mis;
-        uint32_t s[3][4];
-        int rr[3], gg[3];
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            const int it = min(64 * k + lane, nitem - 1);   // lanes past the items re-read the last one
-            rr[k] = (int)(((unsigned)it * mg) >> 16);
-            gg[k] = it - rr[k] * ng;
-        }
-        if (b.aligned) {
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                unsigned off = __umul24((unsigned)rr[k], b.upitch) + 4u * (unsigned)gg[k];
-                __asm__("" : "+v"(off));
-#pragma unroll
-                for (int q = 0; q < 4; q++) s[k][q] = *(const uint32_t*)(abase + off + 8u * q);
-            }
-        } else {
-            // odd pitch (mis = 0): two aligned loads funnel-shifted by the row's own offset
-            const unsigned mb = (unsigned)((uintptr_t)abase & 3);
-            const uint8_t* ab = abase - mb;
-            uint32_t lo[3][4], hi[3][4];
-            unsigned sh[3];
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                unsigned o = __umul24((unsigned)rr[k], b.upitch) + 4u * (unsigned)gg[k] + mb;
-                sh[k] = o & 3u;
-                o &= ~3u;
-                __asm__("" : "+v"(o));
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    lo[k][q] = *(const uint32_t*)(ab + o + 8u * q);
-                    hi[k][q] = *(const uint32_t*)(ab + o + 8u * q + 4u);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < 3; k++)
-#pragma unroll
-                for (int q = 0; q < 4; q++) s[k][q] = __builtin_amdgcn_alignbyte(hi[k][q], lo[k][q], sh[k]);
-        }
-        // zero the score map (its border and every non-survivor read 0) while the loads are in flight
-        for (int idx = lane; idx < FC_MSZ / 16; idx += 64) *(uint4*)&ms[16 * idx] = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            if (64 * k + lane < nitem) {
-                uint32_t w[8];
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    // quad t of the group: byte t of dwords 0..3 (pixels 4g + t + 8q) as four f16-biased u16
-                    const uint32_t sel = 0x0c000c00u | ((4u + t) << 16) | t;
-                    w[2 * t] = __builtin_amdgcn_perm(s[k][1], s[k][0], sel) | 0x64006400u;
-                    w[2 * t + 1] = __builtin_amdgcn_perm(s[k][3], s[k][2], sel) | 0x64006400u;
-                }
-                uint4* d = (uint4*)&roi[rr[k] * FC_S + 4 * gg[k]];
-                d[0] = make_uint4(w[0], w[1], w[2], w[3]);
-                if (gg[k] < 4) d[1] = make_uint4(w[4], w[5], w[6], w[7]);
-            }
-        }
-    }
-    og_wave_lds_sync();
-    const int t1 = thr & 255, t2 = (thr >> 8) & 255;
-    const int tq = min(t1, t2);
-    const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
-    // ---- stage 1: quick test, 4 pixels per lane (columns x + 8k of one row), survivors appended to the wave's list
-    int n = 0;  // survivors so far (uniform)
-    {
-        const int x = lane & 7, sl = lane >> 3;
-        const int srow = (sl >> 2) + 4 * (sl & 3);  // 0, 4, 8, 12 (lanes 0-31) / 1, 5, 9, 13 (lanes 32-63)
-        const uint32_t a_lane = a_roi + 8u * (uint32_t)(srow * FC_S + x + mis);  // top-left sample of the circle
-        auto cmask = [&](int k) -> u64 {
-            const int c = min(max(cw - 8 * k, 0), 8);
-            return (u64)((1u << c) - 1u) * 0x0101010101010101ull;
-        };
-        const u64 col0 = cmask(0), col1 = cmask(1), col2 = cmask(2), col3 = cmask(3);
-        const int nit = ch <= 16 ? 2 : 4;
-#pragma unroll 1
-        for (int it = 0; it < nit; it++) {
-            const int R = 16 * (it >> 1) + 2 * (it & 1);
-            u64 w[17];
-            {
-                // from the top-left sample (dy, dx) = (-3, -3): every offset is a positive immediate
-                typedef const volatile __attribute__((address_space(3))) unsigned long long lds_u64;
-                lds_u64* q64 = (lds_u64*)(uintptr_t)(a_lane + 8u * (uint32_t)(R * FC_S));
-                constexpr int st = FC_S, c0f = 3 * FC_S + 3;
-                const int off[17] = {c0f + 3 * st,     c0f + 1 + 3 * st,  c0f + 2 + 2 * st,  c0f + 3 + 1 * st,
-                                     c0f + 3,          c0f + 3 - 1 * st,  c0f + 2 - 2 * st,  c0f + 1 - 3 * st,
-                                     c0f - 3 * st,     c0f - 1 - 3 * st,  c0f - 2 - 2 * st,  c0f - 3 - 1 * st,
-                                     c0f - 3,          c0f - 3 + 1 * st,  c0f - 2 + 2 * st,  c0f - 1 + 3 * st, c0f};
-                w[16] = q64[off[16]];
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    w[k] = q64[off[k]];
-                    w[k + 8] = q64[off[k + 8]];
-                }
-            }
-            uint32_t c0[16], c1[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                c0[k] = (uint32_t)w[k];
-                c1[k] = (uint32_t)(w[k] >> 32);
-            }
-            const uint2 r0 = og_fast_quick2v(c0, (uint32_t)w[16], tt);          // columns x, x + 8
-            const uint2 r1 = og_fast_quick2v(c1, (uint32_t)(w[16] >> 32), tt);  // columns x + 16, x + 24
-            const u64 rows = R + 13 < ch ? ~0ull : og_lanes_lt(R + srow, ch);
-            const uint32_t a0 = r0.x | r0.y, a1 = r1.x | r1.y;
-            const u64 m[4] = {og_lanes_lo16_nz(a0) & col0 & rows, og_lanes_gt((int)a0, 0xffff) & col1 & rows,
-                              og_lanes_lo16_nz(a1) & col2 & rows, og_lanes_gt((int)a1, 0xffff) & col3 & rows};
-            const int cnt0 = __popcll(m[0]), cnt1 = __popcll(m[1]), cnt2 = __popcll(m[2]), cnt3 = __popcll(m[3]);
-            const int nn = cnt0 + cnt1 + cnt2 + cnt3;
-            if (nn) {
-                const uint32_t base = (uint32_t)(((R + srow) << 7) | x);
-                uint32_t v[4];
-                {
-                    uint32_t d1, b1;
-                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r0.x), "s"(0x00010001u));
-                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r0.y), "s"(0x00020002u));
-                    const uint32_t pb = d1 | b1;
-                    v[0] = (pb << 14) | base;
-                    v[1] = (pb >> 2) | (base + 8u);
-                }
-                {
-                    uint32_t d1, b1;
-                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r1.x), "s"(0x00010001u));
-                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r1.y), "s"(0x00020002u));
-                    const uint32_t pb = d1 | b1;
-                    v[2] = (pb << 14) | (base + 16u);
-                    v[3] = (pb >> 2) | (base + 24u);
-                }
-                const uint32_t ab0 = a_lst + 2u * (uint32_t)n, ab1 = ab0 + 2u * (uint32_t)cnt0,
-                               ab2 = ab1 + 2u * (uint32_t)cnt1, ab3 = ab2 + 2u * (uint32_t)cnt2;
-                og_ds_write_b16_x4(m[0], ab0 + 2u * (uint32_t)og_rank(m[0]), v[0], m[1], ab1 + 2u * (uint32_t)og_rank(m[1]),
-                                   v[1], m[2], ab2 + 2u * (uint32_t)og_rank(m[2]), v[2], m[3],
-                                   ab3 + 2u * (uint32_t)og_rank(m[3]), v[3]);
-                n += nn;
-            }
-        }
-    }
-    og_wave_lds_sync();
-    // ---- stage 2: exact score of every survivor into the score map (u16 reads of the quad layout)
-    const uint16_t* lst = &lstw[wv][0];
-    for (int e = lane; e < n; e += 64) {
-        const int ent = lst[e];
-        const int i = (ent >> 7) & 127, j = ent & 127;
-        const bool dark = (ent & 0x4000) != 0, bright = (ent & 0x8000) != 0;
-        const uint32_t pb = a_roi + 8u * (uint32_t)(i * FC_S + (j & 7) + mis) + 2u * (uint32_t)(j >> 3);
-        int M = og_fast_Mpk<FC_S>(pb, dark ? (_Float16)1 : (_Float16)-1);
-        if (dark && bright) M = max(M, og_fast_Mpk<FC_S>(pb, (_Float16)-1));
-        ms[(i + 1) * FC_MSW + j + 1] = (uint8_t)M;
-    }
-    og_wave_lds_sync();
-    // ---- stage 3: 3x3 NMS at both thresholds; kept flags into bits 14 / 15 of the list entries
-    const int tA = max(t1, 1), tB = max(t2, 1);
-    int k1 = 0, k2 = 0;
-    uint16_t* lstm = &lstw[wv][0];
-    for (int e0 = 0; e0 < n; e0 += 64) {
-        const int e = e0 + lane;
-        int ent = 0, mc = 0, nbm = 0;
-        if (e < n) {
-            ent = lstm[e] & 0x3fff;
-            const uint8_t* q = &ms[((ent >> 7) & 127) * FC_MSW + (ent & 127)];  // top-left neighbour
-            mc = q[FC_MSW + 1];
-            nbm = max(max(max(q[0], q[1]), max(q[2], q[FC_MSW])),
-                      max(max(q[FC_MSW + 2], q[2 * FC_MSW]), max(q[2 * FC_MSW + 1], q[2 * FC_MSW + 2])));
-        }
-        const u64 top = og_lanes_gt(mc, nbm);
-        const u64 K1 = og_lanes_gt(mc, tA) & top, K2 = og_lanes_gt(mc, tB) & top;
-        if (e < n) lstm[e] = (uint16_t)(ent | (mc > tA && mc > nbm ? 0x4000 : 0) | (mc > tB && mc > nbm ? 0x8000 : 0));
-        k1 += __popcll(K1);
-        k2 += __popcll(K2);
-    }
-    // ---- stage 4: the cell's threshold (iniThFAST unless it keeps nothing, src/ORBextractor.cc:809-816), one
-    // reservation, the kept entries in list order
-    const bool useT2 = k1 == 0;
-    const int total = useT2 ? k2 : k1;
-    if (total == 0) return;
-    int old = 0;
-    if (lane == 0) old = atomicAdd(&cand_count[f * nlevels + b.l], total);
-    og_wave_lds_sync();
-    const int sb = __builtin_amdgcn_readfirstlane(old);
-    if (sb + total > b.cand_cap) {  // cannot happen: the capacity is the exact NMS bound
-        if (lane == 0) atomicOr(status, 1);
-        return;
-    }
-    u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb);
-    const unsigned kmask = useT2 ? 0x8000u : 0x4000u;
-    const int ox = b.ox + cj * b.wC, oy = b.oy + ci * b.hC;
-    int run = 0;
-    for (int e0 = 0; e0 < n; e0 += 64) {
-        const int e = e0 + lane;
-        const int ent = e < n ? lst[e] : 0;
-        const unsigned kb = (unsigned)ent & kmask;
-        const u64 mask = og_lanes_ne(kb, 0u);
-        if (kb) {
-            const int i = (ent >> 7) & 127, j = ent & 127;
-            out[og_rank(mask, run)] = og_pack_cand(ox + j, oy + i, ms[(i + 1) * FC_MSW + j + 1] - 1);
-        }
-        run += __popcll(mask);
-    }
 }
 
 hipError_t og_read_fast_prof(unsigned long long* out, int n)
@@ -1774,13 +1334,13 @@ __device__ __forceinline__ void og_wave_count(int* ctr, int addr, bool act)
 #endif
 
 #ifndef OG_OCT_PROFILE
-#define OG_OCT_PROFILE 0
+#define OG_OCT_PROFILE 0  // l + 1: diagnostic clocks of level l (variant "octprof0", tests/test_gpu_variants.py)
 #endif
-#if OG_OCT_PROFILE  // experiment builds only (tools/fast_variants.py): per-round clocks of (frame 0, level 0)
+#if OG_OCT_PROFILE  // diagnostic builds only (tools/octree_profile.py): per-round clocks of (frame 0, level OG_OCT_PROFILE - 1)
 __device__ unsigned long long og_oct_prof[256];
-#define OCT_PROF(slot, v)                                                              \
-    do {                                                                               \
-        if (tid == 0 && f == 0 && l == 0 && (slot) < 256) og_oct_prof[(slot)] = (v); \
+#define OCT_PROF(slot, v)                                                                                    \
+    do {                                                                                                     \
+        if (tid == 0 && f == 0 && l == OG_OCT_PROFILE - 1 && (slot) < 256) og_oct_prof[(slot)] = (v);      \
     } while (0)
 #else
 #define OCT_PROF(slot, v) \
@@ -1871,7 +1431,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     // and level); the final phase then takes each listed node's best from its cells through the position table -- no
     // second pass over the keys.  Used when the keys outweigh the table (workgroup-uniform).
 #ifndef OG_OCT_BESTTAB
-#define OG_OCT_BESTTAB 1
+#define OG_OCT_BESTTAB 1  // 0: the final key pass instead of the cell-best table (variant "octbt0", tests/test_gpu_variants.py)
 #endif
     const int bD0 = tbase(D), cellsD = Ttot - bD0;
     const bool btab = OG_OCT_BESTTAB && tmode && k32 && C >= cellsD;
@@ -3460,11 +3020,6 @@ void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, l
                            pitchA, dstB, pitchB, dst_fstride, g, status);
 }
 
-#ifndef OG_FAST_CELLS
-#define OG_FAST_CELLS 1  // 1: levels with cells <= FC_MAXC x FC_MAXC run og_fast_cell_kernel (one wave per cell)
-#endif
-bool og_fast_cell_level(const OgLevel& L) { return OG_FAST_CELLS && L.wCell <= FC_MAXC && L.hCell <= FC_MAXC; }
-
 void og_launch_fast(hipStream_t s, const OgPlan& P, int lb, int le, const OgFastBlk* table, const uint8_t* img0,
                     long long pitch0, long long fstride0, const uint8_t* pyr, u64* cand, int* cand_count, int* status,
                     int B)
@@ -3472,32 +3027,12 @@ void og_launch_fast(hipStream_t s, const OgPlan& P, int lb, int le, const OgFast
     le = std::min(le, P.nlevels);
     if (lb >= le || B <= 0) return;
     const int thr = std::min(std::max(P.iniTh, 0), 255) | (std::min(std::max(P.minTh, 0), 255) << 8);
-#ifndef OG_FASTQ_KB
-#define OG_FASTQ_KB 1
-#endif
-    // runs of consecutive levels of one kernel; each level's table range starts at a multiple of 8, so workgroup w of
-    // every frame keeps XCD w % 8 (the table's XCD runs)
-    for (int l = lb; l < le;) {
-        const bool cm = og_fast_cell_level(P.lv[l]);
-        int l1 = l + 1;
-        while (l1 < le && og_fast_cell_level(P.lv[l1]) == cm) l1++;
-        const int p0 = P.lv[l].fb_off, p1 = l1 < P.nlevels ? P.lv[l1].fb_off : P.fast_blocks;
-        const int nblocks = p1 - p0;
-        const OgFastBlk* blocks = table + p0;
-        l = l1;
-        if (nblocks <= 0) continue;
-        if (cm) {
-            hipLaunchKernelGGL(og_fast_cell_kernel, dim3(nblocks, B), dim3(64 * FC_NW), 0, s, blocks, nblocks, img0,
-                               pitch0, fstride0, pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels,
-                               thr, status);
-            continue;
-        }
-        // KB blocks per workgroup (og_fast_quad_kernel): G workgroups per frame, a multiple of 8
-        const int G = OG_FASTQ_KB == 1 ? nblocks : ((nblocks + OG_FASTQ_KB - 1) / OG_FASTQ_KB + 7) & ~7;
-        hipLaunchKernelGGL(og_fast_quad_kernel<OG_FASTQ_KB>, dim3(G, B), dim3(FB_NT), 0, s, blocks, nblocks, img0,
-                           pitch0, fstride0, pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels, thr,
-                           status);
-    }
+    // the levels' table range (level-major; each level starts at a multiple of 8, so workgroup w of every frame keeps
+    // XCD w % 8: the table's XCD runs)
+    const int p0 = P.lv[lb].fb_off, p1 = le < P.nlevels ? P.lv[le].fb_off : P.fast_blocks;
+    if (p1 <= p0) return;
+    hipLaunchKernelGGL(og_fast_quad_kernel, dim3(p1 - p0, B), dim3(FB_NT), 0, s, table + p0, p1 - p0, img0, pitch0,
+                       fstride0, pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels, thr, status);
 }
 
 void og_launch_harris(hipStream_t s, const OgPlan& P, int lb, int le, const uint8_t* img0, long long pitch0,

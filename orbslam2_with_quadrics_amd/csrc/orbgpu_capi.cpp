@@ -623,9 +623,7 @@ static void launch_levels(orbgpu_ctx* c, hipStream_t s, int lb, int le, const ui
 // 1080p frame's device time) on the context stream while a second stream builds the pyramid and runs levels >= 1.
 // The fork and join cost more than they hide below ~1 MP (tools/latency.py: 1242x375 0.177 -> 0.211 ms forked,
 // 1920x1080 0.294 -> 0.238 ms), so only frames of at least ORBGPU_FORK_MIN_PIXELS (default 2^20) fork.
-#ifndef OG_FORK_MAX_B
 #define OG_FORK_MAX_B 4
-#endif
 static long long fork_min_pixels()
 {
     static const long long v = [] {

@@ -33,9 +33,7 @@ struct OgRz2Geom {
 };
 // og_resize2_kernel tiles: RZ2_TH rows x 256 columns of the coarser level per workgroup of 16 * RZ2_TH threads
 // (4 output rows x 4 columns per thread in its last pass)
-#ifndef RZ2_TH
-#define RZ2_TH 16
-#endif
+#define RZ2_TH 16  // (32-row tiles measured +7 % pyramid time)
 #define RZ2_NT (16 * RZ2_TH)
 // dynamic LDS of og_resize2_kernel: y-table rows of the tile (AR + RZ2_TH int4), S, A, row misalignments
 static inline size_t og_rz2_lds_bytes(int SR, int SC, int AR, int AC)
@@ -51,9 +49,7 @@ void og_launch_resize(hipStream_t s, const uint8_t* src, long long src_pitch, lo
 hipError_t og_prepare_device();  // per-device kernel attributes (call after hipSetDevice)
 hipError_t og_prepare_device_match();  // (called by og_prepare_device)
 hipError_t og_prepare_device_bow();
-// FAST of levels [lb, le) for each of B frames (table = the whole block table; og_fast_cell_kernel for the levels
-// og_fast_cell_level accepts, og_fast_quad_kernel for the others)
-bool og_fast_cell_level(const OgLevel& L);
+// FAST of levels [lb, le) for each of B frames (table = the whole block table)
 void og_launch_fast(hipStream_t s, const OgPlan& P, int lb, int le, const OgFastBlk* table, const uint8_t* img0,
                     long long pitch0, long long fstride0, const uint8_t* pyr, unsigned long long* cand, int* cand_count,
                     int* status, int B);

@@ -1,7 +1,9 @@
 """Per-round timeline of the level-0 octree workgroup (test infrastructure).
 
-python tools/octree_profile.py --build     # here: variant library with OG_OCT_PROFILE=1
-python tools/octree_profile.py --run [--batch B]  # GPU box: one B-frame (default 64) 1080p batch, per-round cycles
+python tools/octree_profile.py --build [--levels 0,1,..]   # here: variant libraries with OG_OCT_PROFILE=level+1
+python tools/octree_profile.py --run [--batch B] [--shape kitti] [--levels 0,1,..]
+    # GPU box: one B-frame (default 64) batch of 1080p (or KITTI 1241x376) frames; per-round cycles of the octree
+    # workgroup of (frame 0, level l) for each level (one library per level)
 """
 import os
 import sys
@@ -10,23 +12,37 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VLIB = os.path.join(ROOT, "orbslam2_with_quadrics_amd", "variants", "liborbgpu_octprof.so")
+LEVELS = [int(v) for v in sys.argv[sys.argv.index("--levels") + 1].split(",")] if "--levels" in sys.argv else [0]
+
+
+def vlib(level):
+    return os.path.join(ROOT, "orbslam2_with_quadrics_amd", "variants", f"liborbgpu_octprof{level}.so")
 
 
 def build():
     from orbslam2_with_quadrics_amd import build_ext
 
-    os.makedirs(os.path.dirname(VLIB), exist_ok=True)
-    print(build_ext.build(force=True, defines=["OG_OCT_PROFILE=1"], out=VLIB))
+    for lv in LEVELS:
+        os.makedirs(os.path.dirname(vlib(lv)), exist_ok=True)
+        print(build_ext.build(force=True, defines=[f"OG_OCT_PROFILE={lv + 1}"], out=vlib(lv)))
 
 
 def run():
-    os.environ["ORBGPU_LIB"] = VLIB
+    if len(LEVELS) > 1:  # one process per library (the library is loaded once per process)
+        import subprocess
+        for lv in LEVELS:
+            argv = [a for a in sys.argv[1:]]
+            i = argv.index("--levels")
+            argv[i + 1] = str(lv)
+            subprocess.run([sys.executable, os.path.abspath(__file__), *argv], check=True)
+        return
+    os.environ["ORBGPU_LIB"] = vlib(LEVELS[0])
     import torch  # noqa: F401
 
     from orbslam2_with_quadrics_amd import ORBextractor, _lib, synthetic
 
-    rows, cols = 1080, 1920
+    rows, cols = (376, 1241) if "kitti" in sys.argv else (1080, 1920)
+    print(f"level {LEVELS[0]} of {cols}x{rows}")
     B = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else 64
     frames = np.stack([synthetic.frame(i % 8, rows, cols) for i in range(B)])
     ex = ORBextractor(2000, 1.2, 8, 20, 7)
