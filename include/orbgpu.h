@@ -143,7 +143,9 @@ int orbgpu_batch_download(orbgpu_ctx* ctx, int b, orbgpu_keypoint* kps, uint8_t*
  * the header is checked on the device, in stream order.  A record that does not match the context's plan, or
  * whose count exceeds frame_cap, leaves frame 0 with count 0, and the next call that checks the context's status
  * (orbgpu_synchronize, orbgpu_batch_download, or any other call that returns results to the host) returns
- * ORBGPU_ERR_ARG.  Without a planned context, unpack itself returns ORBGPU_ERR_ARG. */
+ * ORBGPU_ERR_ARG.  A batched SearchForInitialization on another context that matches against such a frame raises the
+ * same condition in its own context (its next status check returns ORBGPU_ERR_ARG), so a refused record never passes
+ * as "zero matches".  Without a planned context, unpack itself returns ORBGPU_ERR_ARG. */
 long long orbgpu_frame_record_bytes(const orbgpu_ctx* ctx);
 int orbgpu_frame_record_pack(orbgpu_ctx* ctx, int b, void* d_dst);
 int orbgpu_frame_record_unpack(orbgpu_ctx* ctx, const void* d_src);

@@ -212,10 +212,14 @@ __device__ __forceinline__ uint32_t og_wave_min_u32(uint32_t v)
 __global__ __launch_bounds__(INIT_NT) void og_init_resolve_kernel(
     OgFrameDev F1, int ref, OgFrameDev F2, float nnratio, int checkOri, float* __restrict__ prev_xy,
     int prev_stride, const uint32_t* __restrict__ lists, int list_cap, const int* __restrict__ list_n,
-    int* __restrict__ matches12, int match_stride, int* __restrict__ nmatches, int* __restrict__ status, int ecap)
+    int* __restrict__ matches12, int match_stride, int* __restrict__ nmatches, int* __restrict__ status, int ecap,
+    const int* __restrict__ ref_status)
 {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // F1 from another context: a frame record that context refused (status bit 128, og_record_unpack_kernel: F1 was
+    // left empty) is reported by this context's next status check too, not only as zero matches
+    if (ref_status && b == 0 && tid == 0 && (*ref_status & 128)) atomicOr(status, 128);
     const int n1 = F1.counts[ref];
     const int n2 = F2.counts[b];
     const int c1 = F1.frame_cap, c2 = F2.frame_cap;
@@ -462,7 +466,7 @@ int og_init_keep_bound(float nnratio)
 void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G, float nnratio,
                            int checkOri, int windowSize, float* prev_xy, int prev_stride, int* matches12,
                            int match_stride, int* nmatches, uint32_t* lists, int list_cap, int* list_n, int* status,
-                           int B)
+                           int B, const int* ref_status)
 {
     hipLaunchKernelGGL(og_init_cand_kernel, dim3((F1.frame_cap + 3) / 4, B), dim3(256), 0, s, F1, ref, F2, G,
                        windowSize, og_init_keep_bound(nnratio), prev_xy, prev_stride, lists, list_cap, list_n);
@@ -473,7 +477,7 @@ void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2,
     const size_t shm = og_init_resolve_lds(F1.frame_cap, F2.frame_cap, ecap);
     hipLaunchKernelGGL(og_init_resolve_kernel, dim3(B), dim3(INIT_NT), shm, s, F1, ref, F2, nnratio, checkOri,
                        prev_xy, prev_stride, lists, list_cap, list_n, matches12, match_stride, nmatches, status,
-                       ecap);
+                       ecap, ref_status);
 }
 
 // Tracking::MonocularInitialization (src/Tracking.cc:573-575): vbPrevMatched[i] = F1.mvKeysUn[i].pt,

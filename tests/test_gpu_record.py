@@ -56,3 +56,41 @@ def test_record_round_trip_and_plan_checks(gpu):
     b.synchronize()
     kb, db = b.batch_download(0)
     assert kb.tobytes() == ka.tobytes() and np.array_equal(db, da)
+
+
+def test_refused_record_is_reported_by_the_cross_context_matcher(gpu):
+    """a refused record leaves the receiving context's frame 0 empty; a batched SearchForInitialization on
+    another context that matches against it must not pass that off as "zero matches" -- its own next status check
+    returns ORBGPU_ERR_ARG too (the refusal bit is folded into the matching context's status)."""
+    import torch
+
+    from orbslam2_with_quadrics_amd import _lib, synthetic
+
+    L = _lib.lib()
+    f1, f2 = synthetic.frame_pair(32, 480, 640)
+    ref = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    cur = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    ref(f1)
+    cur(f2)
+    cap = int(L.orbgpu_max_keypoints(ref.ctx))
+    prev = torch.zeros(2 * cap, dtype=torch.float32, device="cuda:0")
+    m12 = torch.zeros(cap, dtype=torch.int32, device="cuda:0")
+    nm = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    g = _lib.GridGeom()
+    _lib.check(cur.ctx, L.orbgpu_grid_geom_for_image(640, 480, C.byref(g)), "grid")
+
+    def match():
+        _lib.check(cur.ctx, L.orbgpu_prev_matched_from_frame(ref.ctx, 0, cur.ctx, C.c_void_p(prev.data_ptr())), "prev")
+        _lib.check(cur.ctx, L.orbgpu_search_for_initialization_batch(
+            ref.ctx, 0, cur.ctx, g, 0.9, 1, 100, C.c_void_p(prev.data_ptr()), C.c_void_p(m12.data_ptr()),
+            C.c_void_p(nm.data_ptr())), "init")
+
+    match()
+    assert L.orbgpu_synchronize(cur.ctx) == _lib.OK and int(nm.item()) > 50
+    zero = torch.zeros(int(L.orbgpu_frame_record_bytes(ref.ctx)), dtype=torch.uint8, device="cuda:0")
+    assert L.orbgpu_frame_record_unpack(ref.ctx, C.c_void_p(zero.data_ptr())) == _lib.OK  # refused on the device
+    match()
+    assert L.orbgpu_synchronize(cur.ctx) == _lib.ERR_ARG
+    assert b"frame record" in L.orbgpu_last_error(cur.ctx)
+    assert int(nm.item()) == 0
+    assert L.orbgpu_synchronize(ref.ctx) == _lib.ERR_ARG  # the receiving context reports it as well
