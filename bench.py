@@ -597,9 +597,23 @@ def setup_stereo(args, env):
     d_out = [e.device_alloc(Bs * cap * 8 + Bs * 4) for e in exL]
     mbf, mb = 386.1448, 386.1448 / 718.856  # Examples/Stereo/KITTI00-02.yaml
 
+    # --serial-pairs (profiling): each right context's stream waits for its left context's extraction, so the L and
+    # R launches of a pair do not overlap and rocprof's per-kernel durations are one context's own
+    serial = None
+    if args.serial_pairs:
+        import torch
+
+        serial = [(torch.cuda.ExternalStream(exL[s_].stream(), device=f"cuda:{dev}"),
+                   torch.cuda.ExternalStream(exR[s_].stream(), device=f"cuda:{dev}"),
+                   torch.cuda.Event()) for s_ in range(S)]
+
     def step():
         for s_ in range(S):
             exL[s_].extract_batch_device(dL + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
+            if serial is not None:
+                sl, sr, ev = serial[s_]
+                ev.record(sl)
+                sr.wait_event(ev)
             exR[s_].extract_batch_device(dR + s_ * Bs * fbytes, Bs, cols, rows, cols, fbytes)
         for s_ in range(S):
             o = d_out[s_]
@@ -982,6 +996,9 @@ def main():
     ap.add_argument("--semantics", type=lambda v: int(v, 0), default=0,
                     help="ORBGPU_SEM_* flags (include/orbgpu.h): which OpenCV/compiler behaviours to reproduce")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--serial-pairs", action="store_true",
+                    help="stereo (profiling): the right extraction of a pair waits for the left one, so per-kernel "
+                         "durations are not inflated by the overlapping L/R launches")
     ap.add_argument("--instrumented-steps", type=int, default=50,
                     help="steps of the separate stage-timed pass (per-stage times and the roofline's launch time)")
     ap.add_argument("--pmc-json", default=None,
@@ -1152,6 +1169,7 @@ def main():
             "frames_per_step_per_gpu": B,
             "streams_per_gpu": S,
             "frames_per_launch": Bs,
+            **({"serial_pairs": True} if args.serial_pairs else {}),
             "resolution": f"{args.cols}x{args.rows}",
             "nfeatures": args.nfeatures,
             "semantics": _lib.semantics_name(args.semantics),
