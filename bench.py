@@ -1138,13 +1138,18 @@ def main():
             if traffic is not None:
                 traffic = int(traffic * scale)
             if pk.get("SQ_INSTS_VALU"):
-                # VALU issue utilisation: a wave64 VALU instruction occupies a SIMD-32 for 2 cycles
-                # (MI355X_MICROARCH.md, wave scheduling); 256 CUs x 4 SIMDs at 2.4 GHz
+                # VALU pipe occupancy, 256 CUs x 4 SIMDs at 2.4 GHz.  A wave64 VALU instruction holds its SIMD-32 for
+                # 2 cycles (v_add_u32, v_and/or/xor, v_add/fma_f32, 16-bit v_max/min/add, v_mov) or 4 cycles (packed
+                # 16-bit, 3-input, v_perm, v_mbcnt, v_cmp, 32-bit v_max/min, v_lshlrev, 24-bit multiplies), measured by
+                # tools/micro/valu_rate.hip (profiles/r05_valu_issue_rates.txt): the two bounds bracket the kernel's mix
                 insts = pk["SQ_INSTS_VALU"] * scale
+                den = dom_ms * 1e-3 * VALU_CLK_HZ * VALU_SIMDS
                 valu = {"insts_per_launch": int(insts),
-                        "issue_frac": round(insts * 2 / (dom_ms * 1e-3 * VALU_CLK_HZ * VALU_SIMDS), 4),
-                        "note": f"PMC SQ_INSTS_VALU ({os.path.relpath(pmc_json, ROOT)}) x 2 cycles / (avg_launch_ms x "
-                                "2.4 GHz x 1024 SIMDs)"}
+                        "busy_frac_if_4cyc": round(insts * 4 / den, 4),
+                        "busy_frac_if_2cyc": round(insts * 2 / den, 4),
+                        "note": f"PMC SQ_INSTS_VALU ({os.path.relpath(pmc_json, ROOT)}) x 4 (or 2) cycles / "
+                                "(avg_launch_ms x 2.4 GHz x 1024 SIMDs); the 4-cycle forms dominate the FAST, describe "
+                                "and resize kernels, so the first is the closer one (DESIGN.md §6)"}
         except Exception:
             traffic = None
             valu = None

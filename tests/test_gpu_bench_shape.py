@@ -134,14 +134,14 @@ def test_grid_csr_batch256_vs_oracle(gpu, oracle):
         ex.device_free(d)
 
 
-@pytest.mark.parametrize("workload", ["tracking", "stereo", "extract"])
+@pytest.mark.parametrize("workload", ["tracking", "stereo", "extract", "stereo --serial-pairs"])
 def test_bench_workload_timed_parity(gpu, workload):
     """Each secondary bench workload end to end (bench.py as the driver runs it, a short run): the timed path's
     own parity check against the oracle goldens must report zero mismatches.  Catches state shared between set-up
     and the timed steps (e.g. the config-5 map record, read through raw pointers by every step)."""
     import subprocess
 
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", workload, "--batch", "8",
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", *workload.split(), "--batch", "8",
                           "--streams", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"],
                          capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
