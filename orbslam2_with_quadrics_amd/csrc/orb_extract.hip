@@ -2766,21 +2766,34 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
     const int xsimd_s = BV == 0 ? ((lw & ~3) - (cx - 18)) : 0;  // window columns < xsimd_s round half-to-even
     // ALLEVEN: every window column is < xsimd_s (the usual case away from the level's right edge)
-    auto blurred = [&](int row, int col, auto alleven) -> int {  // window offsets from the centre, |row|, |col| <= 18
-        const int y = 18 + row, xw = 18 + col;
-        const uint32_t* h = Hp + __mul24(y >> 1, HP_S) + xw;  // (a 24-bit multiply: v_mul_lo_u32 is quarter rate)
-        const bool odd = (y & 1) != 0;
-        const u16x2v w0 = odd ? u16x2v{0, (unsigned short)c0} : u16x2v{(unsigned short)c0, (unsigned short)c1};
-        const u16x2v w1 = odd ? u16x2v{(unsigned short)c1, (unsigned short)c2} : u16x2v{(unsigned short)c2, (unsigned short)c3};
-        const u16x2v w2 = odd ? u16x2v{(unsigned short)c3, (unsigned short)c2} : u16x2v{(unsigned short)c2, (unsigned short)c1};
-        const u16x2v w3 = odd ? u16x2v{(unsigned short)c1, (unsigned short)c0} : u16x2v{(unsigned short)c0, 0};
+    // y = 18 + row, xw = 18 + col: window coordinates of a sample at offsets |row|, |col| <= 18 from the centre
+    const uint32_t hpb = og_lds_addr(Hp);
+    auto blurred = [&](unsigned y, unsigned xw, auto alleven) -> int {
+        // LDS byte address of Hp[(y >> 1) * HP_S + xw]: one 24-bit multiply-add and one shift-add (v_mul_lo_u32 is
+        // quarter rate); the four tap rows are the immediate offsets of two ds_read2_b32
+        typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+        lds_u32* h = (lds_u32*)(uintptr_t)((__umul24(y >> 1, HP_S) + xw) * 4u + hpb);
+        // the tap weights by row parity, each one v_alignbyte of two constants (the odd form, and the even form's high
+        // half): a 16-bit funnel shift for even rows ((2y + 2) & 3 = 2 iff y is even), none for odd rows
+        // (asm: the high dword is an inline constant and the low one an SGPR; the compiler's own choice re-creates each
+        // low constant in a VGPR with a v_mov per sample)
+        const unsigned sh = 2u * y + 2u;
+        auto wsel = [&](auto hi, uint32_t lo) -> u16x2v {
+            uint32_t r;
+            __asm__("v_alignbyte_b32 %0, %1, %2, %3" : "=v"(r) : "n"(decltype(hi)::value), "s"(lo), "v"(sh));
+            return __builtin_bit_cast(u16x2v, r);
+        };
+        const u16x2v w0 = wsel(std::integral_constant<uint32_t, c1>{}, c0 << 16);
+        const u16x2v w1 = wsel(std::integral_constant<uint32_t, c3>{}, c1 | c2 << 16);
+        const u16x2v w2 = wsel(std::integral_constant<uint32_t, c1>{}, c3 | c2 << 16);
+        const u16x2v w3 = wsel(std::integral_constant<uint32_t, 0u>{}, c1 | c0 << 16);
         uint32_t acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, h[0]), w0, 0u, false);
         acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, h[HP_S]), w1, acc, false);
         acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, h[2 * HP_S]), w2, acc, false);
         acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, h[3 * HP_S]), w3, acc, false);
         uint32_t v;
         if (BV == 0) {
-            const uint32_t up = decltype(alleven)::value ? 0u : (xw < xsimd_s ? 0u : 1u);
+            const uint32_t up = decltype(alleven)::value ? 0u : ((int)xw < xsimd_s ? 0u : 1u);
             v = (acc + 0x7fffu + (__builtin_amdgcn_ubfe(acc, 16, 1) | up)) >> 16;
         } else {
             v = (acc + (1u << 15)) >> 16;
@@ -2813,7 +2826,7 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
                             : "=v"(rc)
                             : "v"(xy[q]), "v"(ba), "v"(yab));
                 }
-                val[q] = blurred(og_cvround(rc.x), og_cvround(rc.y), alleven);
+                val[q] = blurred(og_cvround_plus(rc.x, 18), og_cvround_plus(rc.y, 18), alleven);
             }
             words[t] = og_ballot(val[0] < val[1]);
         }

@@ -8,6 +8,20 @@
 // cvRound(float): cvtss2si under the default MXCSR = round-half-even (v_rndne_f32).
 __device__ __forceinline__ int og_cvround(float v) { return (int)__builtin_rintf(v); }
 
+// cvRound(v) + k for |v| < 2^22, as the low bits of v + 1.5 * 2^23: the add rounds v half-to-even to an integer (the
+// float's ulp there is 1) and the bits of 1.5 * 2^23 + n are 0x4B400000 + n.  Two 2-cycle instructions (v_add_f32,
+// v_sub_u32) where v_rndne_f32 + v_cvt_i32_f32 are two 4-cycle ones (profiles/r05_valu_issue_rates.txt).
+// (asm: the compiler would pack two such adds into one v_pk_add_f32 plus a v_mov, and fold the subtraction into
+// every address that uses the result; the empty asm keeps it one v_sub_u32)
+__device__ __forceinline__ unsigned og_cvround_plus(float v, int k)
+{
+    float t;
+    __asm__("v_add_f32 %0, %1, %2" : "=v"(t) : "s"(12582912.0f), "v"(v));
+    unsigned u = __builtin_bit_cast(unsigned, t) - (0x4B400000u - (unsigned)k);
+    __asm__("" : "+v"(u));
+    return u;
+}
+
 // cv::fastAtan2 (OpenCV 3.x scalar, no FMA), called at src/ORBextractor.cc:103.
 __device__ __forceinline__ float og_fast_atan2(float y, float x)
 {
