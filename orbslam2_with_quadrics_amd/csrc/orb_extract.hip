@@ -534,7 +534,7 @@ typedef _Float16 og_h2 __attribute__((ext_vector_type(2)));
 // (D16 loads cannot do it here: with SRAMECC, gfx950's ds_read_u16_d16[_hi] clear the other half).
 #define OG_MPK_OFF(dy, dx) (8 * ((3 + (dy)) * FQ_S_ + 3 + (dx)))
 template <int FQ_S_>
-__device__ __forceinline__ int og_fast_Mpk(uint32_t base, _Float16 sgn)
+__device__ __forceinline__ int og_fast_Mpk(uint32_t base, uint32_t sgm)
 {
     uint32_t w[8];
     uint32_t vc;
@@ -550,11 +550,12 @@ __device__ __forceinline__ int og_fast_Mpk(uint32_t base, _Float16 sgn)
         for (int k = 0; k < 8; k++) w[k] = __builtin_bit_cast(uint32_t, og_h2{c[k], c[k + 8]});
         vc = __builtin_bit_cast(uint16_t, q[0]);
     }
-    const og_h2 sg = {sgn, sgn};
+    // the polarity as a sign flip of both halves (sgm = 0 or 0x80008000): one 2-cycle v_xor_b32 per pair where a
+    // v_pk_mul_f16 by -1 is a 4-cycle one (profiles/r05_valu_issue_rates.txt); -x is exactly x * -1, zeros included
     og_h2 P[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) P[k] = __builtin_bit_cast(og_h2, w[k]) * sg;
-    const _Float16 v = __builtin_bit_cast(og_h2, vc).x * sgn;
+    for (int k = 0; k < 8; k++) P[k] = __builtin_bit_cast(og_h2, w[k] ^ sgm);
+    const _Float16 v = __builtin_bit_cast(og_h2, vc ^ sgm).x;
 #define OG_SW(a) __builtin_shufflevector(a, a, 1, 0)
 #define OG_MX3(a, b, c) __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c)
 #define OG_MN3(a, b, c) __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c)
@@ -973,8 +974,8 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const bool dark = (ent & 0x4000) != 0, bright = (ent & 0x8000) != 0;
         // the exact score with packed f16 pair ops (og_fast_Mpk)
         const uint32_t pb = og_lds_addr(pc) - 8u * (3u * FQ_S + 3u);
-        int M = og_fast_Mpk<FQ_S>(pb, dark ? (_Float16)1 : (_Float16)-1);
-        if (dark && bright) M = max(M, og_fast_Mpk<FQ_S>(pb, (_Float16)-1));
+        int M = og_fast_Mpk<FQ_S>(pb, dark ? 0u : 0x80008000u);
+        if (dark && bright) M = max(M, og_fast_Mpk<FQ_S>(pb, 0x80008000u));
         Ms[og_ms_idx(i, j, wC, hC)] = (uint8_t)M;
     }
     __syncthreads();
@@ -2726,31 +2727,46 @@ __global__ __launch_bounds__(64 * DK_WAVES) void og_describe_kernel(OgPlan P, co
     }
 #endif
     if (active) {
-        for (int it = lane; it < HP_ROWS * 10; it += 64) {
-            const int rp = it / 10, g = it - rp * 10;
-            uint32_t hv[2][4];
+        // item it = lane + 64 k = (row pair rp, 4-column group g) for k = 0..3 (220 items): from one item to the lane's
+        // next, rp advances by 6 and g by 4, with one wrap of g past 10 into rp; the item's raw-window and Hp byte
+        // addresses advance with them (adds and one select per step instead of a division and multiplies per item)
+        int g = lane % 10, rp = lane / 10;
+        uint32_t ar = (uint32_t)(2 * rp * RAW_S + 4 * g);    // byte offset in the raw window: row 2 rp, dword g
+        uint32_t ah = (uint32_t)(4 * (rp * HP_S + 4 * g));   // byte offset of Hp[rp][4 g]
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int r = min(2 * rp + h, RAW_W - 1);  // row 43 (pair 21, high half) is never read
-                const uint32_t* rr = (const uint32_t*)(Rb + r * RAW_S) + g;
-                const uint32_t d0 = rr[0], d1 = rr[1], d2 = rr[2];
-                // output k = sum over the window bytes k .. k+6 of d0:d1:d2: the weights shift, not the data --
-                // 2, 2, 3, 3 dot4 for k = 0..3
-                constexpr uint32_t W00 = c0 | c1 << 8 | c2 << 16 | c3 << 24, W01 = c2 | c1 << 8 | c0 << 16;
-                constexpr uint32_t W10 = c0 << 8 | c1 << 16 | c2 << 24, W11 = c3 | c2 << 8 | c1 << 16 | c0 << 24;
-                constexpr uint32_t W20 = c0 << 16 | c1 << 24, W21 = c2 | c3 << 8 | c2 << 16 | c1 << 24, W22 = c0;
-                constexpr uint32_t W30 = c0 << 24, W31 = c1 | c2 << 8 | c3 << 16 | c2 << 24, W32 = c1 | c0 << 8;
-                hv[h][0] = __builtin_amdgcn_udot4(d1, W01, __builtin_amdgcn_udot4(d0, W00, 0u, false), false);
-                hv[h][1] = __builtin_amdgcn_udot4(d1, W11, __builtin_amdgcn_udot4(d0, W10, 0u, false), false);
-                hv[h][2] = __builtin_amdgcn_udot4(d2, W22, __builtin_amdgcn_udot4(d1, W21, __builtin_amdgcn_udot4(d0, W20, 0u, false), false), false);
-                hv[h][3] = __builtin_amdgcn_udot4(d2, W32, __builtin_amdgcn_udot4(d1, W31, __builtin_amdgcn_udot4(d0, W30, 0u, false), false), false);
+        for (int k = 0; k < 4; k++) {
+            if (k < 3 || lane + 64 * k < HP_ROWS * 10) {
+                uint32_t hv[2][4];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    // row 2 rp + h, clamped to row 42 (pair 21's high half, row 43, is never read)
+                    const uint32_t a = h == 0 || rp < HP_ROWS - 1 ? ar + (uint32_t)(h * RAW_S) : ar;
+                    const uint32_t* rr = (const uint32_t*)(Rb + a);
+                    const uint32_t d0 = rr[0], d1 = rr[1], d2 = rr[2];
+                    // output k = sum over the window bytes k .. k+6 of d0:d1:d2: the weights shift, not the data --
+                    // 2, 2, 3, 3 dot4 for k = 0..3
+                    constexpr uint32_t W00 = c0 | c1 << 8 | c2 << 16 | c3 << 24, W01 = c2 | c1 << 8 | c0 << 16;
+                    constexpr uint32_t W10 = c0 << 8 | c1 << 16 | c2 << 24, W11 = c3 | c2 << 8 | c1 << 16 | c0 << 24;
+                    constexpr uint32_t W20 = c0 << 16 | c1 << 24, W21 = c2 | c3 << 8 | c2 << 16 | c1 << 24, W22 = c0;
+                    constexpr uint32_t W30 = c0 << 24, W31 = c1 | c2 << 8 | c3 << 16 | c2 << 24, W32 = c1 | c0 << 8;
+                    hv[h][0] = __builtin_amdgcn_udot4(d1, W01, __builtin_amdgcn_udot4(d0, W00, 0u, false), false);
+                    hv[h][1] = __builtin_amdgcn_udot4(d1, W11, __builtin_amdgcn_udot4(d0, W10, 0u, false), false);
+                    hv[h][2] = __builtin_amdgcn_udot4(d2, W22, __builtin_amdgcn_udot4(d1, W21, __builtin_amdgcn_udot4(d0, W20, 0u, false), false), false);
+                    hv[h][3] = __builtin_amdgcn_udot4(d2, W32, __builtin_amdgcn_udot4(d1, W31, __builtin_amdgcn_udot4(d0, W30, 0u, false), false), false);
+                }
+                // (row 2 rp, row 2 rp + 1) u16 pairs: one v_perm each (sums <= 65535)
+                *(uint4*)((uint8_t*)Hp + ah) = make_uint4(__builtin_amdgcn_perm(hv[1][0], hv[0][0], 0x05040100u),
+                                                     __builtin_amdgcn_perm(hv[1][1], hv[0][1], 0x05040100u),
+                                                     __builtin_amdgcn_perm(hv[1][2], hv[0][2], 0x05040100u),
+                                                     __builtin_amdgcn_perm(hv[1][3], hv[0][3], 0x05040100u));
             }
-            uint4 o;
-            o.x = hv[0][0] | (hv[1][0] << 16);
-            o.y = hv[0][1] | (hv[1][1] << 16);
-            o.z = hv[0][2] | (hv[1][2] << 16);
-            o.w = hv[0][3] | (hv[1][3] << 16);
-            *(uint4*)&Hp[rp * HP_S + 4 * g] = o;
+            if (k < 3) {
+                const bool wrap = g >= 6;  // g + 4 >= 10
+                g += wrap ? 4 - 10 : 4;
+                rp += wrap ? 7 : 6;
+                ar += wrap ? 6 * 2 * RAW_S + 16 + 2 * RAW_S - 40 : 6 * 2 * RAW_S + 16;
+                ah += 4 * (6 * HP_S + 4 * 4);  // (7 HP_S - 4 * 6 when g wraps: the same 256 dwords)
+            }
         }
     }
     og_dk_sync();
