@@ -213,7 +213,7 @@ __global__ __launch_bounds__(INIT_NT) void og_init_resolve_kernel(
     OgFrameDev F1, int ref, OgFrameDev F2, float nnratio, int checkOri, float* __restrict__ prev_xy,
     int prev_stride, const uint32_t* __restrict__ lists, int list_cap, const int* __restrict__ list_n,
     int* __restrict__ matches12, int match_stride, int* __restrict__ nmatches, int* __restrict__ status, int ecap,
-    const int* __restrict__ ref_status)
+    const int* __restrict__ ref_status, int qcap)
 {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(INIT_NT) void og_init_resolve_kernel(
         for (int base = 0; base < n1; base += INIT_NT) {
             const int i = base + tid;
             int v = 0;
-            if (i < n1) {
+            if (i < n1 && i < qcap) {  // (F1 keypoints from qcap on are past level 0: no candidate kernel wave)
                 const int raw = NC[i];
                 if (raw < 0) atomicOr(status, 16);
                 v = raw < 0 ? 0 : raw;
@@ -466,9 +466,12 @@ int og_init_keep_bound(float nnratio)
 void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G, float nnratio,
                            int checkOri, int windowSize, float* prev_xy, int prev_stride, int* matches12,
                            int match_stride, int* nmatches, uint32_t* lists, int list_cap, int* list_n, int* status,
-                           int B, const int* ref_status)
+                           int B, const int* ref_status, int qcap)
 {
-    hipLaunchKernelGGL(og_init_cand_kernel, dim3((F1.frame_cap + 3) / 4, B), dim3(256), 0, s, F1, ref, F2, G,
+    // queries: F1 keypoints [0, qcap) (only octave-0 keypoints have candidates, :419-421; a frame extracted here
+    // lists its levels in order, so its octave-0 keypoints are the first <= kcap_0)
+    qcap = qcap > 0 ? std::min(qcap, F1.frame_cap) : F1.frame_cap;
+    hipLaunchKernelGGL(og_init_cand_kernel, dim3((qcap + 3) / 4, B), dim3(256), 0, s, F1, ref, F2, G,
                        windowSize, og_init_keep_bound(nnratio), prev_xy, prev_stride, lists, list_cap, list_n);
     const size_t fixed = og_init_resolve_lds(F1.frame_cap, F2.frame_cap, 0);
     // staging for the (pruned, short) lists: a few KB keep several workgroups per CU; one list (<= list_cap)
@@ -477,7 +480,7 @@ void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2,
     const size_t shm = og_init_resolve_lds(F1.frame_cap, F2.frame_cap, ecap);
     hipLaunchKernelGGL(og_init_resolve_kernel, dim3(B), dim3(INIT_NT), shm, s, F1, ref, F2, nnratio, checkOri,
                        prev_xy, prev_stride, lists, list_cap, list_n, matches12, match_stride, nmatches, status,
-                       ecap, ref_status);
+                       ecap, ref_status, qcap);
 }
 
 // Tracking::MonocularInitialization (src/Tracking.cc:573-575): vbPrevMatched[i] = F1.mvKeysUn[i].pt,

@@ -1258,7 +1258,7 @@ int orbgpu_search_for_initialization_batch(orbgpu_ctx* cref, int ref, orbgpu_ctx
     timer_mark(c, "match_init");
     og_launch_search_init(s, f1, ref, f2, G, nnratio, checkOri, windowSize, d_prev_xy, 2 * cref->plan.frame_cap,
                           d_matches12, cref->plan.frame_cap, d_nmatches, c->mlists.p, list_cap, c->mlist_n.p,
-                          c->status.p, c->last_B, cref != c ? cref->status.p : nullptr);
+                          c->status.p, c->last_B, cref != c ? cref->status.p : nullptr, cref->plan.lv[0].kcap);
     timer_mark(c, "search_init");
     HIP_TRY(c, hipGetLastError());
     return ORBGPU_OK;

@@ -82,7 +82,7 @@ struct OgFrameDev {        // device view of one or many frames (batch stride fr
 void og_launch_search_init(hipStream_t s, OgFrameDev F1, int ref, OgFrameDev F2, OgGridGeom G, float nnratio,
                            int checkOri, int windowSize, float* prev_xy, int prev_stride, int* matches12,
                            int match_stride, int* nmatches, uint32_t* lists, int list_cap, int* list_n, int* status,
-                           int B, const int* ref_status = nullptr);
+                           int B, const int* ref_status = nullptr, int qcap = 0);
 
 // LDS bytes of the ordered SearchForInitialization pass for frame capacities cap1/cap2 and `ecap` staged
 // candidate entries; the pass needs og_init_resolve_lds(cap1, cap2, list_cap) <= OG_INIT_LDS_MAX
