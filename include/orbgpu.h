@@ -140,8 +140,9 @@ int orbgpu_batch_download(orbgpu_ctx* ctx, int b, orbgpu_keypoint* kps, uint8_t*
  * (SURVEY §8(e)).  Both calls are enqueued on the context stream; unpack requires a context planned for the
  * same image size and parameters, and records the event the matchers of other contexts wait for.  The record's
  * 16-byte header holds the count, a magic word, frame_cap and the undistortion flag.  Unpack never blocks the host:
- * the header is checked on the device, in stream order.  A record that does not match the context's plan, or
- * whose count exceeds frame_cap, leaves frame 0 with count 0, and the next call that checks the context's status
+ * the header is checked on the device, in stream order.  A record that does not match the context's plan, whose
+ * count exceeds frame_cap, or whose keypoints are not in extraction order (pyramid levels nondecreasing, as pack
+ * writes them), leaves frame 0 with count 0, and the next call that checks the context's status
  * (orbgpu_synchronize, orbgpu_batch_download, or any other call that returns results to the host) returns
  * ORBGPU_ERR_ARG.  A batched SearchForInitialization on another context that matches against such a frame raises the
  * same condition in its own context (its next status check returns ORBGPU_ERR_ARG), so a refused record never passes

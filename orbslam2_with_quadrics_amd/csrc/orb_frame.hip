@@ -201,20 +201,44 @@ void og_launch_pack_host(hipStream_t s, const int* status, const int* counts, co
 // check reports as ORBGPU_ERR_ARG.
 // ------------------------------------------------------------------------------------------------
 #define OG_RECORD_MAGIC 0x5246474fu
-__global__ __launch_bounds__(256) void og_record_unpack_kernel(const uint32_t* __restrict__ rec, int frame_cap, int undist,
-                                                              int* __restrict__ counts, uint32_t* __restrict__ kps,
-                                                              uint32_t* __restrict__ desc, uint32_t* __restrict__ kps_un,
-                                                              int* __restrict__ status)
+// The header and the keypoint order (levels nondecreasing, as extracted: the batched SearchForInitialization takes
+// F1's octave-0 queries from its first kcap0 slots) decide whether the record is accepted; one workgroup writes the
+// count (n, or 0 and status bit 128), the copy kernel after it on the stream moves the data of an accepted header.
+__device__ __forceinline__ bool og_record_header_ok(const uint32_t* rec, int frame_cap, int undist)
 {
     const int n = (int)rec[0];
-    const bool ok = rec[1] == OG_RECORD_MAGIC && rec[2] == (uint32_t)frame_cap && rec[3] == (undist ? 1u : 0u) &&
-                    n >= 0 && n <= frame_cap;
-    const int i0 = blockIdx.x * 256 + threadIdx.x;
-    if (i0 == 0) {
+    return rec[1] == OG_RECORD_MAGIC && rec[2] == (uint32_t)frame_cap && rec[3] == (undist ? 1u : 0u) && n >= 0 &&
+           n <= frame_cap;
+}
+
+__global__ __launch_bounds__(256) void og_record_check_kernel(const uint32_t* __restrict__ rec, int frame_cap, int undist,
+                                                             int kcap0, int* __restrict__ counts, int* __restrict__ status)
+{
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    const bool hdr = og_record_header_ok(rec, frame_cap, undist);
+    const int n = hdr ? (int)rec[0] : 0;
+    const int* oct = (const int*)(rec + 4) + 5;  // orbgpu_kp_dev::octave, 7 words per keypoint
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int o = oct[7 * i], prev = i > 0 ? oct[7 * (i - 1)] : 0;
+        if (o < prev || (o == 0 && i >= kcap0)) bad = 1;  // (benign race: every writer stores 1)
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const bool ok = hdr && !bad;
         counts[0] = ok ? n : 0;
         if (!ok) atomicOr(status, 128);
     }
-    if (!ok) return;
+}
+
+__global__ __launch_bounds__(256) void og_record_unpack_kernel(const uint32_t* __restrict__ rec, int frame_cap, int undist,
+                                                              uint32_t* __restrict__ kps, uint32_t* __restrict__ desc,
+                                                              uint32_t* __restrict__ kps_un)
+{
+    if (!og_record_header_ok(rec, frame_cap, undist)) return;
+    const int n = (int)rec[0];
+    const int i0 = blockIdx.x * 256 + threadIdx.x;
     const uint32_t* rk = rec + 4;
     const uint32_t* rd = rk + 7 * frame_cap;
     const uint32_t* ru = rd + 8 * frame_cap;
@@ -226,9 +250,11 @@ __global__ __launch_bounds__(256) void og_record_unpack_kernel(const uint32_t* _
     }
 }
 
-void og_launch_record_unpack(hipStream_t s, const void* rec, int frame_cap, int undist, int* counts,
+void og_launch_record_unpack(hipStream_t s, const void* rec, int frame_cap, int undist, int kcap0, int* counts,
                              orbgpu_kp_dev* kps, uint8_t* desc, orbgpu_kp_dev* kps_un, int* status)
 {
+    hipLaunchKernelGGL(og_record_check_kernel, dim3(1), dim3(256), 0, s, (const uint32_t*)rec, frame_cap, undist,
+                       kcap0, counts, status);
     hipLaunchKernelGGL(og_record_unpack_kernel, dim3(16), dim3(256), 0, s, (const uint32_t*)rec, frame_cap, undist,
-                       counts, (uint32_t*)kps, (uint32_t*)desc, (uint32_t*)kps_un, status);
+                       (uint32_t*)kps, (uint32_t*)desc, (uint32_t*)kps_un);
 }

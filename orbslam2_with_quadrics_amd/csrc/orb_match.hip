@@ -217,7 +217,7 @@ __global__ __launch_bounds__(INIT_NT) void og_init_resolve_kernel(
 {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    // F1 from another context: a frame record that context refused (status bit 128, og_record_unpack_kernel: F1 was
+    // F1 from another context: a frame record that context refused (status bit 128, og_record_check_kernel: F1 was
     // left empty) is reported by this context's next status check too, not only as zero matches
     if (ref_status && b == 0 && tid == 0 && (*ref_status & 128)) atomicOr(status, 128);
     const int n1 = F1.counts[ref];

@@ -971,9 +971,10 @@ int orbgpu_frame_record_unpack(orbgpu_ctx* c, const void* d_src)
     // the header must describe this context's plan (frame_cap, undistortion) and a count within it; a record from
     // a differently planned context would otherwise be misread, and a larger count would send the matchers past
     // the frame.  Checked on the device, so the call stays stream-ordered (no host synchronisation): a mismatch
-    // leaves count 0 and is reported as ORBGPU_ERR_ARG by the next status check.
+    // leaves count 0 and is reported as ORBGPU_ERR_ARG by the next status check.  So does a record whose keypoints
+    // are not in extraction order (levels nondecreasing): the batched SearchForInitialization relies on it.
     hipStream_t s = c->stream;
-    og_launch_record_unpack(s, d_src, c->plan.frame_cap, c->undist ? 1 : 0, c->counts.p, c->kps.p, c->desc.p,
+    og_launch_record_unpack(s, d_src, c->plan.frame_cap, c->undist ? 1 : 0, c->plan.lv[0].kcap, c->counts.p, c->kps.p, c->desc.p,
                             c->undist ? c->kps_un.p : nullptr, c->status.p);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(c->done, s));  // matchers on other contexts wait for this record

@@ -216,8 +216,9 @@ void og_launch_undistort_points(hipStream_t s, const float* xy, float* out, int 
 // {status, count, 0, 0, frame_cap x 28 B, frame_cap x 32 B} (host_dev: its device-side address)
 void og_launch_pack_host(hipStream_t s, const int* status, const int* counts, const orbgpu_kp_dev* kps,
                          const uint8_t* desc, int frame_cap, void* host_dev);
-// frame-record unpack into frame 0, header validated on the device (mismatch: count 0, status bit 128)
-void og_launch_record_unpack(hipStream_t s, const void* rec, int frame_cap, int undist, int* counts,
+// frame-record unpack into frame 0, header and keypoint level order validated on the device (levels nondecreasing,
+// octave-0 keypoints within the first kcap0 slots; otherwise count 0 and status bit 128)
+void og_launch_record_unpack(hipStream_t s, const void* rec, int frame_cap, int undist, int kcap0, int* counts,
                              orbgpu_kp_dev* kps, uint8_t* desc, orbgpu_kp_dev* kps_un, int* status);
 // Frame::ComputeStereoFromRGBD over B frames (counts == nullptr: one frame of n_fixed keypoints); depth rows
 // are `pitch` bytes apart, frames `fstride` bytes; is_u16: raw CV_16U scaled by `factor`, else CV_32F

@@ -1,7 +1,7 @@
 """Frame records (orbgpu_frame_record_pack / _unpack, the unit bench.py broadcasts from rank 0 to the other ranks
 at set-up): a record unpacked into a second context reproduces the frame exactly, and a record
-that does not fit the receiving context's plan (frame_cap, undistortion) or carries a count above frame_cap is
-refused with ORBGPU_ERR_ARG.  The header is checked on the device, so unpack itself never blocks the
+that does not fit the receiving context's plan (frame_cap, undistortion), carries a count above frame_cap or lists
+its keypoints out of extraction order is refused with ORBGPU_ERR_ARG.  The header is checked on the device, so unpack itself never blocks the
 host: a refused record leaves count 0 and the next status check (orbgpu_synchronize) returns
 ORBGPU_ERR_ARG."""
 import ctypes as C
@@ -51,6 +51,16 @@ def test_record_round_trip_and_plan_checks(gpu):
     # a buffer that is not a record (no magic word) is refused
     zero = torch.zeros_like(rec)
     refused(b.ctx, zero.data_ptr())
+    # keypoints out of extraction order (a level-1 keypoint before a level-0 one) are refused: the batched
+    # SearchForInitialization takes F1's octave-0 queries from its first kcap_0 slots
+    n = int(np.frombuffer(rec[:4].cpu().numpy().tobytes(), np.int32)[0])
+    oct0 = np.where(ka["octave"] == 0)[0]
+    assert n > 2 and oct0.size > 0 and oct0.size < n
+    swapped = rec.clone()
+    kbytes = swapped[16:16 + 28 * n].view(n, 28)
+    first, last = kbytes[0].clone(), kbytes[n - 1].clone()  # a level-0 and the last (top-level) keypoint
+    kbytes[0], kbytes[n - 1] = last, first
+    refused(b.ctx, swapped.data_ptr())
     # and the good record still unpacks after a refusal
     _lib.check(b.ctx, L.orbgpu_frame_record_unpack(b.ctx, C.c_void_p(rec.data_ptr())), "unpack")
     b.synchronize()
