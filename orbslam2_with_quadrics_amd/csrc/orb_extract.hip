@@ -828,13 +828,17 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     __shared__ int sh_base;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);
-    const unsigned f = blockIdx.y;  // grid (workgroups per frame, frames)
+    // the dispatch order lin = (blockIdx.y, blockIdx.x) interleaves the frames: block p of frame f is workgroup
+    // p * B + f, so with B a multiple of 8 every block of a frame runs on XCD f % 8 and shares that L2 with its
+    // neighbours (FAST -0.7 % against frame-major order, profiles/sweeps/r05_ab_fast_frame_interleave.txt)
+    const unsigned lin_ = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned f = lin_ % gridDim.y;
     const int t1 = thr & 255, t2 = (thr >> 8) & 255;  // clamped to [0, 255] on the host
     const int tq = min(t1, t2);
     const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
     const int tA = max(t1, 1), tB = max(t2, 1);
     const uint32_t a_ns = og_lds_addr(&sh_ns), a_lst = og_lds_addr(&lst[0]);
-    const int p = (int)blockIdx.x;
+    const int p = (int)(lin_ / gridDim.y);
     // every kernel argument the block decode reads is fetched before the first of them is used: one scalar-cache round
     // trip (the compiler's order took three before the block record)
     __asm__ volatile("" ::"s"(blocks), "s"(nb), "s"(img0), "s"(pitch0), "s"(fstride0), "s"(pyr), "s"(pyr_per_frame));

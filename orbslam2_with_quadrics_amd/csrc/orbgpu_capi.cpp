@@ -400,11 +400,11 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
     }
     P.total_cells = (int)cells.size();
     // the FAST kernel's block table (OgFastBlk): level-major; each level's range is padded to a multiple of 8
-    // entries (empty entries, lev < 0, exit at once), so workgroup (f, w) of the launch runs on XCD w % 8 for every
-    // frame (dispatch deals consecutive workgroups round-robin over the 8 XCDs).  Within a level, ORBGPU_FAST_ORDER
-    // R (default 4) gives each XCD runs of R row-adjacent blocks: their ROIs share 128-byte lines, which are then
-    // fetched once into that XCD's L2 instead of once per XCD.  R = 1 is plain plan order; giving every XCD a
-    // contiguous eighth of each frame was 7-9 % slower (profiles/sweeps/r03_ab_fast_block_order.txt).
+    // entries (empty entries, lev < 0, exit at once).  The kernel interleaves the frames in dispatch order (block p
+    // of frame f is workgroup p * B + f), so with B a multiple of 8 a frame's blocks all run on XCD f % 8 and the
+    // table order only sets the order of a frame's blocks in time.  Within a level, ORBGPU_FAST_ORDER R (default 4)
+    // groups runs of R row-adjacent blocks (round 3: R-runs per XCD under frame-major dispatch; giving every XCD a
+    // contiguous eighth of each frame was 7-9 % slower, profiles/sweeps/r03_ab_fast_block_order.txt).
     std::vector<OgFastBlk> fblk;
     {
         static const int R = [] {
