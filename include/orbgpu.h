@@ -189,7 +189,9 @@ int orbgpu_search_for_initialization(orbgpu_ctx* ctx, const orbgpu_frame_view* F
 /* Device-resident batch form: frame `ref` of ctx_ref's last batch is F1 for every frame b of ctx's last
  * batch (F2 = frame b), as Tracking::MonocularInitialization matches each new frame against the
  * initial frame (src/Tracking.cc:563-635).  d_prev_xy: B x ref_cap x 2 floats (in/out, device),
- * d_matches12: B x ref_cap ints (device), d_nmatches: B ints (device).  Enqueued on ctx's stream. */
+ * d_matches12: B x ref_cap ints (device), d_nmatches: B ints (device).  Enqueued on ctx's stream.  F1's keypoints
+ * are in extraction order (pyramid levels ascending, as every extracted frame and every accepted frame record has
+ * them), so its octave-0 queries (:419-421) are its first keypoints, at most the level-0 capacity. */
 int orbgpu_search_for_initialization_batch(orbgpu_ctx* ctx_ref, int ref, orbgpu_ctx* ctx,
                                            orbgpu_grid_geom grid, float nnratio, int checkOri,
                                            int windowSize, float* d_prev_xy, int* d_matches12,
