@@ -6,6 +6,10 @@
   R += 32 up to 8 (nunits >> 1) + 2 (w & 1) (og_fast_quad_kernel).
 * FAST's column counts: OgFastBlk::colw byte k = clamp(dw - 16 k, 0, 16), mask (0x10001 << n) - 0x10001 per 16-lane
   group.
+* describe's cvRound of the rotated rBRIEF coordinates (og_cvround_plus, orb_math_dev.h): the bits of the float sum
+  v + 1.5 * 2^23 are 0x4B400000 + rint(v) (round half to even) for |v| < 2^22; the sample coordinates are |v| <= 18.5.
+* the FAST frame-interleaved dispatch (og_fast_quad_kernel): workgroup lin of a (nb, B) grid is block lin / B of frame
+  lin % B, a bijection onto (block, frame), and every block of frame f runs on XCD f % 8 when B % 8 == 0.
 """
 import random
 
@@ -53,3 +57,34 @@ def test_fast_column_masks():
             m32 = ((0x10001 << n) - 0x10001) & 0xFFFFFFFF
             lanes = [lane for lane in range(32) if (m32 >> lane) & 1]
             assert lanes == [lane for lane in range(32) if (lane & 15) + 16 * k < dw], (dw, k)
+
+
+def test_cvround_plus_magic_rounding():
+    import numpy as np
+
+    rng = np.random.default_rng(7)
+    v = np.concatenate([rng.uniform(-20, 20, 200000).astype(np.float32),
+                        (np.arange(-40, 41, dtype=np.float32) / 2),            # every half-integer tie in range
+                        np.nextafter(np.arange(-40, 41, dtype=np.float32) / 2, np.float32(np.inf)),
+                        np.nextafter(np.arange(-40, 41, dtype=np.float32) / 2, np.float32(-np.inf))])
+    t = (v + np.float32(12582912.0)).astype(np.float32)                      # one f32 add, round to nearest even
+    got = (t.view(np.uint32).astype(np.int64) - 0x4B400000)
+    want = np.rint(v).astype(np.int64)                                         # numpy rint: half to even
+    assert np.array_equal(got, want)
+    # with the + 18 the kernel folds into the subtraction: window coordinates 0 .. 36 for |v| <= 18.5
+    k = 18
+    got18 = (t.view(np.uint32).astype(np.int64) - (0x4B400000 - k)) & 0xFFFFFFFF
+    assert np.array_equal(got18[np.abs(v) <= 18.5], (want + k)[np.abs(v) <= 18.5])
+
+
+def test_fast_frame_interleave_mapping():
+    for nb, B in ((13, 8), (7, 3), (530, 256), (1, 1), (5, 16)):
+        seen = set()
+        for lin in range(nb * B):
+            f, p = lin % B, lin // B
+            assert 0 <= p < nb
+            seen.add((p, f))
+            if B % 8 == 0:
+                assert lin % 8 == f % 8
+        assert len(seen) == nb * B
+
