@@ -584,9 +584,9 @@ __device__ __forceinline__ int og_fast_Mpk(uint32_t base, uint32_t sgm)
 //   dark(t)   <=>  max_k min(c_k, c_k+8) < v - t,   bright(t) <=> min_k max(c_k, c_k+8) > v + t.
 // Two pixels at once: each dword holds two pixels as u16 halves 0x6400 | pixel = the f16 value 1024 + pixel
 // (exact, monotone), so the packed f16 ops of gfx950 apply and v_pk_maximum3/minimum3_f16 reduce the 8 pair
-// minima (maxima) in 4 ops.  All values are integers below 2048 (exact in f16); x - x = +0 and
-// max(negative, +0) = +0, so a half of the returned {dark, bright} dwords is nonzero iff that pixel passes
-// that polarity's test.
+// minima (maxima) in 4 ops.  All values are integers below 2048 (exact in f16) and x - x = +0, so a half of the
+// returned {dmax - (v - t), (v + t) - bmin} dwords is negative (sign bit set) iff that pixel passes that
+// polarity's test, and a half of their packed minimum iff the pixel passes either.
 typedef unsigned short og_u16x2 __attribute__((ext_vector_type(2)));
 
 // ------------------------------------------------------------------------------------------------
@@ -616,7 +616,7 @@ __device__ __forceinline__ uint2 og_fast_quick2v(const uint32_t (&c)[16], uint32
 {
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     const h2 v = __builtin_bit_cast(h2, pv);
-    const h2 t = {(_Float16)tt.x, (_Float16)tt.y}, z = {(_Float16)0, (_Float16)0};
+    const h2 t = {(_Float16)tt.x, (_Float16)tt.y};
     h2 mn[8], mx[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
@@ -629,16 +629,15 @@ __device__ __forceinline__ uint2 og_fast_quick2v(const uint32_t (&c)[16], uint32
     const h2 bmin = OG_MIN3(OG_MIN3(mx[0], mx[1], mx[2]), OG_MIN3(mx[3], mx[4], mx[5]), __builtin_elementwise_minimum(mx[6], mx[7]));
 #undef OG_MAX3
 #undef OG_MIN3
-    const h2 dark = __builtin_elementwise_maximum((v - t) - dmax, z);
-    const h2 bright = __builtin_elementwise_maximum(bmin - (v + t), z);
+    const h2 dark = dmax - (v - t), bright = (v + t) - bmin;  // negative: passes
     return make_uint2(__builtin_bit_cast(uint32_t, dark), __builtin_bit_cast(uint32_t, bright));
 }
 
-// lanes whose u16 low half is nonzero (one v_cmp on the low 16 bits)
-__device__ __forceinline__ u64 og_lanes_lo16_nz(uint32_t a)
+// lanes whose u16 low half is negative as an i16 (one v_cmp on the low 16 bits)
+__device__ __forceinline__ u64 og_lanes_lo16_neg(uint32_t a)
 {
     u64 m;
-    __asm__("v_cmp_ne_u16_e64 %0, 0, %1" : "=s"(m) : "v"(a));
+    __asm__("v_cmp_gt_i16_e64 %0, 0, %1" : "=s"(m) : "v"(a));
     return m;
 }
 
@@ -661,8 +660,8 @@ __device__ __forceinline__ og_u32x8 og_fast_block(const OgFastBlk* blocks, int b
 #endif
 }
 
-// Survivor stores of one stage-1 iteration: entry v_k to LDS byte address a_k from the lanes of m_k only.  One
-// exec save, then exec = saved & m_k around each store, one restore.
+// Survivor stores of one stage-1 iteration: entry v_k to LDS byte address a_k from the lanes of m_k only (entries
+// 1 and 3 from the high halves of v_1, v_3).  One exec save, then exec = saved & m_k around each store, one restore.
 __device__ __forceinline__ void og_ds_write_b16_x4(u64 m0, uint32_t a0, uint32_t v0, u64 m1, uint32_t a1, uint32_t v1,
                                                    u64 m2, uint32_t a2, uint32_t v2, u64 m3, uint32_t a3, uint32_t v3)
 {
@@ -670,9 +669,9 @@ __device__ __forceinline__ void og_ds_write_b16_x4(u64 m0, uint32_t a0, uint32_t
     __asm__ volatile(
         "s_mov_b64 %0, exec\n\t"
         "s_and_b64 exec, %0, %1\n\tds_write_b16 %2, %3\n\t"
-        "s_and_b64 exec, %0, %4\n\tds_write_b16 %5, %6\n\t"
+        "s_and_b64 exec, %0, %4\n\tds_write_b16_d16_hi %5, %6\n\t"
         "s_and_b64 exec, %0, %7\n\tds_write_b16 %8, %9\n\t"
-        "s_and_b64 exec, %0, %10\n\tds_write_b16 %11, %12\n\t"
+        "s_and_b64 exec, %0, %10\n\tds_write_b16_d16_hi %11, %12\n\t"
         "s_mov_b64 exec, %0"
         : "=&s"(sv)
         : "s"(m0), "v"(a0), "v"(v0), "s"(m1), "v"(a1), "v"(v1), "s"(m2), "v"(a2), "v"(v2), "s"(m3), "v"(a3), "v"(v3)
@@ -866,7 +865,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const int lg = lane >> 4, c = lane & 15;
         const int lrow = ((lg & 1) << 2) | (lg >> 1);  // 0, 4, 1, 5
         const uint2* Tl = &Tq[(lrow + 3) * FQ_S + (c + 3)];
-        const uint32_t e_lane = (uint32_t)((lrow << 7) | c);
+        const uint32_t e_lane = (uint32_t)((lrow << 7) | c), e_hi = (e_lane + 16u) << 16;
         // lanes whose column c (lane & 15) is below segment k's column count (the block record's byte k, in [0, 16]),
         // in all four 16-lane groups
         auto cmask = [&](int k) -> u64 {
@@ -920,9 +919,14 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                 cm2 &= rows;
                 cm3 &= rows;
             }
-            const uint32_t a0 = r0.x | r0.y, a1 = r1.x | r1.y;
-            const u64 m[4] = {og_lanes_lo16_nz(a0) & cm0, og_lanes_gt((int)a0, 0xffff) & cm1, og_lanes_lo16_nz(a1) & cm2,
-                              og_lanes_gt((int)a1, 0xffff) & cm3};
+            typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+            auto pkmin = [](uint32_t x, uint32_t y) -> uint32_t {
+                return __builtin_bit_cast(uint32_t, __builtin_elementwise_minimum(__builtin_bit_cast(h2, x),
+                                                                                   __builtin_bit_cast(h2, y)));
+            };
+            const uint32_t a0 = pkmin(r0.x, r0.y), a1 = pkmin(r1.x, r1.y);
+            const u64 m[4] = {og_lanes_lo16_neg(a0) & cm0, og_lanes_lt((int)a0, 0) & cm1, og_lanes_lo16_neg(a1) & cm2,
+                              og_lanes_lt((int)a1, 0) & cm3};
             int cnt[4], n = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -939,24 +943,12 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                     : "v"(a_ns), "v"(n)
                     : "memory");
                 const uint32_t ab = a_lst + 2u * (uint32_t)__builtin_amdgcn_readfirstlane(old);
-                const uint32_t base = e_lane + (uint32_t)(R << 7);
-                uint32_t v[4];
-                {
-                    uint32_t d1, b1;
-                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r0.x), "s"(0x00010001u));
-                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r0.y), "s"(0x00020002u));
-                    const uint32_t pb = d1 | b1;
-                    v[0] = (pb << 14) | base;
-                    v[1] = (pb >> 2) | (base + 16u);
-                }
-                {
-                    uint32_t d1, b1;
-                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(d1) : "v"(r1.x), "s"(0x00010001u));
-                    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r1.y), "s"(0x00020002u));
-                    const uint32_t pb = d1 | b1;
-                    v[2] = (pb << 14) | (base + 32u);
-                    v[3] = (pb >> 2) | (base + 48u);
-                }
+                // entries: bits 14 / 15 of each half = the dark / bright sign bits of that pixel; the high pixels'
+                // entries are built in the high half and stored by ds_write_b16_d16_hi
+                const uint32_t base = e_lane + (uint32_t)(R << 7), hbase = e_hi + ((uint32_t)R << 23);
+                const uint32_t X0 = ((r0.x >> 1) & 0x40004000u) | (r0.y & 0x80008000u);
+                const uint32_t X1 = ((r1.x >> 1) & 0x40004000u) | (r1.y & 0x80008000u);
+                const uint32_t v[4] = {X0 | base, X0 | hbase, X1 | (base + 32u), X1 | (hbase + (32u << 16))};
                 const uint32_t ab1 = ab + 2u * (uint32_t)cnt[0], ab2 = ab1 + 2u * (uint32_t)cnt[1],
                                ab3 = ab2 + 2u * (uint32_t)cnt[2];
                 og_ds_write_b16_x4(m[0], ab + 2u * (uint32_t)og_rank(m[0]), v[0], m[1], ab1 + 2u * (uint32_t)og_rank(m[1]),
