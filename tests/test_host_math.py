@@ -10,6 +10,9 @@
   v + 1.5 * 2^23 are 0x4B400000 + rint(v) (round half to even) for |v| < 2^22; the sample coordinates are |v| <= 18.5.
 * the FAST frame-interleaved dispatch (og_fast_quad_kernel): workgroup lin of a (nb, B) grid is block lin / B of frame
   lin % B, a bijection onto (block, frame), and every block of frame f runs on XCD f % 8 when B % 8 == 0.
+* FAST's stage-1 pass test as a sign (og_fast_quick2v and its caller): on the f16-biased pixels (1024 + p), the halves
+  of dmax - (v - t) and (v + t) - bmin are negative exactly when the pixel passes the dark / bright quick test, their
+  packed minimum is negative exactly when it passes either, and the survivor entry's bits 14 / 15 are those signs.
 """
 import random
 
@@ -88,3 +91,41 @@ def test_fast_frame_interleave_mapping():
                 assert lin % 8 == f % 8
         assert len(seen) == nb * B
 
+
+
+def test_fast_quick_test_sign_form():
+    import numpy as np
+
+    rng = np.random.default_rng(11)
+    n = 200000
+    # circle samples and centres: random bytes, plus near-flat patches where the ties (x - x) decide
+    c = rng.integers(0, 256, (n, 16))
+    v = rng.integers(0, 256, n)
+    flat = rng.random(n) < 0.5
+    c[flat] = np.clip(v[flat, None] + rng.integers(-12, 13, (int(flat.sum()), 16)), 0, 255)
+    t = rng.integers(0, 256, n)
+    t[: n // 2] = rng.integers(0, 25, n // 2)
+    # the integer quick test (cv::FAST, pairs {k, k + 8})
+    lo, hi = np.minimum(c[:, :8], c[:, 8:]), np.maximum(c[:, :8], c[:, 8:])
+    dark = (lo < (v - t)[:, None]).all(axis=1)
+    bright = (hi > (v + t)[:, None]).all(axis=1)
+    # the kernel's f16 form: every operand and result is an integer below 2048, exact in f16
+    h = (c + 1024).astype(np.float16)
+    hv, ht = (v + 1024).astype(np.float16), t.astype(np.float16)
+    dmax = np.minimum(h[:, :8], h[:, 8:]).max(axis=1)
+    bmin = np.maximum(h[:, :8], h[:, 8:]).min(axis=1)
+    ed = (dmax - (hv - ht)).astype(np.float16)
+    eb = ((hv + ht) - bmin).astype(np.float16)
+    e = np.minimum(ed, eb)
+
+    def neg(x):  # the sign bit of the f16 (v_cmp_gt_i16 0, x / bit 15 or 31 of the packed dword)
+        return (x.view(np.uint16) & 0x8000) != 0
+
+    assert np.array_equal(neg(ed), dark)
+    assert np.array_equal(neg(eb), bright)
+    assert np.array_equal(neg(e), dark | bright)
+    assert not (ed.view(np.uint16) == 0x8000).any() and not (eb.view(np.uint16) == 0x8000).any()  # no -0
+    # survivor entries: ((ed >> 1) & 0x4000) | (eb & 0x8000) on each 16-bit half
+    ent = ((ed.view(np.uint16).astype(np.uint32) >> 1) & 0x4000) | (eb.view(np.uint16).astype(np.uint32) & 0x8000)
+    assert np.array_equal((ent & 0x4000) != 0, dark) and np.array_equal((ent & 0x8000) != 0, bright)
+    assert dark.any() and bright.any()
