@@ -3052,8 +3052,8 @@ void og_launch_fast(hipStream_t s, const OgPlan& P, int lb, int le, const OgFast
     le = std::min(le, P.nlevels);
     if (lb >= le || B <= 0) return;
     const int thr = std::min(std::max(P.iniTh, 0), 255) | (std::min(std::max(P.minTh, 0), 255) << 8);
-    // the levels' table range (level-major; each level starts at a multiple of 8, so workgroup w of every frame keeps
-    // XCD w % 8: the table's XCD runs)
+    // the levels' table range (level-major, each level padded to a multiple of 8 entries); the kernel interleaves the
+    // frames in dispatch order, so a frame's blocks share one XCD
     const int p0 = P.lv[lb].fb_off, p1 = le < P.nlevels ? P.lv[le].fb_off : P.fast_blocks;
     if (p1 <= p0) return;
     hipLaunchKernelGGL(og_fast_quad_kernel, dim3(p1 - p0, B), dim3(FB_NT), 0, s, table + p0, p1 - p0, img0, pitch0,
