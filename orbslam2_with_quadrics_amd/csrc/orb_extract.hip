@@ -247,21 +247,23 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
 
 // 4 horizontally adjacent outputs of one row from two LDS source rows: sx = byte offsets in the rows, weights
 // (a0, a1) per column (a1 = 0 at the right border), vertical weights (yz, yw)
-// min(t, 255) into byte k of `packed`, the other bytes preserved (SDWA dst_sel: no shift-or per byte)
-__device__ __forceinline__ void og_rz_put_byte(uint32_t& packed, uint32_t t, int k)
+// (s >> 2) into byte k of `packed`, the other bytes preserved (one SDWA shift; byte 0 clears the rest).  For the FX = false form's sums
+// s = t0 + t1 + 2 the result is <= 255 without a clamp: both weight pairs sum to <= 2049 (two cvRound of
+// complementary products, og_plan_tables), so x = d >> 4 <= 2049 * 255 / 16 and t0 + t1 <= 2049 * x / 2^16 < 1021
+__device__ __forceinline__ void og_rz_put_shr2(uint32_t& packed, uint32_t s, int k)
 {
-    if (k == 0)
-        __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                : "+v"(packed) : "v"(t), "s"(255u));
+    if (k == 0)  // (the first byte zeroes the others: `packed` needs no initial value)
+        __asm__("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD"
+                : "=v"(packed) : "v"(s), "s"(2u));
     else if (k == 1)
-        __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                : "+v"(packed) : "v"(t), "s"(255u));
+        __asm__("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                : "+v"(packed) : "v"(s), "s"(2u));
     else if (k == 2)
-        __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                : "+v"(packed) : "v"(t), "s"(255u));
+        __asm__("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                : "+v"(packed) : "v"(s), "s"(2u));
     else
-        __asm__("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                : "+v"(packed) : "v"(t), "s"(255u));
+        __asm__("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                : "+v"(packed) : "v"(s), "s"(2u));
 }
 
 template <bool FX>
@@ -275,8 +277,8 @@ __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t*
         const uint32_t p1 = (uint32_t)R1[sx[k]] | ((uint32_t)R1[sx[k] + 1] << 16);
         const uint32_t d0 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[k], 0u, false);
         const uint32_t d1 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[k], 0u, false);
-        if (!FX)  // og_rz_vert16 up to its final min, which writes byte k of `packed`
-            og_rz_put_byte(packed, (og_mulhi_u24(yz << 8, d0 & ~0xffu) + og_mulhi_u24(yw << 8, d1 & ~0xffu) + 2u) >> 2, k);
+        if (!FX)  // og_rz_vert16 (its clamp never binds, og_rz_put_shr2): the final shift writes byte k of `packed`
+            og_rz_put_shr2(packed, og_mulhi_u24(yz << 8, d0 & ~0xffu) + og_mulhi_u24(yw << 8, d1 & ~0xffu) + 2u, k);
         else
             packed |= og_rz_vert16<FX>(yz, d0, yw, d1) << (8 * k);
     }
@@ -458,8 +460,7 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             if (MH)
-                packed |= min((og_mulhi_u24((unsigned)yt.z << 8, h0[k]) + og_mulhi_u24((unsigned)yt.w << 8, h1[k]) + 2u) >> 2,
-                              255u) << (8 * k);
+                og_rz_put_shr2(packed, og_mulhi_u24((unsigned)yt.z << 8, h0[k]) + og_mulhi_u24((unsigned)yt.w << 8, h1[k]) + 2u, k);
             else
                 packed |= og_rz_vert<FX>((unsigned)yt.z, h0[k], (unsigned)yt.w, h1[k]) << (8 * k);
         }
