@@ -1282,54 +1282,29 @@ __device__ __forceinline__ void og_wave_max32(unsigned* ctr, int addr, unsigned 
     if (act && nxt != a) atomicMax(&ctr[addr], x);
 }
 
-// atomicAdd(&ctr[addr], 1) for every active lane, one LDS atomic per DISTINCT address of the wave: the
-// wave's keys are consecutive FAST outputs (one block's corners), so they fall into few nodes and plain
-// atomics would serialise on the same counters.  Wave-uniform control flow; exact counts.
-#ifndef OCT_WC_IT
-#define OCT_WC_IT 2  // distinct counter addresses per wave aggregated by ballots before plain atomics
-#endif
-#ifndef OCT_WC_RUNS
-#define OCT_WC_RUNS 1  // 0: ballot aggregation over the OCT_WC_IT most common addresses, then atomics
-#endif
+// atomicAdd(&ctr[addr], 1) for every active lane, one LDS atomic per run of equal addresses among the active lanes:
+// the wave's keys are consecutive FAST outputs (one block's corners), so neighbours share nodes and plain atomics
+// would serialise on the same counters.  The first lane of each run adds the run's length.  Wave-uniform control
+// flow; exact counts.  (The round-3 form, ballots over the two most common addresses and then plain atomics, is in
+// git history.)
 __device__ __forceinline__ void og_wave_count(int* ctr, int addr, bool act)
 {
-#if OCT_WC_RUNS
-    // runs of equal addresses among the active lanes (keys arrive in candidate order, so neighbours share
-    // nodes): the first lane of each run adds the run's length -- one atomic per run
-    {
-        const int lane = threadIdx.x & 63;
-        const int a = act ? addr : -1;
-        const int prev = __builtin_amdgcn_update_dpp(-1, a, 0x138, 0xf, 0xf, false);  // wave_shr:1 (lane - 1)
-        const bool head = act && (lane == 0 || prev != a);
-        const u64 heads = og_ballot(head);
-        const u64 actm = og_ballot(act);
-        if (head) {
-            const u64 after = lane == 63 ? 0ull : (heads >> (lane + 1)) << (lane + 1);
-            const int end = after ? __builtin_ctzll(after) : 64;  // next head (or past the wave)
-            const u64 span = (end == 64 ? ~0ull : ((1ull << end) - 1ull)) & ~((1ull << lane) - 1ull);
-            atomicAdd(&ctr[addr], (int)__popcll(actm & span));
-        }
-        return;
-    }
-#endif
-    u64 rem = og_ballot(act);
     const int lane = threadIdx.x & 63;
-    // the two most common addresses of the wave are counted by one atomic each; lanes with any other
-    // address (a wave spread over many nodes) fall back to plain atomics
-#pragma unroll
-    for (int it = 0; it < OCT_WC_IT && rem; it++) {
-        const int ld = __builtin_ctzll(rem);
-        const int a = __builtin_amdgcn_readlane(addr, ld);
-        const u64 m = og_ballot(act && addr == a) & rem;
-        if (lane == ld) atomicAdd(&ctr[a], (int)__popcll(m));
-        rem &= ~m;
+    const int a = act ? addr : -1;
+    const int prev = __builtin_amdgcn_update_dpp(-1, a, 0x138, 0xf, 0xf, false);  // wave_shr:1 (lane - 1)
+    const bool head = act && (lane == 0 || prev != a);
+    const u64 heads = og_ballot(head);
+    const u64 actm = og_ballot(act);
+    if (head) {
+        const u64 after = lane == 63 ? 0ull : (heads >> (lane + 1)) << (lane + 1);
+        const int end = after ? __builtin_ctzll(after) : 64;  // next head (or past the wave)
+        const u64 span = (end == 64 ? ~0ull : ((1ull << end) - 1ull)) & ~((1ull << lane) - 1ull);
+        atomicAdd(&ctr[addr], (int)__popcll(actm & span));
     }
-    if ((rem >> lane) & 1ull) atomicAdd(&ctr[addr], 1);
 }
 
-#ifndef OCT_U
-#define OCT_U 4  // candidates per thread per pass with all loads hoisted (latency batching)
-#endif
+#define OCT_U 4  // candidates per thread per pass with all loads hoisted (latency batching; 8 and 16 measured in
+                 // the table-mode count pass: profiles/sweeps/r05_ab_octree_count_unroll.txt)
 
 #ifndef OG_OCT_PROFILE
 #define OG_OCT_PROFILE 0  // l + 1: diagnostic clocks of level l (variant "octprof0", tests/test_gpu_variants.py)
