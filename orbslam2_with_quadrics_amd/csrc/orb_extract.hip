@@ -94,6 +94,25 @@ __device__ __forceinline__ uint32_t og_rz_vert16(uint32_t b0, uint32_t D0, uint3
                255u);
 }
 
+// (s >> 2) into byte k of `packed`, the other bytes preserved (one SDWA shift; byte 0 clears the rest).  For the FX = false form's sums
+// s = t0 + t1 + 2 the result is <= 255 without a clamp: both weight pairs sum to <= 2049 (two cvRound of
+// complementary products, og_plan_tables), so x = d >> 4 <= 2049 * 255 / 16 and t0 + t1 <= 2049 * x / 2^16 < 1021
+__device__ __forceinline__ void og_rz_put_shr2(uint32_t& packed, uint32_t s, int k)
+{
+    if (k == 0)  // (the first byte zeroes the others: `packed` needs no initial value)
+        __asm__("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD"
+                : "=v"(packed) : "v"(s), "s"(2u));
+    else if (k == 1)
+        __asm__("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                : "+v"(packed) : "v"(s), "s"(2u));
+    else if (k == 2)
+        __asm__("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                : "+v"(packed) : "v"(s), "s"(2u));
+    else
+        __asm__("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                : "+v"(packed) : "v"(s), "s"(2u));
+}
+
 #define RZ_NT 256
 #define RZ_TW 256                      // output columns per workgroup (64 lanes x 4)
 #define RZ_TH 16                       // output rows per workgroup (4 waves x 4 rows)
@@ -193,7 +212,8 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
             const unsigned o = (unsigned)(bp & 3);
             dwk[k] = bp >> 2;
             sel[k] = o | 0x0c00u | ((o + 1u) << 16) | 0x0c000000u;
-            wt[k] = og_rz_u16x2{(unsigned short)a0[k], (unsigned short)a1[k]};  // a1 = 0 at the right border
+            // a1 = 0 at the right border; FX = false: pre-scaled by 16 for the multiply-high form (og_rz_vert16)
+            wt[k] = og_rz_u16x2{(unsigned short)(a0[k] << (FX ? 0 : 4)), (unsigned short)(a1[k] << (FX ? 0 : 4))};
         }
 #pragma unroll
         for (int rr = 0; rr < 4; rr++) {
@@ -209,7 +229,10 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
                 const uint32_t p1 = __builtin_amdgcn_perm(R1[dwk[k] + 1], R1[dwk[k]], sel[k]);
                 const uint32_t d0 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[k], 0u, false);
                 const uint32_t d1 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[k], 0u, false);
-                packed |= og_rz_vert<FX>((unsigned)yt.z, d0, (unsigned)yt.w, d1) << (8 * k);
+                if (!FX)  // og_rz_vert16 (its clamp never binds, og_rz_put_shr2)
+                    og_rz_put_shr2(packed, og_mulhi_u24((unsigned)yt.z << 8, d0 & ~0xffu) + og_mulhi_u24((unsigned)yt.w << 8, d1 & ~0xffu) + 2u, k);
+                else
+                    packed |= og_rz_vert<FX>((unsigned)yt.z, d0, (unsigned)yt.w, d1) << (8 * k);
             }
             store(r, packed);
         }
@@ -247,25 +270,6 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
 
 // 4 horizontally adjacent outputs of one row from two LDS source rows: sx = byte offsets in the rows, weights
 // (a0, a1) per column (a1 = 0 at the right border), vertical weights (yz, yw)
-// (s >> 2) into byte k of `packed`, the other bytes preserved (one SDWA shift; byte 0 clears the rest).  For the FX = false form's sums
-// s = t0 + t1 + 2 the result is <= 255 without a clamp: both weight pairs sum to <= 2049 (two cvRound of
-// complementary products, og_plan_tables), so x = d >> 4 <= 2049 * 255 / 16 and t0 + t1 <= 2049 * x / 2^16 < 1021
-__device__ __forceinline__ void og_rz_put_shr2(uint32_t& packed, uint32_t s, int k)
-{
-    if (k == 0)  // (the first byte zeroes the others: `packed` needs no initial value)
-        __asm__("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD"
-                : "=v"(packed) : "v"(s), "s"(2u));
-    else if (k == 1)
-        __asm__("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                : "+v"(packed) : "v"(s), "s"(2u));
-    else if (k == 2)
-        __asm__("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                : "+v"(packed) : "v"(s), "s"(2u));
-    else
-        __asm__("v_lshrrev_b32_sdwa %0, %2, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                : "+v"(packed) : "v"(s), "s"(2u));
-}
-
 template <bool FX>
 __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t* R1, const int* sx,
                                                const og_rz_u16x2* wt, unsigned yz, unsigned yw)
