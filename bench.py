@@ -11,7 +11,7 @@ One step = one batch of B synthetic 1920x1080 frames already resident in HBM, pe
     stream-ordered against the next step's count copies (no host synchronisation beyond the per-step one).
 Frames are independent, so N GPUs run N frame shards ("scaling": "weak"; value = all frames / max time).
 Within a GPU the B frames are split over S extractor contexts (--streams, one HIP stream each) whose
-kernels run concurrently.
+kernels run concurrently (default: 1 context, 2 for the tracking workload, DEFAULT_STREAMS).
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--streams S]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -940,6 +940,10 @@ def setup_tracking(args, env):
 WORKLOADS = {"mono_init": setup_mono_init, "extract": setup_extract, "stereo": setup_stereo, "tracking": setup_tracking}
 DEFAULT_SHAPE = {"mono_init": (1080, 1920, 2000), "extract": (480, 640, 1000), "stereo": (376, 1241, 2000),
                  "tracking": (1080, 1920, 4000)}
+# extractor contexts (HIP streams) per GPU by default: the faster of 1 and 2 per workload on MI355X, alternated A/B
+# runs (profiles/sweeps/r05_streams_all.txt: one stream +0.2-1.2 % at config 3, +1.8 % at config 4, equal at config
+# 2, -0.5 % at config 5)
+DEFAULT_STREAMS = {"mono_init": 1, "extract": 1, "stereo": 1, "tracking": 2}
 
 
 def cpu_baseline_extract(rows, cols, nfeat, seconds):
@@ -978,7 +982,8 @@ def main():
     ap.add_argument("--steps", type=int, default=500)  # ~5 s timed: long enough for outside GPU-busy sampling
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512, help="frames (pairs) per step per GPU")
-    ap.add_argument("--streams", type=int, default=2, help="concurrent extractor contexts (HIP streams) per GPU")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="concurrent extractor contexts (HIP streams) per GPU (default per workload, DEFAULT_STREAMS)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="mono_init",
                     help="mono_init = BASELINE.json's config 3 (the headline metric); extract = config 2; "
                          "stereo = config 4; tracking = config 5")
@@ -1005,6 +1010,8 @@ def main():
                     help="PMC per-stage summary (tools/pmc_summary.py) the roofline's traffic comes from; default "
                          "profiles/pmc_latest.json (mono_init) or profiles/pmc_latest_<workload>.json")
     args = ap.parse_args()
+    if args.streams is None:
+        args.streams = DEFAULT_STREAMS[args.workload]
     if args.chunks is None:
         args.chunks = 8 if args.host_io else 1
     r0, c0, n0 = DEFAULT_SHAPE[args.workload]
