@@ -3,7 +3,7 @@
 # arguments: uninstrumented timed loop + instrumented pass + CPU baseline), single-frame latency, the FAST phase
 # profile (fastprof variant), a 2-rank gloo rehearsal of config 3 on the one GPU, and a streams sweep
 set -e
-O=gpurun_out/final8
+O=gpurun_out/final9
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
