@@ -50,6 +50,61 @@ def dist_env():
     return world, rank, local
 
 
+def free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def plan_launch(gpus, environ, argv, port=None, python=None):
+    """How this process runs `bench.py --gpus N` (decided before torch is imported or any HIP call is made):
+      ("run", N)     -- this process is one of the N ranks: WORLD_SIZE is set by torch.distributed.run and equals N
+                        (or --gpus was not given), or N == 1 without WORLD_SIZE;
+      ("spawn", cmd) -- N > 1 and no WORLD_SIZE: start N ranks as `python -m torch.distributed.run` on this node, one
+                        process per GPU, as a child process (this one never touches the GPU and never execs);
+    and SystemExit when WORLD_SIZE and --gpus disagree."""
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if gpus is not None and int(ws) != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws} (launched with {ws} ranks); "
+                             f"pass --gpus {ws} or launch {gpus} ranks")
+        return "run", int(ws)
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n} must be >= 1")
+    if n == 1:
+        return "run", 1
+    cmd = [python or sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port if port is not None else free_port()}",
+           os.path.abspath(__file__)] + list(argv)
+    return "spawn", cmd
+
+
+def spawn_ranks(cmd) -> int:
+    """Run the N-rank job as a child process with this process's stdout/stderr (rank 0's JSON line comes through
+    unchanged); SIGTERM/SIGINT are passed on to it.  Returns its exit code."""
+    import signal
+    import subprocess
+
+    log(f"launching the ranks: {' '.join(cmd)}")
+    p = subprocess.Popen(cmd, env=dict(os.environ, ORBGPU_BENCH_LAUNCHER="bench.py --gpus"))
+
+    def fwd(sig, _frame):
+        p.send_signal(sig)
+
+    old = {s: signal.signal(s, fwd) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        rc = p.wait()
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    return rc
+
+
 def dist_init(world: int, backend: str):
     if world <= 1:
         return None
@@ -978,7 +1033,9 @@ def cpu_baseline_stereo(rows, cols, nfeat, seconds):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks, one process per GPU) on this node; N > 1 without torch.distributed.run's "
+                         "WORLD_SIZE starts the N ranks itself (plan_launch); default WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=500)  # ~5 s timed: long enough for outside GPU-busy sampling
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512, help="frames (pairs) per step per GPU")
@@ -1010,6 +1067,9 @@ def main():
                     help="PMC per-stage summary (tools/pmc_summary.py) the roofline's traffic comes from; default "
                          "profiles/pmc_latest.json (mono_init) or profiles/pmc_latest_<workload>.json")
     args = ap.parse_args()
+    how, what = plan_launch(args.gpus, os.environ, sys.argv[1:])
+    if how == "spawn":  # before `import torch`: this process stays off the GPU
+        sys.exit(spawn_ranks(what))
     if args.streams is None:
         args.streams = DEFAULT_STREAMS[args.workload]
     if args.chunks is None:
@@ -1203,6 +1263,11 @@ def main():
             "valu": valu,
         },
         "parity": parity,
+        # what the collectives ran on: the process group's own world size (RCCL = backend "nccl" on ROCm)
+        "collective": {"backend": dist.get_backend() if dist is not None else None,
+                       "world_size": dist.get_world_size() if dist is not None else 1,
+                       "launcher": os.environ.get("ORBGPU_BENCH_LAUNCHER",
+                                                  "torch.distributed.run" if world > 1 else "single process")},
         "stages_ms_per_launch": {k: round(v, 4) for k, v in stages.items()},
         "stages_busy_ms_per_step": {k: round(v / n_inst, 4) for k, v in union_acc.items()},
         # the pass the stages and the roofline's launch time come from (HIP-event stage timing on; not `value`)

@@ -2872,12 +2872,16 @@ __device__ __forceinline__ void og_sort_cell(T* SI, int b, int e)
 }
 #define GRID_NT 1024
 // one 1024-thread workgroup per frame, everything in LDS (~72 KB): each keypoint's cell is computed once (kept in
-// cellOf), counted, scanned, scattered into LDS, and the per-cell insertion sort restores index order
+// cellOf), counted, scanned, scattered into LDS, and the per-cell insertion sort restores index order.
+// record_refused (the extraction's grid launch only): frame 0 now holds an extracted frame, so the context's
+// "frame 0 came from a refused record" word (status[1], og_record_check_kernel) is cleared
 __global__ __launch_bounds__(GRID_NT) void og_grid_kernel(const orbgpu_kp_dev* __restrict__ kps,
                                                           const int* __restrict__ counts, int frame_cap,
                                                           OgGridGeom G, int* __restrict__ cell_start,
-                                                          int* __restrict__ cell_items, int* __restrict__ status)
+                                                          int* __restrict__ cell_items, int* __restrict__ status,
+                                                          int* __restrict__ record_refused)
 {
+    if (record_refused && blockIdx.x == 0 && threadIdx.x == 0) *record_refused = 0;
     __shared__ int cnt[OG_GRID_CELLS + 1];
     __shared__ int wsum[32];
     __shared__ int starts[OG_GRID_CELLS + 1];
@@ -3088,8 +3092,8 @@ void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, lon
 }
 
 void og_launch_grid(hipStream_t s, const orbgpu_kp_dev* kps, const int* counts, int frame_cap, OgGridGeom G,
-                    int* cell_start, int* cell_items, int* status, int B)
+                    int* cell_start, int* cell_items, int* status, int B, int* record_refused)
 {
     hipLaunchKernelGGL(og_grid_kernel, dim3(B), dim3(GRID_NT), 0, s, kps, counts, frame_cap, G, cell_start, cell_items,
-                       status);
+                       status, record_refused);
 }

@@ -198,7 +198,9 @@ void og_launch_pack_host(hipStream_t s, const int* status, const int* counts, co
 // device so the call stays stream-ordered: every block checks the 16-byte header {count, magic, frame_cap,
 // undistortion} against the receiving plan.  A matching record's `count` keypoints, descriptors (and undistorted
 // keypoints) are copied into frame 0; a mismatch writes count 0 and raises status bit 128, which the next status
-// check reports as ORBGPU_ERR_ARG.
+// check reports as ORBGPU_ERR_ARG.  status[1] says whether frame 0 currently holds a refused record: every unpack
+// overwrites it (1 refused, 0 accepted) and every extraction clears it (og_grid_kernel), so unlike the sticky bit 128
+// it describes the frame now in the slot -- the word other contexts' matchers fold into their own status.
 // ------------------------------------------------------------------------------------------------
 #define OG_RECORD_MAGIC 0x5246474fu
 // The header and the keypoint order (levels nondecreasing, as extracted: the batched SearchForInitialization takes
@@ -228,6 +230,7 @@ __global__ __launch_bounds__(256) void og_record_check_kernel(const uint32_t* __
     if (threadIdx.x == 0) {
         const bool ok = hdr && !bad;
         counts[0] = ok ? n : 0;
+        status[1] = ok ? 0 : 1;
         if (!ok) atomicOr(status, 128);
     }
 }

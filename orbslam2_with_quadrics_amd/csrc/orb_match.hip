@@ -217,9 +217,9 @@ __global__ __launch_bounds__(INIT_NT) void og_init_resolve_kernel(
 {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    // F1 from another context: a frame record that context refused (status bit 128, og_record_check_kernel: F1 was
-    // left empty) is reported by this context's next status check too, not only as zero matches
-    if (ref_status && b == 0 && tid == 0 && (*ref_status & 128)) atomicOr(status, 128);
+    // F1 from another context whose frame 0 now holds a refused frame record (ref_status[1], og_record_check_kernel:
+    // F1 was left empty) is reported by this context's next status check too (bit 256), not only as zero matches
+    if (ref_status && b == 0 && tid == 0 && ref_status[1]) atomicOr(status, 256);
     const int n1 = F1.counts[ref];
     const int n2 = F2.counts[b];
     const int c1 = F1.frame_cap, c2 = F2.frame_cap;

@@ -662,7 +662,7 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
     timer_mark(c, "describe");
     if (c->undist) og_launch_undistort(s, c->kps.p, c->kps_un.p, c->counts.p, 0, P.frame_cap, c->und, B);
     og_launch_grid(s, kps_match(c), c->counts.p, P.frame_cap, c->grid_geom, c->cell_start.p, c->cell_items.p,
-                   c->status.p, B);
+                   c->status.p, B, c->status.p + 1);
     timer_mark(c, "grid");
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(c->done, s));
@@ -695,11 +695,16 @@ static int check_status(orbgpu_ctx* c)
     int st[4] = {0};
     HIP_TRY(c, hipMemcpyAsync(st, c->status.p, sizeof(st), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (st[0]) {  // read and clear: the flags of every launch since the last check
-        HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(st), c->stream));
+    if (st[0]) {  // read and clear: the flags of every launch since the last check (word 0 only: word 1 is frame 0's
+                  // refused-record state, owned by unpack / extraction, og_record_check_kernel)
+        HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(int), c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         if (st[0] == 128) {  // og_record_unpack_kernel: a refused frame record (a caller error, not a device guard)
             c->err = "frame record does not match this context's plan (frame_cap / undistortion) or has a bad count";
+            return ORBGPU_ERR_ARG;
+        }
+        if ((st[0] & ~128) == 256) {  // og_init_resolve_kernel: F1 is another context's frame 0 and that is a refused record
+            c->err = "the reference frame (frame 0 of the reference context) holds a refused frame record";
             return ORBGPU_ERR_ARG;
         }
         c->err = "device capacity guard tripped (status " + std::to_string(st[0]) + ")";
@@ -1020,8 +1025,8 @@ static int download_single(orbgpu_ctx* c, orbgpu_keypoint* kps, uint8_t* desc, i
     collect_timer(c);
     int hdr[2];
     std::memcpy(hdr, c->hpin, sizeof(hdr));
-    if (hdr[0]) {  // capacity guard: read and clear, as check_status
-        HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(int) * 4, c->stream));
+    if (hdr[0]) {  // capacity guard: read and clear word 0, as check_status
+        HIP_TRY(c, hipMemsetAsync(c->status.p, 0, sizeof(int), c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         c->err = "device capacity guard tripped (status " + std::to_string(hdr[0]) + ")";
         return ORBGPU_ERR_INTERNAL;

@@ -295,3 +295,46 @@ def test_interval_union():
     assert bench.interval_union([(0.0, 2.0), (1.0, 3.0)]) == 3.0
     assert bench.interval_union([(5.0, 6.0), (0.0, 1.0), (0.5, 0.75)]) == 2.0
     assert bench.interval_union([(-1.0, 1.0), (1.0, 2.0)]) == 3.0
+
+
+def test_gpus_flag_plans_the_launch():
+    """`bench.py --gpus N` runs N ranks by itself.  Without WORLD_SIZE, N > 1 starts
+    torch.distributed.run as a child (one process per GPU, 127.0.0.1 rendezvous) with the same arguments; under
+    torch.distributed.run (WORLD_SIZE set) the process is a rank; a mismatch is refused."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    argv = ["--gpus", "8", "--steps", "20", "--warmup", "2"]
+    how, cmd = bench.plan_launch(8, {}, argv, port=29511, python="/usr/bin/python3")
+    assert how == "spawn"
+    assert cmd == ["/usr/bin/python3", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+                   "--master-addr=127.0.0.1", "--master-port=29511", os.path.join(ROOT, "bench.py")] + argv
+    assert bench.plan_launch(1, {}, []) == ("run", 1)
+    assert bench.plan_launch(None, {}, []) == ("run", 1)
+    assert bench.plan_launch(8, {"WORLD_SIZE": "8"}, argv) == ("run", 8)
+    assert bench.plan_launch(None, {"WORLD_SIZE": "4"}, []) == ("run", 4)
+    with pytest.raises(SystemExit, match="WORLD_SIZE=2"):
+        bench.plan_launch(8, {"WORLD_SIZE": "2"}, argv)
+    with pytest.raises(SystemExit, match="WORLD_SIZE=8"):
+        bench.plan_launch(1, {"WORLD_SIZE": "8"}, [])
+    with pytest.raises(SystemExit, match=">= 1"):
+        bench.plan_launch(0, {}, [])
+
+
+def test_gpus_flag_spawns_ranks_without_touching_the_gpu():
+    """The real `python bench.py --gpus 2` on this GPU-less host: the parent starts two ranks through
+    torch.distributed.run, each rank gets as far as its device pick (no GPU here, so each refuses), and the parent exits
+    with the job's failing status -- the parent itself never imports torch."""
+    import subprocess
+
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("CPU-host test (on a GPU box the ranks would run the bench)")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--batch", "2", "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode != 0
+    assert "launching the ranks:" in r.stderr and "--nproc-per-node=2" in r.stderr
+    assert r.stderr.count("no GPU visible") >= 2, r.stderr[-3000:]
+    assert r.stdout == ""

@@ -1,8 +1,10 @@
-"""The headline timed path at its own shape (bench.py config 3): 1920x1080, 2000 features, 256 frames per launch on
-each of two concurrently running extractor contexts (HIP streams), SearchForInitialization of every frame against
-the initial frame.  Every one of the 512 frames is checked against the oracle's hashes of the same frame
-(tests/golden/bench_golden.json, made by tests/golden/make_golden.py from bench._frames), and frames 0, 1, 128 and
-255 of each stream field by field against a live oracle run."""
+"""The headline timed path at its own shape (bench.py config 3): 1920x1080, 2000 features, 512 frames per step --
+bench.py's default, one extractor context (HIP stream) x 512 frames per launch, and the two-context form, 2 x 256
+frames on concurrently running streams -- SearchForInitialization of every frame against the initial frame.  Every
+one of the 512 frames is checked against the oracle's hashes of the same frame (tests/golden/bench_golden.json, made
+by tests/golden/make_golden.py from bench._frames), and the first, second, middle and last frame of each launch field
+by field against a live oracle run.  Also bench.py itself: `--gpus 2` starting its own two ranks (gloo on the one
+GPU), and the secondary workloads' timed parity."""
 import hashlib
 import json
 import os
@@ -20,7 +22,8 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-def test_bench_shape_two_streams_b256(gpu, oracle):
+@pytest.mark.parametrize("S,Bs", [(1, 512), (2, 256)], ids=["default_1x512", "two_streams_2x256"])
+def test_bench_shape(gpu, oracle, S, Bs):
     import ctypes as C
 
     sys.path.insert(0, ROOT)
@@ -28,7 +31,8 @@ def test_bench_shape_two_streams_b256(gpu, oracle):
     from orbslam2_with_quadrics_amd import _lib, synthetic
     from orbslam2_with_quadrics_amd.extractor import KP_DTYPE
 
-    rows, cols, NF, S, Bs = 1080, 1920, 2000, 2, 256
+    rows, cols, NF = 1080, 1920, 2000
+    assert S == bench.DEFAULT_STREAMS["mono_init"] or S == 2
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_golden.json")))["ranks"][0]
     f1, frames = bench._frames(synthetic, rows, cols, S * Bs, 0)
     L = _lib.lib()
@@ -78,7 +82,7 @@ def test_bench_shape_two_streams_b256(gpu, oracle):
                 if not (_sha(k) == gf["kps_sha256"] and _sha(d) == gf["desc_sha256"] and NM[b] == gf["nmatches"]
                         and _sha(m) == gf["matches12_sha256"] and _sha(p) == gf["prev_sha256"]):
                     bad.append((s, b))
-                if b in (0, 1, 128, 255):  # field by field against the live oracle
+                if b in (0, 1, Bs // 2, Bs - 1):  # field by field against the live oracle
                     ko, do = oe(frames[s * Bs + b])
                     assert len(k) == len(ko)
                     for f in FIELDS:
@@ -148,3 +152,25 @@ def test_bench_workload_timed_parity(gpu, workload):
     line = json.loads(out.stdout.strip().splitlines()[-1])
     assert line["parity"]["status"] == "checked", line["parity"]
     assert line["parity"]["frames"] > 0 and line["parity"]["mismatches"] == 0, (line["parity"], out.stderr[-1000:])
+
+
+def test_bench_gpus2_starts_its_own_ranks(gpu):
+    """`python bench.py --gpus 2` (no torch.distributed.run around it) starts two ranks itself and
+    reports n_gpus 2, both ranks' step times, the process group's world size, and the timed path's parity over both
+    ranks' frames (each rank's own frames against its own oracle goldens).  gloo stands in for RCCL, so the two ranks
+    can share the one GPU of the test box."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    env["ORBGPU_BENCH_BACKEND"] = "gloo"
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "8", "--steps", "2",
+                          "--warmup", "1"], capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2
+    assert len(line["per_rank_ms_per_step"]) == 2
+    assert line["collective"] == {"backend": "gloo", "world_size": 2, "launcher": "bench.py --gpus"}
+    p = line["parity"]
+    assert p["status"] == "checked" and p["ranks"] == 2 and p["ranks_checked"] == 2, p
+    assert p["frames"] == 2 * 9 and p["mismatches"] == 0, p
+    assert line["value"] == pytest.approx(2 * 8 * 2 / (line["ms_per_step"] * 2e-3), rel=0.01)

@@ -104,3 +104,66 @@ def test_refused_record_is_reported_by_the_cross_context_matcher(gpu):
     assert b"frame record" in L.orbgpu_last_error(cur.ctx)
     assert int(nm.item()) == 0
     assert L.orbgpu_synchronize(ref.ctx) == _lib.ERR_ARG  # the receiving context reports it as well
+
+
+def test_cross_context_fold_follows_the_frame_now_in_the_slot(gpu):
+    """the fold reads a per-frame refusal word that every unpack of frame 0 overwrites and every
+    extraction clears (status[1]), not the sticky status bit 128.  A refused unpack followed by a good unpack -- or by a
+    fresh extraction -- leaves a valid F1, and a batch match on another context against it returns OK with matches,
+    although the reference context's own status still reports the earlier refusal (bit 128, read and cleared once)."""
+    import torch
+
+    from orbslam2_with_quadrics_amd import _lib, synthetic
+
+    L = _lib.lib()
+    f1, f2 = synthetic.frame_pair(32, 480, 640)
+    ref = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    cur = gpu.ORBextractor(1000, 1.2, 8, 20, 7)
+    ref(f1)
+    cur(f2)
+    cap = int(L.orbgpu_max_keypoints(ref.ctx))
+    prev = torch.zeros(2 * cap, dtype=torch.float32, device="cuda:0")
+    m12 = torch.zeros(cap, dtype=torch.int32, device="cuda:0")
+    nm = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    g = _lib.GridGeom()
+    _lib.check(cur.ctx, L.orbgpu_grid_geom_for_image(640, 480, C.byref(g)), "grid")
+    rec = torch.zeros(int(L.orbgpu_frame_record_bytes(ref.ctx)), dtype=torch.uint8, device="cuda:0")
+    _lib.check(ref.ctx, L.orbgpu_frame_record_pack(ref.ctx, 0, C.c_void_p(rec.data_ptr())), "pack")
+    zero = torch.zeros_like(rec)
+    d_f1 = ref.device_alloc(f1.nbytes)
+    ref.h2d(d_f1, f1)
+
+    def match():
+        _lib.check(cur.ctx, L.orbgpu_prev_matched_from_frame(ref.ctx, 0, cur.ctx, C.c_void_p(prev.data_ptr())), "prev")
+        _lib.check(cur.ctx, L.orbgpu_search_for_initialization_batch(
+            ref.ctx, 0, cur.ctx, g, 0.9, 1, 100, C.c_void_p(prev.data_ptr()), C.c_void_p(m12.data_ptr()),
+            C.c_void_p(nm.data_ptr())), "init")
+
+    try:
+        match()
+        assert L.orbgpu_synchronize(cur.ctx) == _lib.OK
+        n_good = int(nm.item())
+        assert n_good > 50
+        # refused, then a good record: F1 is valid again
+        assert L.orbgpu_frame_record_unpack(ref.ctx, C.c_void_p(zero.data_ptr())) == _lib.OK
+        assert L.orbgpu_frame_record_unpack(ref.ctx, C.c_void_p(rec.data_ptr())) == _lib.OK
+        match()
+        assert L.orbgpu_synchronize(cur.ctx) == _lib.OK, L.orbgpu_last_error(cur.ctx)
+        assert int(nm.item()) == n_good
+        # refused, then a fresh extraction of frame 0: F1 is valid again
+        assert L.orbgpu_frame_record_unpack(ref.ctx, C.c_void_p(zero.data_ptr())) == _lib.OK
+        ref.extract_batch_device(d_f1, 1, 640, 480, 640, f1.nbytes)
+        match()
+        assert L.orbgpu_synchronize(cur.ctx) == _lib.OK, L.orbgpu_last_error(cur.ctx)
+        assert int(nm.item()) == n_good
+        # the reference context's own check still reports its refusals (read and cleared once)
+        assert L.orbgpu_synchronize(ref.ctx) == _lib.ERR_ARG
+        assert L.orbgpu_synchronize(ref.ctx) == _lib.OK
+        # and a refused record in the slot now is still folded, with the cross-context message
+        assert L.orbgpu_frame_record_unpack(ref.ctx, C.c_void_p(zero.data_ptr())) == _lib.OK
+        match()
+        assert L.orbgpu_synchronize(cur.ctx) == _lib.ERR_ARG
+        assert b"reference frame" in L.orbgpu_last_error(cur.ctx)
+        assert int(nm.item()) == 0
+    finally:
+        ref.device_free(d_f1)
