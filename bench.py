@@ -211,8 +211,8 @@ def stage_bytes(stage, B, P, cand_total, kp_total, mappoints=0):
     """Algorithmic HBM bytes of one launch of `stage` for a batch of B frames."""
     if stage == "pyramid":  # read levels 0..L-2, write levels 1..L-1
         return B * (sum(P[:-1]) + sum(P[1:]))
-    if stage == "fast":  # every pyramid pixel once + packed candidates written
-        return B * sum(P) + 8 * cand_total
+    if stage == "fast":  # every pyramid pixel once (SURVEY.md §8(d)); the candidates it writes: candidate_bytes
+        return B * sum(P)
     if stage == "octree":  # candidates read once + 5 B per selected keypoint written
         return 8 * cand_total + 5 * kp_total
     if stage == "describe":  # 43x43 raw neighbourhood per keypoint + 28 B keypoint + 32 B descriptor
@@ -229,6 +229,38 @@ def stage_bytes(stage, B, P, cand_total, kp_total, mappoints=0):
         # each left keypoint, uRight / depth / SAD out (kp_total = left keypoints; right ones taken as many)
         return kp_total * (2 * 60 + 121 + 231 + 12)
     return 0
+
+
+def candidate_bytes(stage, cand_total):
+    """Bytes a launch writes beside stage_bytes' algorithmic ones: FAST's packed candidates, 8 B each (reported beside
+    the roofline, not in it)."""
+    return 8 * cand_total if stage == "fast" else 0
+
+
+def roofline_record(dom, dom_bytes, cand_bytes, dom_ms, dom_ms_span, traffic, valu):
+    """The bench line's roofline object.  `bound` names the resource that binds the dominant kernel: the VALU issue
+    pipe when the PMC VALU count is known (the FAST / resize / describe kernels issue ~0.84 of the pipe's 4-cycle
+    slots while reading HBM at < 0.1 of its peak), and then `achieved` / `peak` / `frac` are VALU
+    wave-instruction issue rates; the HBM figure (SURVEY.md §8(d) algorithmic bytes / launch time against 8 TB/s, and
+    the PMC traffic) is always given under `hbm`.  Without PMC data the HBM figure is the top level."""
+    ach = dom_bytes / (dom_ms * 1e-3) / 1e9
+    hbm = {"achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
+           "traffic": traffic, "algorithmic_bytes_per_launch": int(dom_bytes),
+           "candidate_bytes_per_launch": int(cand_bytes),
+           "traffic_over_algorithmic": round(traffic / dom_bytes, 3) if traffic and dom_bytes else None,
+           "bytes": "SURVEY.md §8(d): every pyramid pixel once for FAST (candidate writes reported separately)"}
+    out = {"kernel": dom, "avg_launch_ms": round(dom_ms, 4), "avg_launch_span_ms": round(dom_ms_span, 4),
+           "launch_time": "union of the kernel's HIP-event intervals over the concurrent streams / launches"}
+    if valu is not None:
+        peak = VALU_SIMDS * VALU_CLK_HZ / 4 / 1e9  # G wave-instructions/s when every instruction is a 4-cycle form
+        rate = valu["insts_per_launch"] / (dom_ms * 1e-3) / 1e9
+        out.update(bound="valu", achieved=round(rate, 2), peak=round(peak, 1),
+                   unit="G VALU wave-instructions/s (4-cycle issue: 1024 SIMDs x 2.4 GHz / 4)",
+                   frac=round(rate / peak, 4), traffic=traffic, valu=valu, hbm=hbm)
+    else:
+        out.update(bound="hbm", achieved=hbm["achieved"], peak=HBM_PEAK_GBS, unit="GB/s", frac=hbm["frac"],
+                   traffic=traffic, valu=None, hbm=hbm)
+    return out
 
 
 def interval_union(iv):
@@ -1191,7 +1223,6 @@ def main():
     dom_ms = union_acc[dom] / max(launches, 1)
     dom_ms_span = kernels[dom]
     dom_bytes = stage_bytes(dom, Bs, P, cand_total, kp_total, args.mappoints)
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
     valu = None
     pmc_json = args.pmc_json or os.path.join(ROOT, "profiles", "pmc_latest.json" if args.workload == "mono_init"
@@ -1248,20 +1279,8 @@ def main():
             "parallelism": f"frame-sharded x{world} GPUs, {S} streams per GPU (RCCL all-gather of keypoint "
                            f"counts only)",
         }, **extra),
-        "roofline": {
-            "bound": "hbm",
-            "kernel": dom,
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": int(dom_bytes),
-            "avg_launch_ms": round(dom_ms, 4),
-            "avg_launch_span_ms": round(dom_ms_span, 4),
-            "launch_time": "union of the kernel's HIP-event intervals over the concurrent streams / launches",
-            "valu": valu,
-        },
+        "roofline": roofline_record(dom, dom_bytes, candidate_bytes(dom, cand_total), dom_ms, dom_ms_span, traffic,
+                                    valu),
         "parity": parity,
         # what the collectives ran on: the process group's own world size (RCCL = backend "nccl" on ROCm)
         "collective": {"backend": dist.get_backend() if dist is not None else None,

@@ -485,53 +485,21 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
 // M(p) = max over the 16 contiguous 9-arcs and both polarities of min |I(p) - I(arc)|; the pixel is a
 // FAST corner at threshold t iff M > t and then cornerScore<16> == M - 1.  Per polarity on the
 // circle values themselves: the dark score is v - A with A = min_k max_arc c, the bright one B - v with
-// B = max_k min_arc c.  og_fast_M1 computes ONE polarity: with fm = 0xff the values are complemented
-// (255 - x == x ^ 0xff), which turns the bright score into the dark form.  A survivor of the quick test at tq
+// B = max_k min_arc c.  The bright score is the dark form on complemented values, so one polarity's instructions
+// serve both.  A survivor of the quick test at tq
 // that fails one polarity's quick test has that polarity's score <= tq, and scores <= tq never decide anything
 // (a kept corner needs M > max(t, 1) >= tq and then beats every neighbour <= tq), so the passing polarity's
 // score stands for M; the rare survivors passing both take the max of the two.  Each 9-arc [k, k+8] is the
-// max3 of the 3-arcs at k, k+3, k+6: ~40 integer ops per polarity, exact.
-template <int SX, typename E>
-__device__ __forceinline__ int og_fast_M1(const E* p, int st, int fm)
-{
-    const int v = p[0] ^ fm;
-    int c[16];
-    c[0] = p[3 * st] ^ fm;
-    c[1] = p[1 * SX + 3 * st] ^ fm;
-    c[2] = p[2 * SX + 2 * st] ^ fm;
-    c[3] = p[3 * SX + 1 * st] ^ fm;
-    c[4] = p[3 * SX] ^ fm;
-    c[5] = p[3 * SX - 1 * st] ^ fm;
-    c[6] = p[2 * SX - 2 * st] ^ fm;
-    c[7] = p[1 * SX - 3 * st] ^ fm;
-    c[8] = p[-3 * st] ^ fm;
-    c[9] = p[-1 * SX - 3 * st] ^ fm;
-    c[10] = p[-2 * SX - 2 * st] ^ fm;
-    c[11] = p[-3 * SX - 1 * st] ^ fm;
-    c[12] = p[-3 * SX] ^ fm;
-    c[13] = p[-3 * SX + 1 * st] ^ fm;
-    c[14] = p[-2 * SX + 2 * st] ^ fm;
-    c[15] = p[-1 * SX + 3 * st] ^ fm;
-    int mx3[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) mx3[k] = max(max(c[k], c[(k + 1) & 15]), c[(k + 2) & 15]);
-    int mx9[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) mx9[k] = max(max(mx3[k], mx3[(k + 3) & 15]), mx3[(k + 6) & 15]);
-    int a[6];
-#pragma unroll
-    for (int k = 0; k < 5; k++) a[k] = min(min(mx9[3 * k], mx9[3 * k + 1]), mx9[3 * k + 2]);
-    a[5] = mx9[15];
-    const int A = min(min(min(a[0], a[1]), a[2]), min(min(a[3], a[4]), a[5]));
-    return max(v - A, 0);
-}
+// max3 of the 3-arcs at k, k+3, k+6, exact.  (The scalar integer form of this score, og_fast_M1, was the reference
+// og_fast_Mpk was checked against bit for bit until round 5; it is in git history.  The CPU restatement of
+// cornerScore<16> is the checker the GPU tests hold every keypoint response to.)
 
 
 // The same score on the f16-biased quad ROI (0x6400 | pixel = the f16 value 1024 + pixel) with packed f16 ops: the
 // opposite samples (c_k, c_k+8) share a dword, so one v_pk_maximum3_f16 forms two 3-arc maxima (k and k + 8) and
 // the arcs that wrap past c_15 take the swapped halves (op_sel).  The polarity is a per-lane sign: the bright score
 // B - v = max_k min_arc(c) - v is the dark form v' - min_k max_arc(c') on c' = -c, v' = -v, so both polarities run
-// the same instructions.  All values are integers of magnitude < 2048 (exact in f16): bit-exact with og_fast_M1.
+// the same instructions.  All values are integers of magnitude < 2048 (exact in f16): exact integer arithmetic.
 // p = the centre's u16 in the quad ROI; SX = element step of one column, st = of one row.
 typedef _Float16 og_h2 __attribute__((ext_vector_type(2)));
 // base = LDS byte address of the sample 3 rows up and 3 columns left of the centre; FQ_S_ = row stride in qwords

@@ -70,6 +70,12 @@ void og_launch_grid(hipStream_t s, const orbgpu_kp_dev* kps, const int* counts, 
                     int* cell_start, int* cell_items, int* status, int B, int* record_refused = nullptr);
 
 // matchers (orb_match.hip)
+// Ordering invariant of every writer of a context's keypoint slots (kps / kps_un): a frame's keypoints are in
+// extraction order, levels nondecreasing (src/ORBextractor.cc:1076-1104), so its octave-0 keypoints are the first
+// ones and number at most kcap_0 = plan.lv[0].kcap.  The batched SearchForInitialization queries F1's keypoints
+// [0, qcap = kcap_0) only (og_init_resolve_kernel skips i >= qcap).  The writers today: the describe kernel
+// (extraction, in order by construction) and og_record_unpack_kernel (refuses a record that breaks the order, status
+// bit 128).  A future writer (host-supplied frames into a context's batch, reordering) must keep it or pass qcap = 0.
 struct OgFrameDev {        // device view of one or many frames (batch stride frame_cap)
     const orbgpu_kp_dev* kps;
     const uint8_t* desc;

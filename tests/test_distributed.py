@@ -338,3 +338,24 @@ def test_gpus_flag_spawns_ranks_without_touching_the_gpu():
     assert "launching the ranks:" in r.stderr and "--nproc-per-node=2" in r.stderr
     assert r.stderr.count("no GPU visible") >= 2, r.stderr[-3000:]
     assert r.stdout == ""
+
+
+def test_roofline_record_names_the_binding_resource():
+    """with the PMC VALU count the line's bound is the VALU pipe (frac = 4-cycle busy fraction) and
+    the HBM figure -- FAST's pixel bytes of SURVEY.md §8(d), candidates reported separately -- sits beside it."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    P = [100, 50]
+    assert bench.stage_bytes("fast", 4, P, 10, 0) == 4 * 150
+    assert bench.candidate_bytes("fast", 10) == 80 and bench.candidate_bytes("describe", 10) == 0
+    valu = {"insts_per_launch": 2_633_533_273, "busy_frac_if_4cyc": 0.8381}
+    r = bench.roofline_record("fast", 3_286_692_352, 277_000_000, 5.1146, 5.1146, 5_241_057_176, valu)
+    assert r["bound"] == "valu" and r["kernel"] == "fast"
+    assert r["frac"] == pytest.approx(0.8381, abs=2e-4)
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=1e-3)
+    assert r["hbm"]["frac"] == pytest.approx(3_286_692_352 / 5.1146e-3 / 8e12, rel=1e-4)
+    assert r["hbm"]["candidate_bytes_per_launch"] == 277_000_000
+    assert r["traffic"] == r["hbm"]["traffic"] == 5_241_057_176
+    h = bench.roofline_record("fast", 3_286_692_352, 0, 5.1146, 5.1146, None, None)
+    assert h["bound"] == "hbm" and h["frac"] == h["hbm"]["frac"] and h["unit"] == "GB/s"

@@ -98,8 +98,9 @@ def make_config(cfg):
     raise ValueError(cfg)
 
 
-def single_core(cfg, n, warm, core=0):
+def single_core(cfg, n, warm, core=None):
     prev = os.sched_getaffinity(0)
+    core = min(prev) if core is None else core  # the lowest core this process may use (a box's cpuset may lack 0)
     os.sched_setaffinity(0, {core})
     try:
         work, frame, desc = make_config(cfg)
@@ -111,9 +112,11 @@ def single_core(cfg, n, warm, core=0):
             t = time.perf_counter()
             work(f)
             ts.append(time.perf_counter() - t)
+            if len(ts) % 50 == 0:
+                print(f"config {cfg}: {len(ts)}/{n} frames on core {core}", file=sys.stderr, flush=True)
     finally:
         os.sched_setaffinity(0, prev)
-    return desc, ts
+    return desc, ts, core
 
 
 def _worker(args):
@@ -150,19 +153,19 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--configs", default="2,3,4,5")
     ap.add_argument("--max-cores", type=int, default=16, help="workers of the all-cores run (the GPU box's CPU share)")
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r02_cpu_baseline.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r06_cpu_baseline.json"))
     args = ap.parse_args()
     out = {"cpu_model": cpu_model(), "nproc": os.cpu_count(), "oracle_build": "gcc -O3 -march=native "
            "-ffp-contract=off (oracle/Makefile liborb_oracle_fast.so; bit-identical to the checker build)",
            "kind": "port", "caveat": "the oracle's resize / FAST / GaussianBlur are scalar C; an OpenCV SIMD build of "
            "the reference would be faster", "configs": {}}
     for cfg in [int(c) for c in args.configs.split(",")]:
-        desc, ts = single_core(cfg, args.frames, args.warmup)
+        desc, ts, core = single_core(cfg, args.frames, args.warmup)
         med = statistics.median(ts)
         entry = {"workload": desc, "single_core": {"frames": len(ts), "warmup": args.warmup,
                                                   "median_ms": round(med * 1e3, 3),
                                                   "mean_ms": round(statistics.mean(ts) * 1e3, 3),
-                                                  "frames_per_s_median": round(1 / med, 3), "pinned_core": 0}}
+                                                  "frames_per_s_median": round(1 / med, 3), "pinned_core": core}}
         entry["all_cores"] = all_cores(cfg, args.frames, args.max_cores)
         out["configs"][str(cfg)] = entry
         print(cfg, json.dumps(entry), flush=True)

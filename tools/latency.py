@@ -43,10 +43,13 @@ def main():
     n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else 300
     L = _lib.lib()
     vp = C.c_void_p
-    out = {"note": "milliseconds per frame; one frame at a time (Frame::ExtractORB call pattern)"}
+    out = {"note": "milliseconds per frame; one frame at a time (Frame::ExtractORB call pattern)",
+           "graph_replay": os.environ.get("ORBGPU_GRAPH", "default")}
+    keep = []  # every context lives to the end (as a SLAM process's extractors do)
     for rows, cols, nf in ((480, 640, 1000), (375, 1242, 2000), (1080, 1920, 2000)):
         img = np.ascontiguousarray(synthetic.frame(3, rows, cols))
         ex = ORBextractor(nf, 1.2, 8, 20, 7)
+        keep.append(ex)
         cap = L.orbgpu_max_keypoints(ex.ctx)
         kps = np.zeros(cap, KP_DTYPE)
         desc = np.zeros((cap, 32), np.uint8)

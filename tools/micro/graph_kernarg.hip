@@ -1,0 +1,128 @@
+// HIP-graph replay probe (test infrastructure): does replaying a long-lived graph exec still
+// launch its kernels with the arguments it was captured with after OTHER graph execs were instantiated, launched and
+// destroyed in between?  That is the sequence under which the round-5 small-batch graph replay faulted
+// (profiles/sweeps/r05_small_batch_graph_replay_tests.log: ex1000's replay after test_odd_and_small_shapes' contexts
+// captured, replayed and destroyed theirs).
+//
+// Every buffer stays allocated until the end, so a replay that runs with another exec's arguments writes into that
+// exec's (live) buffer instead of faulting: the probe counts such writes.  Each graph mimics run_batch's launch
+// sequence: a memset node, then 15 kernel nodes alternating a small argument list and a ~1.5 KB by-value struct
+// (OgPlan is passed by value to the octree and describe kernels).
+//   build: hipcc --offload-arch=gfx950 -O2 -o tools/micro/graph_kernarg tools/micro/graph_kernarg.hip
+//   run:   tools/micro/graph_kernarg [rounds]    (prints one JSON line)
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                                   \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess) {                                                                 \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            std::exit(2);                                                                       \
+        }                                                                                       \
+    } while (0)
+
+struct Big {
+    long long w[190];  // 1520 bytes, like a by-value plan
+};
+
+constexpr int NK = 15, SLOTS = 64;
+
+__global__ void k_small(int* p, int slot, int tag)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0) p[slot] = tag;
+}
+
+__global__ void k_big(int* p, int slot, Big b)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0) p[slot] = (int)b.w[slot % 190];
+}
+
+// capture the launch sequence of one "context" writing tags base + i into buf
+static hipGraphExec_t capture(hipStream_t s, int* buf, int base)
+{
+    Big b;
+    for (int i = 0; i < 190; i++) b.w[i] = base + i;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    CK(hipMemsetAsync(buf, 0, sizeof(int) * SLOTS, s));
+    for (int i = 0; i < NK; i++) {
+        if (i & 1)
+            hipLaunchKernelGGL(k_big, dim3(4), dim3(64), 0, s, buf, i, b);
+        else
+            hipLaunchKernelGGL(k_small, dim3(4), dim3(64), 0, s, buf, i, base + i);
+    }
+    hipGraph_t g = nullptr;
+    CK(hipStreamEndCapture(s, &g));
+    hipGraphExec_t x = nullptr;
+    CK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+    CK(hipGraphDestroy(g));
+    return x;
+}
+
+// the tags a correct replay of `base`'s graph leaves in its buffer
+static bool expected(const int* h, int base)
+{
+    for (int i = 0; i < NK; i++)
+        if (h[i] != base + i) return false;
+    for (int i = NK; i < SLOTS; i++)
+        if (h[i] != 0) return false;
+    return true;
+}
+
+int main(int argc, char** argv)
+{
+    const int rounds = argc > 1 ? std::atoi(argv[1]) : 64;
+    hipStream_t sA, sL;
+    CK(hipStreamCreateWithFlags(&sA, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&sL, hipStreamNonBlocking));
+    int *bufA, *bufL;
+    CK(hipMalloc(&bufA, sizeof(int) * SLOTS));
+    CK(hipMalloc(&bufL, sizeof(int) * SLOTS));
+    std::vector<int*> bufT(rounds);
+    for (auto& p : bufT) CK(hipMalloc(&p, sizeof(int) * SLOTS));
+    // two long-lived execs (ex1000's and ex2000's), captured first
+    hipGraphExec_t xA = capture(sA, bufA, 1000);
+    hipGraphExec_t xL = capture(sL, bufL, 2000);
+    std::vector<int> h(SLOTS);
+    int bad_replays = 0, foreign_writes = 0, bad_transient = 0;
+    for (int r = 0; r < rounds; r++) {
+        // a transient context: own stream and graph, launched twice, then (stream synchronised) destroyed
+        hipStream_t sT;
+        CK(hipStreamCreateWithFlags(&sT, hipStreamNonBlocking));
+        hipGraphExec_t xT = capture(sT, bufT[r], 10000 + 100 * r);
+        CK(hipGraphLaunch(xT, sT));
+        CK(hipGraphLaunch(xT, sT));
+        CK(hipStreamSynchronize(sT));
+        CK(hipMemcpy(h.data(), bufT[r], sizeof(int) * SLOTS, hipMemcpyDeviceToHost));
+        bad_transient += !expected(h.data(), 10000 + 100 * r);
+        CK(hipGraphExecDestroy(xT));
+        CK(hipStreamDestroy(sT));
+        // every transient buffer cleared, then the long-lived execs replayed
+        for (int q = 0; q <= r; q++) CK(hipMemset(bufT[q], 0, sizeof(int) * SLOTS));
+        CK(hipMemset(bufA, 0, sizeof(int) * SLOTS));
+        CK(hipMemset(bufL, 0, sizeof(int) * SLOTS));
+        CK(hipDeviceSynchronize());
+        CK(hipGraphLaunch(xA, sA));
+        CK(hipGraphLaunch(xL, sL));
+        CK(hipStreamSynchronize(sA));
+        CK(hipStreamSynchronize(sL));
+        CK(hipMemcpy(h.data(), bufA, sizeof(int) * SLOTS, hipMemcpyDeviceToHost));
+        bad_replays += !expected(h.data(), 1000);
+        CK(hipMemcpy(h.data(), bufL, sizeof(int) * SLOTS, hipMemcpyDeviceToHost));
+        bad_replays += !expected(h.data(), 2000);
+        for (int q = 0; q <= r; q++) {
+            CK(hipMemcpy(h.data(), bufT[q], sizeof(int) * SLOTS, hipMemcpyDeviceToHost));
+            for (int i = 0; i < SLOTS; i++) foreign_writes += h[i] != 0;
+        }
+    }
+    const char* pc = std::getenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE");
+    std::printf("{\"rounds\": %d, \"kernel_nodes\": %d, \"bad_long_lived_replays\": %d, \"writes_into_destroyed_execs_"
+                "buffers\": %d, \"bad_transient_replays\": %d, \"DEBUG_CLR_GRAPH_PACKET_CAPTURE\": \"%s\"}\n",
+                rounds, NK, bad_replays, foreign_writes, bad_transient, pc ? pc : "(default)");
+    CK(hipGraphExecDestroy(xA));
+    CK(hipGraphExecDestroy(xL));
+    return bad_replays || foreign_writes || bad_transient ? 1 : 0;
+}
