@@ -543,21 +543,30 @@ static void timer_begin(orbgpu_ctx* c)
 }
 // ORBGPU_DEBUG_SYNC=1 (diagnostics only): synchronise after every stage and report the first stage whose
 // kernels failed, so a device fault names its kernel instead of surfacing at the next unrelated sync
-static bool debug_sync()
+// (ORBGPU_DEBUG_SYNC=2 also prints every stage as it completes: a hang names the stage that never does)
+static int debug_sync_level()
 {
-    static const int on = [] {
+    static const int lv = [] {
         const char* e = std::getenv("ORBGPU_DEBUG_SYNC");
-        return e && e[0] == '1' ? 1 : 0;
+        return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
     }();
-    return on != 0;
+    return lv;
 }
+static bool debug_sync() { return debug_sync_level() != 0; }
 
 static void timer_mark(orbgpu_ctx* c, const char* name)
 {
     if (debug_sync()) {
+        if (debug_sync_level() == 2) {
+            std::fprintf(stderr, "orbgpu: stage '%s' enqueued, synchronising\n", name);
+            std::fflush(stderr);
+        }
         const hipError_t e = hipStreamSynchronize(c->stream);
         if (e != hipSuccess) {
             std::fprintf(stderr, "orbgpu: stage '%s' failed: %s\n", name, hipGetErrorString(e));
+            std::fflush(stderr);
+        } else if (debug_sync_level() == 2) {
+            std::fprintf(stderr, "orbgpu: stage '%s' done\n", name);
             std::fflush(stderr);
         }
     }

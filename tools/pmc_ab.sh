@@ -17,7 +17,7 @@ for name in "$@"; do
       rocprofv3 --pmc $grp --output-format csv -d "$ROOT/$OUT/$name/p$i" -o pmc -- python3 "$ROOT/bench.py" \
       --steps 3 --warmup 1 --no-cpu-baseline > "$ROOT/$OUT/$name/p$i.json" 2> "$ROOT/$OUT/$name/p$i.err")
   done
-  python3 tools/pmc_summary.py "$OUT/$name" --json "$OUT/$name.json" --batch 256 > /dev/null
+  python3 tools/pmc_summary.py "$OUT/$name" --json "$OUT/$name.json" --batch ${PMC_BATCH:-512} > /dev/null
   python3 -c "
 import json,sys; k=json.load(open('$OUT/$name.json'))['kernels']['fast']
 print('$name', ' '.join('%s=%.4g' % (c, k[c]) for c in ('SQ_WAVES','SQ_INSTS_VALU','SQ_INSTS_SALU','SQ_INSTS_LDS','SQ_WAVE_CYCLES','SQ_WAIT_ANY','SQ_WAIT_INST_ANY','SQ_ACTIVE_INST_ANY','SQ_LDS_BANK_CONFLICT','SQ_LDS_IDX_ACTIVE','GRBM_GUI_ACTIVE') if c in k))
