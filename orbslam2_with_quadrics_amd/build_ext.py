@@ -81,6 +81,7 @@ ENV_VARIANTS = {
     "order8": {"ORBGPU_FAST_ORDER": "8"},
     "forkall": {"ORBGPU_FORK_MIN_PIXELS": "0"},    # every small batch forks level 0 onto its own stream
     "forknone": {"ORBGPU_FORK_MIN_PIXELS": "1000000000000"},
+    "forkbatch": {"ORBGPU_FORK_MAX_B": "1024"},    # every batch forks (measured -1 % at config 3, r06)
     "debugsync": {"ORBGPU_DEBUG_SYNC": "1"},       # synchronise after every stage (diagnostics)
 }
 

@@ -633,6 +633,15 @@ static void launch_levels(orbgpu_ctx* c, hipStream_t s, int lb, int le, const ui
 // The fork and join cost more than they hide below ~1 MP (tools/latency.py: 1242x375 0.177 -> 0.211 ms forked,
 // 1920x1080 0.294 -> 0.238 ms), so only frames of at least ORBGPU_FORK_MIN_PIXELS (default 2^20) fork.
 #define OG_FORK_MAX_B 4
+// ORBGPU_FORK_MAX_B (measurement): fork batches up to this size instead (level 0's octree beside levels 1-7's FAST)
+static int fork_max_b()
+{
+    static const int v = [] {
+        const char* e = std::getenv("ORBGPU_FORK_MAX_B");
+        return e && *e ? std::atoi(e) : OG_FORK_MAX_B;
+    }();
+    return v;
+}
 static long long fork_min_pixels()
 {
     static const long long v = [] {
@@ -650,7 +659,7 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
     timer_mark(c, "start");
     HIP_TRY(c, hipMemsetAsync(c->cand_count.p, 0, sizeof(int) * (size_t)B * P.nlevels, s));
     // stage timing and the debug sync keep the serial order (their marks are stage boundaries on one stream)
-    const bool fork = B <= OG_FORK_MAX_B && P.nlevels > 1 && !c->timer.on && !debug_sync() && c->stream2 &&
+    const bool fork = B <= fork_max_b() && P.nlevels > 1 && !c->timer.on && !debug_sync() && c->stream2 &&
                       (long long)c->W * c->H >= fork_min_pixels();
     if (fork) {
         HIP_TRY(c, hipEventRecord(c->ev_fork, s));

@@ -8,12 +8,20 @@
 // exec's (live) buffer instead of faulting: the probe counts such writes.  Each graph mimics run_batch's launch
 // sequence: a memset node, then 15 kernel nodes alternating a small argument list and a ~1.5 KB by-value struct
 // (OgPlan is passed by value to the octree and describe kernels).
+// Mode "copies" (round 6): between two replays of one exec, the operations the round-5 fault needed on the same
+// context (tests/test_gpu_extract.py::test_pyramid_and_candidates: pyramid levels read back with hipMemcpy2DAsync
+// into pageable memory on the replaying stream, candidates with a synchronous hipMemcpy), each in its own round.
+// Its kernels never dereference an argument they were not captured with: each checks its pointer against the buffer
+// address kept in a device global and counts a mismatch there instead of writing, so corrupted arguments show as a
+// count, not as a fault.
 //   build: hipcc --offload-arch=gfx950 -O2 -o tools/micro/graph_kernarg tools/micro/graph_kernarg.hip
-//   run:   tools/micro/graph_kernarg [rounds]    (prints one JSON line)
+//   run:   tools/micro/graph_kernarg [rounds]           (transient execs; prints one JSON line)
+//          tools/micro/graph_kernarg copies [rounds]    (copies between replays; one JSON line per operation)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                                   \
@@ -31,14 +39,33 @@ struct Big {
 
 constexpr int NK = 15, SLOTS = 64;
 
+__device__ int* g_valid[2];   // the buffers a kernel may write (mode "copies": every other pointer is counted)
+__device__ int g_bad_args;
+
+__device__ __forceinline__ bool arg_ok(const int* p, int slot)
+{
+    if (!g_valid[0]) return slot >= 0 && slot < SLOTS;  // transient mode: every buffer stays allocated
+    return (p == g_valid[0] || p == g_valid[1]) && slot >= 0 && slot < SLOTS;
+}
+
 __global__ void k_small(int* p, int slot, int tag)
 {
-    if (threadIdx.x == 0 && blockIdx.x == 0) p[slot] = tag;
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        if (arg_ok(p, slot))
+            p[slot] = tag;
+        else
+            atomicAdd(&g_bad_args, 1);
+    }
 }
 
 __global__ void k_big(int* p, int slot, Big b)
 {
-    if (threadIdx.x == 0 && blockIdx.x == 0) p[slot] = (int)b.w[slot % 190];
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        if (arg_ok(p, slot))
+            p[slot] = (int)b.w[slot % 190];
+        else
+            atomicAdd(&g_bad_args, 1);
+    }
 }
 
 // capture the launch sequence of one "context" writing tags base + i into buf
@@ -72,8 +99,70 @@ static bool expected(const int* h, int base)
     return true;
 }
 
+// mode "copies": replay exec A, then one kind of operation on A's stream / the null stream, then replay A again
+static int copies_mode(int rounds)
+{
+    hipStream_t sA;
+    CK(hipStreamCreateWithFlags(&sA, hipStreamNonBlocking));
+    int *bufA, *dev;
+    CK(hipMalloc(&bufA, sizeof(int) * SLOTS));
+    const int W = 640, H = 480;
+    CK(hipMalloc(&dev, W * H));
+    CK(hipMemset(dev, 7, W * H));
+    int* valid[2] = {bufA, bufA};
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_valid), valid, sizeof(valid)));
+    const int zero = 0;
+    std::vector<unsigned char> host(W * H);  // pageable, as a numpy array is
+    std::vector<int> h(SLOTS);
+    hipGraphExec_t xA = capture(sA, bufA, 1000);
+    const char* names[] = {"none", "memcpy2d_d2h_pageable_on_stream", "memcpy_d2h_sync_null_stream",
+                           "memcpy_h2d_pageable_on_stream", "kernel_on_stream"};
+    int status = 0;
+    for (int op = 0; op < 5; op++) {
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_bad_args), &zero, sizeof(int)));
+        int bad_replays = 0;
+        for (int r = 0; r < rounds; r++) {
+            CK(hipGraphLaunch(xA, sA));
+            CK(hipStreamSynchronize(sA));
+            switch (op) {
+            case 1:
+                CK(hipMemcpy2DAsync(host.data(), W, dev, W, W, H, hipMemcpyDeviceToHost, sA));
+                CK(hipStreamSynchronize(sA));
+                break;
+            case 2:
+                CK(hipMemcpy(host.data(), dev, 4096, hipMemcpyDeviceToHost));
+                break;
+            case 3:
+                CK(hipMemcpyAsync(dev, host.data(), W * H, hipMemcpyHostToDevice, sA));
+                break;
+            case 4:
+                hipLaunchKernelGGL(k_small, dim3(1), dim3(64), 0, sA, bufA, SLOTS - 1, 0);
+                break;
+            default:
+                break;
+            }
+            CK(hipMemsetAsync(bufA, 0, sizeof(int) * SLOTS, sA));
+            CK(hipGraphLaunch(xA, sA));
+            CK(hipStreamSynchronize(sA));
+            CK(hipMemcpy(h.data(), bufA, sizeof(int) * SLOTS, hipMemcpyDeviceToHost));
+            bad_replays += !expected(h.data(), 1000);
+        }
+        int bad_args = 0;
+        CK(hipMemcpyFromSymbol(&bad_args, HIP_SYMBOL(g_bad_args), sizeof(int)));
+        const char* pc = std::getenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE");
+        std::printf("{\"mode\": \"copies\", \"operation\": \"%s\", \"rounds\": %d, \"bad_replays\": %d, "
+                    "\"kernels_with_foreign_args\": %d, \"DEBUG_CLR_GRAPH_PACKET_CAPTURE\": \"%s\"}\n",
+                    names[op], rounds, bad_replays, bad_args, pc ? pc : "(default)");
+        std::fflush(stdout);
+        status |= bad_replays || bad_args;
+    }
+    CK(hipGraphExecDestroy(xA));
+    return status ? 1 : 0;
+}
+
 int main(int argc, char** argv)
 {
+    if (argc > 1 && std::string(argv[1]) == "copies") return copies_mode(argc > 2 ? std::atoi(argv[2]) : 16);
     const int rounds = argc > 1 ? std::atoi(argv[1]) : 64;
     hipStream_t sA, sL;
     CK(hipStreamCreateWithFlags(&sA, hipStreamNonBlocking));
