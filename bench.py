@@ -300,7 +300,7 @@ def _cpu_model():
     return "unknown"
 
 
-def timed_cpu_frames(work, frame, seconds, warmup=3):
+def timed_cpu_frames(work, frame, seconds, warmup=10):
     """Median seconds per frame of work(frame(i)) on one pinned core (the lowest core this process may use)."""
     import statistics
 
@@ -326,8 +326,10 @@ def timed_cpu_frames(work, frame, seconds, warmup=3):
 def cpu_record(med, n, warmup, what):
     return {"value": round(1.0 / med, 3), "unit": "frames/s", "cores": 1, "kind": "port",
             "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
-            "sample": f"median of {n} frames after 3 warm-up frames, one pinned core: {what}; oracle built -O3 "
-                      f"-march=native (plain C, scalar; OpenCV's SIMD build of the reference would be faster)"}
+            "sample": f"median of {n} frames after {warmup} warm-up frames, one pinned core: {what}; oracle built -O3 "
+                      f"-march=native (plain C, scalar; OpenCV's SIMD build of the reference would be faster); the "
+                      f"full plan (>= 200 frames, 16-core run): tools/cpu_baseline.py, profiles/r06_cpu_baseline.json",
+            "full_plan": "profiles/r06_cpu_baseline.json"}
 
 
 def cpu_baseline(rows, cols, nfeat, seconds):
@@ -348,7 +350,7 @@ def cpu_baseline(rows, cols, nfeat, seconds):
 
     med, n = timed_cpu_frames(work, lambda i: synthetic.render(scene, rows, cols, 3 + i % 9, 2 + i % 5,
                                                                 noise_seed=100 + i), seconds)
-    return cpu_record(med, n, 3, f"{cols}x{rows}, {nfeat} features, oracle extract + SearchForInitialization")
+    return cpu_record(med, n, 10, f"{cols}x{rows}, {nfeat} features, oracle extract + SearchForInitialization")
 
 
 # ------------------------------------------------------------------------------------------------
@@ -866,7 +868,7 @@ def cpu_baseline_tracking(rows, cols, nfeat, M, seconds):
                                                                           desc=mp["desc"]), 0.8, 1.0)
 
     med, n = timed_cpu_frames(work, lambda i: i, seconds)
-    return cpu_record(med, n, 3, f"{cols}x{rows}, {nfeat} features, oracle extraction + isInFrustum + "
+    return cpu_record(med, n, 10, f"{cols}x{rows}, {nfeat} features, oracle extraction + isInFrustum + "
                                  f"SearchByProjection vs a {M}-point local map (th 1)")
 
 
@@ -1041,7 +1043,7 @@ def cpu_baseline_extract(rows, cols, nfeat, seconds):
     scene = synthetic.make_scene(synthetic.SEED_BASE + 998, rows, cols)
     med, n = timed_cpu_frames(lambda f: ex(f), lambda i: synthetic.render(scene, rows, cols, i % 9, i % 5,
                                                                           noise_seed=100 + i), seconds)
-    return cpu_record(med, n, 3, f"{cols}x{rows}, {nfeat} features, oracle extraction")
+    return cpu_record(med, n, 10, f"{cols}x{rows}, {nfeat} features, oracle extraction")
 
 
 def cpu_baseline_stereo(rows, cols, nfeat, seconds):
@@ -1057,7 +1059,7 @@ def cpu_baseline_stereo(rows, cols, nfeat, seconds):
         O.stereo_matches(exL, exR, kL, dL, kR, dR, 386.1448, 386.1448 / 718.856)
 
     med, n = timed_cpu_frames(work, lambda i: pairs[i % 4], seconds)
-    r = cpu_record(med, n, 3, f"{cols}x{rows} stereo pairs, {nfeat} features, oracle L+R extraction + "
+    r = cpu_record(med, n, 10, f"{cols}x{rows} stereo pairs, {nfeat} features, oracle L+R extraction + "
                               f"ComputeStereoMatches")
     r["unit"] = "pairs/s"
     return r

@@ -440,7 +440,10 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     for (int q = 0; q < 4; q++) {
         const int r = 4 * rgu + q;
         if (r >= nyB) break;
-        const int4 yt = YB[r];
+        // the row's table entry is wave-uniform: in SGPRs, its row addresses and reuse tests are scalar work
+        const int4 ytv = YB[r];
+        const int4 yt = make_int4(__builtin_amdgcn_readfirstlane(ytv.x), __builtin_amdgcn_readfirstlane(ytv.y),
+                                  __builtin_amdgcn_readfirstlane(ytv.z), __builtin_amdgcn_readfirstlane(ytv.w));
         uint32_t h0[4], h1[4];
         if (yt.x == ry) {
 #pragma unroll

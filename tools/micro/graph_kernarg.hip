@@ -69,12 +69,13 @@ __global__ void k_big(int* p, int slot, Big b)
 }
 
 // capture the launch sequence of one "context" writing tags base + i into buf
-static hipGraphExec_t capture(hipStream_t s, int* buf, int base)
+static hipGraphExec_t capture(hipStream_t s, int* buf, int base, void* extra = nullptr, size_t extra_bytes = 0)
 {
     Big b;
     for (int i = 0; i < 190; i++) b.w[i] = base + i;
     CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     CK(hipMemsetAsync(buf, 0, sizeof(int) * SLOTS, s));
+    if (extra) CK(hipMemsetAsync(extra, 0, extra_bytes, s));
     for (int i = 0; i < NK; i++) {
         if (i & 1)
             hipLaunchKernelGGL(k_big, dim3(4), dim3(64), 0, s, buf, i, b);
@@ -113,20 +114,27 @@ static int copies_mode(int rounds)
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_valid), valid, sizeof(valid)));
     const int zero = 0;
     std::vector<unsigned char> host(W * H);  // pageable, as a numpy array is
+    std::vector<unsigned char> big_host(1 << 20);
+    unsigned char *dev_big, *gbig;
+    CK(hipMalloc(&dev_big, 1 << 20));
+    CK(hipMemset(dev_big, 3, 1 << 20));
+    CK(hipMalloc(&gbig, 1 << 16));
     std::vector<int> h(SLOTS);
-    hipGraphExec_t xA = capture(sA, bufA, 1000);
-    const char* names[] = {"none", "memcpy2d_d2h_pageable_on_stream", "memcpy_d2h_sync_null_stream",
-                           "memcpy_h2d_pageable_on_stream", "kernel_on_stream"};
+    hipGraphExec_t xA = capture(sA, bufA, 1000, gbig, 1 << 16);
+    const char* names[] = {"none", "memcpy2d_d2h_pitched_pageable_on_stream", "memcpy_d2h_sync_null_stream",
+                           "memcpy_h2d_pageable_on_stream", "kernel_on_stream", "all_of_them",
+                           "many_memcpy_d2h_sync_16KB", "many_memcpy_d2h_sync_4B", "memcpy_d2h_sync_24KB_x8",
+                           "memcpy_d2h_sync_64KB_x8", "memcpy_d2h_sync_1MB_x8", "memcpy_d2h_sync_24KB_of_graph_buffer_x8"};
     int status = 0;
-    for (int op = 0; op < 5; op++) {
+    for (int op = 0; op < 12; op++) {
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_bad_args), &zero, sizeof(int)));
         int bad_replays = 0;
         for (int r = 0; r < rounds; r++) {
             CK(hipGraphLaunch(xA, sA));
             CK(hipStreamSynchronize(sA));
             switch (op) {
-            case 1:
-                CK(hipMemcpy2DAsync(host.data(), W, dev, W, W, H, hipMemcpyDeviceToHost, sA));
+            case 1:  // the pyramid read-back: a true 2-D region (width 533 of pitch 576, as level 1 of 640x480)
+                CK(hipMemcpy2DAsync(host.data(), 533, dev, 576, 533, 400, hipMemcpyDeviceToHost, sA));
                 CK(hipStreamSynchronize(sA));
                 break;
             case 2:
@@ -138,10 +146,38 @@ static int copies_mode(int rounds)
             case 4:
                 hipLaunchKernelGGL(k_small, dim3(1), dim3(64), 0, sA, bufA, SLOTS - 1, 0);
                 break;
+            case 5:  // test_pyramid_and_candidates' sequence: 8 levels, each a 2-D read-back and two synchronous copies
+                for (int l = 0; l < 8; l++) {
+                    CK(hipMemcpy2DAsync(host.data(), 533 - 40 * l, dev, 576, 533 - 40 * l, 400 - 30 * l,
+                                        hipMemcpyDeviceToHost, sA));
+                    CK(hipStreamSynchronize(sA));
+                    CK(hipStreamSynchronize(sA));
+                    CK(hipMemcpy(host.data(), dev, 4, hipMemcpyDeviceToHost));
+                    CK(hipMemcpy(host.data(), dev, 8 * 300, hipMemcpyDeviceToHost));
+                }
+                break;
+            case 6:  // debug_candidates at scale: synchronous D2H copies of device memory, 16 KB each
+                for (int q = 0; q < 256; q++) CK(hipMemcpy(host.data(), dev, 16384, hipMemcpyDeviceToHost));
+                break;
+            case 7:  // ... and of 4 bytes (the per-level count)
+                for (int q = 0; q < 256; q++) CK(hipMemcpy(host.data(), dev, 4, hipMemcpyDeviceToHost));
+                break;
+            case 8:  // the candidate read-back's sizes (8 B per candidate, thousands of candidates per level)
+            case 9:
+            case 10:
+                for (int q = 0; q < 8; q++)
+                    CK(hipMemcpy(big_host.data(), dev_big, op == 8 ? 24576 : op == 9 ? 65536 : (1 << 20),
+                                 hipMemcpyDeviceToHost));
+                break;
+            case 11:  // a buffer the graph writes (its memset node), as the candidates are
+                for (int q = 0; q < 8; q++) CK(hipMemcpy(big_host.data(), gbig, 24576, hipMemcpyDeviceToHost));
+                break;
             default:
                 break;
             }
-            CK(hipMemsetAsync(bufA, 0, sizeof(int) * SLOTS, sA));
+            // non-zero before the replay: the graph's own memset node must clear slots NK.. (a skipped or misdirected
+            // memset shows as a bad replay)
+            CK(hipMemsetAsync(bufA, 0xff, sizeof(int) * SLOTS, sA));
             CK(hipGraphLaunch(xA, sA));
             CK(hipStreamSynchronize(sA));
             CK(hipMemcpy(h.data(), bufA, sizeof(int) * SLOTS, hipMemcpyDeviceToHost));
