@@ -3062,6 +3062,19 @@ void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, lon
                        pyr, oct_xy, oct_resp, oct_count, kps, desc, counts, dmagic);
 }
 
+// the batch's per-(frame, level) candidate counters to zero: a kernel rather than hipMemsetAsync, so that a batch's
+// launch sequence holds kernels only (a captured memset node replayed after synchronous device-to-host copies
+// faulted under the runtime's graph packet capture)
+__global__ __launch_bounds__(256) void og_zero_kernel(int* __restrict__ p, int n)
+{
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) p[i] = 0;
+}
+
+void og_launch_zero(hipStream_t s, int* p, int n)
+{
+    if (n > 0) hipLaunchKernelGGL(og_zero_kernel, dim3(std::min((n + 255) / 256, 1024)), dim3(256), 0, s, p, n);
+}
+
 void og_launch_grid(hipStream_t s, const orbgpu_kp_dev* kps, const int* counts, int frame_cap, OgGridGeom G,
                     int* cell_start, int* cell_items, int* status, int B, int* record_refused)
 {

@@ -657,7 +657,7 @@ static int run_batch(orbgpu_ctx* c, const uint8_t* d_imgs, int B, long long pitc
     hipStream_t s = c->stream;
     timer_begin(c);
     timer_mark(c, "start");
-    HIP_TRY(c, hipMemsetAsync(c->cand_count.p, 0, sizeof(int) * (size_t)B * P.nlevels, s));
+    og_launch_zero(s, c->cand_count.p, B * P.nlevels);
     // stage timing and the debug sync keep the serial order (their marks are stage boundaries on one stream)
     const bool fork = B <= fork_max_b() && P.nlevels > 1 && !c->timer.on && !debug_sync() && c->stream2 &&
                       (long long)c->W * c->H >= fork_min_pixels();

@@ -65,6 +65,8 @@ void og_launch_octree(hipStream_t s, const OgPlan& P, int lb, int le, const unsi
 void og_launch_describe(hipStream_t s, const OgPlan& P, const uint8_t* img0, long long pitch0, long long fstride0,
                         const uint8_t* pyr, const uint32_t* oct_xy, const uint32_t* oct_resp, const int* oct_count,
                         orbgpu_kp_dev* kps, uint8_t* desc, int* counts, int B);
+// n ints at p to zero (one small kernel; the batch's candidate counters)
+void og_launch_zero(hipStream_t s, int* p, int n);
 // record_refused: non-null when the frames are a fresh extraction (clears the context's refused-record word)
 void og_launch_grid(hipStream_t s, const orbgpu_kp_dev* kps, const int* counts, int frame_cap, OgGridGeom G,
                     int* cell_start, int* cell_items, int* status, int B, int* record_refused = nullptr);
