@@ -269,7 +269,8 @@ __global__ __launch_bounds__(RZ_NT) void og_resize_kernel(const uint8_t* __restr
 // ------------------------------------------------------------------------------------------------
 
 // 4 horizontally adjacent outputs of one row from two LDS source rows: sx = byte offsets in the rows, weights
-// (a0, a1) per column (a1 = 0 at the right border), vertical weights (yz, yw)
+// (a0, a1) per column (a1 = 0 at the right border), vertical weights (yz, yw) -- for FX = false already shifted left
+// by 8 (the multiply-high operand of og_rz_vert16; og_resize2_kernel stages its y table that way)
 template <bool FX>
 __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t* R1, const int* sx,
                                                const og_rz_u16x2* wt, unsigned yz, unsigned yw)
@@ -282,7 +283,7 @@ __device__ __forceinline__ uint32_t og_rz_quad(const uint8_t* R0, const uint8_t*
         const uint32_t d0 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p0), wt[k], 0u, false);
         const uint32_t d1 = __builtin_amdgcn_udot2(__builtin_bit_cast(og_rz_u16x2, p1), wt[k], 0u, false);
         if (!FX)  // og_rz_vert16 (its clamp never binds, og_rz_put_shr2): the final shift writes byte k of `packed`
-            og_rz_put_shr2(packed, og_mulhi_u24(yz << 8, d0 & ~0xffu) + og_mulhi_u24(yw << 8, d1 & ~0xffu) + 2u, k);
+            og_rz_put_shr2(packed, og_mulhi_u24(yz, d0 & ~0xffu) + og_mulhi_u24(yw, d1 & ~0xffu) + 2u, k);
         else
             packed |= og_rz_vert16<FX>(yz, d0, yw, d1) << (8 * k);
     }
@@ -392,7 +393,9 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
             }
         }
     }
-    if (tid < nrA) YA[tid] = ya;
+    // the A pass's table rows relative to the staged region (row - sr0) and, for FX = false, with the vertical weights
+    // pre-shifted for the multiply-high form: once per tile instead of once per row and thread
+    if (tid < nrA) YA[tid] = make_int4(ya.x - sr0, ya.y - sr0, FX ? ya.z : ya.z << 8, FX ? ya.w : ya.w << 8);
     if (tid < nyB) YB[tid] = yb;
     __syncthreads();
     // ---- level A region -> LDS (and the owned part -> HBM)
@@ -401,16 +404,34 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
         // ac0 is a multiple of 4 (host plan): every quad left of own_c1 is one aligned dword store
         const bool own_c = cA < own_c1;
         const int nown = min(4, own_c1 - cA);
-        for (int rr = rga; rr < nrA; rr += G) {
-            const int4 yt = YA[rr];
-            const int r = ar0 + rr;
-            const int r0 = yt.x - sr0, r1 = yt.y - sr0;
-            // a 16-byte multiple pitch gives every staged row the first row's misalignment mb: no per-row lookups
-            const unsigned m0 = (upitch & 15u) == 0 ? mb : (unsigned)mis[r0], m1 = (upitch & 15u) == 0 ? mb : (unsigned)mis[r1];
-            const uint32_t packed = og_rz_quad<FX>(S + __umul24((unsigned)r0, (unsigned)g.SC) + m0, S + __umul24((unsigned)r1, (unsigned)g.SC) + m1, sxA, wtA,
-                                               (unsigned)yt.z, (unsigned)yt.w);
-            *(uint32_t*)&A[rr * g.AC + 4 * qa] = packed;
-            if (r < own_r1 && own_c) og_rz_store4(DA + (__umul24((unsigned)r, (unsigned)pitchA) + (unsigned)cA), packed, nown);
+        if ((upitch & 15u) == 0) {
+            // a 16-byte multiple pitch gives every staged row the first row's misalignment mb: folded into the lane's
+            // column offsets once, so a row's four byte addresses are one multiply-add and four adds
+            int sxm[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) sxm[k] = sxA[k] + (int)mb;
+            for (int rr = rga; rr < nrA; rr += G) {
+                const int4 yt = YA[rr];
+                const int r = ar0 + rr;
+                const int r0 = yt.x, r1 = yt.y;
+                const uint32_t packed = og_rz_quad<FX>(S + __umul24((unsigned)r0, (unsigned)g.SC),
+                                                       S + __umul24((unsigned)r1, (unsigned)g.SC), sxm, wtA,
+                                                       (unsigned)yt.z, (unsigned)yt.w);
+                *(uint32_t*)&A[rr * g.AC + 4 * qa] = packed;
+                if (r < own_r1 && own_c) og_rz_store4(DA + (__umul24((unsigned)r, (unsigned)pitchA) + (unsigned)cA), packed, nown);
+            }
+        } else {
+            for (int rr = rga; rr < nrA; rr += G) {
+                const int4 yt = YA[rr];
+                const int r = ar0 + rr;
+                const int r0 = yt.x, r1 = yt.y;
+                const unsigned m0 = (unsigned)mis[r0], m1 = (unsigned)mis[r1];
+                const uint32_t packed = og_rz_quad<FX>(S + __umul24((unsigned)r0, (unsigned)g.SC) + m0,
+                                                       S + __umul24((unsigned)r1, (unsigned)g.SC) + m1, sxA, wtA,
+                                                       (unsigned)yt.z, (unsigned)yt.w);
+                *(uint32_t*)&A[rr * g.AC + 4 * qa] = packed;
+                if (r < own_r1 && own_c) og_rz_store4(DA + (__umul24((unsigned)r, (unsigned)pitchA) + (unsigned)cA), packed, nown);
+            }
         }
     }
     __syncthreads();
