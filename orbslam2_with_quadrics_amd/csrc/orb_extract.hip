@@ -599,6 +599,7 @@ typedef unsigned short og_u16x2 __attribute__((ext_vector_type(2)));
 #define FB_MW 80                 // detection height capacity of a block (2 x 40 or 1 x 64); width <= 64
 #define FB_MSW (FB_MW + 3)       // score map stride: a zero gap column before, between and after the cells
 #define FB_MSZ ((FB_MSW * FB_MSW + 15) & ~15)  // 16-byte multiple: zeroed by 16-byte stores
+#define FB_FCHUNK 64u            // frames per dispatch chunk of og_fast_quad_kernel (a multiple of 8)
 
 // score-map index of detection pixel (i, j): one zero row/column separates the block's cells and surrounds
 // them, so a pixel's 8 neighbours outside its cell (or outside the detection area) read 0 without checks
@@ -797,7 +798,7 @@ __device__ __forceinline__ void og_fastq_roi_put(const OgFB& b, int tid, const u
 __device__ unsigned long long og_fast_prof[4096 * 8];
 #define FAST_PROF(slot)                                                                                         \
     do {                                                                                                        \
-        if (tid == 0 && f == gridDim.y / 2 && p < 4096) og_fast_prof[p * 8 + (slot)] = __builtin_amdgcn_s_memtime(); \
+        if (tid == 0 && f == (unsigned)nframes / 2 && p < 4096) og_fast_prof[p * 8 + (slot)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #else
 #define FAST_PROF(slot) \
@@ -813,7 +814,7 @@ __device__ unsigned long long og_fast_prof[4096 * 8];
 __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void og_fast_quad_kernel(
     const OgFastBlk* __restrict__ blocks, int nb, const uint8_t* __restrict__ img0, long long pitch0, long long fstride0,
     const uint8_t* __restrict__ pyr, long long pyr_per_frame, u64* __restrict__ cand, long long cand_per_frame,
-    int* __restrict__ cand_count, int nlevels, int thr, int* __restrict__ status)
+    int* __restrict__ cand_count, int nlevels, int thr, int* __restrict__ status, int nframes)
 {
     __shared__ __attribute__((aligned(16))) uint2 roiq[FQ_ROWS * FQ_S];
     __shared__ __attribute__((aligned(16))) uint8_t Ms[FB_MSZ];
@@ -824,17 +825,20 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     __shared__ int sh_base;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);
-    // the dispatch order lin = (blockIdx.y, blockIdx.x) interleaves the frames: block p of frame f is workgroup
-    // p * B + f, so with B a multiple of 8 every block of a frame runs on XCD f % 8 and shares that L2 with its
-    // neighbours (FAST -0.7 % against frame-major order, profiles/sweeps/r05_ab_fast_frame_interleave.txt)
-    const unsigned lin_ = blockIdx.y * gridDim.x + blockIdx.x;
-    const unsigned f = lin_ % gridDim.y;
+    // grid (G, blocks, chunks), G = min(B, FB_FCHUNK): the dispatch order (x fastest) interleaves the G frames of a
+    // chunk, so every block of frame f runs on XCD f % 8 and shares that L2 with its neighbours (G a multiple of 8
+    // when B >= 8; FAST -0.7 % against frame-major order, profiles/sweeps/r05_ab_fast_frame_interleave.txt), and a
+    // frame's neighbouring blocks, which share halo lines, are dispatched G workgroups apart rather than B.  With the
+    // frames interleaved over a whole 512-frame batch the launch fetched 9.8 GB, 3.1x its pixel bytes; chunks of 64
+    // fetch 3.2 GB (profiles/sweeps/r06_ab_fast_chunk.txt).  No division in the index.
+    const unsigned f = blockIdx.z * gridDim.x + blockIdx.x;
+    if (f >= (unsigned)nframes) return;  // the last chunk's unused frame slots
     const int t1 = thr & 255, t2 = (thr >> 8) & 255;  // clamped to [0, 255] on the host
     const int tq = min(t1, t2);
     const og_u16x2 tt = {(unsigned short)tq, (unsigned short)tq};
     const int tA = max(t1, 1), tB = max(t2, 1);
     const uint32_t a_ns = og_lds_addr(&sh_ns), a_lst = og_lds_addr(&lst[0]);
-    const int p = (int)(lin_ / gridDim.y);
+    const int p = (int)blockIdx.y;
     // every kernel argument the block decode reads is fetched before the first of them is used: one scalar-cache round
     // trip (the compiler's order took three before the block record)
     __asm__ volatile("" ::"s"(blocks), "s"(nb), "s"(img0), "s"(pitch0), "s"(fstride0), "s"(pyr), "s"(pyr_per_frame));
@@ -1055,7 +1059,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 #if OG_FAST_PROFILE
     __builtin_amdgcn_s_waitcnt(0);  // the candidate stores issued
     FAST_PROF(6);
-    if (tid == 0 && f == gridDim.y / 2 && p < 4096) og_fast_prof[p * 8 + 7] = (unsigned long long)ns | ((unsigned long long)b.l << 32);
+    if (tid == 0 && f == (unsigned)nframes / 2 && p < 4096) og_fast_prof[p * 8 + 7] = (unsigned long long)ns | ((unsigned long long)b.l << 32);
 #endif
 }
 
@@ -3032,8 +3036,10 @@ void og_launch_fast(hipStream_t s, const OgPlan& P, int lb, int le, const OgFast
     // frames in dispatch order, so a frame's blocks share one XCD
     const int p0 = P.lv[lb].fb_off, p1 = le < P.nlevels ? P.lv[le].fb_off : P.fast_blocks;
     if (p1 <= p0) return;
-    hipLaunchKernelGGL(og_fast_quad_kernel, dim3(p1 - p0, B), dim3(FB_NT), 0, s, table + p0, p1 - p0, img0, pitch0,
-                       fstride0, pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels, thr, status);
+    const int G = std::min(B, (int)FB_FCHUNK);
+    hipLaunchKernelGGL(og_fast_quad_kernel, dim3(G, p1 - p0, (B + G - 1) / G), dim3(FB_NT), 0, s, table + p0, p1 - p0,
+                       img0, pitch0, fstride0, pyr, P.pyr_per_frame, cand, P.cand_per_frame, cand_count, P.nlevels, thr,
+                       status, B);
 }
 
 void og_launch_harris(hipStream_t s, const OgPlan& P, int lb, int le, const uint8_t* img0, long long pitch0,
