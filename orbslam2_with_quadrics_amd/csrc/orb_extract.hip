@@ -822,7 +822,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                                                // then kept at t1/t2 (stages 3-4)
     __shared__ int sh_ns;
     __shared__ __attribute__((aligned(16))) int wk[FB_NW][8];  // per wave: kept at t1 per cell [0..3], at t2 [4..7]
-    __shared__ int sh_base;
+    __shared__ int sh_base, sh_nk, sh_out;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);
     // grid (G, blocks, chunks), G = min(B, FB_FCHUNK): the dispatch order (x fastest) interleaves the G frames of a
@@ -962,6 +962,10 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     __syncthreads();
     FAST_PROF(2);
     const int ns = sh_ns;
+    if (tid == 0) {
+        sh_nk = 0;
+        sh_out = 0;
+    }
     // ---- stage 2: exact M for every survivor; single pixels are u16 reads of the quad layout (element step 4)
     const uint16_t* T16 = (const uint16_t*)Tq;
     for (int e = tid; e < ns; e += FB_NT) {
@@ -977,8 +981,13 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     }
     __syncthreads();
     FAST_PROF(3);
-    // ---- stage 3: same-cell 3x3 NMS at both thresholds; each wave walks every 8th 64-entry chunk of the list
+    // ---- stage 3: same-cell 3x3 NMS at both thresholds; each wave walks every 8th 64-entry chunk of the list.  The
+    // entries kept at either threshold are compacted into the ROI buffer (free after stage 2) as (entry | kept at t1
+    // << 14 | kept at t2 << 15 | M << 16), so that the emission walks those few instead of every survivor (a strict
+    // 3x3 maximum per cell: at most 20 x 16 per cell, 1280 per block, against 4816 u32 of the buffer)
     int c1[4] = {0, 0, 0, 0}, c2[4] = {0, 0, 0, 0};
+    uint32_t* kl = (uint32_t*)roiq;
+    const uint32_t a_nk = og_lds_addr(&sh_nk);
     for (int e0 = wvu * 64; e0 < ns; e0 += FB_NT) {
         const int e = e0 + lane;
         int ent = 0, mc = 0, nbm = 0;
@@ -992,12 +1001,26 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const u64 top = og_lanes_gt(mc, nbm);
         const u64 K1 = og_lanes_gt(mc, tA) & top, K2 = og_lanes_gt(mc, tB) & top;
         const u64 ci = og_lanes_gt(ent >> 7, hC - 1), cj = og_lanes_gt(ent & 127, wC - 1);
-        if (e < ns) lst[e] = (uint16_t)(ent | (mc > tA && mc > nbm ? 0x4000 : 0) | (mc > tB && mc > nbm ? 0x8000 : 0));
         const u64 cm[4] = {~ci & ~cj, ~ci & cj, ci & ~cj, ci & cj};
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) {
             c1[cc] += __popcll(K1 & cm[cc]);
             c2[cc] += __popcll(K2 & cm[cc]);
+        }
+        const u64 K = K1 | K2;
+        if (K) {  // wave-uniform
+            uint32_t old;
+            u64 sv;
+            const int nk = __popcll(K);
+            __asm__ volatile(
+                "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_waitcnt lgkmcnt(0)\n\t"
+                "s_mov_b64 exec, %1"
+                : "=&v"(old), "=&s"(sv)
+                : "v"(a_nk), "v"(nk)
+                : "memory");
+            const int kb = __builtin_amdgcn_readfirstlane(old);
+            const uint32_t v = (uint32_t)ent | ((uint32_t)mc << 16) | (mc > tA ? 0x4000u : 0u) | (mc > tB ? 0x8000u : 0u);
+            if ((K >> lane) & 1ull) kl[og_rank(K, kb)] = v;
         }
     }
     if (lane == 0) {
@@ -1025,8 +1048,7 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     sc += __builtin_amdgcn_update_dpp(0, sc, 0x112, 0xf, 0xf, true);
     sc += __builtin_amdgcn_update_dpp(0, sc, 0x114, 0xf, 0xf, true);
     const int total = __builtin_amdgcn_readlane(sc, FB_NW - 1);
-    const int kept = __builtin_amdgcn_readlane(kx, wvu);
-    const int before = __builtin_amdgcn_readlane(sc, wvu) - kept;
+    const int nk = sh_nk;  // (written before the stage-3 barrier)
     // ---- stage 4: one reservation per block; each wave writes its kept entries at its offset
     int sb = 0;
     if (total != 0) {  // block-uniform
@@ -1039,22 +1061,33 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         sb = sh_base;
     }
     FAST_PROF(5);
-    const bool emit = total != 0 && sb + total <= b.cand_cap && kept != 0;
-    u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb + before);
-    int run = 0;
-    for (int e0 = wvu * 64; e0 < ns; e0 += FB_NT) {
-        const int e = e0 + lane;
-        int ent = 0;
-        if (e < ns) ent = lst[e];
-        const int i = (ent >> 7) & 127, j = ent & 127;
-        const int cell = (i >= hC) * 2 + (j >= wC);
-        const unsigned kbit = (unsigned)ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
-        const u64 mask = og_lanes_ne(kbit, 0u);
-        if (e < ns) {
-            uint8_t* mcell = &Ms[og_ms_idx(i, j, wC, hC)];
-            if (emit && kbit) out[og_rank(mask, run)] = og_pack_cand(b.ox + j, b.oy + i, *mcell - 1);
+    // ---- emission: the kept entries of the compacted list (the cell's threshold picks the flag), each wave's at an
+    // offset from one LDS counter (a block's candidates are unordered: every consumer orders them itself)
+    const bool emit = total != 0 && sb + total <= b.cand_cap;
+    u64* out = cand + (unsigned long long)f * (unsigned long long)cand_per_frame + (unsigned)(b.cand_off + sb);
+    const uint32_t a_out = og_lds_addr(&sh_out);
+    if (emit) {
+        for (int e0 = wvu * 64; e0 < nk; e0 += FB_NT) {
+            const int e = e0 + lane;
+            const uint32_t ent = e < nk ? kl[e] : 0u;
+            const int i = (ent >> 7) & 127, j = ent & 127;
+            const int cell = (i >= hC) * 2 + (j >= wC);
+            const unsigned kbit = ent & (((useT2 >> cell) & 1u) ? 0x8000u : 0x4000u);
+            const u64 mask = og_lanes_ne(kbit, 0u);
+            if (mask) {  // wave-uniform
+                uint32_t old;
+                u64 sv;
+                const int n = __popcll(mask);
+                __asm__ volatile(
+                    "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_waitcnt lgkmcnt(0)\n\t"
+                    "s_mov_b64 exec, %1"
+                    : "=&v"(old), "=&s"(sv)
+                    : "v"(a_out), "v"(n)
+                    : "memory");
+                const int ob = __builtin_amdgcn_readfirstlane(old);
+                if (kbit) out[og_rank(mask, ob)] = og_pack_cand(b.ox + j, b.oy + i, (int)(ent >> 16) - 1);
+            }
         }
-        run += __popcll(mask);
     }
 #if OG_FAST_PROFILE
     __builtin_amdgcn_s_waitcnt(0);  // the candidate stores issued
