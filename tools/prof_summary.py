@@ -24,8 +24,11 @@ def main():
         k = short(r["Kernel_Name"])
         gx, gy, gz = int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]), int(r["Grid_Size_Z"])
         wx, wy, wz = int(r["Workgroup_Size_X"]), int(r["Workgroup_Size_Y"]), int(r["Workgroup_Size_Z"])
-        # frames per launch: z for the pyramid kernel, x/8 for the octree, x for the matchers, y for the others
-        if k.startswith("og_resize"):
+        # frames per launch: z for the pyramid kernel, x/8 for the octree, x for the matchers, x * z for FAST (frame
+        # chunks of up to 64 on x, chunks on z: B rounded up to a chunk multiple), y for the others
+        if k.startswith("og_fast_quad"):
+            batch = gx // max(wx, 1) * gz
+        elif k.startswith("og_resize"):
             batch = gz // max(wz, 1)
         elif k.startswith("og_octree"):  # level-major 1-D grid: 8 levels x B frames (the single-frame fork splits
             batch = max(1, round(gx // max(wx, 1) / 8))  # level 0 from levels 1-7: 1 and 7 workgroups, one frame)
