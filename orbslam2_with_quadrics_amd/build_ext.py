@@ -77,8 +77,6 @@ VARIANTS = {
 }
 # the run-time switches (environment variables read by liborbgpu.so), checked the same way with the default build
 ENV_VARIANTS = {
-    "order1": {"ORBGPU_FAST_ORDER": "1"},          # FAST blocks in plain plan order instead of XCD runs of 4
-    "order8": {"ORBGPU_FAST_ORDER": "8"},
     "forkall": {"ORBGPU_FORK_MIN_PIXELS": "0"},    # every small batch forks level 0 onto its own stream
     "forknone": {"ORBGPU_FORK_MIN_PIXELS": "1000000000000"},
     "forkbatch": {"ORBGPU_FORK_MAX_B": "1024"},    # every batch forks (measured -1 % at config 3, r06)

@@ -844,7 +844,6 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     __asm__ volatile("" ::"s"(blocks), "s"(nb), "s"(img0), "s"(pitch0), "s"(fstride0), "s"(pyr), "s"(pyr_per_frame));
     if (p >= nb) return;
     const OgFB b = og_fast_decode(blocks, p, f, img0, pitch0, fstride0, pyr, pyr_per_frame);
-    if (b.l < 0) return;  // padding entry of the level (the table pads each level to 8 entries)
     FAST_PROF(0);
     uint32_t sroi[2][4];
     og_fastq_roi_load(b, tid, sroi);
@@ -3065,8 +3064,8 @@ void og_launch_fast(hipStream_t s, const OgPlan& P, int lb, int le, const OgFast
     le = std::min(le, P.nlevels);
     if (lb >= le || B <= 0) return;
     const int thr = std::min(std::max(P.iniTh, 0), 255) | (std::min(std::max(P.minTh, 0), 255) << 8);
-    // the levels' table range (level-major, each level padded to a multiple of 8 entries); the kernel interleaves the
-    // frames in dispatch order, so a frame's blocks share one XCD
+    // the levels' table range (level-major); the kernel interleaves the frames of each 64-frame chunk in dispatch
+    // order, so a frame's blocks share one XCD
     const int p0 = P.lv[lb].fb_off, p1 = le < P.nlevels ? P.lv[le].fb_off : P.fast_blocks;
     if (p1 <= p0) return;
     const int G = std::min(B, (int)FB_FCHUNK);

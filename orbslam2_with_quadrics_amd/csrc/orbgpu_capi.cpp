@@ -399,42 +399,24 @@ static int build_plan(orbgpu_ctx* c, int W, int H)
         return ORBGPU_ERR_UNSUPPORTED;
     }
     P.total_cells = (int)cells.size();
-    // the FAST kernel's block table (OgFastBlk): level-major; each level's range is padded to a multiple of 8
-    // entries (empty entries, lev < 0, exit at once).  The kernel interleaves the frames in dispatch order (block p
-    // of frame f is workgroup p * B + f), so with B a multiple of 8 a frame's blocks all run on XCD f % 8 and the
-    // table order only sets the order of a frame's blocks in time.  Within a level, ORBGPU_FAST_ORDER R (default 4)
-    // groups runs of R row-adjacent blocks (round 3: R-runs per XCD under frame-major dispatch; giving every XCD a
-    // contiguous eighth of each frame was 7-9 % slower, profiles/sweeps/r03_ab_fast_block_order.txt).
+    // the FAST kernel's block table (OgFastBlk): level-major, each level's blocks in plan order (row-major), no
+    // padding.  The kernel's grid is (64 frames, blocks, frame chunks), so a frame's blocks all run on XCD f % 8
+    // whatever the table holds; the table order only sets the order of a frame's blocks in time.  Runs of 4 or 8
+    // row-adjacent blocks (round 3's XCD runs under frame-major dispatch) were 0.4 % slower under the chunked
+    // dispatch (profiles/sweeps/r06_ab_fast_table_padding_order.txt) and are gone.
     std::vector<OgFastBlk> fblk;
     {
-        static const int R = [] {
-            const char* e = std::getenv("ORBGPU_FAST_ORDER");
-            const int v = e && *e ? std::atoi(e) : 4;
-            return v == 1 || v == 2 || v == 4 || v == 8 ? v : 4;
-        }();
-        std::vector<int> order;  // table entry -> cell index (-1 = padding)
+        std::vector<int> order;  // table entry -> cell index
         for (int l = 0; l < P.nlevels; l++) {
             OgLevel& L = P.lv[l];
             L.fb_off = (int)order.size();
-            const int n = L.ncells, npad = (n + 7) & ~7, G = 8 * R;
-            for (int w = 0; w < npad; w++) {
-                int b = w;
-                if (w < n / G * G) {  // slot w = G q + 8 h + x -> block G q + R x + h
-                    const int q = w / G, h = (w % G) / 8, x = w % 8;
-                    b = G * q + R * x + h;
-                }
-                order.push_back(b < n ? L.cell_base + b : -1);
-            }
+            for (int b = 0; b < L.ncells; b++) order.push_back(L.cell_base + b);
         }
         const int n = (int)order.size();
         fblk.resize(n);
         for (int p = 0; p < n; p++) {
             OgFastBlk& r = fblk[p];
             std::memset(&r, 0, sizeof(r));
-            if (order[p] < 0) {
-                r.lev = -1;
-                continue;
-            }
             const OgCell& cd = cells[order[p]];
             const OgLevel& L = P.lv[cd.level];
             const int rw = cd.x1 - cd.x0, rh = cd.y1 - cd.y0;

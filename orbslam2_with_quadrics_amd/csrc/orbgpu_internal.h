@@ -69,7 +69,7 @@ struct OgFastBlk {
     int src_off;           // levels >= 1: byte offset of ROI pixel (0, 0) inside the frame's pyramid block;
                            // level 0: the ROI's first column (the row term y0 * pitch0 is added at run time)
     int pitch;             // row pitch of the level (levels >= 1); 0 for level 0 (the caller's pitch)
-    short y0, lev;         // ROI first row (level 0's row term), pyramid level (< 0: empty entry, skipped)
+    short y0, lev;         // ROI first row (level 0's row term), pyramid level
     unsigned char rw, rh;  // ROI size (detection area + 6): rw - 6 <= 64, rh - 6 <= 80
     unsigned char wC, hC;  // FAST cell size of the level
     int cand_off;          // the level's candidate slots inside a frame (entries)

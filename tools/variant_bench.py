@@ -5,6 +5,8 @@ frames/s and the per-stage HIP-event times of each, so a kernel change is judged
 headline number.  Build variants here first, e.g. with build_ext.build(defines=[...], out=...).
 
 python tools/variant_bench.py [--streams S] [--names a,b,...] [--json out.json] [-- extra bench args]
+
+A name may carry environment settings for its run: `lib@KEY=VAL:KEY2=VAL2` (e.g. `head@ORBGPU_FORK_MAX_B=1024`).
 """
 import json
 import os
@@ -27,7 +29,9 @@ def main():
         names = argv[argv.index("--names") + 1].split(",")
     res = {}
     for name in names:
-        env = dict(os.environ, ORBGPU_LIB=os.path.join(VDIR, f"liborbgpu_{name}.so"))
+        lib, _, sets = name.partition("@")
+        env = dict(os.environ, ORBGPU_LIB=os.path.join(VDIR, f"liborbgpu_{lib}.so"))
+        env.update(kv.split("=", 1) for kv in sets.split(":") if kv)
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--warmup", "2", "--streams", streams,
                "--no-cpu-baseline", *extra]
         out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
