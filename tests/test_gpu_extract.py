@@ -97,6 +97,29 @@ def test_pure_noise_stresses_octree(ex2000, oracle):
     assert_same(k, d, ko, do)
 
 
+def test_dense_corners_candidate_sets(gpu, oracle):
+    """Pure noise at thresholds (3, 1): nearly every pixel passes the quick test and a block keeps hundreds of NMS
+    maxima, so FAST's compacted kept list (stage 3, written into the ROI buffer; bound: one strict 3x3 maximum per
+    2x2 pixels of a cell, 1280 per block) runs near its densest.  The candidate sets of every level and the final
+    keypoints/descriptors must equal the oracle's (src/ORBextractor.cc:789-829 + cv::FAST NMS)."""
+    img = synthetic.pure_noise(23, 480, 640)
+    params = (3000, 1.2, 8, 3, 1)
+    ex = gpu.ORBextractor(*params)
+    k, d = ex(img)
+    oe = oracle.OracleExtractor(*params)
+    ko, do = oe(img)
+    assert_same(k, d, ko, do)
+    dense = 0
+    for l in range(8):
+        c = ex.debug_candidates(0, l)
+        g = set(zip((c & 0xFFFF).tolist(), ((c >> 16) & 0xFFFF).tolist(), ((c >> 32) & 0xFF).tolist()))
+        xy, r = oe.candidates(l)
+        o = set(zip(xy[:, 0].astype(int).tolist(), xy[:, 1].astype(int).tolist(), r.astype(int).tolist()))
+        assert g == o, l
+        dense = max(dense, len(g))
+    assert dense > 20000  # (level 0: about one kept maximum per 10 pixels)
+
+
 def test_threshold_fallback_and_other_params(gpu, oracle):
     img = synthetic.frame(19, 480, 640)
     for params in [(1500, 1.2, 8, 30, 10), (800, 1.3, 6, 12, 5), (4000, 1.2, 8, 20, 7)]:
