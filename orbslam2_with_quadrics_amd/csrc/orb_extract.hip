@@ -323,10 +323,10 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
                                                            int* __restrict__ status)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t rz2_lds[];
-    // LDS layout (og_rz2_lds_bytes): the tile's rows of both y tables, then S, A and the row misalignments
+    // LDS layout (og_rz2_lds_bytes): the tile's rows of the A pass's y table, then S, A and the row misalignments (the
+    // B pass reads its wave-uniform y-table rows with scalar loads)
     int4* YA = (int4*)rz2_lds;                     // [AR]  ytabA[ar0 + i]
-    int4* YB = YA + g.AR;                          // [RZ2_TH]  ytabB[by0 + i]
-    uint8_t* S = (uint8_t*)(YB + RZ2_TH);           // [SR][SC] staged source rows (own misalignment each)
+    uint8_t* S = (uint8_t*)(YA + g.AR);             // [SR][SC] staged source rows (own misalignment each)
     uint8_t* A = S + g.SR * g.SC;                  // [AR][AC] level-A region, column ac0 at byte 0
     int* mis = (int*)(A + g.AR * g.AC);            // [SR]
     const int f = blockIdx.z, tid = threadIdx.x;
@@ -369,7 +369,6 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     // tile ride along (each pass below reads its vertical weights from LDS, not from a global load per row)
     const int nIt = nrS * nch;
     const int4 ya = tid < nrA ? g.ytabA[ar0 + tid] : make_int4(0, 0, 0, 0);
-    const int4 yb = tid < nyB ? g.ytabB[by0 + tid] : make_int4(0, 0, 0, 0);
     for (int it0 = tid; it0 < nIt; it0 += RZ2_NT * RZ2_U) {
         uint4 v[RZ2_U];
 #pragma unroll
@@ -396,7 +395,6 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     // the A pass's table rows relative to the staged region (row - sr0) and, for FX = false, with the vertical weights
     // pre-shifted for the multiply-high form: once per tile instead of once per row and thread
     if (tid < nrA) YA[tid] = make_int4(ya.x - sr0, ya.y - sr0, FX ? ya.z : ya.z << 8, FX ? ya.w : ya.w << 8);
-    if (tid < nyB) YB[tid] = yb;
     __syncthreads();
     // ---- level A region -> LDS (and the owned part -> HBM)
     uint8_t* DA = dstA + (long long)f * dst_fstride;
@@ -461,10 +459,13 @@ __global__ __launch_bounds__(RZ2_NT) void og_resize2_kernel(const uint8_t* __res
     for (int q = 0; q < 4; q++) {
         const int r = 4 * rgu + q;
         if (r >= nyB) break;
-        // the row's table entry is wave-uniform: in SGPRs, its row addresses and reuse tests are scalar work
-        const int4 ytv = YB[r];
-        const int4 yt = make_int4(__builtin_amdgcn_readfirstlane(ytv.x), __builtin_amdgcn_readfirstlane(ytv.y),
-                                  __builtin_amdgcn_readfirstlane(ytv.z), __builtin_amdgcn_readfirstlane(ytv.w));
+        // the row's table entry is wave-uniform: one scalar load (constant address space) into SGPRs, so its row
+        // addresses and reuse tests are scalar work
+#if defined(__HIP_DEVICE_COMPILE__)
+        const int4 yt = ((const __attribute__((address_space(4))) int4*)g.ytabB)[by0 + r];
+#else
+        const int4 yt = g.ytabB[by0 + r];  // (host pass of the device function: never called)
+#endif
         uint32_t h0[4], h1[4];
         if (yt.x == ry) {
 #pragma unroll

@@ -35,10 +35,10 @@ struct OgRz2Geom {
 // (4 output rows x 4 columns per thread in its last pass)
 #define RZ2_TH 16  // (32-row tiles measured +7 % pyramid time)
 #define RZ2_NT (16 * RZ2_TH)
-// dynamic LDS of og_resize2_kernel: y-table rows of the tile (AR + RZ2_TH int4), S, A, row misalignments
+// dynamic LDS of og_resize2_kernel: the A pass's y-table rows of the tile (AR int4), S, A, row misalignments
 static inline size_t og_rz2_lds_bytes(int SR, int SC, int AR, int AC)
 {
-    return 16 * ((size_t)AR + RZ2_TH) + (size_t)SR * SC + (size_t)AR * AC + 4 * (size_t)SR;
+    return 16 * (size_t)AR + (size_t)SR * SC + (size_t)AR * AC + 4 * (size_t)SR;
 }
 void og_launch_resize2(hipStream_t s, const uint8_t* src, long long src_pitch, long long src_fstride, uint8_t* dstA,
                        long long pitchA, uint8_t* dstB, long long pitchB, long long dst_fstride, const OgRz2Geom& g,
