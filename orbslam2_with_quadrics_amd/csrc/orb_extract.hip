@@ -937,24 +937,25 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             if (n) {
                 uint32_t old;
                 u64 sv;
+                // the reservation is issued, and waited for only after the entries and ranks are formed
                 __asm__ volatile(
-                    "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_waitcnt lgkmcnt(0)\n\t"
-                    "s_mov_b64 exec, %1"
+                    "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_mov_b64 exec, %1"
                     : "=&v"(old), "=&s"(sv)
                     : "v"(a_ns), "v"(n)
                     : "memory");
-                const uint32_t ab = a_lst + 2u * (uint32_t)__builtin_amdgcn_readfirstlane(old);
                 // entries: bits 14 / 15 of each half = the dark / bright sign bits of that pixel; the high pixels'
                 // entries are built in the high half and stored by ds_write_b16_d16_hi
                 const uint32_t base = e_lane + (uint32_t)(R << 7), hbase = e_hi + ((uint32_t)R << 23);
                 const uint32_t X0 = ((r0.x >> 1) & 0x40004000u) | (r0.y & 0x80008000u);
                 const uint32_t X1 = ((r1.x >> 1) & 0x40004000u) | (r1.y & 0x80008000u);
                 const uint32_t v[4] = {X0 | base, X0 | hbase, X1 | (base + 32u), X1 | (hbase + (32u << 16))};
-                const uint32_t ab1 = ab + 2u * (uint32_t)cnt[0], ab2 = ab1 + 2u * (uint32_t)cnt[1],
-                               ab3 = ab2 + 2u * (uint32_t)cnt[2];
-                og_ds_write_b16_x4(m[0], ab + 2u * (uint32_t)og_rank(m[0]), v[0], m[1], ab1 + 2u * (uint32_t)og_rank(m[1]),
-                                   v[1], m[2], ab2 + 2u * (uint32_t)og_rank(m[2]), v[2], m[3],
-                                   ab3 + 2u * (uint32_t)og_rank(m[3]), v[3]);
+                const int c1 = cnt[0], c2 = c1 + cnt[1], c3 = c2 + cnt[2];
+                const uint32_t k0 = (uint32_t)og_rank(m[0]), k1 = (uint32_t)og_rank(m[1], c1),
+                               k2 = (uint32_t)og_rank(m[2], c2), k3 = (uint32_t)og_rank(m[3], c3);
+                __asm__ volatile("s_waitcnt lgkmcnt(0)" : "+v"(old) : : "memory");
+                const uint32_t ab = a_lst + 2u * (uint32_t)__builtin_amdgcn_readfirstlane(old);
+                og_ds_write_b16_x4(m[0], ab + 2u * k0, v[0], m[1], ab + 2u * k1, v[1], m[2], ab + 2u * k2, v[2], m[3],
+                                   ab + 2u * k3, v[3]);
             }
         }
     }
