@@ -1014,14 +1014,16 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             u64 sv;
             const int nk = __popcll(K);
             __asm__ volatile(
-                "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_waitcnt lgkmcnt(0)\n\t"
-                "s_mov_b64 exec, %1"
+                "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_mov_b64 exec, %1"
                 : "=&v"(old), "=&s"(sv)
                 : "v"(a_nk), "v"(nk)
                 : "memory");
-            const int kb = __builtin_amdgcn_readfirstlane(old);
+            // the entry and its rank while the reservation is in flight
             const uint32_t v = (uint32_t)ent | ((uint32_t)mc << 16) | (mc > tA ? 0x4000u : 0u) | (mc > tB ? 0x8000u : 0u);
-            if ((K >> lane) & 1ull) kl[og_rank(K, kb)] = v;
+            const int rk = og_rank(K);
+            __asm__ volatile("s_waitcnt lgkmcnt(0)" : "+v"(old) : : "memory");
+            const int kb = __builtin_amdgcn_readfirstlane(old);
+            if ((K >> lane) & 1ull) kl[kb + rk] = v;
         }
     }
     if (lane == 0) {
@@ -1080,13 +1082,15 @@ __global__ __launch_bounds__(FB_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                 u64 sv;
                 const int n = __popcll(mask);
                 __asm__ volatile(
-                    "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_waitcnt lgkmcnt(0)\n\t"
-                    "s_mov_b64 exec, %1"
+                    "s_mov_b64 %1, exec\n\ts_mov_b64 exec, 1\n\tds_add_rtn_u32 %0, %2, %3\n\ts_mov_b64 exec, %1"
                     : "=&v"(old), "=&s"(sv)
                     : "v"(a_out), "v"(n)
                     : "memory");
+                const u64 cv = og_pack_cand(b.ox + j, b.oy + i, (int)(ent >> 16) - 1);
+                const int rk = og_rank(mask);
+                __asm__ volatile("s_waitcnt lgkmcnt(0)" : "+v"(old) : : "memory");
                 const int ob = __builtin_amdgcn_readfirstlane(old);
-                if (kbit) out[og_rank(mask, ob)] = og_pack_cand(b.ox + j, b.oy + i, (int)(ent >> 16) - 1);
+                if (kbit) out[ob + rk] = cv;
             }
         }
     }
