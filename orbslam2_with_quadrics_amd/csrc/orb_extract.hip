@@ -600,9 +600,8 @@ typedef unsigned short og_u16x2 __attribute__((ext_vector_type(2)));
 #define FB_MW 80                 // detection height capacity of a block (2 x 40 or 1 x 64); width <= 64
 #define FB_MSW (FB_MW + 3)       // score map stride: a zero gap column before, between and after the cells
 #define FB_MSZ ((FB_MSW * FB_MSW + 15) & ~15)  // 16-byte multiple: zeroed by 16-byte stores
-#ifndef FB_FCHUNK
-#define FB_FCHUNK 64u            // frames per dispatch chunk of og_fast_quad_kernel (a multiple of 8)
-#endif
+#define FB_FCHUNK 64u            // frames per dispatch chunk of og_fast_quad_kernel (a multiple of 8; 16-128 measured,
+                                 // profiles/sweeps/r06_ab_fast_chunk_size.txt)
 
 // score-map index of detection pixel (i, j): one zero row/column separates the block's cells and surrounds
 // them, so a pixel's 8 neighbours outside its cell (or outside the detection area) read 0 without checks
