@@ -1552,8 +1552,11 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                     a = bD + pth;
                     if (!btab) NO[k] = (uint16_t)a;  // (with the cell table only a leave pass needs it: recomputed)
                 }
-                og_wave_count(childCnt, a, k < C);
-                if (btab) og_wave_max32(cellbest, a - bD, key32, k < C);
+                og_wave_count(childCnt, a, k < C);  // (one LDS atomicAdd per key instead: 3 % slower)
+                // the cell's best key: one LDS atomicMax per key (a segmented wave maximum first, og_wave_max32, was 2 %
+                // slower: its 6 DPP steps cost more VALU than the same-address atomics serialise,
+                // profiles/sweeps/r06_ab_octree_plain_atomics.txt)
+                if (btab && k < C) atomicMax(&cellbest[a - bD], key32);
             }
         }
         __syncthreads();
@@ -1927,7 +1930,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                     }
                 }
                 if (!done) og_wave_count(NCC, a, cnt);  // `done`, k32 are workgroup-uniform
-                else if (k32) og_wave_max32(best32, a, key32, k < C);
+                else if (k32 && k < C) atomicMax(&best32[a], key32);  // (plain LDS atomics: see the count pass)
             }
         }
         __syncthreads();
@@ -1979,7 +1982,7 @@ __global__ __launch_bounds__(OCT_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                     else
                         atomicMax(&best[n], ((u64)resp << 32) | (u64)(0xffffffffu - og_cand_order_m(x, y, L, mW, mH)));
                 }
-                if (k32) og_wave_max32(best32, n, key32, k < C);
+                if (k32 && k < C) atomicMax(&best32[n], key32);
             }
         }
         __syncthreads();
